@@ -1,0 +1,352 @@
+"""TEST INFRASTRUCTURE ONLY -- CPU restatement of the SA-VQA model_v=3 hot path.
+
+This module is the parity oracle (task rule: only tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg may use it; the product path never does).
+
+It restates, in plain fp32 PyTorch-CPU tensor ops over a flat dict of the
+reference's state_dict keys, the algorithm of
+  /root/reference/models/modules.py      (layer_normalization, multihead_attention,
+                                          new_multihead_attention, feedforward,
+                                          label_smoothing)
+  /root/reference/models/AttModel_x3.py  (AttModel_vis_grid, AttModel_syb, MIL_NCE
+                                          only_obj branch, AttModel heads)
+  /root/reference/models/main_itp_ddp_tar_super_node.py:335-366 (loss, Adam step)
+Each function cites the reference lines it follows. Backward is torch autograd
+over these ops.
+
+Pinning: tests/test_oracle_golden.py checks this restatement against the golden
+vectors in tests/golden/, which tools/make_golden.py produced by importing and
+running the reference itself in the build container.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict
+
+import torch
+import torch.nn.functional as F
+
+PAD = 400000          # AttModel_x3.py:13
+PAD_NEG = -2 ** 32 + 1  # modules.py:261 (becomes -4294967296.0 in fp32)
+
+
+# --------------------------------------------------------------------------- blocks
+def layer_norm(x, gamma, beta, eps=1e-8):
+    """modules.py:62-65 -- unbiased std, eps added to std."""
+    mean = x.mean(-1, keepdim=True)
+    std = x.std(-1, keepdim=True)
+    return gamma * (x - mean) / (std + eps) + beta
+
+
+def linear(x, P, name, relu=False):
+    y = F.linear(x, P[name + ".weight"], P[name + ".bias"])
+    return F.relu(y) if relu else y
+
+
+def _heads(X, h):
+    """torch.cat(torch.chunk(X, h, 2), 0): (N,T,C) -> (h*N, T, C/h), head-major."""
+    return torch.cat(torch.chunk(X, h, dim=2), dim=0)
+
+
+def _unheads(X, h):
+    return torch.cat(torch.chunk(X, h, dim=0), dim=2)
+
+
+def _mask_scores(S, keys, h, Tq):
+    """modules.py:257-263 key masking by exact-zero feature sums."""
+    km = torch.sign(torch.abs(torch.sum(keys, dim=-1)))          # (N, Tk)
+    km = km.repeat(h, 1).unsqueeze(1).repeat(1, Tq, 1)           # (hN, Tq, Tk)
+    cond = km.eq(0.).float()
+    pad = torch.ones_like(S) * PAD_NEG
+    return pad * cond + S * (1. - cond)
+
+
+def _query_mask(queries, h, Tk):
+    qm = torch.sign(torch.abs(torch.sum(queries, dim=-1)))       # (N, Tq)
+    return qm.repeat(h, 1).unsqueeze(2).repeat(1, 1, Tk)
+
+
+def graph_mha(P, pre, queries, keys, values, graph, h=8, return_att=False):
+    """new_multihead_attention.forward, modules.py:236-311 (dropout p=0)."""
+    Q = linear(queries, P, pre + ".Q_proj.0", relu=True)
+    K = linear(keys, P, pre + ".K_proj.0", relu=True)
+    V = linear(values, P, pre + ".V_proj.0", relu=True)
+    Q_, K_, V_ = _heads(Q, h), _heads(K, h), _heads(V, h)
+    S = torch.bmm(Q_, K_.permute(0, 2, 1)) / (K_.size(-1) ** 0.5)
+    S = _mask_scores(S, keys, h, queries.size(1))
+    A = F.softmax(S, dim=-1)
+    A = graph.repeat(h, 1, 1) * A                                # :280-284
+    A = F.normalize(A, p=1, dim=-1)                              # :285
+    att = A.clone()
+    A = A * _query_mask(queries, h, keys.size(1))                # :289-292
+    O = _unheads(torch.bmm(A, V_), h)                            # :298-301
+    O = O + queries                                              # :304
+    out = layer_norm(O, P[pre + ".normalization.gamma"], P[pre + ".normalization.beta"])
+    return (out, att) if return_att else out
+
+
+def causal_mha(P, pre, queries, keys, values, h=8):
+    """multihead_attention.forward with causality, modules.py:143-207."""
+    Q = linear(queries, P, pre + ".Q_proj.0", relu=True)
+    K = linear(keys, P, pre + ".K_proj.0", relu=True)
+    V = linear(values, P, pre + ".V_proj.0", relu=True)
+    Q_, K_, V_ = _heads(Q, h), _heads(K, h), _heads(V, h)
+    S = torch.bmm(Q_, K_.permute(0, 2, 1)) / (K_.size(-1) ** 0.5)
+    S = _mask_scores(S, keys, h, queries.size(1))
+    tril = torch.tril(torch.ones(S.shape[1:], dtype=S.dtype))
+    cond = tril.unsqueeze(0).repeat(S.size(0), 1, 1).eq(0.).float()
+    S = torch.ones_like(S) * PAD_NEG * cond + S * (1. - cond)
+    A = F.softmax(S, dim=-1)
+    A = A * _query_mask(queries, h, keys.size(1))
+    O = _unheads(torch.bmm(A, V_), h) + queries
+    return layer_norm(O, P[pre + ".normalization.gamma"], P[pre + ".normalization.beta"])
+
+
+def feedforward(P, pre, x):
+    """feedforward.forward, Linear path, modules.py:432-447."""
+    hdn = linear(x, P, pre + ".conv1.0", relu=True)
+    out = linear(hdn, P, pre + ".conv2") + x
+    return layer_norm(out, P[pre + ".normalization.gamma"], P[pre + ".normalization.beta"])
+
+
+# --------------------------------------------------------------------------- graphs
+def build_graphs(node_mask, q_mask, q_graph, node_graph=None, decMask=True):
+    """Per-sample graph construction, AttModel_x3.py:103-122 (vis) / :229-247 (syb).
+
+    Returns (graph_diag, graph, dec_mask). graph_cross is the same tensor as
+    graph in the reference (alias at :118-120 / :244-245), so layers 2-5 all
+    use `graph`.
+    """
+    B, Nn = node_mask.shape[:2]
+    Lq = q_mask.shape[1]
+    T = Nn + Lq
+    mask = torch.zeros((B, T, T))
+    graph_diag = torch.zeros((B, T, T))
+    dec_mask = torch.zeros((B, 1, T))
+    for i in range(B):
+        mask[i] = torch.block_diag(node_mask[i], q_mask[i])
+        graph_diag[i, -Lq:, -Lq:] = q_mask[i].float()
+        if decMask:
+            rs = torch.sum(mask[i], dim=1)
+            rs[rs.nonzero()] = 1
+            dec_mask[i, 0, :] = rs
+    graph = 1 - mask
+    if node_graph is None:
+        graph[:, :Nn, :Nn] = 1
+    else:
+        graph[:, :Nn, :Nn] = node_graph.float()
+    graph[:, Nn:, Nn:] = q_graph.float()
+    return graph_diag, graph, dec_mask
+
+
+# --------------------------------------------------------------------------- stacks
+def _encoder_decoder(P, pre, fea, graph_diag, graph, dec_mask, num_blocks=6, h=8):
+    """Encoder schedule AttModel_x3.py:127-139 and decoder :141-154."""
+    x = fea
+    for i in range(num_blocks):
+        g = graph_diag if i < 2 else graph
+        x = graph_mha(P, f"{pre}.enc_self_attention_{i}", x, x, x, g, h)
+        x = feedforward(P, f"{pre}.enc_feed_forward_{i}", x)
+    B = fea.size(0)
+    d = fea.size(2)
+    dec_in = torch.full((B, 1), 2, dtype=torch.long)
+    dec = F.embedding(dec_in, P[f"{pre}.dec_emb.lookup_table"], 0) * (d ** 0.5)  # modules.py:40-43
+    dec = dec + F.embedding(torch.zeros((B, 1), dtype=torch.long),
+                            P[f"{pre}.dec_positional_encoding.lookup_table"], -1)
+    for i in range(num_blocks):
+        dec = causal_mha(P, f"{pre}.dec_self_attention_{i}", dec, dec, dec, h)
+        dec = graph_mha(P, f"{pre}.dec_vanilla_attention_{i}", dec, x, x, dec_mask, h)
+        dec = feedforward(P, f"{pre}.dec_feed_forward_{i}", dec)
+    return dec
+
+
+def vis_grid_forward(P, vis_fea, vis_mask, q_ipt, q_graph, q_mask, decMask=True,
+                     num_blocks=6, h=8, pre="att_vis_grid"):
+    """AttModel_vis_grid.forward, AttModel_x3.py:91-156."""
+    q = F.embedding(q_ipt, P[f"{pre}.syb_emb.weight"])
+    q = linear(q, P, f"{pre}.syb_mlp.0", relu=True)
+    fea = linear(torch.cat([vis_fea, q], dim=1), P, f"{pre}.syb_mlp2")
+    T = fea.size(1)
+    pos = torch.arange(T).unsqueeze(0).repeat(fea.size(0), 1)
+    fea = fea + F.embedding(pos, P[f"{pre}.syb_positional_encoding.0.lookup_table"], -1)
+    gd, g, dm = build_graphs(vis_mask, q_mask, q_graph, None, decMask)
+    return _encoder_decoder(P, pre, fea, gd, g, dm, num_blocks, h)
+
+
+def syb_forward(P, syb_ipt, syb_mask, syb_graph, q_ipt, q_graph, q_mask, decMask=True,
+                num_blocks=6, h=8, pre="att_syb"):
+    """AttModel_syb.forward, AttModel_x3.py:214-282."""
+    q = F.embedding(q_ipt, P[f"{pre}.syb_emb.weight"])
+    q = linear(q, P, f"{pre}.syb_mlp.0", relu=True)
+    fea = linear(torch.cat([syb_ipt, q], dim=1), P, f"{pre}.syb_mlp2")
+    T = fea.size(1)
+    pos = torch.arange(T).unsqueeze(0).repeat(fea.size(0), 1)
+    fea = fea + F.embedding(pos, P[f"{pre}.syb_positional_encoding.lookup_table"], -1)
+    gd, g, dm = build_graphs(syb_mask, q_mask, q_graph, syb_graph, decMask)
+    return _encoder_decoder(P, pre, fea, gd, g, dm, num_blocks, h)
+
+
+def mil_nce_forward(P, vis_fea, macro_ipt, macro_obj_loc, pos_obj, neg_obj, obj_mask,
+                    pre="MIL_NCE", eps=1e-6):
+    """MIL_NCE.forward only_obj branch, AttModel_x3.py:338-380 and :441."""
+    E = P[f"{pre}.syb_emb.weight"]
+    macro = linear(F.embedding(macro_ipt, E), P, f"{pre}.marco_mlp.0", relu=True).detach()
+    Pf = linear(F.embedding(pos_obj, E), P, f"{pre}.syb_mlp.0", relu=True)   # (B,Nv,K,H)
+    Nf = linear(F.embedding(neg_obj, E), P, f"{pre}.syb_mlp.0", relu=True)
+    v = linear(vis_fea, P, f"{pre}.vis_mlp.0", relu=True).unsqueeze(3)       # (B,Nv,H,1)
+    m4 = obj_mask.unsqueeze(3)
+    sp = m4 * torch.matmul(Pf, v)                                             # (B,Nv,K,1)
+    sn = m4 * torch.matmul(Nf, v)
+    zeros = torch.zeros(sn.size())
+    mil = torch.mean(torch.logsumexp(torch.cat((sp.clamp(min=eps), zeros.clamp(min=eps)), 1), 2)
+                     - torch.logsumexp(torch.cat((sp.clamp(min=eps), sn.clamp(min=eps)), 1), 2))
+    w = F.softmax(torch.matmul(Pf, v), dim=2)                                 # :372-374
+    obj = torch.sum(w * Pf, dim=2)                                            # (B,Nv,H)
+    valid = (macro_obj_loc >= 0).nonzero()                                    # :377-380
+    macro[valid[:, 0], macro_obj_loc[valid[:, 0], valid[:, 1]].long(), :] = obj[valid[:, 0], valid[:, 1], :]
+    out = linear(macro, P, f"{pre}.ipt_mlp.0", relu=True)
+    return out, mil, 0
+
+
+def heads(P, fea_vis, fea_syb):
+    """AttModel.forward heads, AttModel_x3.py:531-541 (mcb=False, dropout p=0)."""
+    def head(x, name):
+        return linear(linear(x, P, f"{name}.0", relu=True), P, f"{name}.3")
+    logits_vis = head(fea_vis, "cls_vis").squeeze(1)
+    logits_syb = head(fea_syb, "cls_syb").squeeze(1)
+    fea = torch.cat((fea_syb.squeeze(1), fea_vis.squeeze(1)), 1)
+    logits_concat = head(fea, "cls")
+    return logits_concat, logits_vis, logits_syb
+
+
+def attmodel_forward(P, inp: Dict[str, torch.Tensor], decMask=True, num_blocks=6, h=8):
+    """AttModel.forward, AttModel_x3.py:512-542 (only_obj, mcb=False)."""
+    new_macro, mil_obj, mil_rel = mil_nce_forward(
+        P, inp["vis_fea"], inp["macro_ipt"], inp["macro_obj_loc"],
+        inp["micro_positive_obj"], inp["micro_negative_obj"], inp["micro_obj_mask"])
+    f_vis = vis_grid_forward(P, inp["vis_fea"], inp["vis_mask"], inp["q_ipt"], inp["q_graph"],
+                             inp["q_mask"], decMask, num_blocks, h)
+    f_syb = syb_forward(P, new_macro, inp["macro_mask"], inp["macro_graph"], inp["q_ipt"],
+                        inp["q_graph"], inp["q_mask"], decMask, num_blocks, h)
+    lc, lv, ls = heads(P, f_vis, f_syb)
+    return lc, lv, ls, mil_obj, mil_rel
+
+
+# --------------------------------------------------------------------------- loss / optim
+def train_loss(logits_concat, logits_vis, logits_syb, answer, mil_nce_obj,
+               with_milnce=True, epsilon=0.1):
+    """main_itp_ddp_tar_super_node.py:335-361 with label_smoothing modules.py:461-463."""
+    lsm = (F.log_softmax(logits_vis, -1) + F.log_softmax(logits_syb, -1)
+           + F.log_softmax(logits_concat, -1)) / 3
+    oh = torch.zeros_like(logits_concat)
+    oh.scatter_(1, answer.view(-1, 1), 1)
+    oh = (1 - epsilon) * oh + epsilon / oh.size(-1)
+    loss = (-(oh * lsm).sum(-1)).mean()
+    if with_milnce:
+        loss = loss + (-mil_nce_obj)
+    return loss, lsm
+
+
+def adam_step(params, grads, state, step, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8):
+    """torch.optim.Adam single-tensor update (main:206, :366), restated."""
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    for k, p in params.items():
+        g = grads.get(k)
+        if g is None:
+            continue
+        m, v = state.setdefault(k, (torch.zeros_like(p), torch.zeros_like(p)))
+        m.mul_(beta1).add_(g, alpha=1 - beta1)
+        v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+        denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+        p.addcdiv_(m, denom, value=-(lr / bc1))
+
+
+# --------------------------------------------------------------------------- params
+def model_param_shapes(hidden=512, hidden_mil=1024, num_classes=914, maxlen_q=40, maxlen=450,
+                       maxlen_v=49, num_blocks=6, num_relations=311, vocab=407000, emb=300):
+    """Reference state_dict keys and shapes in registration order (AttModel_x3.py:20-510)."""
+    d = hidden
+    out = []
+
+    def lin(name, i, o):
+        out.append((f"{name}.weight", (o, i)))
+        out.append((f"{name}.bias", (o,)))
+
+    def ln(name):
+        out.append((f"{name}.gamma", (d,)))
+        out.append((f"{name}.beta", (d,)))
+
+    def mha(name):
+        for p in ("Q_proj", "K_proj", "V_proj"):
+            lin(f"{name}.{p}.0", d, d)
+        ln(f"{name}.normalization")
+
+    def ffn(name):
+        lin(f"{name}.conv1.0", d, 4 * d)
+        lin(f"{name}.conv2", 4 * d, d)
+        ln(f"{name}.normalization")
+
+    v = "att_vis_grid"
+    out.append((f"{v}.syb_emb.weight", (vocab, emb)))
+    lin(f"{v}.syb_mlp.0", emb, 2048)
+    lin(f"{v}.syb_mlp2", 2048, d)
+    lin(f"{v}.v_mlp.0", 2048, d)
+    lin(f"{v}.v_mlp.2", d, d)
+    out.append((f"{v}.v_positional_encoding.0.lookup_table", (maxlen_v, d)))
+    lin(f"{v}.input_proj", 2048, d)
+    for i in range(num_blocks):
+        mha(f"{v}.enc_self_attention_{i}")
+        ffn(f"{v}.enc_feed_forward_{i}")
+    lin(f"{v}.q_mlp.0", emb, d)
+    lin(f"{v}.q_mlp.2", d, d)
+    out.append((f"{v}.q_positional_encoding.0.lookup_table", (maxlen_q, d)))
+    out.append((f"{v}.syb_positional_encoding.0.lookup_table", (maxlen, d)))
+    out.append((f"{v}.dec_emb.lookup_table", (num_classes, d)))
+    out.append((f"{v}.dec_positional_encoding.lookup_table", (maxlen, d)))
+    for i in range(num_blocks):
+        mha(f"{v}.dec_self_attention_{i}")
+        mha(f"{v}.dec_vanilla_attention_{i}")
+        ffn(f"{v}.dec_feed_forward_{i}")
+
+    s = "att_syb"
+    out.append((f"{s}.syb_emb.weight", (vocab, emb)))
+    lin(f"{s}.syb_mlp.0", emb, 2048)
+    lin(f"{s}.syb_mlp2", 2048, d)
+    out.append((f"{s}.syb_positional_encoding.lookup_table", (maxlen + maxlen_q, d)))
+    lin(f"{s}.q_mlp.0", emb, d)
+    lin(f"{s}.q_mlp.1", d, d)
+    out.append((f"{s}.q_positional_encoding.0.lookup_table", (maxlen_q, d)))
+    out.append((f"{s}.dec_emb.lookup_table", (num_classes, d)))
+    out.append((f"{s}.dec_positional_encoding.lookup_table", (maxlen + maxlen_q, d)))
+    for i in range(num_blocks):
+        mha(f"{s}.dec_self_attention_{i}")
+        mha(f"{s}.dec_vanilla_attention_{i}")
+        ffn(f"{s}.dec_feed_forward_{i}")
+    for i in range(num_blocks):
+        mha(f"{s}.enc_self_attention_{i}")
+        ffn(f"{s}.enc_feed_forward_{i}")
+
+    m = "MIL_NCE"
+    H = hidden_mil
+    out.append((f"{m}.R", (num_relations, H, H)))
+    out.append((f"{m}.syb_emb.weight", (vocab, emb)))
+    lin(f"{m}.marco_mlp.0", emb, H)
+    lin(f"{m}.syb_mlp.0", emb, H)
+    lin(f"{m}.vis_mlp.0", 2048, H)
+    lin(f"{m}.rel_mlp.0", H, H)
+    lin(f"{m}.rel_mlp.2", H, 1)
+    out.append((f"{m}.bilinear.weight", (num_relations, H, H)))
+    lin(f"{m}.ipt_mlp.0", H, 2048)
+
+    lin("cls.0", 2 * d, d)
+    lin("cls.3", d, num_classes)
+    lin("cls_vis.0", d, d)
+    lin("cls_vis.3", d, num_classes)
+    lin("cls_syb.0", d, d)
+    lin("cls_syb.3", d, num_classes)
+    out.append(("mcb.sketch1", (d, 16000)))
+    out.append(("mcb.sketch2", (d, 16000)))
+    lin("cls_mcb.0", 16000, d)
+    lin("cls_mcb.3", d, num_classes)
+    return out

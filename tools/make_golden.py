@@ -1,0 +1,252 @@
+#!/usr/bin/env python
+"""Generate golden vectors by importing and running the REFERENCE (build container only).
+
+Runs /root/reference/models/{modules.py, AttModel_x3.py} on CPU with the harness
+shims of SURVEY.md section 8(c) (the reference files are never modified, no
+bytecode is written under /root/reference):
+  (1) torch.Tensor.cuda -> identity (hard-coded .cuda() calls),
+  (2) construction under torch.no_grad() (in-place writes into leaf Parameters),
+  (3) glove = SimpleNamespace(vectors=...) (torchtext absent),
+  (4) dropout_rate = 0 (ReLU -> inplace Dropout backward error on torch 2.x),
+  (5) mcb=False (torch.rfft removed).
+All weights and inputs come from oracle/hashfill.py, so no weights are committed.
+The loss / Adam step restate main_itp_ddp_tar_super_node.py:335-366 inline here
+because that file imports azureml (not installed) and cannot be imported.
+
+Outputs (committed): tests/golden/*.npz and tests/golden/state_dict_keys.json.
+No-op when /root/reference is absent (e.g. on the GPU box).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+REF = "/root/reference/models"
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+OUT = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from oracle import cases, hashfill  # noqa: E402
+
+torch.Tensor.cuda = lambda self, *a, **k: self  # shim (1)
+torch.set_num_threads(os.cpu_count() or 8)
+
+# geometry of the parity cases (cfg 1 shapes; num_relations kept small: R/bilinear are
+# dead in only_obj mode and only their shapes enter the state_dict)
+CFG = dict(hidden=512, hidden_mil=1024, num_classes=914, maxlen_q=40, maxlen=450,
+           maxlen_v=49, num_blocks=6, heads=8, num_relations=4)
+
+
+def n_sample(name, n, k=24):
+    return np.unique(hashfill.randint("sample:" + name, (k,), 0, n))
+
+
+def grad_digest(name, g: torch.Tensor):
+    """Compact digest of a gradient: sums + sampled entries (+ touched rows for tables)."""
+    flat = g.detach().reshape(-1).double()
+    idx = n_sample(name, flat.numel())
+    d = {"sum": float(flat.sum()), "abssum": float(flat.abs().sum()),
+         "idx": idx.astype(np.int64), "val": flat[idx].float().numpy()}
+    return d
+
+
+make_inputs = cases.make_inputs
+
+def fill_params(model):
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            p.copy_(torch.from_numpy(hashfill.param_value(name, tuple(p.shape))))
+        for name, b in model.named_buffers():
+            pass
+
+
+def ref_loss(lc, lv, ls, answer, mil_obj, eps=0.1):
+    # main_itp_ddp_tar_super_node.py:335-361 (with_smooth_labeling, with_MILNCE_loss)
+    lsm = (F.log_softmax(lv, -1) + F.log_softmax(ls, -1) + F.log_softmax(lc, -1)) / 3
+    oh = torch.zeros((lc.size(0), lc.size(1)))
+    oh.scatter_(1, answer.view(-1, 1), 1)
+    oh = ((1 - eps) * oh) + (eps / oh.size(-1))
+    loss = -(oh * lsm).sum(-1)
+    loss = loss.mean()
+    loss = loss + (-mil_obj)
+    return loss
+
+
+def to_t(inp):
+    return {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in inp.items()}
+
+
+def full_model_cases(modules_mod, att_mod):
+    glove = types.SimpleNamespace(vectors=torch.zeros(8, 300))
+    with torch.no_grad():
+        model = att_mod.AttModel(glove, CFG["hidden"], CFG["hidden_mil"], CFG["num_classes"],
+                                 CFG["maxlen_q"], CFG["maxlen"], CFG["maxlen_v"],
+                                 CFG["num_blocks"], CFG["heads"], 0.0, 0.0,
+                                 CFG["num_relations"], True)
+    model.train()
+    keys = [(k, list(v.shape)) for k, v in model.state_dict().items()]
+    with open(os.path.join(OUT, "state_dict_keys.json"), "w") as f:
+        json.dump({"num_relations": CFG["num_relations"], "keys": keys}, f)
+    print("state_dict keys:", len(keys))
+    fill_params(model)
+
+    runs = {
+        "full_b4": dict(B=4, Nv=[36, 30, 22, 36], Lq=[14, 9, 12, 6], Ns=[59, 40, 31, 50], decMask=True),
+        "full_b2_nodec": dict(B=2, Nv=[36, 17], Lq=[14, 11], Ns=[59, 23], decMask=False),
+    }
+    for cname, c in runs.items():
+        inp = make_inputs(c["B"], c["Nv"], c["Lq"], c["Ns"], tag=cname)
+        t = to_t(inp)
+        empty = torch.empty((c["B"], 0))
+        fill_params(model)
+        opt = torch.optim.Adam(model.parameters(), 1e-4)
+
+        def fwd():
+            return model(t["vis_fea"], t["vis_mask"], t["q_ipt"], t["q_mask"], t["q_graph"],
+                         t["macro_ipt"], t["macro_mask"], t["macro_graph"], t["macro_obj_loc"],
+                         t["micro_positive_obj"], t["micro_negative_obj"], t["micro_obj_mask"],
+                         empty, empty, empty, empty, decMask=c["decMask"], mcb=False)
+
+        lc, lv, ls, mil, _ = fwd()
+        loss = ref_loss(lc, lv, ls, t["answer"], mil)
+        opt.zero_grad()
+        loss.backward()
+        out = dict(inp)
+        out.update(logits_concat=lc.detach().numpy(), logits_vis=lv.detach().numpy(),
+                   logits_syb=ls.detach().numpy(), mil_nce_obj=np.float32(mil.item()),
+                   loss=np.float32(loss.item()), decMask=np.int32(c["decMask"]))
+        gnames = []
+        for name, p in model.named_parameters():
+            if p.grad is None:
+                continue
+            gnames.append(name)
+            d = grad_digest(name, p.grad)
+            out[f"g:{name}:sum"] = np.float64(d["sum"])
+            out[f"g:{name}:abssum"] = np.float64(d["abssum"])
+            out[f"g:{name}:idx"] = d["idx"]
+            out[f"g:{name}:val"] = d["val"]
+            if name.endswith("syb_emb.weight"):
+                rows = np.unique(np.concatenate([inp["q_ipt"].ravel(), inp["micro_negative_obj"].ravel()]))
+                rows = rows[:12]
+                out[f"g:{name}:rows"] = rows
+                out[f"g:{name}:rowval"] = p.grad[torch.from_numpy(rows)].numpy()
+        out["grad_names"] = np.array(gnames)
+        # two Adam steps: logits after each (exercises loss->backward->Adam end to end)
+        opt.step()
+        for s in (1, 2):
+            lc, lv, ls, mil, _ = fwd()
+            out[f"step{s}_logits_concat"] = lc.detach().numpy()
+            out[f"step{s}_mil"] = np.float32(mil.item())
+            if s == 1:
+                loss = ref_loss(lc, lv, ls, t["answer"], mil)
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+        np.savez_compressed(os.path.join(OUT, f"{cname}.npz"), **out)
+        print("wrote", cname, "loss", float(out["loss"]))
+    del model
+
+
+def block_cases(modules_mod):
+    out = {}
+    torch.manual_seed(0)
+    d = 512
+
+    def mk(cls, name, *a, **k):
+        m = cls(*a, **k)
+        with torch.no_grad():
+            for pn, p in m.named_parameters():
+                p.copy_(torch.from_numpy(hashfill.param_value(f"{name}.{pn}", tuple(p.shape))))
+        return m
+
+    # encoder self-attention, several graph patterns
+    for T, gnames in ((50, ("rand", "diag")), (73, ("rand", "ones"))):
+        x, graphs = cases.block_mha_inputs(T)
+        m = mk(modules_mod.new_multihead_attention, f"blk.mha{T}", d, 8, 0, False, True)
+        for gname in gnames:
+            g = graphs[gname]
+            xx = x.clone().requires_grad_(True)
+            o, att = m(xx, xx, xx, g)
+            dout = torch.from_numpy(hashfill.fill(f"blk:dout:{T}:{gname}", o.shape, 1.0))
+            m.zero_grad()
+            (o * dout).sum().backward()
+            key = f"mha_T{T}_{gname}"
+            out[f"{key}:out"] = o.detach().numpy()
+            out[f"{key}:att"] = att.detach().numpy()
+            out[f"{key}:dx"] = xx.grad.numpy()
+            for pn, p in m.named_parameters():
+                out[f"{key}:g:{pn}"] = p.grad.numpy().copy() if p.grad.numel() <= 1024 else \
+                    p.grad.numpy()[:4].copy()
+                out[f"{key}:gsum:{pn}"] = np.float64(p.grad.double().sum())
+
+    # decoder cross attention (T_q = 1) with a dec_mask that has zeros
+    B, T = 3, 73
+    q = torch.from_numpy(hashfill.fill("blk:xq", (B, 1, d), 1.0))
+    kv = torch.from_numpy(hashfill.fill("blk:kv", (B, T, d), 1.0))
+    dm = torch.from_numpy(hashfill.bernoulli("blk:dm", (B, 1, T), 0.7)).float()
+    dm[2] = 0.0  # a sample whose decoder attends to nothing
+    m = mk(modules_mod.new_multihead_attention, "blk.cross", d, 8, 0, False, True)
+    qq = q.clone().requires_grad_(True)
+    kk = kv.clone().requires_grad_(True)
+    o, att = m(qq, kk, kk, dm)
+    dout = torch.from_numpy(hashfill.fill("blk:cross:dout", o.shape, 1.0))
+    (o * dout).sum().backward()
+    out.update({"cross:q": q.numpy(), "cross:kv": kv.numpy(), "cross:dm": dm.numpy(),
+                "cross:out": o.detach().numpy(), "cross:att": att.detach().numpy(),
+                "cross:dout": dout.numpy(), "cross:dq": qq.grad.numpy(), "cross:dkv": kk.grad.numpy()})
+
+    # decoder causal self-attention, T = 1
+    m = mk(modules_mod.multihead_attention, "blk.causal", d, 8, 0, True)
+    qq = q.clone().requires_grad_(True)
+    o = m(qq, qq, qq)
+    (o * dout).sum().backward()
+    out.update({"causal:out": o.detach().numpy(), "causal:dq": qq.grad.numpy(),
+                "causal:gQ": np.float64(m.Q_proj[0].weight.grad.abs().sum()),
+                "causal:gV": np.float64(m.V_proj[0].weight.grad.double().sum())})
+
+    # layer norm and feed-forward
+    x = torch.from_numpy(hashfill.fill("blk:lnx", (4, 7, d), 2.0, 0.3))
+    ln = mk(modules_mod.layer_normalization, "blk.ln", d)
+    xx = x.clone().requires_grad_(True)
+    o = ln(xx)
+    dout = torch.from_numpy(hashfill.fill("blk:ln:dout", o.shape, 1.0))
+    (o * dout).sum().backward()
+    out.update({"ln:x": x.numpy(), "ln:out": o.detach().numpy(), "ln:dout": dout.numpy(),
+                "ln:dx": xx.grad.numpy(), "ln:dgamma": ln.gamma.grad.numpy(), "ln:dbeta": ln.beta.grad.numpy()})
+    ff = mk(modules_mod.feedforward, "blk.ffn", d, [4 * d, d])
+    xx = x.clone().requires_grad_(True)
+    o = ff(xx)
+    (o * dout).sum().backward()
+    out.update({"ffn:out": o.detach().numpy(), "ffn:dx": xx.grad.numpy(),
+                "ffn:g:conv1.0.bias": ff.conv1[0].bias.grad.numpy(),
+                "ffn:g:conv2.bias": ff.conv2.bias.grad.numpy(),
+                "ffn:gsum:conv1.0.weight": np.float64(ff.conv1[0].weight.grad.double().sum())})
+    np.savez_compressed(os.path.join(OUT, "blocks.npz"), **out)
+    print("wrote blocks.npz")
+
+
+def main():
+    if not os.path.isdir(REF):
+        print("reference absent; nothing to do")
+        return
+    os.makedirs(OUT, exist_ok=True)
+    sys.path.insert(0, REF)
+    import modules as modules_mod  # noqa: E402  (reference)
+    import AttModel_x3 as att_mod  # noqa: E402  (reference)
+    which = sys.argv[1:] or ["blocks", "full"]
+    if "blocks" in which:
+        block_cases(modules_mod)
+    if "full" in which:
+        full_model_cases(modules_mod, att_mod)
+
+
+if __name__ == "__main__":
+    main()
