@@ -1,0 +1,195 @@
+/*
+ * savqa.h -- C ABI of libsavqa.so, the MI355X (gfx950) kernel library behind the
+ * SA-VQA model_v=3 structured-alignment hot path.
+ *
+ * The reference (Peixixiong/Structured-Alignment-VQA) has no FFI: every op is a
+ * PyTorch/ATen call from Python. Each entry point below replaces the ATen op
+ * sequence of the reference function cited in its comment (file:line under
+ * models/). The host side (structured-alignment-vqa_amd/, imported as savqa_amd)
+ * binds these with ctypes.
+ *
+ * Conventions (all entry points):
+ *  - every pointer is a device pointer owned by the caller; the library never
+ *    allocates or frees device memory and keeps no state between calls;
+ *  - all work is enqueued asynchronously on `stream` (a hipStream_t); no host
+ *    synchronisation happens inside, so calls are capturable into hipGraphs;
+ *  - tensors are fp32 unless stated; index tensors are int64 (as the reference's
+ *    collate_fn produces them); mask/graph inputs are int32;
+ *  - return 0 on success, a hipError_t (>0) or a negative SAVQA_E* code on
+ *    failure; savqa_last_error() returns a thread-local message.
+ */
+#ifndef SAVQA_H
+#define SAVQA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SAVQA_EINVAL (-1)   /* bad shape / argument */
+#define SAVQA_EUNSUP (-2)   /* shape outside what the kernel supports */
+
+int savqa_version(void);
+const char* savqa_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * GEMM:  C[crow(m)][n] (op)= epilogue( sum_k A(m,k) * B(k,n) )
+ * Replaces every nn.Linear of the path (modules.py:135-137, 227-229, 428-429;
+ * AttModel_x3.py:42-44, 173-175, 316-335, 482-500) and their backward GEMMs.
+ *   A(m,k) = a_trans ? A[ra(k)*lda + m] : A[ra(m)*lda + k]   ra(i) = a_rows ? a_rows[i] : i
+ *   B(k,n) = b_trans ? B[rb(n)*ldb + k] : B[rb(k)*ldb + n]   rb(i) = b_rows ? b_rows[i] : i
+ *            (b_trans=1: nn.Linear weight [N][K]; the *_rows gathers implement F.embedding)
+ *   crow(m) = c_rows ? c_rows[m] : (m / c_group) * c_stride + (m % c_group) + c_offset
+ *   v = acc*alpha + bias[n] + rowvec[(m % rowvec_period)*ldrv + n]
+ *   v = relu ? max(v,0) : v ;  v *= rowscale[m] ;
+ *   v = (mask && !(mask[mr*ldmask+n] > 0)) ? 0 : v   mr = mask_arows ? a_rows[m] : m
+ *   v += resid[m*ldr + n]
+ *   C = atomic ? C + v (atomicAdd) : v + beta*C
+ * split_k > 1 splits K across workgroups and forces atomic accumulation.
+ * ------------------------------------------------------------------------ */
+typedef struct savqa_gemm_desc {
+    int64_t M, N, K;
+    const float* A; int64_t lda; int32_t a_trans; int32_t _pad0;
+    const int64_t* a_rows;
+    const float* B; int64_t ldb; int32_t b_trans; int32_t _pad1;
+    const int64_t* b_rows;
+    float* C; int64_t ldc;
+    int64_t c_group, c_stride, c_offset;
+    const int64_t* c_rows;
+    const float* bias;
+    const float* rowvec; int64_t ldrv; int64_t rowvec_period;
+    const float* resid; int64_t ldr;
+    const float* mask; int64_t ldmask; int64_t mask_arows;
+    const float* rowscale;
+    float alpha, beta;
+    int32_t relu, atomic, split_k, _pad2;
+} savqa_gemm_desc;
+
+int savqa_gemm(void* stream, const savqa_gemm_desc* d);
+
+/* out[c] += sum_r X[r*ldx + c]  (bias gradients of every Linear above) */
+int savqa_colsum_acc(void* stream, const float* X, int64_t rows, int64_t cols, int64_t ldx, float* out);
+
+/* ------------------------------------------------------------------------
+ * Residual + layer_normalization (modules.py:62-65: mean, UNBIASED std, eps on std),
+ * fused with the residual add of modules.py:304 / :439:
+ *   z = x*xscale[row] + r ;  y = gamma*(z-mean)/(std+eps) + beta   (xscale, r optional;
+ *   xscale carries the decoder self-attention's query mask, modules.py:187-190)
+ * Saves z (if z_out), mean, rden = 1/(std+eps), std; flag[row] = sign(|sum_c y|)
+ * (the key/query mask of the next attention, modules.py:257/:289) if flag != NULL.
+ * ------------------------------------------------------------------------ */
+int savqa_ln_fwd(void* stream, const float* x, const float* xscale, const float* r,
+                 int64_t rows, int64_t cols,
+                 const float* gamma, const float* beta, float eps,
+                 float* z_out, float* y, float* mean, float* rden, float* stdv, float* flag);
+
+/* Backward of the above: dz = dLN/dz (+ dz_add), dgamma += ..., dbeta += ... */
+int savqa_ln_bwd(void* stream, const float* dy, const float* z, const float* mean,
+                 const float* rden, const float* stdv, const float* gamma,
+                 int64_t rows, int64_t cols, const float* dz_add, float* dz,
+                 float* dgamma, float* dbeta);
+
+/* flag[r] = sign(|sum_c X[r*ldx+c]|)  (modules.py:257 key mask / :289 query mask) */
+int savqa_rowflag(void* stream, const float* X, int64_t rows, int64_t cols, int64_t ldx, float* flag);
+
+/* ------------------------------------------------------------------------
+ * Graph-guided attention core, new_multihead_attention.forward modules.py:246-301
+ * (after the ReLU'd projections, before the residual):
+ *   S = Q_h K_h^T / sqrt(dk);  S[:, j] = -4294967296 where kflag[b,j] == 0
+ *   A = softmax_row(S);  Bm = A * G[b];  N = Bm / max(sum|Bm|, 1e-12);  P = N * qflag[b,i]
+ *   O_h = P V_h
+ * Q/K/V are strided views: row (b*Tq+i) of Q at q + (b*Tq+i)*ldq + h*dk, etc.
+ * G is (B, Tq, Tk) fp32 (dense graph / dec_mask). att (optional) receives N in the
+ * reference's head-major (h*B + b, Tq, Tk) layout (return_att, modules.py:286).
+ * ------------------------------------------------------------------------ */
+int savqa_gattn_fwd(void* stream, const float* q, int64_t ldq, const float* k, int64_t ldk,
+                    const float* v, int64_t ldv, const float* G, const float* kflag,
+                    const float* qflag, int64_t B, int64_t Tq, int64_t Tk, int64_t H, int64_t dk,
+                    float* o, int64_t ldo, float* att);
+
+/* Backward: given dO, recompute P and write dQ/dK/dV already multiplied by the
+ * ReLU masks of the projections (Q>0 etc.), i.e. the pre-activation gradients. */
+int savqa_gattn_bwd(void* stream, const float* q, int64_t ldq, const float* k, int64_t ldk,
+                    const float* v, int64_t ldv, const float* G, const float* kflag,
+                    const float* qflag, int64_t B, int64_t Tq, int64_t Tk, int64_t H, int64_t dk,
+                    const float* dout, int64_t lddo, float* dq, int64_t lddq, float* dk_, int64_t lddk,
+                    float* dv, int64_t lddv);
+
+/* ------------------------------------------------------------------------
+ * Graph construction, AttModel_x3.py:103-122 (vis, node_graph == NULL) and
+ * :229-247 (syb): graph_diag, graph (== graph_cross, aliased in the reference),
+ * dec_mask. Inputs int32 (B,Nn,Nn), (B,Lq,Lq), (B,Lq,Lq), optional (B,Nn,Nn).
+ * ------------------------------------------------------------------------ */
+int savqa_graph_build(void* stream, const int32_t* node_mask, const int32_t* q_mask,
+                      const int32_t* q_graph, const int32_t* node_graph, int64_t B, int64_t Nn,
+                      int64_t Lq, int32_t dec_mask_on, float* graph_diag, float* graph,
+                      float* dec_mask);
+
+/* dec0[b,:] = emb[idx,:]*scale + pos[0,:]   (AttModel_x3.py:141-146, modules.py:40-43) */
+int savqa_dec_init(void* stream, const float* emb, int64_t idx, float scale, const float* pos,
+                   int64_t B, int64_t d, float* out);
+
+/* backward of savqa_dec_init: demb[idx,:] += scale*sum_b g[b,:]; dpos[0,:] += sum_b g[b,:] */
+int savqa_dec_init_bwd(void* stream, const float* g, int64_t B, int64_t d, int64_t idx, float scale,
+                       float* demb, float* dpos);
+
+/* out[t][c] += sum_b X[(b*T+t)*ldx + c]: gradient of the learned position tables
+ * (syb_positional_encoding, AttModel_x3.py:100-101, :225-226; padding_idx=-1 row untouched
+ * as long as T < maxlen, which the loader guarantees). */
+int savqa_period_sum_acc(void* stream, const float* X, int64_t B, int64_t T, int64_t C, int64_t ldx,
+                         float* out);
+
+/* dst rows: dst[(r/group)*stride + r%group + offset][:cols] = src[r][:cols]  (torch.cat) */
+int savqa_copy_rows(void* stream, const float* src, int64_t rows, int64_t cols, int64_t lds,
+                    float* dst, int64_t ldd, int64_t group, int64_t stride, int64_t offset);
+
+/* ------------------------------------------------------------------------
+ * MIL-NCE only_obj core, AttModel_x3.py:361-374:
+ *   s+ = Pf.v, s- = Nf.v (per (b,n,k)); w = softmax_k(s+); obj[b,n] = sum_k w Pf
+ *   term[b,n] = LSE_k(eps) - LSE_k(max(mask*s-, eps));  mil = sum term / (2*B*Nv)
+ * Pf, Nf: (B*Nv*K, H) post-ReLU; v: (B*Nv, H) post-ReLU; mask int32 (B,Nv,K).
+ * mil_out: device scalar. ws: (B*Nv) floats of workspace.
+ * ------------------------------------------------------------------------ */
+int savqa_mil_fwd(void* stream, const float* Pf, const float* Nf, const float* v,
+                  const int32_t* mask, int64_t BN, int64_t K, int64_t H, float eps,
+                  float* obj, float* ws, float* mil_out);
+/* Backward: dobj (BN,H) (may be NULL), dmil (device scalar) -> dPf, dNf, dv (pre-ReLU). */
+int savqa_mil_bwd(void* stream, const float* Pf, const float* Nf, const float* v,
+                  const int32_t* mask, int64_t BN, int64_t K, int64_t H, float eps,
+                  const float* dobj, const float* dmil, float* dPf, float* dNf, float* dv);
+
+/* macro[b*Ns + loc[b,n]][:] = obj[b*Nv+n][:] for loc >= 0 (AttModel_x3.py:377-380),
+ * and its backward dobj[b*Nv+n] = dmacro[b*Ns+loc] (dobj rows with loc < 0 zeroed). */
+int savqa_index_put_rows(void* stream, const int64_t* loc, int64_t B, int64_t Nv, int64_t Ns,
+                         int64_t H, const float* obj, float* macro);
+int savqa_index_get_rows(void* stream, const int64_t* loc, int64_t B, int64_t Nv, int64_t Ns,
+                         int64_t H, const float* dmacro, float* dobj);
+
+/* ------------------------------------------------------------------------
+ * Loss, main_itp_ddp_tar_super_node.py:335-361 + label_smoothing modules.py:461-463:
+ *   lsm = (lsm(vis)+lsm(syb)+lsm(concat))/3; y = (1-eps)*onehot + eps/C
+ *   loss = mean_b(-sum_c y*lsm) - (with_mil ? mil : 0)
+ * Also writes dlogits (3,B,C) = d loss / d logits (order concat, vis, syb), and
+ * lsm (B,C) if non-NULL. loss: device scalar. ws: B floats.
+ * ------------------------------------------------------------------------ */
+int savqa_loss_fwd(void* stream, const float* lc, const float* lv, const float* ls,
+                   const int64_t* answer, int64_t B, int64_t C, float eps, const float* mil,
+                   int32_t with_mil, float* loss, float* dlogits, float* lsm, float* ws);
+
+/* out[i] = in[i] * (*scale)  (chain rule with a device-side upstream gradient) */
+int savqa_scale_by(void* stream, const float* in, const float* scale, int64_t n, float* out);
+
+/* ------------------------------------------------------------------------
+ * Adam (torch.optim.Adam semantics, main:206/:366) over one flat fp32 range:
+ *   g' = g*grad_scale; m = b1 m + (1-b1) g'; v = b2 v + (1-b2) g'^2
+ *   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+ * ------------------------------------------------------------------------ */
+int savqa_adam(void* stream, float* p, const float* g, float* m, float* v, int64_t n,
+               float lr, float beta1, float beta2, float eps, float bc1, float bc2,
+               float grad_scale);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAVQA_H */

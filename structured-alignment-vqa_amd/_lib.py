@@ -1,0 +1,104 @@
+"""ctypes binding of libsavqa.so (C ABI declared in include/savqa.h).
+
+The library is built in-tree (structured-alignment-vqa_amd/libsavqa.so) by
+`make -C structured-alignment-vqa_amd/csrc` or __graft_entry__.build(). There is no
+fallback: every op raises if the library (or a HIP device) is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsavqa.so")
+
+c_i64 = C.c_int64
+c_i32 = C.c_int32
+c_f = C.c_float
+c_p = C.c_void_p
+
+
+class GemmDesc(C.Structure):
+    _fields_ = [
+        ("M", c_i64), ("N", c_i64), ("K", c_i64),
+        ("A", c_p), ("lda", c_i64), ("a_trans", c_i32), ("_pad0", c_i32),
+        ("a_rows", c_p),
+        ("B", c_p), ("ldb", c_i64), ("b_trans", c_i32), ("_pad1", c_i32),
+        ("b_rows", c_p),
+        ("C", c_p), ("ldc", c_i64),
+        ("c_group", c_i64), ("c_stride", c_i64), ("c_offset", c_i64),
+        ("c_rows", c_p),
+        ("bias", c_p),
+        ("rowvec", c_p), ("ldrv", c_i64), ("rowvec_period", c_i64),
+        ("resid", c_p), ("ldr", c_i64),
+        ("mask", c_p), ("ldmask", c_i64), ("mask_arows", c_i64),
+        ("rowscale", c_p),
+        ("alpha", c_f), ("beta", c_f),
+        ("relu", c_i32), ("atomic", c_i32), ("split_k", c_i32), ("_pad2", c_i32),
+    ]
+
+
+# name -> argtypes (restype is always int except savqa_last_error)
+_SIGS = {
+    "savqa_version": [],
+    "savqa_gemm": [c_p, C.POINTER(GemmDesc)],
+    "savqa_colsum_acc": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
+    "savqa_ln_fwd": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p],
+    "savqa_ln_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p],
+    "savqa_rowflag": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
+    "savqa_gattn_fwd": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
+                        c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p],
+    "savqa_gattn_bwd": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
+                        c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64,
+                        c_p, c_i64],
+    "savqa_graph_build": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p],
+    "savqa_dec_init": [c_p, c_p, c_i64, c_f, c_p, c_i64, c_i64, c_p],
+    "savqa_dec_init_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p],
+    "savqa_period_sum_acc": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p],
+    "savqa_copy_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64],
+    "savqa_mil_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_p],
+    "savqa_mil_bwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_p, c_p, c_p],
+    "savqa_index_put_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
+    "savqa_index_get_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
+    "savqa_loss_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f, c_p, c_i32, c_p, c_p, c_p, c_p],
+    "savqa_scale_by": [c_p, c_p, c_p, c_i64, c_p],
+    "savqa_adam": [c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_f, c_f],
+}
+
+_lib = None
+
+
+class SavqaError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libsavqa.so and bind every declared entry point (raises if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SavqaError(f"libsavqa.so not built ({path}); run __graft_entry__.build() "
+                         "or `make -C structured-alignment-vqa_amd/csrc`")
+    lib = C.CDLL(path)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_int
+    lib.savqa_last_error.argtypes = []
+    lib.savqa_last_error.restype = C.c_char_p
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(_SIGS) + ["savqa_last_error"]
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.savqa_last_error().decode("utf-8", "replace")
+        raise SavqaError(f"{name} failed (rc={rc}): {msg}")
+    return rc

@@ -1,0 +1,29 @@
+// C-ABI plumbing of libsavqa.so: version and thread-local error reporting.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "common.h"
+
+namespace savqa {
+static thread_local std::string g_err;
+
+void set_error(const std::string& msg) { g_err = msg; }
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return (int)e;
+  }
+  return 0;
+}
+}  // namespace savqa
+
+extern "C" int savqa_version(void) { return 1; }
+extern "C" const char* savqa_last_error(void) { return savqa::g_err.c_str(); }

@@ -1,0 +1,225 @@
+// Residual + layer_normalization forward/backward and row flags.
+//
+// Reference: layer_normalization.forward, models/modules.py:62-65 (mean, UNBIASED
+// std, eps=1e-8 added to std) applied to the residual sums of modules.py:304
+// (attention) and :439 (feed-forward). One wave per row; rows are 512 (or 1024)
+// floats, loaded as float4 (2 per lane at d=512). The forward also emits the
+// exact-zero row flag sign(|sum_c y|) that the NEXT attention uses as its key and
+// query mask (modules.py:257, :289), so that mask never re-reads the activations.
+#include "common.h"
+
+namespace savqa {
+
+constexpr int LN_MAXV = 4;  // float4 per lane -> cols <= 1024
+
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x,
+                                                     const float* __restrict__ xscale,
+                                                     const float* __restrict__ r, int64_t rows,
+                                                     int cols, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     float* __restrict__ z_out,
+                                                     float* __restrict__ y,
+                                                     float* __restrict__ mean_out,
+                                                     float* __restrict__ rden_out,
+                                                     float* __restrict__ std_out,
+                                                     float* __restrict__ flag) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nv = cols >> 8;  // float4 per lane (cols % 256 == 0)
+  const float4* xr = reinterpret_cast<const float4*>(x + row * cols);
+  const float4* rr = r ? reinterpret_cast<const float4*>(r + row * cols) : nullptr;
+  float4 v[LN_MAXV];
+  float s = 0.f;
+  const float xs = xscale ? xscale[row] : 1.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    if (i < nv) {
+      float4 a = xr[lane + 64 * i];
+      if (xscale) { a.x *= xs; a.y *= xs; a.z *= xs; a.w *= xs; }
+      if (rr) {
+        float4 b = rr[lane + 64 * i];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      v[i] = a;
+      s += (a.x + a.y) + (a.z + a.w);
+    }
+  }
+  const float mean = wave_sum(s) / (float)cols;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    if (i < nv) {
+      const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, e = v[i].w - mean;
+      ss += (a * a + b * b) + (c * c + e * e);
+    }
+  }
+  const float var = wave_sum(ss) / (float)(cols - 1);
+  const float sd = sqrtf(var);
+  const float den = sd + eps;
+  float fsum = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    if (i < nv) {
+      const int c4 = lane + 64 * i;
+      const float4 g = reinterpret_cast<const float4*>(gamma)[c4];
+      const float4 bt = reinterpret_cast<const float4*>(beta)[c4];
+      float4 o;
+      o.x = g.x * (v[i].x - mean) / den + bt.x;
+      o.y = g.y * (v[i].y - mean) / den + bt.y;
+      o.z = g.z * (v[i].z - mean) / den + bt.z;
+      o.w = g.w * (v[i].w - mean) / den + bt.w;
+      reinterpret_cast<float4*>(y + row * cols)[c4] = o;
+      if (z_out) reinterpret_cast<float4*>(z_out + row * cols)[c4] = v[i];
+      fsum += (o.x + o.y) + (o.z + o.w);
+    }
+  }
+  if (flag) fsum = wave_sum(fsum);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rden_out[row] = 1.f / den;
+    std_out[row] = sd;
+    if (flag) flag[row] = fsum != 0.f ? 1.f : 0.f;
+  }
+}
+
+// Backward. Each wave walks rows with a grid stride, keeping its dgamma/dbeta
+// partial sums in registers; the 4 waves reduce through LDS and add once per
+// column per block.
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy,
+                                                     const float* __restrict__ z,
+                                                     const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rden_in,
+                                                     const float* __restrict__ std_in,
+                                                     const float* __restrict__ gamma,
+                                                     int64_t rows, int cols,
+                                                     const float* __restrict__ dz_add,
+                                                     float* __restrict__ dz,
+                                                     float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta) {
+  __shared__ float4 red[2][4][64 * LN_MAXV];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int nv = cols >> 8;
+  float4 dg[LN_MAXV], db[LN_MAXV], g[LN_MAXV];
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    dg[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    db[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < nv) g[i] = reinterpret_cast<const float4*>(gamma)[lane + 64 * i];
+  }
+  const float invN = 1.f / (float)cols;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += (int64_t)gridDim.x * 4) {
+    const float mean = mean_in[row], rden = rden_in[row], sd = std_in[row];
+    const float4* dyr = reinterpret_cast<const float4*>(dy + row * cols);
+    const float4* zr = reinterpret_cast<const float4*>(z + row * cols);
+    float4 gg[LN_MAXV], xc[LN_MAXV];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      if (i < nv) {
+        const float4 d4 = dyr[lane + 64 * i];
+        const float4 z4 = zr[lane + 64 * i];
+        xc[i] = make_float4(z4.x - mean, z4.y - mean, z4.z - mean, z4.w - mean);
+        gg[i] = make_float4(d4.x * g[i].x, d4.y * g[i].y, d4.z * g[i].z, d4.w * g[i].w);
+        sg += (gg[i].x + gg[i].y) + (gg[i].z + gg[i].w);
+        sgx += (gg[i].x * xc[i].x + gg[i].y * xc[i].y) + (gg[i].z * xc[i].z + gg[i].w * xc[i].w);
+        dg[i].x += d4.x * xc[i].x * rden; dg[i].y += d4.y * xc[i].y * rden;
+        dg[i].z += d4.z * xc[i].z * rden; dg[i].w += d4.w * xc[i].w * rden;
+        db[i].x += d4.x; db[i].y += d4.y; db[i].z += d4.z; db[i].w += d4.w;
+      }
+    }
+    sg = wave_sum(sg);
+    sgx = wave_sum(sgx);
+    const float mg = sg * invN;
+    // d std / dz_k = xc_k / ((N-1) std); guard std == 0 (constant row)
+    const float c = sd > 0.f ? sgx * rden * rden / ((float)(cols - 1) * sd) : 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      if (i < nv) {
+        float4 o;
+        o.x = (gg[i].x - mg) * rden - c * xc[i].x;
+        o.y = (gg[i].y - mg) * rden - c * xc[i].y;
+        o.z = (gg[i].z - mg) * rden - c * xc[i].z;
+        o.w = (gg[i].w - mg) * rden - c * xc[i].w;
+        if (dz_add) {
+          const float4 a = reinterpret_cast<const float4*>(dz_add + row * cols)[lane + 64 * i];
+          o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+        }
+        reinterpret_cast<float4*>(dz + row * cols)[lane + 64 * i] = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    red[0][w][lane + 64 * i] = dg[i];
+    red[1][w][lane + 64 * i] = db[i];
+  }
+  __syncthreads();
+  // 256 threads reduce the cols/4 float4 columns of both accumulators
+  for (int c4 = threadIdx.x; c4 < nv * 64; c4 += 256) {
+    float4 a = red[0][0][c4], b = red[1][0][c4];
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) {
+      const float4 a2 = red[0][ww][c4], b2 = red[1][ww][c4];
+      a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
+      b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
+    }
+    // column index of float4 slot c4: lane + 64*i  ->  floats 4*c4 .. 4*c4+3
+    atomicAdd(&dgamma[4 * c4 + 0], a.x); atomicAdd(&dgamma[4 * c4 + 1], a.y);
+    atomicAdd(&dgamma[4 * c4 + 2], a.z); atomicAdd(&dgamma[4 * c4 + 3], a.w);
+    atomicAdd(&dbeta[4 * c4 + 0], b.x); atomicAdd(&dbeta[4 * c4 + 1], b.y);
+    atomicAdd(&dbeta[4 * c4 + 2], b.z); atomicAdd(&dbeta[4 * c4 + 3], b.w);
+  }
+}
+
+__global__ __launch_bounds__(256) void rowflag_kernel(const float* __restrict__ X, int64_t rows,
+                                                      int64_t cols, int64_t ldx,
+                                                      float* __restrict__ flag) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float s = 0.f;
+  for (int64_t c = lane; c < cols; c += 64) s += X[row * ldx + c];
+  s = wave_sum(s);
+  if (lane == 0) flag[row] = s != 0.f ? 1.f : 0.f;
+}
+
+}  // namespace savqa
+
+using namespace savqa;
+
+extern "C" int savqa_ln_fwd(void* stream, const float* x, const float* xscale, const float* r,
+                            int64_t rows,
+                            int64_t cols, const float* gamma, const float* beta, float eps,
+                            float* z_out, float* y, float* mean, float* rden, float* stdv,
+                            float* flag) {
+  if (rows <= 0) return 0;
+  if (cols % 256 != 0 || cols > 256 * LN_MAXV)
+    return fail(SAVQA_EUNSUP, "savqa_ln_fwd: cols must be a multiple of 256 and <= 1024");
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream), x, xscale,
+                     r, rows, (int)cols, gamma, beta, eps, z_out, y, mean, rden, stdv, flag);
+  return check_launch("savqa_ln_fwd");
+}
+
+extern "C" int savqa_ln_bwd(void* stream, const float* dy, const float* z, const float* mean,
+                            const float* rden, const float* stdv, const float* gamma,
+                            int64_t rows, int64_t cols, const float* dz_add, float* dz,
+                            float* dgamma, float* dbeta) {
+  if (rows <= 0) return 0;
+  if (cols % 256 != 0 || cols > 256 * LN_MAXV)
+    return fail(SAVQA_EUNSUP, "savqa_ln_bwd: cols must be a multiple of 256 and <= 1024");
+  int64_t blocks = (rows + 3) / 4;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), dy, z, mean,
+                     rden, stdv, gamma, rows, (int)cols, dz_add, dz, dgamma, dbeta);
+  return check_launch("savqa_ln_bwd");
+}
+
+extern "C" int savqa_rowflag(void* stream, const float* X, int64_t rows, int64_t cols,
+                             int64_t ldx, float* flag) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(rowflag_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream), X,
+                     rows, cols, ldx, flag);
+  return check_launch("savqa_rowflag");
+}

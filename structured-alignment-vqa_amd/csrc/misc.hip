@@ -1,0 +1,534 @@
+// Bandwidth-bound pieces of the model_v=3 step: graph construction, decoder input,
+// row copies (torch.cat), MIL-NCE core, index_put/get, loss, Adam.
+#include "common.h"
+
+namespace savqa {
+
+// ------------------------------------------------------------------ graph build
+// AttModel_x3.py:103-122 / :229-247. One block per (b, row i), threads over j.
+__global__ __launch_bounds__(256) void graph_build_kernel(
+    const int32_t* __restrict__ nm, const int32_t* __restrict__ qm, const int32_t* __restrict__ qg,
+    const int32_t* __restrict__ ng, int Nn, int Lq, int dec_on, float* __restrict__ gdiag,
+    float* __restrict__ graph, float* __restrict__ dec_mask) {
+  __shared__ float part[4];
+  const int T = Nn + Lq;
+  const int b = blockIdx.x / T, i = blockIdx.x % T;
+  float rs = 0.f;
+  for (int j = threadIdx.x; j < T; j += blockDim.x) {
+    float m = 0.f, gd = 0.f, g = 1.f;  // off-diagonal blocks: 1 - 0
+    if (i < Nn && j < Nn) {
+      m = (float)nm[((int64_t)b * Nn + i) * Nn + j];
+      g = ng ? (float)ng[((int64_t)b * Nn + i) * Nn + j] : 1.f;
+    } else if (i >= Nn && j >= Nn) {
+      const int64_t o = ((int64_t)b * Lq + (i - Nn)) * Lq + (j - Nn);
+      m = (float)qm[o];
+      gd = m;
+      g = (float)qg[o];
+    }
+    const int64_t o = ((int64_t)b * T + i) * T + j;
+    gdiag[o] = gd;
+    graph[o] = g;
+    rs += m;
+  }
+  rs = wave_sum(rs);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = rs;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
+    dec_mask[(int64_t)b * T + i] = (dec_on && t != 0.f) ? 1.f : 0.f;
+  }
+}
+
+// ------------------------------------------------------------------ decoder input
+__global__ void dec_init_kernel(const float* __restrict__ emb, int64_t idx, float scale,
+                                const float* __restrict__ pos, int64_t B, int64_t d,
+                                float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * d) return;
+  const int64_t c = t % d;
+  out[t] = emb[idx * d + c] * scale + pos[c];
+}
+
+// d emb[idx] += scale * sum_b g[b], d pos[0] += sum_b g[b]
+__global__ void dec_init_bwd_kernel(const float* __restrict__ g, int64_t B, int64_t d,
+                                    int64_t idx, float scale, float* __restrict__ demb,
+                                    float* __restrict__ dpos) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d) return;
+  float s = 0.f, ss = 0.f;
+  for (int64_t b = 0; b < B; ++b) {
+    const float v = g[b * d + c];
+    s += v * scale;
+    ss += v;
+  }
+  if (demb) demb[idx * d + c] += s;
+  if (dpos) dpos[c] += ss;
+}
+
+// out[t][c] += sum_b X[(b*T + t)*ldx + c]  (gradient of a learned position table)
+__global__ void period_sum_kernel(const float* __restrict__ X, int64_t B, int64_t T, int64_t C,
+                                  int64_t ldx, float* __restrict__ out) {
+  const int64_t t = blockIdx.y;
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < B; ++b) s += X[(b * T + t) * ldx + c];
+  out[t * C + c] += s;
+}
+
+// ------------------------------------------------------------------ row copy (cat)
+__global__ void copy_rows_kernel(const float* __restrict__ src, int64_t rows, int64_t cols,
+                                 int64_t lds, float* __restrict__ dst, int64_t ldd, int64_t group,
+                                 int64_t stride, int64_t offset) {
+  const int64_t r = blockIdx.x;
+  const int64_t dr = (r / group) * stride + (r % group) + offset;
+  const float* s = src + r * lds;
+  float* d = dst + dr * ldd;
+  if ((cols & 3) == 0 && (((uintptr_t)s | (uintptr_t)d) & 15) == 0) {
+    for (int64_t c = threadIdx.x; c < cols / 4; c += blockDim.x)
+      reinterpret_cast<float4*>(d)[c] = reinterpret_cast<const float4*>(s)[c];
+  } else {
+    for (int64_t c = threadIdx.x; c < cols; c += blockDim.x) d[c] = s[c];
+  }
+}
+
+// ------------------------------------------------------------------ MIL-NCE
+// one wave per (b, n) row; lanes over H (float4), K (= topN) <= 16 candidates.
+constexpr int MIL_KMAX = 16;
+
+__global__ __launch_bounds__(256) void mil_fwd_kernel(const float* __restrict__ Pf,
+                                                      const float* __restrict__ Nf,
+                                                      const float* __restrict__ v,
+                                                      const int32_t* __restrict__ mask,
+                                                      int64_t BN, int K, int H, float eps,
+                                                      float* __restrict__ obj,
+                                                      float* __restrict__ term) {
+  const int lane = threadIdx.x & 63;
+  const int64_t bn = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (bn >= BN) return;
+  const int h4 = H / 4;
+  const float4* vr = reinterpret_cast<const float4*>(v + bn * H);
+  float sp[MIL_KMAX], sn[MIL_KMAX];
+  for (int k = 0; k < K; ++k) {
+    const float4* pr = reinterpret_cast<const float4*>(Pf + (bn * K + k) * H);
+    const float4* nr = reinterpret_cast<const float4*>(Nf + (bn * K + k) * H);
+    float a = 0.f, c = 0.f;
+    for (int i = lane; i < h4; i += 64) {
+      const float4 vv = vr[i], pp = pr[i], qq = nr[i];
+      a += (pp.x * vv.x + pp.y * vv.y) + (pp.z * vv.z + pp.w * vv.w);
+      c += (qq.x * vv.x + qq.y * vv.y) + (qq.z * vv.z + qq.w * vv.w);
+    }
+    sp[k] = wave_sum(a);
+    sn[k] = wave_sum(c);
+  }
+  // softmax over k of the raw positive scores (AttModel_x3.py:372-373)
+  float mx = -INFINITY;
+  for (int k = 0; k < K; ++k) mx = fmaxf(mx, sp[k]);
+  float den = 0.f;
+  for (int k = 0; k < K; ++k) { sp[k] = expf(sp[k] - mx); den += sp[k]; }
+  for (int k = 0; k < K; ++k) sp[k] = sp[k] / den;
+  for (int i = lane; i < h4; i += 64) {
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < K; ++k) {
+      const float4 pp = reinterpret_cast<const float4*>(Pf + (bn * K + k) * H)[i];
+      o.x = fmaf(sp[k], pp.x, o.x); o.y = fmaf(sp[k], pp.y, o.y);
+      o.z = fmaf(sp[k], pp.z, o.z); o.w = fmaf(sp[k], pp.w, o.w);
+    }
+    reinterpret_cast<float4*>(obj + bn * H)[i] = o;
+  }
+  if (lane == 0) {
+    // LSE_k(clamp(mask*s-, eps)) (AttModel_x3.py:367)
+    float m2 = -INFINITY;
+    for (int k = 0; k < K; ++k) {
+      sn[k] = fmaxf((float)mask[bn * K + k] * sn[k], eps);
+      m2 = fmaxf(m2, sn[k]);
+    }
+    float s2 = 0.f;
+    for (int k = 0; k < K; ++k) s2 += expf(sn[k] - m2);
+    const float lse_neg = m2 + logf(s2);
+    const float lse_eps = eps + logf((float)K);
+    term[bn] = lse_eps - lse_neg;
+  }
+}
+
+__global__ void mean_reduce_kernel(const float* __restrict__ x, int64_t n, float scale,
+                                   float* __restrict__ out) {
+  __shared__ float part[16];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += x[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
+    *out = t * scale;
+  }
+}
+
+__global__ __launch_bounds__(256) void mil_bwd_kernel(
+    const float* __restrict__ Pf, const float* __restrict__ Nf, const float* __restrict__ v,
+    const int32_t* __restrict__ mask, int64_t BN, int K, int H, float eps,
+    const float* __restrict__ dobj, const float* __restrict__ dmil, float* __restrict__ dPf,
+    float* __restrict__ dNf, float* __restrict__ dv) {
+  const int lane = threadIdx.x & 63;
+  const int64_t bn = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (bn >= BN) return;
+  const int h4 = H / 4;
+  const float4* vr = reinterpret_cast<const float4*>(v + bn * H);
+  const float4* dor = dobj ? reinterpret_cast<const float4*>(dobj + bn * H) : nullptr;
+  float sp[MIL_KMAX], sn[MIL_KMAX], dw[MIL_KMAX];
+  for (int k = 0; k < K; ++k) {
+    const float4* pr = reinterpret_cast<const float4*>(Pf + (bn * K + k) * H);
+    const float4* nr = reinterpret_cast<const float4*>(Nf + (bn * K + k) * H);
+    float a = 0.f, c = 0.f, e = 0.f;
+    for (int i = lane; i < h4; i += 64) {
+      const float4 vv = vr[i], pp = pr[i], qq = nr[i];
+      a += (pp.x * vv.x + pp.y * vv.y) + (pp.z * vv.z + pp.w * vv.w);
+      c += (qq.x * vv.x + qq.y * vv.y) + (qq.z * vv.z + qq.w * vv.w);
+      if (dor) {
+        const float4 g = dor[i];
+        e += (g.x * pp.x + g.y * pp.y) + (g.z * pp.z + g.w * pp.w);
+      }
+    }
+    sp[k] = wave_sum(a);
+    sn[k] = wave_sum(c);
+    dw[k] = wave_sum(e);
+  }
+  // softmax weights w and their backward dsp = w*(dw - sum w dw)
+  float mx = -INFINITY;
+  for (int k = 0; k < K; ++k) mx = fmaxf(mx, sp[k]);
+  float den = 0.f;
+  for (int k = 0; k < K; ++k) { sp[k] = expf(sp[k] - mx); den += sp[k]; }
+  float wdw = 0.f;
+  for (int k = 0; k < K; ++k) { sp[k] = sp[k] / den; wdw += sp[k] * dw[k]; }
+  float dsp[MIL_KMAX], dsn[MIL_KMAX];
+  for (int k = 0; k < K; ++k) dsp[k] = sp[k] * (dw[k] - wdw);
+  // term = LSE(eps) - LSE(snc): d snc_k = -dterm * softmax_k(snc); clamp passes where >= eps
+  const float dterm = (*dmil) / (2.f * (float)BN);
+  {
+    float m2 = -INFINITY;
+    float snc[MIL_KMAX];
+    for (int k = 0; k < K; ++k) {
+      const float mk = (float)mask[bn * K + k];
+      snc[k] = fmaxf(mk * sn[k], eps);
+      m2 = fmaxf(m2, snc[k]);
+    }
+    float s2 = 0.f;
+    for (int k = 0; k < K; ++k) { dsn[k] = expf(snc[k] - m2); s2 += dsn[k]; }
+    for (int k = 0; k < K; ++k) {
+      const float mk = (float)mask[bn * K + k];
+      const float d_snc = -dterm * (dsn[k] / s2);
+      dsn[k] = (mk * sn[k] >= eps) ? d_snc * mk : 0.f;
+    }
+  }
+  for (int i = lane; i < h4; i += 64) {
+    const float4 vv = vr[i];
+    float4 g = dor ? dor[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < K; ++k) {
+      const int64_t off = (bn * K + k) * H;
+      const float4 pp = reinterpret_cast<const float4*>(Pf + off)[i];
+      const float4 qq = reinterpret_cast<const float4*>(Nf + off)[i];
+      float4 dp, dn;
+      dp.x = pp.x > 0.f ? sp[k] * g.x + dsp[k] * vv.x : 0.f;
+      dp.y = pp.y > 0.f ? sp[k] * g.y + dsp[k] * vv.y : 0.f;
+      dp.z = pp.z > 0.f ? sp[k] * g.z + dsp[k] * vv.z : 0.f;
+      dp.w = pp.w > 0.f ? sp[k] * g.w + dsp[k] * vv.w : 0.f;
+      dn.x = qq.x > 0.f ? dsn[k] * vv.x : 0.f;
+      dn.y = qq.y > 0.f ? dsn[k] * vv.y : 0.f;
+      dn.z = qq.z > 0.f ? dsn[k] * vv.z : 0.f;
+      dn.w = qq.w > 0.f ? dsn[k] * vv.w : 0.f;
+      reinterpret_cast<float4*>(dPf + off)[i] = dp;
+      reinterpret_cast<float4*>(dNf + off)[i] = dn;
+      acc.x += dsp[k] * pp.x + dsn[k] * qq.x;
+      acc.y += dsp[k] * pp.y + dsn[k] * qq.y;
+      acc.z += dsp[k] * pp.z + dsn[k] * qq.z;
+      acc.w += dsp[k] * pp.w + dsn[k] * qq.w;
+    }
+    float4 o;
+    o.x = vv.x > 0.f ? acc.x : 0.f; o.y = vv.y > 0.f ? acc.y : 0.f;
+    o.z = vv.z > 0.f ? acc.z : 0.f; o.w = vv.w > 0.f ? acc.w : 0.f;
+    reinterpret_cast<float4*>(dv + bn * H)[i] = o;
+  }
+}
+
+// macro[b*Ns + loc[b,n]] = obj[b*Nv + n], n ascending (last write wins, as the
+// reference's index_put on CPU); one block per sample keeps that order.
+__global__ void index_put_rows_kernel(const int64_t* __restrict__ loc, int64_t Nv, int64_t Ns,
+                                      int64_t H, const float* __restrict__ obj,
+                                      float* __restrict__ macro) {
+  const int64_t b = blockIdx.x;
+  for (int64_t n = 0; n < Nv; ++n) {
+    const int64_t l = loc[b * Nv + n];
+    if (l < 0) continue;
+    for (int64_t c = threadIdx.x; c < H; c += blockDim.x)
+      macro[(b * Ns + l) * H + c] = obj[(b * Nv + n) * H + c];
+    __syncthreads();
+  }
+}
+
+__global__ void index_get_rows_kernel(const int64_t* __restrict__ loc, int64_t Nv, int64_t Ns,
+                                      int64_t H, const float* __restrict__ dmacro,
+                                      float* __restrict__ dobj) {
+  const int64_t bn = blockIdx.x;
+  const int64_t b = bn / Nv;
+  const int64_t l = loc[bn];
+  for (int64_t c = threadIdx.x; c < H; c += blockDim.x)
+    dobj[bn * H + c] = l >= 0 ? dmacro[(b * Ns + l) * H + c] : 0.f;
+}
+
+// ------------------------------------------------------------------ loss
+// one block per sample; three heads of C logits each.
+__global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ lc,
+                                                   const float* __restrict__ lv,
+                                                   const float* __restrict__ ls,
+                                                   const int64_t* __restrict__ answer, int64_t B,
+                                                   int C, float eps, float* __restrict__ dlogits,
+                                                   float* __restrict__ lsm_out,
+                                                   float* __restrict__ row_loss) {
+  __shared__ float red[4];
+  __shared__ float stat[6];
+  const int64_t b = blockIdx.x;
+  const float* heads[3] = {lc + b * C, lv + b * C, ls + b * C};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  auto block_reduce = [&](float v, bool is_max) -> float {
+    v = is_max ? wave_max(v) : wave_sum(v);
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int i = 1; i < 4; ++i) r = is_max ? fmaxf(r, red[i]) : r + red[i];
+    return r;
+  };
+  for (int hd = 0; hd < 3; ++hd) {
+    float mx = -INFINITY;
+    for (int c = threadIdx.x; c < C; c += 256) mx = fmaxf(mx, heads[hd][c]);
+    mx = block_reduce(mx, true);
+    float s = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) s += expf(heads[hd][c] - mx);
+    s = block_reduce(s, false);
+    if (threadIdx.x == 0) { stat[2 * hd] = mx; stat[2 * hd + 1] = logf(s); }
+  }
+  __syncthreads();
+  const int64_t ans = answer[b];
+  const float off = eps / (float)C;
+  float ysum = 0.f, part = 0.f;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float y = (c == ans ? (1.f - eps) : 0.f) + off;
+    // reference order: (vis + syb + concat) / 3
+    const float lsv = heads[1][c] - stat[2] - stat[3];
+    const float lss = heads[2][c] - stat[4] - stat[5];
+    const float lsc = heads[0][c] - stat[0] - stat[1];
+    const float l = (lsv + lss + lsc) / 3.f;
+    if (lsm_out) lsm_out[b * C + c] = l;
+    part += y * l;
+    ysum += y;
+  }
+  part = block_reduce(part, false);
+  ysum = block_reduce(ysum, false);
+  const float k = -1.f / (3.f * (float)B);
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float y = (c == ans ? (1.f - eps) : 0.f) + off;
+    for (int hd = 0; hd < 3; ++hd) {
+      const float p = expf(heads[hd][c] - stat[2 * hd] - stat[2 * hd + 1]);
+      dlogits[((int64_t)hd * B + b) * C + c] = k * (y - p * ysum);
+    }
+  }
+  if (threadIdx.x == 0) row_loss[b] = -part;
+}
+
+__global__ void loss_final_kernel(const float* __restrict__ row_loss, int64_t B,
+                                  const float* __restrict__ mil, int with_mil,
+                                  float* __restrict__ loss) {
+  __shared__ float part[4];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < B; i += blockDim.x) s += row_loss[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = part[0] + part[1] + part[2] + part[3];
+    t = t / (float)B;
+    if (with_mil) t = t + (-(*mil));
+    *loss = t;
+  }
+}
+
+__global__ void scale_by_kernel(const float* __restrict__ in, const float* __restrict__ scale,
+                                int64_t n, float* __restrict__ out) {
+  const float s = *scale;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = in[i] * s;
+}
+
+// ------------------------------------------------------------------ Adam
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   int64_t n, float lr, float b1, float b2,
+                                                   float eps, float step_size, float sbc2,
+                                                   float gs) {
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+#define ADAM1(X)                                                      \
+  {                                                                   \
+    const float gx = gg.X * gs;                                       \
+    mm.X = mm.X + (1.f - b1) * (gx - mm.X);                           \
+    vv.X = b2 * vv.X + (1.f - b2) * gx * gx;                          \
+    const float den = sqrtf(vv.X) / sbc2 + eps;                       \
+    pp.X = pp.X - step_size * (mm.X / den);                           \
+  }
+    ADAM1(x) ADAM1(y) ADAM1(z) ADAM1(w)
+#undef ADAM1
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+  // scalar tail
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gx = g[i] * gs;
+    m[i] = m[i] + (1.f - b1) * (gx - m[i]);
+    v[i] = b2 * v[i] + (1.f - b2) * gx * gx;
+    const float den = sqrtf(v[i]) / sbc2 + eps;
+    p[i] = p[i] - step_size * (m[i] / den);
+  }
+}
+
+}  // namespace savqa
+
+using namespace savqa;
+
+extern "C" int savqa_graph_build(void* stream, const int32_t* node_mask, const int32_t* q_mask,
+                                 const int32_t* q_graph, const int32_t* node_graph, int64_t B,
+                                 int64_t Nn, int64_t Lq, int32_t dec_mask_on, float* graph_diag,
+                                 float* graph, float* dec_mask) {
+  if (B <= 0) return 0;
+  if (Nn < 0 || Lq <= 0) return fail(SAVQA_EINVAL, "savqa_graph_build: bad sizes");
+  const int64_t T = Nn + Lq;
+  hipLaunchKernelGGL(graph_build_kernel, dim3(B * T), dim3(T <= 64 ? 64 : (T <= 128 ? 128 : 256)),
+                     0, as_stream(stream), node_mask, q_mask, q_graph, node_graph, (int)Nn,
+                     (int)Lq, dec_mask_on, graph_diag, graph, dec_mask);
+  return check_launch("savqa_graph_build");
+}
+
+extern "C" int savqa_dec_init(void* stream, const float* emb, int64_t idx, float scale,
+                              const float* pos, int64_t B, int64_t d, float* out) {
+  const int64_t n = B * d;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(dec_init_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), emb,
+                     idx, scale, pos, B, d, out);
+  return check_launch("savqa_dec_init");
+}
+
+extern "C" int savqa_dec_init_bwd(void* stream, const float* g, int64_t B, int64_t d, int64_t idx,
+                                  float scale, float* demb, float* dpos) {
+  if (B <= 0 || d <= 0) return 0;
+  hipLaunchKernelGGL(dec_init_bwd_kernel, dim3((d + 255) / 256), dim3(256), 0, as_stream(stream), g,
+                     B, d, idx, scale, demb, dpos);
+  return check_launch("savqa_dec_init_bwd");
+}
+
+extern "C" int savqa_period_sum_acc(void* stream, const float* X, int64_t B, int64_t T, int64_t C,
+                                    int64_t ldx, float* out) {
+  if (B <= 0 || T <= 0 || C <= 0) return 0;
+  hipLaunchKernelGGL(period_sum_kernel, dim3((C + 255) / 256, T), dim3(256), 0, as_stream(stream),
+                     X, B, T, C, ldx, out);
+  return check_launch("savqa_period_sum_acc");
+}
+
+extern "C" int savqa_copy_rows(void* stream, const float* src, int64_t rows, int64_t cols,
+                               int64_t lds, float* dst, int64_t ldd, int64_t group, int64_t stride,
+                               int64_t offset) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (group <= 0) { group = rows; stride = rows; }
+  hipLaunchKernelGGL(copy_rows_kernel, dim3(rows), dim3(256), 0, as_stream(stream), src, rows, cols,
+                     lds, dst, ldd, group, stride, offset);
+  return check_launch("savqa_copy_rows");
+}
+
+extern "C" int savqa_mil_fwd(void* stream, const float* Pf, const float* Nf, const float* v,
+                             const int32_t* mask, int64_t BN, int64_t K, int64_t H, float eps,
+                             float* obj, float* ws, float* mil_out) {
+  if (BN <= 0) return 0;
+  if (K <= 0 || K > MIL_KMAX || H % 4 != 0)
+    return fail(SAVQA_EUNSUP, "savqa_mil_fwd: need 1 <= topN <= 16 and H % 4 == 0");
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(mil_fwd_kernel, dim3((BN + 3) / 4), dim3(256), 0, s, Pf, Nf, v, mask, BN,
+                     (int)K, (int)H, eps, obj, ws);
+  hipLaunchKernelGGL(mean_reduce_kernel, dim3(1), dim3(1024), 0, s, ws, BN, 1.f / (2.f * (float)BN),
+                     mil_out);
+  return check_launch("savqa_mil_fwd");
+}
+
+extern "C" int savqa_mil_bwd(void* stream, const float* Pf, const float* Nf, const float* v,
+                             const int32_t* mask, int64_t BN, int64_t K, int64_t H, float eps,
+                             const float* dobj, const float* dmil, float* dPf, float* dNf,
+                             float* dv) {
+  if (BN <= 0) return 0;
+  if (K <= 0 || K > MIL_KMAX || H % 4 != 0)
+    return fail(SAVQA_EUNSUP, "savqa_mil_bwd: need 1 <= topN <= 16 and H % 4 == 0");
+  hipLaunchKernelGGL(mil_bwd_kernel, dim3((BN + 3) / 4), dim3(256), 0, as_stream(stream), Pf, Nf, v,
+                     mask, BN, (int)K, (int)H, eps, dobj, dmil, dPf, dNf, dv);
+  return check_launch("savqa_mil_bwd");
+}
+
+extern "C" int savqa_index_put_rows(void* stream, const int64_t* loc, int64_t B, int64_t Nv,
+                                    int64_t Ns, int64_t H, const float* obj, float* macro) {
+  if (B <= 0 || Nv <= 0) return 0;
+  hipLaunchKernelGGL(index_put_rows_kernel, dim3(B), dim3(256), 0, as_stream(stream), loc, Nv, Ns, H,
+                     obj, macro);
+  return check_launch("savqa_index_put_rows");
+}
+
+extern "C" int savqa_index_get_rows(void* stream, const int64_t* loc, int64_t B, int64_t Nv,
+                                    int64_t Ns, int64_t H, const float* dmacro, float* dobj) {
+  if (B <= 0 || Nv <= 0) return 0;
+  hipLaunchKernelGGL(index_get_rows_kernel, dim3(B * Nv), dim3(256), 0, as_stream(stream), loc, Nv,
+                     Ns, H, dmacro, dobj);
+  return check_launch("savqa_index_get_rows");
+}
+
+extern "C" int savqa_loss_fwd(void* stream, const float* lc, const float* lv, const float* ls,
+                              const int64_t* answer, int64_t B, int64_t C, float eps,
+                              const float* mil, int32_t with_mil, float* loss, float* dlogits,
+                              float* lsm, float* ws) {
+  if (B <= 0) return fail(SAVQA_EINVAL, "savqa_loss_fwd: empty batch");
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(loss_kernel, dim3(B), dim3(256), 0, s, lc, lv, ls, answer, B, (int)C, eps,
+                     dlogits, lsm, ws);
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, s, ws, B, mil, with_mil, loss);
+  return check_launch("savqa_loss_fwd");
+}
+
+extern "C" int savqa_scale_by(void* stream, const float* in, const float* scale, int64_t n,
+                              float* out) {
+  if (n <= 0) return 0;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(scale_by_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), in, scale, n,
+                     out);
+  return check_launch("savqa_scale_by");
+}
+
+extern "C" int savqa_adam(void* stream, float* p, const float* g, float* m, float* v, int64_t n,
+                          float lr, float beta1, float beta2, float eps, float bc1, float bc2,
+                          float grad_scale) {
+  if (n <= 0) return 0;
+  if ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) != 0)
+    return fail(SAVQA_EINVAL, "savqa_adam: buffers must be 16-B aligned");
+  const float step_size = lr / bc1;
+  const float sbc2 = sqrtf(bc2);
+  int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr,
+                     beta1, beta2, eps, step_size, sbc2, grad_scale);
+  return check_launch("savqa_adam");
+}

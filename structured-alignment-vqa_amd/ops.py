@@ -1,0 +1,197 @@
+"""Thin Python wrappers over the libsavqa C ABI (include/savqa.h).
+
+Every function takes torch tensors that already live on the current HIP device and
+enqueues work on torch's current stream. Nothing here computes with torch ops:
+torch provides device memory and the stream only. There is no CPU fallback -- a
+missing library or a CPU tensor raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import GemmDesc, call
+
+Tensor = torch.Tensor
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: Optional[Tensor]):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise _lib.SavqaError("savqa ops need device tensors (got a CPU tensor)")
+    return t.data_ptr()
+
+
+def _f32(t: Optional[Tensor], name: str):
+    if t is not None and t.dtype != torch.float32:
+        raise _lib.SavqaError(f"{name}: expected float32, got {t.dtype}")
+
+
+# ------------------------------------------------------------------------------ GEMM
+def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
+         ldc: int, a_trans=False, b_trans=False, a_rows=None, b_rows=None, c_rows=None,
+         c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None, ldrv=0, rowvec_period=0,
+         resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False, rowscale=None, relu=False,
+         alpha=1.0, beta=0.0, atomic=False, split_k=1):
+    """Generic fp32 MFMA GEMM with fused epilogue (see savqa_gemm in include/savqa.h)."""
+    d = GemmDesc()
+    d.M, d.N, d.K = int(M), int(N), int(K)
+    d.A, d.lda, d.a_trans = _p(A), int(lda), int(bool(a_trans))
+    d.a_rows = _p(a_rows)
+    d.B, d.ldb, d.b_trans = _p(B), int(ldb), int(bool(b_trans))
+    d.b_rows = _p(b_rows)
+    d.C, d.ldc = _p(Cm), int(ldc)
+    d.c_group, d.c_stride, d.c_offset = int(c_group), int(c_stride), int(c_offset)
+    d.c_rows = _p(c_rows)
+    d.bias = _p(bias)
+    d.rowvec, d.ldrv, d.rowvec_period = _p(rowvec), int(ldrv), int(rowvec_period)
+    d.resid, d.ldr = _p(resid), int(ldr)
+    d.mask, d.ldmask, d.mask_arows = _p(mask), int(ldmask), int(bool(mask_arows))
+    d.rowscale = _p(rowscale)
+    d.alpha, d.beta = float(alpha), float(beta)
+    d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
+    call("savqa_gemm", _stream(), C.byref(d))
+
+
+def linear(X: Tensor, W: Tensor, b: Optional[Tensor], out: Tensor, *, relu=False,
+           rows: Optional[int] = None, a_rows=None, rowvec=None, rowvec_period=0, resid=None,
+           c_group=0, c_stride=0, c_offset=0, ldx=None, ldo=None, rowscale=None):
+    """out = act(X W^T + b [+ rowvec]) [+ resid]  -- nn.Linear forward (W is [out, in])."""
+    N, K = W.shape
+    M = rows if rows is not None else (a_rows.numel() if a_rows is not None else X.numel() // K)
+    gemm(X, W, out, M, N, K, lda=ldx if ldx is not None else K, ldb=K,
+         ldc=ldo if ldo is not None else N, b_trans=True, a_rows=a_rows, bias=b, rowvec=rowvec,
+         ldrv=N, rowvec_period=rowvec_period, resid=resid, ldr=N, relu=relu, c_group=c_group,
+         c_stride=c_stride, c_offset=c_offset, rowscale=rowscale)
+
+
+def linear_dx(dY: Tensor, W: Tensor, dX: Tensor, *, rows: int, a_rows=None, mask=None,
+              ldmask=0, mask_arows=False, resid=None, c_rows=None, atomic=False, beta=0.0,
+              lddy=None, lddx=None):
+    """dX = dY W  (mask: ReLU-backward gate of the producer of X; c_rows: scatter-add)."""
+    N, K = W.shape  # dY has N cols, dX has K cols
+    gemm(dY, W, dX, rows, K, N, lda=lddy if lddy is not None else N, ldb=K,
+         ldc=lddx if lddx is not None else K, a_rows=a_rows, mask=mask, ldmask=ldmask,
+         mask_arows=mask_arows, resid=resid, ldr=K, c_rows=c_rows, atomic=atomic, beta=beta)
+
+
+def _split_for(m_out: int, n_out: int, k: int) -> int:
+    tiles = ((m_out + 127) // 128) * ((n_out + 127) // 128)
+    if tiles >= 192:
+        want = max(1, 512 // tiles)
+    else:
+        tiles64 = ((m_out + 63) // 64) * ((n_out + 63) // 64)
+        want = max(1, 512 // max(tiles64, 1))
+    return int(max(1, min(want, k // 256)))
+
+
+def linear_dw(dY: Tensor, X: Tensor, dW: Tensor, db: Optional[Tensor], *, rows: int,
+              x_rows=None, lddy=None, ldx=None):
+    """dW += dY^T X ; db += colsum(dY)   (accumulating into the grad arena)."""
+    N, K = dW.shape
+    split = _split_for(N, K, rows)
+    gemm(dY, X, dW, N, K, rows, lda=lddy if lddy is not None else N,
+         ldb=ldx if ldx is not None else K, ldc=K, a_trans=True, b_rows=x_rows, atomic=True,
+         split_k=split)
+    if db is not None:
+        colsum_acc(dY, rows, N, lddy if lddy is not None else N, db)
+
+
+def colsum_acc(X: Tensor, rows: int, cols: int, ldx: int, out: Tensor):
+    call("savqa_colsum_acc", _stream(), _p(X), int(rows), int(cols), int(ldx), _p(out))
+
+
+# ------------------------------------------------------------------------------ LN
+def ln_fwd(x: Tensor, gamma: Tensor, beta: Tensor, y: Tensor, mean: Tensor, rden: Tensor,
+           std: Tensor, *, r=None, z_out=None, flag=None, xscale=None, eps=1e-8):
+    cols = gamma.numel()
+    rows = x.numel() // cols
+    call("savqa_ln_fwd", _stream(), _p(x), _p(xscale), _p(r), rows, cols, _p(gamma), _p(beta),
+         float(eps), _p(z_out), _p(y), _p(mean), _p(rden), _p(std), _p(flag))
+
+
+def ln_bwd(dy: Tensor, z: Tensor, mean: Tensor, rden: Tensor, std: Tensor, gamma: Tensor,
+           dz: Tensor, dgamma: Tensor, dbeta: Tensor, *, dz_add=None):
+    cols = gamma.numel()
+    rows = z.numel() // cols
+    call("savqa_ln_bwd", _stream(), _p(dy), _p(z), _p(mean), _p(rden), _p(std), _p(gamma), rows,
+         cols, _p(dz_add), _p(dz), _p(dgamma), _p(dbeta))
+
+
+def rowflag(X: Tensor, rows: int, cols: int, ldx: int, flag: Tensor):
+    call("savqa_rowflag", _stream(), _p(X), int(rows), int(cols), int(ldx), _p(flag))
+
+
+# ------------------------------------------------------------------------------ attention
+def gattn_fwd(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, o, ldo, att=None, dk=64):
+    call("savqa_gattn_fwd", _stream(), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G), _p(kflag),
+         _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(att))
+
+
+def gattn_bwd(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout, lddo, dq, lddq, dk_,
+              lddk, dv, lddv, dk=64):
+    call("savqa_gattn_bwd", _stream(), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G), _p(kflag),
+         _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo, _p(dq), lddq, _p(dk_), lddk, _p(dv), lddv)
+
+
+# ------------------------------------------------------------------------------ misc
+def graph_build(node_mask, q_mask, q_graph, node_graph, B, Nn, Lq, dec_on, gdiag, graph, dec_mask):
+    call("savqa_graph_build", _stream(), _p(node_mask), _p(q_mask), _p(q_graph), _p(node_graph),
+         B, Nn, Lq, int(bool(dec_on)), _p(gdiag), _p(graph), _p(dec_mask))
+
+
+def dec_init(emb, idx, scale, pos, B, d, out):
+    call("savqa_dec_init", _stream(), _p(emb), int(idx), float(scale), _p(pos), B, d, _p(out))
+
+
+def dec_init_bwd(g, B, d, idx, scale, demb, dpos):
+    call("savqa_dec_init_bwd", _stream(), _p(g), B, d, int(idx), float(scale), _p(demb), _p(dpos))
+
+
+def period_sum_acc(X, B, T, Cc, ldx, out):
+    call("savqa_period_sum_acc", _stream(), _p(X), B, T, Cc, ldx, _p(out))
+
+
+def copy_rows(src, rows, cols, lds, dst, ldd, group=0, stride=0, offset=0):
+    call("savqa_copy_rows", _stream(), _p(src), rows, cols, lds, _p(dst), ldd, group, stride,
+         offset)
+
+
+def mil_fwd(Pf, Nf, v, mask, BN, K, H, eps, obj, ws, mil_out):
+    call("savqa_mil_fwd", _stream(), _p(Pf), _p(Nf), _p(v), _p(mask), BN, K, H, float(eps),
+         _p(obj), _p(ws), _p(mil_out))
+
+
+def mil_bwd(Pf, Nf, v, mask, BN, K, H, eps, dobj, dmil, dPf, dNf, dv):
+    call("savqa_mil_bwd", _stream(), _p(Pf), _p(Nf), _p(v), _p(mask), BN, K, H, float(eps),
+         _p(dobj), _p(dmil), _p(dPf), _p(dNf), _p(dv))
+
+
+def index_put_rows(loc, B, Nv, Ns, H, obj, macro):
+    call("savqa_index_put_rows", _stream(), _p(loc), B, Nv, Ns, H, _p(obj), _p(macro))
+
+
+def index_get_rows(loc, B, Nv, Ns, H, dmacro, dobj):
+    call("savqa_index_get_rows", _stream(), _p(loc), B, Nv, Ns, H, _p(dmacro), _p(dobj))
+
+
+def loss_fwd(lc, lv, ls, answer, B, Cc, eps, mil, with_mil, loss, dlogits, lsm, ws):
+    call("savqa_loss_fwd", _stream(), _p(lc), _p(lv), _p(ls), _p(answer), B, Cc, float(eps),
+         _p(mil), int(bool(with_mil)), _p(loss), _p(dlogits), _p(lsm), _p(ws))
+
+
+def scale_by(inp, scale, n, out):
+    call("savqa_scale_by", _stream(), _p(inp), _p(scale), int(n), _p(out))
+
+
+def adam(p, g, m, v, n, lr, beta1, beta2, eps, bc1, bc2, grad_scale=1.0):
+    call("savqa_adam", _stream(), _p(p), _p(g), _p(m), _p(v), int(n), float(lr), float(beta1),
+         float(beta2), float(eps), float(bc1), float(bc2), float(grad_scale))

@@ -1,0 +1,293 @@
+"""Kernel-level parity of libsavqa (HIP, gfx950) against plain PyTorch fp32 references
+and the CPU oracle. Each test calls through the C ABI (savqa_amd.ops -> libsavqa.so)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _setup():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    torch.backends.cuda.matmul.allow_tf32 = False
+    import savqa_amd._lib as L
+    L.load()
+
+
+def ops():
+    from savqa_amd import ops as O
+    return O
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def g(*shape, seed=0, relu=False):
+    t = torch.randn(*shape, generator=torch.Generator().manual_seed(seed))
+    if relu:
+        t = t.clamp_min(0)
+    return t.to(dev)
+
+
+@pytest.mark.parametrize("M,N,K", [(77, 130, 300), (256, 512, 512), (1000, 1536, 512), (300, 2048, 64)])
+def test_gemm_nt_epilogues(M, N, K):
+    O = ops()
+    X, W, b = g(M, K, seed=1), g(N, K, seed=2), g(N, seed=3)
+    pos = g(7, N, seed=4)
+    res = g(M, N, seed=5)
+    out = torch.empty(M, N, device=dev)
+    O.linear(X, W, b, out, relu=True, rowvec=pos, rowvec_period=7, resid=res)
+    ref = torch.relu(X @ W.t() + b + pos[torch.arange(M, device=dev) % 7]) + res
+    assert rel(out, ref) < 2e-6
+
+
+def test_gemm_gather_scatter_and_maps():
+    O = ops()
+    table = g(1000, 300, seed=6)
+    idx = torch.randint(0, 1000, (90,), generator=torch.Generator().manual_seed(7)).to(dev)
+    W, b = g(64, 300, seed=8), g(64, seed=9)
+    # gathered rows written into a (B=10, T=13) "cat" layout at rows [4, 13)
+    out = torch.zeros(10 * 13, 64, device=dev)
+    O.linear(table, W, b, out, relu=True, a_rows=idx, c_group=9, c_stride=13, c_offset=4)
+    ref = torch.relu(table[idx] @ W.t() + b)
+    got = out.view(10, 13, 64)[:, 4:].reshape(90, 64)
+    assert rel(got, ref) < 2e-6
+    assert float(out.view(10, 13, 64)[:, :4].abs().max()) == 0.0
+    # scatter-add back (embedding grad): dtable[idx] += dY W
+    dY = g(90, 64, seed=10)
+    dtab = torch.zeros_like(table)
+    O.linear_dx(dY, W, dtab, rows=90, c_rows=idx, atomic=True)
+    ref = torch.zeros_like(table).index_add_(0, idx, dY @ W)
+    assert rel(dtab, ref) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(77, 130, 300), (4000, 512, 1536)])
+def test_gemm_dx_dw(M, N, K):
+    O = ops()
+    dY, W, X = g(M, N, seed=11), g(N, K, seed=12), g(M, K, seed=13)
+    H = g(M, K, seed=14, relu=True)
+    res = g(M, K, seed=15)
+    dX = torch.empty(M, K, device=dev)
+    O.linear_dx(dY, W, dX, rows=M, mask=H, ldmask=K, resid=res)
+    ref = (dY @ W) * (H > 0) + res
+    assert rel(dX, ref) < 2e-6
+    dW = g(N, K, seed=16)
+    db = g(N, seed=17)
+    dW0, db0 = dW.clone(), db.clone()
+    O.linear_dw(dY, X, dW, db, rows=M)
+    assert rel(dW, dW0 + dY.t() @ X) < 1e-5
+    assert rel(db, db0 + dY.sum(0)) < 1e-5
+    # b_rows gather on the TN layout
+    table = g(500, K, seed=18)
+    idx = torch.randint(0, 500, (M,), generator=torch.Generator().manual_seed(19)).to(dev)
+    dW2 = torch.zeros(N, K, device=dev)
+    O.linear_dw(dY, table, dW2, None, rows=M, x_rows=idx)
+    assert rel(dW2, dY.t() @ table[idx]) < 1e-5
+
+
+def test_gemm_mask_arows_rowscale():
+    O = ops()
+    M, N, K = 50, 96, 64
+    src = g(200, N, seed=20, relu=True)       # mask source in gathered-row space
+    A = g(200, K, seed=21)
+    idx = torch.randperm(200, generator=torch.Generator().manual_seed(22))[:M].to(dev)
+    W = g(K, N, seed=23)                       # B stored [K][N]
+    out = torch.empty(M, N, device=dev)
+    O.gemm(A, W, out, M, N, K, lda=K, ldb=N, ldc=N, a_rows=idx, mask=src, ldmask=N, mask_arows=True)
+    ref = (A[idx] @ W) * (src[idx] > 0)
+    assert rel(out, ref) < 2e-6
+    rs = (torch.arange(M, device=dev) % 3 != 0).float()
+    W2 = g(N, K, seed=24)
+    O.linear(A, W2, None, out, relu=True, rows=M, a_rows=idx, rowscale=rs)
+    ref = torch.relu(A[idx] @ W2.t()) * rs[:, None]
+    assert rel(out, ref) < 2e-6
+
+
+def _ln_ref(z, gam, bet):
+    m = z.mean(-1, keepdim=True)
+    return gam * (z - m) / (z.std(-1, keepdim=True) + 1e-8) + bet
+
+
+def test_layernorm_fwd_bwd():
+    O = ops()
+    R, Cc = 333, 512
+    x, r = g(R, Cc, seed=30), g(R, Cc, seed=31)
+    gam, bet = g(Cc, seed=32) * 0.2 + 1, g(Cc, seed=33) * 0.2
+    y, z = torch.empty_like(x), torch.empty_like(x)
+    mean, rden, std, flag = (torch.empty(R, device=dev) for _ in range(4))
+    xs = (torch.arange(R, device=dev) % 5 != 0).float()
+    O.ln_fwd(x, gam, bet, y, mean, rden, std, r=r, z_out=z, flag=flag, xscale=xs)
+    zz = (x * xs[:, None] + r)
+    ref = _ln_ref(zz.double(), gam.double(), bet.double())
+    assert rel(y, ref) < 5e-6
+    assert torch.equal(flag.cpu(), (ref.sum(-1) != 0).float().cpu())
+    dy = g(R, Cc, seed=34)
+    dz = torch.empty_like(x)
+    dg, db = torch.zeros(Cc, device=dev), torch.zeros(Cc, device=dev)
+    O.ln_bwd(dy, z, mean, rden, std, gam, dz, dg, db)
+    zd = zz.double().cpu().requires_grad_(True)
+    gd, bd = gam.double().cpu().requires_grad_(True), bet.double().cpu().requires_grad_(True)
+    (_ln_ref(zd, gd, bd) * dy.double().cpu()).sum().backward()
+    assert rel(dz, zd.grad) < 1e-5
+    assert rel(dg, gd.grad) < 1e-5
+    assert rel(db, bd.grad) < 1e-5
+
+
+def _attn_ref(Q, K, V, G, kf, qf, h=8):
+    """modules.py:246-301 core on already-projected (post-ReLU) Q, K, V."""
+    B, Tq, D = Q.shape
+    Tk = K.shape[1]
+    cat = lambda X: torch.cat(torch.chunk(X, h, 2), 0)
+    S = torch.bmm(cat(Q), cat(K).permute(0, 2, 1)) / 8.0
+    km = kf.repeat(h, 1).unsqueeze(1).repeat(1, Tq, 1)
+    cond = km.eq(0).to(S.dtype)
+    S = torch.ones_like(S) * (-2 ** 32 + 1) * cond + S * (1 - cond)
+    A = F.softmax(S, -1) * G.repeat(h, 1, 1)
+    N = F.normalize(A, p=1, dim=-1)
+    P = N * qf.repeat(h, 1).unsqueeze(2)
+    Oc = torch.bmm(P, cat(V))
+    return torch.cat(torch.chunk(Oc, h, 0), 2), N
+
+
+@pytest.mark.parametrize("B,Tq,Tk,kind", [(3, 50, 50, "self"), (2, 73, 73, "self"),
+                                           (5, 1, 73, "cross"), (2, 20, 100, "self")])
+def test_graph_attention_fwd_bwd(B, Tq, Tk, kind):
+    O = ops()
+    H, D = 8, 512
+    qkv = g(B * Tk, 3 * D, seed=40, relu=True) if kind == "self" and Tq == Tk else None
+    if qkv is not None:
+        Q, K, V = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+        ldq = ldk = ldv = 3 * D
+    else:
+        Q = g(B * Tq, D, seed=41, relu=True)
+        kv = g(B * Tk, 2 * D, seed=42, relu=True)
+        K, V = kv[:, :D], kv[:, D:]
+        ldq, ldk, ldv = D, 2 * D, 2 * D
+    G = (torch.rand(B, Tq, Tk, generator=torch.Generator().manual_seed(43)) < 0.4).float().to(dev)
+    G[0, :3] = 0.0  # rows that attend to nothing
+    kf = torch.ones(B, Tk, device=dev)
+    kf[0, 2] = 0.0
+    kf[-1, -1] = 0.0
+    qf = torch.ones(B, Tq, device=dev)
+    qf[-1, 0] = 0.0
+    out = torch.empty(B * Tq, D, device=dev)
+    att = torch.empty(H * B, Tq, Tk, device=dev)
+    O.gattn_fwd(Q, ldq, K, ldk, V, ldv, G, kf, qf, B, Tq, Tk, H, out, D, att)
+    Qr = Q.reshape(B, Tq, D).double().cpu().requires_grad_(True)
+    Kr = K.reshape(B, Tk, D).double().cpu().requires_grad_(True)
+    Vr = V.reshape(B, Tk, D).double().cpu().requires_grad_(True)
+    ref, Nref = _attn_ref(Qr, Kr, Vr, G.double().cpu(), kf.double().cpu(), qf.double().cpu())
+    assert rel(out.view(B, Tq, D), ref) < 2e-5
+    assert rel(att, Nref) < 2e-5
+    dO = g(B * Tq, D, seed=44)
+    (ref * dO.view(B, Tq, D).double().cpu()).sum().backward()
+    dq = torch.empty(B * Tq, D, device=dev)
+    dk = torch.empty(B * Tk, D, device=dev)
+    dv = torch.empty(B * Tk, D, device=dev)
+    O.gattn_bwd(Q, ldq, K, ldk, V, ldv, G, kf, qf, B, Tq, Tk, H, dO, D, dq, D, dk, D, dv, D)
+    mq, mk, mv = (Qr > 0), (Kr > 0), (Vr > 0)
+    assert rel(dq.view(B, Tq, D), Qr.grad * mq) < 5e-5
+    assert rel(dk.view(B, Tk, D), Kr.grad * mk) < 5e-5
+    assert rel(dv.view(B, Tk, D), Vr.grad * mv) < 5e-5
+
+
+def test_graph_build_matches_oracle():
+    from oracle import savqa_oracle as OR
+    O = ops()
+    B, Nn, Lq = 3, 9, 5
+    gen = torch.Generator().manual_seed(50)
+    nm = torch.zeros(B, Nn, Nn, dtype=torch.int32)
+    qm = torch.zeros(B, Lq, Lq, dtype=torch.int32)
+    for b, (n, l) in enumerate([(9, 5), (4, 3), (0, 5)]):
+        nm[b, :n, :n] = 1
+        qm[b, :l, :l] = 1
+    qg = (torch.rand(B, Lq, Lq, generator=gen) < 0.3).int()
+    ng = (torch.rand(B, Nn, Nn, generator=gen) < 0.3).int()
+    T = Nn + Lq
+    for node_graph in (None, ng):
+        for dec in (True, False):
+            gd, gr, dm = (torch.empty(B, T, T, device=dev), torch.empty(B, T, T, device=dev),
+                          torch.empty(B, 1, T, device=dev))
+            O.graph_build(nm.to(dev), qm.to(dev), qg.to(dev),
+                          None if node_graph is None else node_graph.to(dev), B, Nn, Lq, dec, gd, gr, dm)
+            rgd, rg, rdm = OR.build_graphs(nm, qm, qg, node_graph, dec)
+            assert torch.equal(gd.cpu(), rgd) and torch.equal(gr.cpu(), rg) and torch.equal(dm.cpu(), rdm)
+
+
+def test_mil_core_fwd_bwd():
+    O = ops()
+    B, Nv, K, H, eps = 3, 7, 5, 64, 1e-6
+    Pf = g(B * Nv * K, H, seed=60, relu=True) * 0.2
+    Nf = g(B * Nv * K, H, seed=61, relu=True) * 0.2
+    v = g(B * Nv, H, seed=62, relu=True) * 0.2
+    mask = torch.ones(B, Nv, K, dtype=torch.int32)
+    mask[1, 3:] = 0
+    obj = torch.empty(B * Nv, H, device=dev)
+    ws = torch.empty(B * Nv, device=dev)
+    mil = torch.empty((), device=dev)
+    O.mil_fwd(Pf, Nf, v, mask.to(dev), B * Nv, K, H, eps, obj, ws, mil)
+    P4 = Pf.view(B, Nv, K, H).double().cpu().requires_grad_(True)
+    N4 = Nf.view(B, Nv, K, H).double().cpu().requires_grad_(True)
+    v4 = v.view(B, Nv, H).double().cpu().requires_grad_(True)
+    m4 = mask.double().unsqueeze(3)
+    vv = v4.unsqueeze(3)
+    sp = m4 * torch.matmul(P4, vv)
+    sn = m4 * torch.matmul(N4, vv)
+    z = torch.zeros(sn.size(), dtype=torch.double)
+    ref_mil = torch.mean(torch.logsumexp(torch.cat((sp.clamp(min=eps), z.clamp(min=eps)), 1), 2)
+                         - torch.logsumexp(torch.cat((sp.clamp(min=eps), sn.clamp(min=eps)), 1), 2))
+    ref_obj = torch.sum(F.softmax(torch.matmul(P4, vv), dim=2) * P4, dim=2)
+    assert abs(float(mil) - float(ref_mil)) < 1e-5 * max(1.0, abs(float(ref_mil)))
+    assert rel(obj.view(B, Nv, H), ref_obj) < 1e-5
+    dobj = g(B * Nv, H, seed=63)
+    dmil = torch.tensor(-1.7, device=dev)
+    (ref_obj * dobj.view(B, Nv, H).double().cpu()).sum().add(ref_mil * -1.7).backward()
+    dPf, dNf, dv = torch.empty_like(Pf), torch.empty_like(Nf), torch.empty_like(v)
+    O.mil_bwd(Pf, Nf, v, mask.to(dev), B * Nv, K, H, eps, dobj, dmil, dPf, dNf, dv)
+    assert rel(dPf.view(B, Nv, K, H), P4.grad * (P4 > 0)) < 1e-5
+    assert rel(dNf.view(B, Nv, K, H), N4.grad * (N4 > 0)) < 1e-5
+    assert rel(dv.view(B, Nv, H), v4.grad * (v4 > 0)) < 1e-5
+
+
+def test_loss_matches_oracle():
+    from oracle import savqa_oracle as OR
+    O = ops()
+    B, Cc = 6, 914
+    lc, lv, ls = g(B, Cc, seed=70), g(B, Cc, seed=71), g(B, Cc, seed=72)
+    ans = torch.randint(1, Cc, (B,), generator=torch.Generator().manual_seed(73))
+    mil = torch.tensor(0.37, device=dev)
+    loss = torch.empty((), device=dev)
+    dl = torch.empty(3, B, Cc, device=dev)
+    lsm = torch.empty(B, Cc, device=dev)
+    ws = torch.empty(B, device=dev)
+    O.loss_fwd(lc, lv, ls, ans.to(dev), B, Cc, 0.1, mil, True, loss, dl, lsm, ws)
+    t = [x.double().cpu().requires_grad_(True) for x in (lc, lv, ls)]
+    ref, ref_lsm = OR.train_loss(t[0], t[1], t[2], ans, torch.tensor(0.37, dtype=torch.double))
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 1e-5 * abs(float(ref))
+    assert rel(lsm, ref_lsm) < 1e-6
+    for i in range(3):
+        assert rel(dl[i], t[i].grad) < 1e-5
+
+
+def test_adam_matches_oracle():
+    from oracle import savqa_oracle as OR
+    O = ops()
+    n = 10003
+    p, gr = g(n, seed=80), g(n, seed=81)
+    m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    P = {"x": p.cpu().clone()}
+    st = {}
+    for step in (1, 2, 3):
+        gg = gr * step
+        O.adam(p, gg, m, v, n, 1e-4, 0.9, 0.999, 1e-8, 1 - 0.9 ** step, 1 - 0.999 ** step)
+        OR.adam_step(P, {"x": gg.cpu()}, st, step)
+    assert rel(p, P["x"]) < 1e-6
