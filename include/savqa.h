@@ -177,6 +177,22 @@ int savqa_loss_fwd(void* stream, const float* lc, const float* lv, const float* 
                    const int64_t* answer, int64_t B, int64_t C, float eps, const float* mil,
                    int32_t with_mil, float* loss, float* dlogits, float* lsm, float* ws);
 
+/* out[r][c] = in[r][c] * rowscale[r] * (mask[r][c] > 0)   (either optional): ReLU backward of
+ * the decoder self-attention value path, LN(qm * relu(V_proj(x)) + x) (modules.py:187-205) */
+int savqa_rowscale_mask(void* stream, const float* in, const float* rowscale, const float* mask,
+                        int64_t rows, int64_t cols, float* out);
+
+/* out = a*in + b   (label_smoothing.forward, modules.py:461-463) */
+int savqa_affine(void* stream, const float* in, int64_t n, float a, float b, float* out);
+
+/* embedding.forward (modules.py:40-43): out[r] = table[idx[r]] * scale; and its backward
+ * dtable[idx[r]] += g[r] * scale for idx[r] != padding_idx (pass -1 for none... the
+ * reference's padding_idx=-1 means the LAST row: the caller passes vocab-1). */
+int savqa_gather_rows(void* stream, const float* table, const int64_t* idx, int64_t rows,
+                      int64_t cols, float scale, float* out);
+int savqa_scatter_rows(void* stream, const float* g, const int64_t* idx, int64_t rows,
+                       int64_t cols, float scale, int64_t padding_idx, float* dtable);
+
 /* out[i] = in[i] * (*scale)  (chain rule with a device-side upstream gradient) */
 int savqa_scale_by(void* stream, const float* in, const float* scale, int64_t n, float* out);
 

@@ -1,0 +1,304 @@
+"""Model API mirroring the reference's models/AttModel_x3.py (model_v=3).
+
+Same classes (AttModel_vis_grid, AttModel_syb, MIL_NCE, CompactBilinearPooling,
+AttModel), constructor signatures, attribute names and parameter registration
+order, so the 498 state_dict keys are identical and checkpoints interchange both
+ways (DDP's `module.` prefix is handled by utils.strip_module_prefix).
+
+AttModel.forward(16 tensors, decMask, mcb) returns (logits_concat, logits_vis,
+logits_syb, mil_nce_obj, mil_nce_rel) exactly like AttModel_x3.py:512-542, but the
+whole forward is ONE autograd node whose body is the libsavqa kernel chain in
+engine.py; parameters live in one flat fp32 arena (params.py).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+from torch.nn.parameter import Parameter
+
+from .engine import ModelEngine
+from .modules import embedding, feedforward, label_smoothing, multihead_attention, \
+    new_multihead_attention
+from .params import ParamArena
+
+PAD = 400000          # AttModel_x3.py:13
+UNK = 400001
+END = 400003
+INVALID = 400003
+VIS_PAD = -1
+LOC_PAD = -1
+VOCAB = 407000        # AttModel_x3.py:36 (GloVe 400k + 7000 extra rows)
+
+
+def _glove_table(glove, init: bool):
+    t = torch.empty(VOCAB, 300)
+    if init:
+        nn.init.xavier_normal_(t)
+        if glove is not None and getattr(glove, "vectors", None) is not None:
+            v = glove.vectors
+            t[:v.shape[0], :] = v
+    return t
+
+
+class AttModel_vis_grid(nn.Module):
+    """AttModel_x3.py:20-156 (parameters; the forward runs inside AttModel's engine)."""
+
+    def __init__(self, glove, hidden_size, maxlen, maxlen_q, num_blocks, num_heads, dropout_rate,
+                 maxlen_v, num_classes, _init=True):
+        super().__init__()
+        self.hidden_size = hidden_size
+        self.num_blocks = num_blocks
+        self.num_heads = num_heads
+        self.maxlen_q = maxlen_q
+        self.maxlen = maxlen
+        self.dropout_rate = dropout_rate
+        self.enc_dropout = nn.Dropout(dropout_rate)
+        self.dec_dropout = nn.Dropout(dropout_rate)
+        self.syb_emb = nn.Embedding.from_pretrained(_glove_table(glove, _init), freeze=False)
+        self.syb_mlp = nn.Sequential(nn.Linear(300, 2048), nn.ReLU(inplace=True))
+        self.syb_mlp2 = nn.Linear(2048, hidden_size)
+        self.v_mlp = nn.Sequential(nn.Linear(2048, hidden_size), nn.ReLU(inplace=True),
+                                   nn.Linear(hidden_size, hidden_size))
+        self.v_positional_encoding = nn.Sequential(
+            embedding(maxlen_v, hidden_size, zeros_pad=False, scale=False), nn.Dropout(dropout_rate))
+        self.input_proj = nn.Linear(2048, hidden_size)
+        for i in range(num_blocks):
+            self.__setattr__('enc_self_attention_%d' % i, new_multihead_attention(
+                num_units=hidden_size, num_heads=num_heads, dropout_rate=0, causality=False))
+            self.__setattr__('enc_feed_forward_%d' % i, feedforward(hidden_size, [4 * hidden_size,
+                                                                                 hidden_size]))
+        self.q_mlp = nn.Sequential(nn.Linear(300, hidden_size), nn.ReLU(inplace=True),
+                                   nn.Linear(hidden_size, hidden_size))
+        self.q_positional_encoding = nn.Sequential(
+            embedding(maxlen_q, hidden_size, zeros_pad=False, scale=False), nn.Dropout(dropout_rate))
+        self.syb_positional_encoding = nn.Sequential(
+            embedding(maxlen, hidden_size, zeros_pad=False, scale=False), nn.Dropout(dropout_rate))
+        self.dec_emb = embedding(num_classes, hidden_size, scale=True)
+        self.dec_positional_encoding = embedding(maxlen, hidden_size, zeros_pad=False, scale=False)
+        for i in range(num_blocks):
+            self.__setattr__('dec_self_attention_%d' % i, multihead_attention(
+                num_units=hidden_size, num_heads=num_heads, dropout_rate=0, causality=True))
+            self.__setattr__('dec_vanilla_attention_%d' % i, new_multihead_attention(
+                num_units=hidden_size, num_heads=num_heads, dropout_rate=0, causality=False))
+            self.__setattr__('dec_feed_forward_%d' % i, feedforward(hidden_size, [4 * hidden_size,
+                                                                                 hidden_size]))
+
+    def forward(self, *a, **k):
+        raise RuntimeError("AttModel_vis_grid runs inside AttModel.forward (savqa engine)")
+
+
+class AttModel_syb(nn.Module):
+    """AttModel_x3.py:158-282."""
+
+    def __init__(self, glove, hidden_size, maxlen, maxlen_q, num_blocks, num_heads, dropout_rate,
+                 num_classes, _init=True):
+        super().__init__()
+        self.num_blocks = num_blocks
+        self.num_heads = num_heads
+        self.hidden_size = hidden_size
+        self.dropout_rate = dropout_rate
+        self.maxlen = maxlen
+        self.maxlen_q = maxlen_q
+        self.syb_emb = nn.Embedding.from_pretrained(_glove_table(glove, _init), freeze=False)
+        self.syb_mlp = nn.Sequential(nn.Linear(300, 2048), nn.ReLU(inplace=True))
+        self.syb_mlp2 = nn.Linear(2048, hidden_size)
+        self.enc_dropout = nn.Dropout(dropout_rate)
+        self.syb_positional_encoding = embedding(maxlen + maxlen_q, hidden_size, zeros_pad=False,
+                                                 scale=False)
+        self.q_mlp = nn.Sequential(nn.Linear(300, hidden_size), nn.Linear(hidden_size, hidden_size))
+        self.q_positional_encoding = nn.Sequential(
+            embedding(maxlen_q, hidden_size, zeros_pad=False, scale=False), nn.Dropout(dropout_rate))
+        self.dec_emb = embedding(num_classes, hidden_size, scale=True)
+        self.dec_positional_encoding = embedding(maxlen + maxlen_q, hidden_size, zeros_pad=False,
+                                                 scale=False)
+        self.dec_dropout = nn.Dropout(dropout_rate)
+        for i in range(num_blocks):
+            self.__setattr__('dec_self_attention_%d' % i, multihead_attention(
+                num_units=hidden_size, num_heads=num_heads, dropout_rate=0, causality=True))
+            self.__setattr__('dec_vanilla_attention_%d' % i, new_multihead_attention(
+                num_units=hidden_size, num_heads=num_heads, dropout_rate=0, causality=False))
+            self.__setattr__('dec_feed_forward_%d' % i, feedforward(hidden_size, [4 * hidden_size,
+                                                                                 hidden_size]))
+        for i in range(num_blocks):
+            self.__setattr__('enc_self_attention_%d' % i, new_multihead_attention(
+                num_units=hidden_size, num_heads=num_heads, dropout_rate=0, causality=False))
+            self.__setattr__('enc_feed_forward_%d' % i, feedforward(hidden_size, [4 * hidden_size,
+                                                                                 hidden_size]))
+
+    def forward(self, *a, **k):
+        raise RuntimeError("AttModel_syb runs inside AttModel.forward (savqa engine)")
+
+
+class MIL_NCE(nn.Module):
+    """AttModel_x3.py:285-443 (only_obj branch runs in the engine; the relation branch
+    :382-440 is the next scope row and raises)."""
+
+    def __init__(self, glove, hidden_size, dropout_rate, num_relations, only_obj, _init=True):
+        super().__init__()
+        self.only_obj = only_obj
+        self.dropout_rate = dropout_rate
+        self.num_relations = num_relations
+        self.hidden_size = hidden_size
+        self.R = Parameter(torch.empty(num_relations, hidden_size, hidden_size))
+        if _init:
+            nn.init.xavier_normal_(self.R)
+        self.syb_emb = nn.Embedding.from_pretrained(_glove_table(glove, _init), freeze=False)
+        self.marco_mlp = nn.Sequential(nn.Linear(300, hidden_size), nn.ReLU(inplace=True))
+        self.syb_mlp = nn.Sequential(nn.Linear(300, hidden_size), nn.ReLU(inplace=True))
+        self.vis_mlp = nn.Sequential(nn.Linear(2048, hidden_size), nn.ReLU(inplace=True))
+        self.rel_mlp = nn.Sequential(nn.Linear(hidden_size, hidden_size), nn.ReLU(inplace=True),
+                                     nn.Linear(hidden_size, 1))
+        self.softmax = torch.nn.Softmax(dim=2)
+        self.softmax_bilinear = torch.nn.Softmax(dim=0)
+        self.bilinear = nn.Bilinear(hidden_size, hidden_size, num_relations, bias=False)
+        self.ipt_mlp = nn.Sequential(nn.Linear(hidden_size, 2048), nn.ReLU(inplace=True))
+
+    def forward(self, *a, **k):
+        raise RuntimeError("MIL_NCE runs inside AttModel.forward (savqa engine)")
+
+
+class CompactBilinearPooling(nn.Module):
+    """AttModel_x3.py:444-469. Parameters only: the mcb path needs torch.rfft (removed
+    from torch >= 1.8) and is off in the published config; forward raises."""
+
+    def __init__(self, input_dims, output_dim):
+        super().__init__()
+        self.output_dim = output_dim
+
+        def sketch(input_dim):
+            h = torch.randint(output_dim, size=(input_dim,))
+            s = (2 * torch.randint(2, size=(input_dim,)) - 1).float()
+            m = torch.zeros(input_dim, output_dim)
+            m[torch.arange(input_dim), h] = s
+            return m
+
+        self.sketch1 = nn.Parameter(sketch(input_dims), requires_grad=False)
+        self.sketch2 = nn.Parameter(sketch(input_dims), requires_grad=False)
+
+    def forward(self, x1, x2):
+        raise NotImplementedError("mcb=True (CompactBilinearPooling) is out of scope")
+
+
+class _AttModelFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, decMask, anchor, *tensors):
+        inp = dict(zip(_INPUT_NAMES, tensors))
+        (lc, lv, ls, mil), saved = model._engine.forward(inp, decMask)
+        ctx.model = model
+        ctx.saved = saved
+        return lc, lv, ls, mil
+
+    @staticmethod
+    def backward(ctx, dlc, dlv, dls, dmil):
+        model = ctx.model
+        dev = model._arena.flat.device
+
+        def z(g, shape):
+            return g.contiguous() if g is not None else torch.zeros(shape, device=dev)
+
+        B = ctx.saved[1].B
+        Cc = model.num_classes
+        model._engine.backward(ctx.saved, z(dlc, (B, Cc)), z(dlv, (B, Cc)), z(dls, (B, Cc)),
+                               z(dmil, ()))
+        ctx.saved = None
+        return (None, None, None) + (None,) * len(_INPUT_NAMES)
+
+
+_INPUT_NAMES = ("vis_fea", "vis_mask", "q_ipt", "q_mask", "q_graph", "macro_ipt", "macro_mask",
+                "macro_graph", "macro_obj_loc", "micro_positive_obj", "micro_negative_obj",
+                "micro_obj_mask")
+
+
+class AttModel(nn.Module):
+    """AttModel_x3.py:471-542."""
+
+    def __init__(self, glove, hidden_size, hidden_size_mil, num_classes, maxlen_q, maxlen, maxlen_v,
+                 num_blocks, num_heads, dropout_rate, dropout_rate_mcb, num_relations, only_obj,
+                 device=None, init=True):
+        super().__init__()
+        self.only_obj = only_obj
+        self.num_classes = num_classes
+        self.hidden_size = hidden_size
+        self.num_blocks = num_blocks
+        self.num_heads = num_heads
+        self.dropout_rate = dropout_rate
+        self.att_vis_grid = AttModel_vis_grid(glove, hidden_size, maxlen, maxlen_q, num_blocks,
+                                              num_heads, dropout_rate, maxlen_v, num_classes, init)
+        self.att_syb = AttModel_syb(glove, hidden_size, maxlen, maxlen_q, num_blocks, num_heads,
+                                    dropout_rate, num_classes, init)
+        self.MIL_NCE = MIL_NCE(glove, hidden_size_mil, dropout_rate, num_relations, self.only_obj,
+                               init)
+        self.cls = nn.Sequential(nn.Linear(hidden_size * 2, hidden_size), nn.ReLU(),
+                                 nn.Dropout(dropout_rate, inplace=True),
+                                 nn.Linear(hidden_size, num_classes))
+        self.cls_vis = nn.Sequential(nn.Linear(hidden_size, hidden_size), nn.ReLU(),
+                                     nn.Dropout(dropout_rate, inplace=True),
+                                     nn.Linear(hidden_size, num_classes))
+        self.cls_syb = nn.Sequential(nn.Linear(hidden_size, hidden_size), nn.ReLU(),
+                                     nn.Dropout(dropout_rate, inplace=True),
+                                     nn.Linear(hidden_size, num_classes))
+        self.mcb_out = 16000
+        self.mcb = CompactBilinearPooling(hidden_size, self.mcb_out)
+        self.mcb_dropout = nn.Dropout(dropout_rate_mcb)
+        self.cls_mcb = nn.Sequential(nn.Linear(self.mcb_out, hidden_size), nn.ReLU(),
+                                     nn.Dropout(dropout_rate, inplace=True),
+                                     nn.Linear(hidden_size, num_classes))
+        self.label_smoothing = label_smoothing()
+        # flatten every parameter into the arena (state_dict keys unchanged)
+        object.__setattr__(self, "_arena", ParamArena(self, num_blocks, device=device))
+        object.__setattr__(self, "_engine", ModelEngine(self._arena, num_blocks, hidden_size,
+                                                        num_heads))
+
+    # parameters live in the arena: moving the module moves the arena
+    def _apply(self, fn, recurse=True):
+        arena = self.__dict__.get("_arena")
+        if arena is None:
+            return super()._apply(fn, recurse)
+        arena.apply(fn)
+        self._engine.rebind()
+        return self
+
+    def forward(self, vis_fea, vis_mask, q_ipt, q_mask, q_graph,
+                macro_ipt, macro_mask, macro_graph, macro_obj_loc,
+                micro_positive_obj, micro_negative_obj, micro_obj_mask,
+                micro_positive_rel, micro_negative_rel, micro_positive_rel_loc,
+                micro_negative_rel_loc, decMask=True, mcb=False):
+        if mcb:
+            raise NotImplementedError("mcb=True needs torch.rfft (removed in torch>=1.8); out of scope")
+        if not self.only_obj:
+            raise NotImplementedError("MIL-NCE relation branch (only_obj=False) is the next scope "
+                                      "row (SURVEY.md 8f); use only_obj=True")
+        if self.training and self.dropout_rate > 0:
+            raise NotImplementedError(
+                "dropout_rate > 0 in training mode is not implemented; the reference itself "
+                "cannot backpropagate it on torch>=2 (ReLU -> Dropout(inplace) in the heads, "
+                "AttModel_x3.py:482-500)")
+        dev = self._arena.flat.device
+        if dev.type != "cuda":
+            raise RuntimeError("savqa AttModel runs on a HIP device: call model.cuda() first")
+
+        def f32(t):
+            return t.to(device=dev, dtype=torch.float32).contiguous()
+
+        def i32(t):
+            return t.to(device=dev, dtype=torch.int32).contiguous()
+
+        def i64(t):
+            return t.to(device=dev, dtype=torch.int64).contiguous()
+
+        tensors = (f32(vis_fea), i32(vis_mask), i64(q_ipt), i32(q_mask), i32(q_graph), i64(macro_ipt),
+                   i32(macro_mask), i32(macro_graph), i64(macro_obj_loc), i64(micro_positive_obj),
+                   i64(micro_negative_obj), i32(micro_obj_mask))
+        anchor = self._arena_anchor()
+        lc, lv, ls, mil = _AttModelFn.apply(self, bool(decMask), anchor, *tensors)
+        return lc, lv, ls, mil, 0
+
+    def _arena_anchor(self):
+        # any parameter that requires grad links the autograd node into the graph
+        for p in self.cls.parameters():
+            if p.requires_grad and torch.is_grad_enabled():
+                return p
+        return None

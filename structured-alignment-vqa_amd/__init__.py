@@ -9,3 +9,16 @@ Host code mirrors the reference's nn.Module API; the compute runs in libsavqa.so
 __version__ = "0.1.0"
 
 from . import _lib  # noqa: F401
+
+
+def __getattr__(name):  # lazy: importing the package must not need a GPU
+    if name in ("AttModel",):
+        from .AttModel_x3 import AttModel
+        return AttModel
+    if name == "Adam":
+        from .optim import Adam
+        return Adam
+    if name == "smoothed_loss":
+        from .loss import smoothed_loss
+        return smoothed_loss
+    raise AttributeError(name)

@@ -62,6 +62,10 @@ _SIGS = {
     "savqa_index_get_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "savqa_loss_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f, c_p, c_i32, c_p, c_p, c_p, c_p],
     "savqa_scale_by": [c_p, c_p, c_p, c_i64, c_p],
+    "savqa_rowscale_mask": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p],
+    "savqa_affine": [c_p, c_p, c_i64, c_f, c_f, c_p],
+    "savqa_gather_rows": [c_p, c_p, c_p, c_i64, c_i64, c_f, c_p],
+    "savqa_scatter_rows": [c_p, c_p, c_p, c_i64, c_i64, c_f, c_i64, c_p],
     "savqa_adam": [c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_f, c_f],
 }
 

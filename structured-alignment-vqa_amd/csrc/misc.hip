@@ -364,6 +364,47 @@ __global__ void scale_by_kernel(const float* __restrict__ in, const float* __res
     out[i] = in[i] * s;
 }
 
+// out = in * rowscale[row] * (mask > 0)   (ReLU backward of a row-gated activation)
+__global__ void rowscale_mask_kernel(const float* __restrict__ in, const float* __restrict__ rs,
+                                     const float* __restrict__ mask, int64_t rows, int64_t cols,
+                                     float* __restrict__ out) {
+  const int64_t n = rows * cols;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cols;
+    float v = in[i];
+    if (rs) v *= rs[r];
+    if (mask && !(mask[i] > 0.f)) v = 0.f;
+    out[i] = v;
+  }
+}
+
+// out = a*in + b  (label_smoothing, modules.py:461-463)
+__global__ void affine_kernel(const float* __restrict__ in, int64_t n, float a, float b,
+                              float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = a * in[i] + b;
+}
+
+// out[r][:] = table[idx[r]][:] * scale   (embedding.forward, modules.py:40-43)
+__global__ void gather_rows_kernel(const float* __restrict__ table, const int64_t* __restrict__ idx,
+                                   int64_t rows, int64_t cols, float scale, float* __restrict__ out) {
+  const int64_t r = blockIdx.x;
+  const int64_t t = idx[r];
+  for (int64_t c = threadIdx.x; c < cols; c += blockDim.x) out[r * cols + c] = table[t * cols + c] * scale;
+}
+
+// dtable[idx[r]][:] += g[r][:] * scale, skipping padding_idx rows (F.embedding backward)
+__global__ void scatter_rows_kernel(const float* __restrict__ g, const int64_t* __restrict__ idx,
+                                    int64_t rows, int64_t cols, float scale, int64_t padding_idx,
+                                    float* __restrict__ dtable) {
+  const int64_t r = blockIdx.x;
+  const int64_t t = idx[r];
+  if (t == padding_idx) return;
+  for (int64_t c = threadIdx.x; c < cols; c += blockDim.x) atomicAdd(&dtable[t * cols + c], g[r * cols + c] * scale);
+}
+
 // ------------------------------------------------------------------ Adam
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
@@ -531,4 +572,39 @@ extern "C" int savqa_adam(void* stream, float* p, const float* g, float* m, floa
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr,
                      beta1, beta2, eps, step_size, sbc2, grad_scale);
   return check_launch("savqa_adam");
+}
+
+extern "C" int savqa_rowscale_mask(void* stream, const float* in, const float* rowscale,
+                                   const float* mask, int64_t rows, int64_t cols, float* out) {
+  const int64_t n = rows * cols;
+  if (n <= 0) return 0;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(rowscale_mask_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), in,
+                     rowscale, mask, rows, cols, out);
+  return check_launch("savqa_rowscale_mask");
+}
+
+extern "C" int savqa_affine(void* stream, const float* in, int64_t n, float a, float b, float* out) {
+  if (n <= 0) return 0;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(affine_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), in, n, a, b, out);
+  return check_launch("savqa_affine");
+}
+
+extern "C" int savqa_gather_rows(void* stream, const float* table, const int64_t* idx, int64_t rows,
+                                 int64_t cols, float scale, float* out) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(rows), dim3(cols >= 256 ? 256 : 64), 0,
+                     as_stream(stream), table, idx, rows, cols, scale, out);
+  return check_launch("savqa_gather_rows");
+}
+
+extern "C" int savqa_scatter_rows(void* stream, const float* g, const int64_t* idx, int64_t rows,
+                                  int64_t cols, float scale, int64_t padding_idx, float* dtable) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3(rows), dim3(cols >= 256 ? 256 : 64), 0,
+                     as_stream(stream), g, idx, rows, cols, scale, padding_idx, dtable);
+  return check_launch("savqa_scatter_rows");
 }

@@ -1,0 +1,477 @@
+"""Forward / backward orchestration of the model_v=3 hot path on libsavqa kernels.
+
+One autograd node covers the whole AttModel.forward (AttModel_x3.py:512-542): the
+forward enqueues ~150 kernels per stack on the current HIP stream and keeps every
+activation the backward needs; the backward replays the chain in reverse and writes
+parameter gradients straight into the flat gradient arena (params.py) -- weight
+GEMMs accumulate with split-K atomics, bias / LN / table gradients with column
+reductions and row scatters. Per-stack schedule (AttModel_x3.py:91-156, 214-282):
+
+  cat[B,T,2048] = [node features ; relu(syb_emb[q] W_q^T + b)]    (gather fused in GEMM)
+  x0 = cat W_in^T + b_in + pos[t]                                 (pos add fused)
+  enc i: qkv = relu(x W_qkv^T + b)    (one N=1536 GEMM)
+         o   = graph_attention(qkv, G_i, flags)                    (attn.hip)
+         y1  = LN(o + x) ; h = relu(y1 W1^T + b1) ; x' = LN(h W2^T + b2 + y1)
+  kv_all = relu(x6 [Wk_0;Wv_0;...;Wk_5;Wv_5]^T + b)  (one N=6144 GEMM for all 6 layers)
+  dec i: d1 = LN(qflag(dec) * relu(dec Wv^T + bv) + dec)          (T=1 causal attention)
+         d2 = LN(graph_attention(relu(d1 Wq^T + bq), kv_i, dec_mask) + d1)
+         dec' = LN(relu(d2 W1^T + b1) W2^T + b2 + d2)
+The decoder self-attention's Q/K projections are skipped: with one key the softmax
+is exactly 1 (modules.py:184), so their outputs never reach the result and their
+gradients are exactly zero in the reference too.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+
+from . import ops
+
+F32 = torch.float32
+
+
+def _empty(*shape, dev):
+    return torch.empty(*shape, dtype=F32, device=dev)
+
+
+def _rows_index(B: int, T: int, start: int, count: int, dev) -> torch.Tensor:
+    """int64 row ids b*T + start + t for t < count (gather index into a [B,T,...] buffer)."""
+    return (torch.arange(B, device=dev, dtype=torch.int64).unsqueeze(1) * T
+            + start + torch.arange(count, device=dev, dtype=torch.int64).unsqueeze(0)).reshape(-1)
+
+
+# ----------------------------------------------------------------------------- weights
+class StackWeights:
+    """Views of one stack's parameters (and of its gradients) in the arena."""
+
+    def __init__(self, arena, pre: str, num_blocks: int, d: int, grad: bool = False):
+        v = arena.gview if grad else arena.view
+        sp = arena.gspan if grad else arena.span
+        self.E = v(f"{pre}.syb_emb.weight")
+        self.Wq, self.bq = v(f"{pre}.syb_mlp.0.weight"), v(f"{pre}.syb_mlp.0.bias")
+        self.Win, self.bin = v(f"{pre}.syb_mlp2.weight"), v(f"{pre}.syb_mlp2.bias")
+        self.pos = v(f"{pre}.syb_positional_encoding.0.lookup_table" if pre == "att_vis_grid"
+                     else f"{pre}.syb_positional_encoding.lookup_table")
+        self.enc = []
+        for i in range(num_blocks):
+            a, f = f"{pre}.enc_self_attention_{i}", f"{pre}.enc_feed_forward_{i}"
+            self.enc.append(dict(
+                Wqkv=sp(f"{a}.Q_proj.0.weight", f"{a}.V_proj.0.weight", (3 * d, d)),
+                bqkv=sp(f"{a}.Q_proj.0.bias", f"{a}.V_proj.0.bias", (3 * d,)),
+                g1=v(f"{a}.normalization.gamma"), b1=v(f"{a}.normalization.beta"),
+                W1=v(f"{f}.conv1.0.weight"), c1=v(f"{f}.conv1.0.bias"),
+                W2=v(f"{f}.conv2.weight"), c2=v(f"{f}.conv2.bias"),
+                g2=v(f"{f}.normalization.gamma"), b2=v(f"{f}.normalization.beta")))
+        c0, cl = f"{pre}.dec_vanilla_attention_0", f"{pre}.dec_vanilla_attention_{num_blocks - 1}"
+        self.Wkv = sp(f"{c0}.K_proj.0.weight", f"{cl}.V_proj.0.weight", (2 * num_blocks * d, d))
+        self.bkv = sp(f"{c0}.K_proj.0.bias", f"{cl}.V_proj.0.bias", (2 * num_blocks * d,))
+        self.dec_emb = v(f"{pre}.dec_emb.lookup_table")
+        self.dec_pos = v(f"{pre}.dec_positional_encoding.lookup_table")
+        self.dec = []
+        for i in range(num_blocks):
+            s, c, f = (f"{pre}.dec_self_attention_{i}", f"{pre}.dec_vanilla_attention_{i}",
+                       f"{pre}.dec_feed_forward_{i}")
+            self.dec.append(dict(
+                Wv=v(f"{s}.V_proj.0.weight"), bv=v(f"{s}.V_proj.0.bias"),
+                gs=v(f"{s}.normalization.gamma"), bs=v(f"{s}.normalization.beta"),
+                Wqc=v(f"{c}.Q_proj.0.weight"), bqc=v(f"{c}.Q_proj.0.bias"),
+                gc=v(f"{c}.normalization.gamma"), bc=v(f"{c}.normalization.beta"),
+                W1=v(f"{f}.conv1.0.weight"), c1=v(f"{f}.conv1.0.bias"),
+                W2=v(f"{f}.conv2.weight"), c2=v(f"{f}.conv2.bias"),
+                g2=v(f"{f}.normalization.gamma"), b2=v(f"{f}.normalization.beta")))
+
+
+class MilWeights:
+    def __init__(self, arena, grad=False):
+        v = arena.gview if grad else arena.view
+        m = "MIL_NCE"
+        self.E = v(f"{m}.syb_emb.weight")
+        self.Ws, self.bs = v(f"{m}.syb_mlp.0.weight"), v(f"{m}.syb_mlp.0.bias")
+        self.Wv, self.bv = v(f"{m}.vis_mlp.0.weight"), v(f"{m}.vis_mlp.0.bias")
+        self.Wipt, self.bipt = v(f"{m}.ipt_mlp.0.weight"), v(f"{m}.ipt_mlp.0.bias")
+        if not grad:
+            self.Wm, self.bm = v(f"{m}.marco_mlp.0.weight"), v(f"{m}.marco_mlp.0.bias")
+
+
+class HeadWeights:
+    def __init__(self, arena, grad=False):
+        v = arena.gview if grad else arena.view
+        self.h = {k: (v(f"{k}.0.weight"), v(f"{k}.0.bias"), v(f"{k}.3.weight"), v(f"{k}.3.bias"))
+                  for k in ("cls", "cls_vis", "cls_syb")}
+
+
+# ----------------------------------------------------------------------------- stack
+@dataclass
+class StackSaved:
+    B: int = 0
+    Nn: int = 0
+    Lq: int = 0
+    T: int = 0
+    cat: torch.Tensor = None
+    x0: torch.Tensor = None
+    gdiag: torch.Tensor = None
+    graph: torch.Tensor = None
+    dmask: torch.Tensor = None
+    q_flat: torch.Tensor = None
+    enc: List[dict] = field(default_factory=list)
+    x6: torch.Tensor = None
+    f6: torch.Tensor = None
+    kv: torch.Tensor = None
+    dec: List[dict] = field(default_factory=list)
+    out: torch.Tensor = None
+
+
+def _ln_stats(rows, dev):
+    return _empty(rows, dev=dev), _empty(rows, dev=dev), _empty(rows, dev=dev)
+
+
+def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
+                  q_ipt: torch.Tensor, node_mask, q_mask, q_graph, node_graph, decMask: bool,
+                  H: int, d: int) -> StackSaved:
+    """AttModel_vis_grid.forward (:91-156) / AttModel_syb.forward (:214-282).
+
+    `cat` is the [B*T, 2048] input buffer whose node rows [0, Nn) of every sample
+    are already filled by the caller; the question rows are produced here."""
+    dev = cat.device
+    T = Nn + Lq
+    M = B * T
+    s = StackSaved(B=B, Nn=Nn, Lq=Lq, T=T, cat=cat)
+    s.q_flat = q_ipt.reshape(-1)
+    # question tokens: relu(syb_emb[q] W^T + b) straight into rows [Nn, T) of cat
+    ops.linear(W.E, W.Wq, W.bq, cat, relu=True, rows=B * Lq, a_rows=s.q_flat, c_group=Lq,
+               c_stride=T, c_offset=Nn, ldo=cat.shape[1])
+    s.x0 = _empty(M, d, dev=dev)
+    ops.linear(cat, W.Win, W.bin, s.x0, rowvec=W.pos, rowvec_period=T)
+    flag = _empty(M, dev=dev)
+    ops.rowflag(s.x0, M, d, d, flag)
+    s.gdiag, s.graph = _empty(B, T, T, dev=dev), _empty(B, T, T, dev=dev)
+    s.dmask = _empty(B, 1, T, dev=dev)
+    ops.graph_build(node_mask, q_mask, q_graph, node_graph, B, Nn, Lq, decMask, s.gdiag, s.graph,
+                    s.dmask)
+    x = s.x0
+    for i, L in enumerate(W.enc):
+        G = s.gdiag if i < 2 else s.graph
+        e = dict(x=x, flag=flag)
+        qkv = _empty(M, 3 * d, dev=dev)
+        ops.linear(x, L["Wqkv"], L["bqkv"], qkv, relu=True)
+        o = _empty(M, d, dev=dev)
+        ops.gattn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag, flag, B, T, T,
+                      H, o, d)
+        z1, y1 = _empty(M, d, dev=dev), _empty(M, d, dev=dev)
+        st1 = _ln_stats(M, dev)
+        ops.ln_fwd(o, L["g1"], L["b1"], y1, *st1, r=x, z_out=z1)
+        h = _empty(M, 4 * d, dev=dev)
+        ops.linear(y1, L["W1"], L["c1"], h, relu=True)
+        z2 = _empty(M, d, dev=dev)
+        ops.linear(h, L["W2"], L["c2"], z2, resid=y1)
+        xn = _empty(M, d, dev=dev)
+        st2 = _ln_stats(M, dev)
+        fn = _empty(M, dev=dev)
+        ops.ln_fwd(z2, L["g2"], L["b2"], xn, *st2, flag=fn)
+        e.update(qkv=qkv, z1=z1, st1=st1, y1=y1, h=h, z2=z2, st2=st2)
+        s.enc.append(e)
+        x, flag = xn, fn
+    s.x6, s.f6 = x, flag
+    nb = len(W.dec)
+    s.kv = _empty(M, 2 * nb * d, dev=dev)
+    ops.linear(x, W.Wkv, W.bkv, s.kv, relu=True)
+    dec = _empty(B, d, dev=dev)
+    ops.dec_init(W.dec_emb, 2, math.sqrt(d), W.dec_pos, B, d, dec)
+    fdec = _empty(B, dev=dev)
+    ops.rowflag(dec, B, d, d, fdec)
+    for i, L in enumerate(W.dec):
+        e = dict(dec=dec, fdec=fdec)
+        v = _empty(B, d, dev=dev)
+        ops.linear(dec, L["Wv"], L["bv"], v, relu=True)
+        zs, d1 = _empty(B, d, dev=dev), _empty(B, d, dev=dev)
+        sts = _ln_stats(B, dev)
+        f1 = _empty(B, dev=dev)
+        ops.ln_fwd(v, L["gs"], L["bs"], d1, *sts, xscale=fdec, r=dec, z_out=zs, flag=f1)
+        qc = _empty(B, d, dev=dev)
+        ops.linear(d1, L["Wqc"], L["bqc"], qc, relu=True)
+        oc = _empty(B, d, dev=dev)
+        kvi = s.kv[:, 2 * i * d:]
+        ops.gattn_fwd(qc, d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6, f1, B, 1, T, H,
+                      oc, d)
+        zc, d2 = _empty(B, d, dev=dev), _empty(B, d, dev=dev)
+        stc = _ln_stats(B, dev)
+        ops.ln_fwd(oc, L["gc"], L["bc"], d2, *stc, r=d1, z_out=zc)
+        h = _empty(B, 4 * d, dev=dev)
+        ops.linear(d2, L["W1"], L["c1"], h, relu=True)
+        z2 = _empty(B, d, dev=dev)
+        ops.linear(h, L["W2"], L["c2"], z2, resid=d2)
+        dn = _empty(B, d, dev=dev)
+        st2 = _ln_stats(B, dev)
+        fn = _empty(B, dev=dev)
+        ops.ln_fwd(z2, L["g2"], L["b2"], dn, *st2, flag=fn)
+        e.update(v=v, zs=zs, sts=sts, d1=d1, f1=f1, qc=qc, zc=zc, stc=stc, d2=d2, h=h, z2=z2,
+                 st2=st2)
+        s.dec.append(e)
+        dec, fdec = dn, fn
+    s.out = dec
+    return s
+
+
+def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.Tensor, H: int,
+                   d: int, want_node_grad: bool) -> Optional[torch.Tensor]:
+    """Backward of stack_forward; accumulates parameter grads into G (arena views).
+
+    Returns d(pre-activation of the node rows of cat) [B*Nn, 2048] when want_node_grad
+    (the syb stack feeds it to the MIL-NCE backward), else None."""
+    dev = dout.device
+    B, T, Nn, Lq = s.B, s.T, s.Nn, s.Lq
+    M = B * T
+    nb = len(W.dec)
+    ddec = dout
+    dkv = _empty(M, 2 * nb * d, dev=dev)
+    for i in reversed(range(nb)):
+        L, Lg, e = W.dec[i], G.dec[i], s.dec[i]
+        # feed-forward
+        dz2 = _empty(B, d, dev=dev)
+        ops.ln_bwd(ddec, e["z2"], *e["st2"], L["g2"], dz2, Lg["g2"], Lg["b2"])
+        ops.linear_dw(dz2, e["h"], Lg["W2"], Lg["c2"], rows=B)
+        dh = _empty(B, 4 * d, dev=dev)
+        ops.linear_dx(dz2, L["W2"], dh, rows=B, mask=e["h"], ldmask=4 * d)
+        ops.linear_dw(dh, e["d2"], Lg["W1"], Lg["c1"], rows=B)
+        dd2 = _empty(B, d, dev=dev)
+        ops.linear_dx(dh, L["W1"], dd2, rows=B, resid=dz2)
+        # cross attention
+        dzc = _empty(B, d, dev=dev)
+        ops.ln_bwd(dd2, e["zc"], *e["stc"], L["gc"], dzc, Lg["gc"], Lg["bc"])
+        dqc = _empty(B, d, dev=dev)
+        kvi, dkvi = s.kv[:, 2 * i * d:], dkv[:, 2 * i * d:]
+        ops.gattn_bwd(e["qc"], d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6, e["f1"], B,
+                      1, T, H, dzc, d, dqc, d, dkvi, 2 * nb * d, dkvi[:, d:], 2 * nb * d)
+        ops.linear_dw(dqc, e["d1"], Lg["Wqc"], Lg["bqc"], rows=B)
+        dd1 = _empty(B, d, dev=dev)
+        ops.linear_dx(dqc, L["Wqc"], dd1, rows=B, resid=dzc)
+        # self attention (T = 1): z = fdec * relu(dec Wv^T + bv) + dec
+        dzs = _empty(B, d, dev=dev)
+        ops.ln_bwd(dd1, e["zs"], *e["sts"], L["gs"], dzs, Lg["gs"], Lg["bs"])
+        dvp = _empty(B, d, dev=dev)
+        ops.rowscale_mask(dzs, e["fdec"], e["v"], B, d, dvp)
+        ops.linear_dw(dvp, e["dec"], Lg["Wv"], Lg["bv"], rows=B)
+        dprev = _empty(B, d, dev=dev)
+        ops.linear_dx(dvp, L["Wv"], dprev, rows=B, resid=dzs)
+        ddec = dprev
+    ops.dec_init_bwd(ddec, B, d, 2, math.sqrt(d), G.dec_emb, G.dec_pos)
+    # all decoder K/V projections at once
+    ops.linear_dw(dkv, s.x6, G.Wkv, G.bkv, rows=M)
+    dx = _empty(M, d, dev=dev)
+    ops.linear_dx(dkv, W.Wkv, dx, rows=M)
+    del dkv
+    for i in reversed(range(len(W.enc))):
+        L, Lg, e = W.enc[i], G.enc[i], s.enc[i]
+        Gm = s.gdiag if i < 2 else s.graph
+        dz2 = _empty(M, d, dev=dev)
+        ops.ln_bwd(dx, e["z2"], *e["st2"], L["g2"], dz2, Lg["g2"], Lg["b2"])
+        ops.linear_dw(dz2, e["h"], Lg["W2"], Lg["c2"], rows=M)
+        dh = _empty(M, 4 * d, dev=dev)
+        ops.linear_dx(dz2, L["W2"], dh, rows=M, mask=e["h"], ldmask=4 * d)
+        ops.linear_dw(dh, e["y1"], Lg["W1"], Lg["c1"], rows=M)
+        dy1 = _empty(M, d, dev=dev)
+        ops.linear_dx(dh, L["W1"], dy1, rows=M, resid=dz2)
+        del dh
+        dz1 = _empty(M, d, dev=dev)
+        ops.ln_bwd(dy1, e["z1"], *e["st1"], L["g1"], dz1, Lg["g1"], Lg["b1"])
+        dqkv = _empty(M, 3 * d, dev=dev)
+        qkv = e["qkv"]
+        ops.gattn_bwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, Gm, e["flag"], e["flag"],
+                      B, T, T, H, dz1, d, dqkv, 3 * d, dqkv[:, d:], 3 * d, dqkv[:, 2 * d:], 3 * d)
+        ops.linear_dw(dqkv, e["x"], Lg["Wqkv"], Lg["bqkv"], rows=M)
+        dxn = _empty(M, d, dev=dev)
+        ops.linear_dx(dqkv, L["Wqkv"], dxn, rows=M, resid=dz1)
+        dx = dxn
+    # input projection, position table, question-token MLP and embedding table
+    ops.period_sum_acc(dx, B, T, d, d, G.pos)
+    ops.linear_dw(dx, s.cat, G.Win, G.bin, rows=M)
+    qrows = _rows_index(B, T, Nn, Lq, dev)
+    dq = _empty(B * Lq, W.Win.shape[1], dev=dev)
+    ops.linear_dx(dx, W.Win, dq, rows=B * Lq, a_rows=qrows, mask=s.cat, ldmask=s.cat.shape[1],
+                  mask_arows=True)
+    ops.linear_dw(dq, W.E, G.Wq, G.bq, rows=B * Lq, x_rows=s.q_flat)
+    ops.linear_dx(dq, W.Wq, G.E, rows=B * Lq, c_rows=s.q_flat, atomic=True)
+    del dq
+    if not want_node_grad:
+        return None
+    nrows = _rows_index(B, T, 0, Nn, dev)
+    dnode = _empty(B * Nn, W.Win.shape[1], dev=dev)
+    ops.linear_dx(dx, W.Win, dnode, rows=B * Nn, a_rows=nrows, mask=s.cat, ldmask=s.cat.shape[1],
+                  mask_arows=True)
+    return dnode
+
+
+# ----------------------------------------------------------------------------- MIL-NCE
+@dataclass
+class MilSaved:
+    B: int = 0
+    Nv: int = 0
+    Ns: int = 0
+    K: int = 0
+    pos: torch.Tensor = None
+    neg: torch.Tensor = None
+    loc: torch.Tensor = None
+    mask: torch.Tensor = None
+    vis: torch.Tensor = None
+    Pf: torch.Tensor = None
+    Nf: torch.Tensor = None
+    vv: torch.Tensor = None
+    macro: torch.Tensor = None
+
+
+def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb, T_syb: int,
+                mil_out: torch.Tensor, eps: float = 1e-6) -> MilSaved:
+    """MIL_NCE.forward only_obj branch (AttModel_x3.py:352-380, :441). Writes
+    relu(new_macro W_ipt^T + b) into the node rows of the syb stack's cat buffer."""
+    dev = vis_fea.device
+    B, Nv, Dv = vis_fea.shape
+    Ns = macro_ipt.shape[1]
+    K = pos.shape[2]
+    Hm = W.Ws.shape[0]
+    s = MilSaved(B=B, Nv=Nv, Ns=Ns, K=K, pos=pos.reshape(-1), neg=neg.reshape(-1),
+                 loc=loc.reshape(-1), mask=omask, vis=vis_fea.reshape(B * Nv, Dv))
+    s.Pf = _empty(B * Nv * K, Hm, dev=dev)
+    s.Nf = _empty(B * Nv * K, Hm, dev=dev)
+    ops.linear(W.E, W.Ws, W.bs, s.Pf, relu=True, a_rows=s.pos)
+    ops.linear(W.E, W.Ws, W.bs, s.Nf, relu=True, a_rows=s.neg)
+    s.vv = _empty(B * Nv, Hm, dev=dev)
+    ops.linear(s.vis, W.Wv, W.bv, s.vv, relu=True)
+    s.macro = _empty(B * Ns, Hm, dev=dev)
+    ops.linear(W.E, W.Wm, W.bm, s.macro, relu=True, a_rows=macro_ipt.reshape(-1))
+    obj = _empty(B * Nv, Hm, dev=dev)
+    ws = _empty(B * Nv, dev=dev)
+    ops.mil_fwd(s.Pf, s.Nf, s.vv, omask, B * Nv, K, Hm, eps, obj, ws, mil_out)
+    ops.index_put_rows(s.loc, B, Nv, Ns, Hm, obj, s.macro)
+    ops.linear(s.macro, W.Wipt, W.bipt, cat_syb, relu=True, rows=B * Ns, c_group=Ns,
+               c_stride=T_syb, c_offset=0, ldo=cat_syb.shape[1])
+    return s
+
+
+def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torch.Tensor],
+                 dmil: torch.Tensor, eps: float = 1e-6):
+    dev = dmil.device
+    B, Nv, Ns, K = s.B, s.Nv, s.Ns, s.K
+    Hm = W.Ws.shape[0]
+    dobj = None
+    if dnode is not None:
+        ops.linear_dw(dnode, s.macro, G.Wipt, G.bipt, rows=B * Ns)
+        dmacro = _empty(B * Ns, Hm, dev=dev)
+        ops.linear_dx(dnode, W.Wipt, dmacro, rows=B * Ns)
+        dobj = _empty(B * Nv, Hm, dev=dev)
+        ops.index_get_rows(s.loc, B, Nv, Ns, Hm, dmacro, dobj)
+        del dmacro
+    dPf, dNf = torch.empty_like(s.Pf), torch.empty_like(s.Nf)
+    dvv = torch.empty_like(s.vv)
+    ops.mil_bwd(s.Pf, s.Nf, s.vv, s.mask, B * Nv, K, Hm, eps, dobj, dmil, dPf, dNf, dvv)
+    n = B * Nv * K
+    ops.linear_dw(dPf, W.E, G.Ws, G.bs, rows=n, x_rows=s.pos)
+    ops.linear_dw(dNf, W.E, G.Ws, G.bs, rows=n, x_rows=s.neg)
+    ops.linear_dx(dPf, W.Ws, G.E, rows=n, c_rows=s.pos, atomic=True)
+    ops.linear_dx(dNf, W.Ws, G.E, rows=n, c_rows=s.neg, atomic=True)
+    ops.linear_dw(dvv, s.vis, G.Wv, G.bv, rows=B * Nv)
+
+
+# ----------------------------------------------------------------------------- heads
+def heads_forward(Wh: HeadWeights, f_vis, f_syb, d: int):
+    """AttModel.forward heads, AttModel_x3.py:531-541 (mcb=False)."""
+    dev = f_vis.device
+    B = f_vis.shape[0]
+    fcat = _empty(B, 2 * d, dev=dev)
+    ops.copy_rows(f_syb, B, d, d, fcat, 2 * d)
+    ops.copy_rows(f_vis, B, d, d, fcat[:, d:], 2 * d)
+    saved = {"fcat": fcat, "f_vis": f_vis, "f_syb": f_syb}
+    outs = []
+    for name, x in (("cls", fcat), ("cls_vis", f_vis), ("cls_syb", f_syb)):
+        W0, b0, W3, b3 = Wh.h[name]
+        h = _empty(B, W0.shape[0], dev=dev)
+        ops.linear(x, W0, b0, h, relu=True)
+        lo = _empty(B, W3.shape[0], dev=dev)
+        ops.linear(h, W3, b3, lo)
+        saved[name] = h
+        outs.append(lo)
+    return outs, saved
+
+
+def heads_backward(Wh: HeadWeights, Gh: HeadWeights, saved, dlc, dlv, dls, d: int):
+    dev = dlc.device
+    B = dlc.shape[0]
+    dx = {}
+    for name, dlo, x in (("cls", dlc, saved["fcat"]), ("cls_vis", dlv, saved["f_vis"]),
+                         ("cls_syb", dls, saved["f_syb"])):
+        W0, b0, W3, b3 = Wh.h[name]
+        gW0, gb0, gW3, gb3 = Gh.h[name]
+        h = saved[name]
+        ops.linear_dw(dlo, h, gW3, gb3, rows=B)
+        dh = _empty(B, W0.shape[0], dev=dev)
+        ops.linear_dx(dlo, W3, dh, rows=B, mask=h, ldmask=W0.shape[0])
+        ops.linear_dw(dh, x, gW0, gb0, rows=B)
+        dx[name] = dh
+    dfcat = _empty(B, 2 * d, dev=dev)
+    W0 = Wh.h["cls"][0]
+    ops.linear_dx(dx["cls"], W0, dfcat, rows=B)
+    df_syb, df_vis = _empty(B, d, dev=dev), _empty(B, d, dev=dev)
+    ops.linear_dx(dx["cls_syb"], Wh.h["cls_syb"][0], df_syb, rows=B, resid=dfcat, ldr=2 * d)
+    ops.linear_dx(dx["cls_vis"], Wh.h["cls_vis"][0], df_vis, rows=B, resid=dfcat[:, d:], ldr=2 * d)
+    return df_vis, df_syb
+
+
+# ----------------------------------------------------------------------------- model
+class ModelEngine:
+    """Binds arena views once; runs the whole-model forward / backward."""
+
+    def __init__(self, arena, num_blocks: int, hidden: int, heads: int):
+        self.arena = arena
+        self.nb, self.d, self.H = num_blocks, hidden, heads
+        self.rebind()
+
+    def rebind(self):
+        a = self.arena
+        self.vis = StackWeights(a, "att_vis_grid", self.nb, self.d)
+        self.syb = StackWeights(a, "att_syb", self.nb, self.d)
+        self.mil = MilWeights(a)
+        self.head = HeadWeights(a)
+        self._gbound = None
+
+    def grads(self):
+        g = self.arena.ensure_grads()
+        if self._gbound is not g:
+            a = self.arena
+            self.gvis = StackWeights(a, "att_vis_grid", self.nb, self.d, grad=True)
+            self.gsyb = StackWeights(a, "att_syb", self.nb, self.d, grad=True)
+            self.gmil = MilWeights(a, grad=True)
+            self.ghead = HeadWeights(a, grad=True)
+            self._gbound = g
+
+    def forward(self, inp: Dict[str, torch.Tensor], decMask: bool):
+        d, H = self.d, self.H
+        vis = inp["vis_fea"]
+        dev = vis.device
+        B, Nv, Dv = vis.shape
+        Lq = inp["q_ipt"].shape[1]
+        Ns = inp["macro_ipt"].shape[1]
+        Tv, Ts = Nv + Lq, Ns + Lq
+        mil_val = _empty((), dev=dev)
+        cat_syb = _empty(B * Ts, Dv, dev=dev)
+        ms = mil_forward(self.mil, vis, inp["macro_ipt"], inp["macro_obj_loc"],
+                         inp["micro_positive_obj"], inp["micro_negative_obj"],
+                         inp["micro_obj_mask"], cat_syb, Ts, mil_val)
+        cat_vis = _empty(B * Tv, Dv, dev=dev)
+        ops.copy_rows(vis.reshape(B * Nv, Dv), B * Nv, Dv, Dv, cat_vis, Dv, Nv, Tv, 0)
+        sv = stack_forward(self.vis, cat_vis, B, Nv, Lq, inp["q_ipt"], inp["vis_mask"],
+                           inp["q_mask"], inp["q_graph"], None, decMask, H, d)
+        ss = stack_forward(self.syb, cat_syb, B, Ns, Lq, inp["q_ipt"], inp["macro_mask"],
+                           inp["q_mask"], inp["q_graph"], inp["macro_graph"], decMask, H, d)
+        (lc, lv, ls), hs = heads_forward(self.head, sv.out, ss.out, d)
+        return (lc, lv, ls, mil_val), (ms, sv, ss, hs)
+
+    def backward(self, saved, dlc, dlv, dls, dmil):
+        self.grads()
+        ms, sv, ss, hs = saved
+        d, H = self.d, self.H
+        df_vis, df_syb = heads_backward(self.head, self.ghead, hs, dlc, dlv, dls, d)
+        stack_backward(self.vis, self.gvis, sv, df_vis, H, d, want_node_grad=False)
+        dnode = stack_backward(self.syb, self.gsyb, ss, df_syb, H, d, want_node_grad=True)
+        mil_backward(self.mil, self.gmil, ms, dnode, dmil)

@@ -74,13 +74,14 @@ def linear(X: Tensor, W: Tensor, b: Optional[Tensor], out: Tensor, *, relu=False
 
 
 def linear_dx(dY: Tensor, W: Tensor, dX: Tensor, *, rows: int, a_rows=None, mask=None,
-              ldmask=0, mask_arows=False, resid=None, c_rows=None, atomic=False, beta=0.0,
-              lddy=None, lddx=None):
+              ldmask=0, mask_arows=False, resid=None, ldr=None, c_rows=None, atomic=False,
+              beta=0.0, lddy=None, lddx=None):
     """dX = dY W  (mask: ReLU-backward gate of the producer of X; c_rows: scatter-add)."""
     N, K = W.shape  # dY has N cols, dX has K cols
     gemm(dY, W, dX, rows, K, N, lda=lddy if lddy is not None else N, ldb=K,
          ldc=lddx if lddx is not None else K, a_rows=a_rows, mask=mask, ldmask=ldmask,
-         mask_arows=mask_arows, resid=resid, ldr=K, c_rows=c_rows, atomic=atomic, beta=beta)
+         mask_arows=mask_arows, resid=resid, ldr=ldr if ldr is not None else K, c_rows=c_rows,
+         atomic=atomic, beta=beta)
 
 
 def _split_for(m_out: int, n_out: int, k: int) -> int:
@@ -190,6 +191,25 @@ def loss_fwd(lc, lv, ls, answer, B, Cc, eps, mil, with_mil, loss, dlogits, lsm, 
 
 def scale_by(inp, scale, n, out):
     call("savqa_scale_by", _stream(), _p(inp), _p(scale), int(n), _p(out))
+
+
+def rowscale_mask(inp, rowscale, mask, rows, cols, out):
+    call("savqa_rowscale_mask", _stream(), _p(inp), _p(rowscale), _p(mask), int(rows), int(cols),
+         _p(out))
+
+
+def affine(inp, n, a, b, out):
+    call("savqa_affine", _stream(), _p(inp), int(n), float(a), float(b), _p(out))
+
+
+def gather_rows(table, idx, rows, cols, scale, out):
+    call("savqa_gather_rows", _stream(), _p(table), _p(idx), int(rows), int(cols), float(scale),
+         _p(out))
+
+
+def scatter_rows(g, idx, rows, cols, scale, padding_idx, dtable):
+    call("savqa_scatter_rows", _stream(), _p(g), _p(idx), int(rows), int(cols), float(scale),
+         int(padding_idx), _p(dtable))
 
 
 def adam(p, g, m, v, n, lr, beta1, beta2, eps, bc1, bc2, grad_scale=1.0):

@@ -1,0 +1,48 @@
+"""Fused Adam over the flat parameter arena (torch.optim.Adam semantics, main:206/:366).
+
+One HIP launch updates every live parameter: the arena keeps them contiguous, and the
+gradient all-reduce's 1/world scaling is folded into the same pass (grad_scale).
+Parameters that never receive a gradient (the reference's Adam skips grad=None) lie
+outside the live range and are untouched.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+
+class Adam(torch.optim.Optimizer):
+    def __init__(self, model, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        if weight_decay != 0.0:
+            raise NotImplementedError("weight_decay (the reference uses none)")
+        arena = model._arena
+        params = [arena.params[n] for n in arena.live_names]
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0.0))
+        self.arena = arena
+        self.step_count = 0
+        self.m = None
+        self.v = None
+        self.grad_scale = 1.0
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        a = self.arena
+        g = a.grad
+        if g is None:
+            return loss
+        if self.m is None or self.m.device != a.flat.device:
+            self.m = torch.zeros(a.n_live, dtype=torch.float32, device=a.flat.device)
+            self.v = torch.zeros_like(self.m)
+        self.step_count += 1
+        grp = self.param_groups[0]
+        b1, b2 = grp["betas"]
+        t = self.step_count
+        ops.adam(a.flat[:a.n_live], g, self.m, self.v, a.n_live, grp["lr"], b1, b2, grp["eps"],
+                 1 - b1 ** t, 1 - b2 ** t, self.grad_scale)
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        # keep the arena views attached; zero the live gradient range in one memset
+        self.arena.zero_grad()

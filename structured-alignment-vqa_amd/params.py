@@ -1,0 +1,167 @@
+"""Flat parameter / gradient arena for AttModel.
+
+All 498 reference parameters (state_dict keys unchanged) become views into ONE flat
+fp32 buffer laid out MI355X-first:
+  * "live" parameters (those the reference's Adam updates in only_obj mode) come
+    first, in the order the backward pass FINISHES them, so the gradient all-reduce
+    can stream contiguous finished buckets while backward is still running;
+  * projections that the engine fuses are adjacent: per encoder layer [Wq;Wk;Wv]
+    as one [3d, d] matrix, per stack all 6 decoder cross-attention [Wk_i;Wv_i] as
+    one [12d, d] matrix (the 6 decoder layers read the same encoder output);
+  * "dead" parameters (never receive a gradient in the reference: v_mlp, input_proj,
+    q_mlp, the unused position tables, MIL_NCE.R / rel_mlp / bilinear / marco_mlp,
+    mcb sketches, cls_mcb) follow, so Adam and the all-reduce touch only
+    [0, n_live).
+Every parameter starts on a 64-float (256 B) boundary.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Dict, List, Tuple
+
+import torch
+import torch.nn as nn
+
+ALIGN = 64
+
+
+def _live_order(num_blocks: int) -> List[str]:
+    """Live parameter names in backward-completion order (see module docstring)."""
+    out: List[str] = []
+    for head in ("cls", "cls_vis", "cls_syb"):
+        out += [f"{head}.3.weight", f"{head}.3.bias", f"{head}.0.weight", f"{head}.0.bias"]
+    for pre in ("att_vis_grid", "att_syb"):
+        for i in reversed(range(num_blocks)):
+            f = f"{pre}.dec_feed_forward_{i}"
+            out += [f"{f}.normalization.gamma", f"{f}.normalization.beta", f"{f}.conv2.weight",
+                    f"{f}.conv2.bias", f"{f}.conv1.0.weight", f"{f}.conv1.0.bias"]
+            c = f"{pre}.dec_vanilla_attention_{i}"
+            out += [f"{c}.normalization.gamma", f"{c}.normalization.beta", f"{c}.Q_proj.0.weight",
+                    f"{c}.Q_proj.0.bias"]
+            s = f"{pre}.dec_self_attention_{i}"
+            out += [f"{s}.normalization.gamma", f"{s}.normalization.beta", f"{s}.V_proj.0.weight",
+                    f"{s}.V_proj.0.bias", f"{s}.Q_proj.0.weight", f"{s}.Q_proj.0.bias",
+                    f"{s}.K_proj.0.weight", f"{s}.K_proj.0.bias"]
+        out += [f"{pre}.dec_emb.lookup_table", f"{pre}.dec_positional_encoding.lookup_table"]
+        # fused decoder cross-attention K/V of all layers: weights then biases
+        for i in range(num_blocks):
+            c = f"{pre}.dec_vanilla_attention_{i}"
+            out += [f"{c}.K_proj.0.weight", f"{c}.V_proj.0.weight"]
+        for i in range(num_blocks):
+            c = f"{pre}.dec_vanilla_attention_{i}"
+            out += [f"{c}.K_proj.0.bias", f"{c}.V_proj.0.bias"]
+        for i in reversed(range(num_blocks)):
+            f = f"{pre}.enc_feed_forward_{i}"
+            out += [f"{f}.normalization.gamma", f"{f}.normalization.beta", f"{f}.conv2.weight",
+                    f"{f}.conv2.bias", f"{f}.conv1.0.weight", f"{f}.conv1.0.bias"]
+            a = f"{pre}.enc_self_attention_{i}"
+            out += [f"{a}.normalization.gamma", f"{a}.normalization.beta",
+                    f"{a}.Q_proj.0.weight", f"{a}.K_proj.0.weight", f"{a}.V_proj.0.weight",
+                    f"{a}.Q_proj.0.bias", f"{a}.K_proj.0.bias", f"{a}.V_proj.0.bias"]
+        pos = (f"{pre}.syb_positional_encoding.0.lookup_table" if pre == "att_vis_grid"
+               else f"{pre}.syb_positional_encoding.lookup_table")
+        out += [pos, f"{pre}.syb_mlp2.weight", f"{pre}.syb_mlp2.bias", f"{pre}.syb_mlp.0.weight",
+                f"{pre}.syb_mlp.0.bias", f"{pre}.syb_emb.weight"]
+    m = "MIL_NCE"
+    out += [f"{m}.ipt_mlp.0.weight", f"{m}.ipt_mlp.0.bias", f"{m}.syb_mlp.0.weight",
+            f"{m}.syb_mlp.0.bias", f"{m}.vis_mlp.0.weight", f"{m}.vis_mlp.0.bias",
+            f"{m}.syb_emb.weight"]
+    return out
+
+
+class ParamArena:
+    """Owns the flat parameter and gradient buffers of an AttModel."""
+
+    def __init__(self, model: nn.Module, num_blocks: int, device=None):
+        named = OrderedDict(model.named_parameters())
+        live = [n for n in _live_order(num_blocks) if n in named]
+        missing = set(_live_order(num_blocks)) - set(named)
+        if missing:
+            raise RuntimeError(f"ParamArena: model lacks live params {sorted(missing)[:4]}")
+        dead = [n for n in named if n not in set(live)]
+        self.order = live + dead
+        self.offsets: Dict[str, Tuple[int, torch.Size]] = {}
+        off = 0
+        for n in self.order:
+            self.offsets[n] = (off, named[n].shape)
+            off += (named[n].numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.total = off
+        self.n_live = self.offsets[dead[0]][0] if dead else off
+        self.live_names = live
+        self.params = named
+        dev = device if device is not None else next(iter(named.values())).device
+        flat = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.flat = flat
+        self.grad = None  # allocated on first backward (device of flat)
+        if flat.device.type == "meta":  # layout-only arena (host-side tests)
+            return
+        with torch.no_grad():
+            for n in self.order:
+                o, shp = self.offsets[n]
+                flat[o:o + named[n].numel()].copy_(named[n].detach().reshape(-1))
+        self._bind()
+
+    # ------------------------------------------------------------------ views
+    def view(self, name: str, buf=None) -> torch.Tensor:
+        o, shp = self.offsets[name]
+        b = self.flat if buf is None else buf
+        n = 1
+        for s in shp:
+            n *= s
+        return b[o:o + n].view(shp)
+
+    def span(self, first: str, last: str, shape, buf=None) -> torch.Tensor:
+        """View over the contiguous range first..last (must be adjacent in the arena)."""
+        o0, _ = self.offsets[first]
+        o1, s1 = self.offsets[last]
+        n = 1
+        for s in shape:
+            n *= s
+        if o0 + n != o1 + int(torch.Size(s1).numel()):
+            raise RuntimeError(f"ParamArena.span: {first}..{last} is not contiguous")
+        b = self.flat if buf is None else buf
+        return b[o0:o0 + n].view(shape)
+
+    def _bind(self):
+        for n, p in self.params.items():
+            p.data = self.view(n)
+
+    def apply(self, fn):
+        new = fn(self.flat)
+        if new.dtype != torch.float32:
+            raise RuntimeError("savqa AttModel parameters are fp32 (flat arena); dtype casts unsupported")
+        self.flat = new
+        if self.grad is not None and self.grad.device != new.device:
+            self.grad = None
+        self._bind()
+        for n in self.live_names:
+            self.params[n].grad = None
+
+    # ------------------------------------------------------------------ grads
+    def ensure_grads(self):
+        """Attach .grad views of the flat gradient buffer to every live parameter.
+
+        If a caller reset grads to None (torch's default zero_grad), the live range is
+        zeroed and re-attached, so accumulation semantics match autograd's."""
+        if self.grad is None or self.grad.device != self.flat.device:
+            self.grad = torch.zeros(self.n_live, dtype=torch.float32, device=self.flat.device)
+            reattach = True
+        else:
+            p0 = self.params[self.live_names[0]]
+            reattach = p0.grad is None or p0.grad.data_ptr() != self.grad.data_ptr() + \
+                self.offsets[self.live_names[0]][0] * 4
+        if reattach:
+            self.grad.zero_()
+            for n in self.live_names:
+                self.params[n].grad = self.view(n, self.grad)
+        return self.grad
+
+    def gview(self, name: str) -> torch.Tensor:
+        return self.view(name, self.grad)
+
+    def gspan(self, first: str, last: str, shape) -> torch.Tensor:
+        return self.span(first, last, shape, self.grad)
+
+    def zero_grad(self):
+        if self.grad is not None:
+            self.grad.zero_()

@@ -1,0 +1,102 @@
+"""End-to-end parity of savqa_amd.AttModel (HIP path, via libsavqa) against the
+reference's golden vectors (tests/golden/full_*.npz, produced by running the reference
+itself) and the CPU oracle: logits, MIL-NCE term, loss, gradients of every trained
+parameter, and logits after two Adam steps.
+
+Tolerances (north star): fp32 outputs within 1e-3 relative, answer argmax exact.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import hashfill
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+INPUTS = ("vis_fea", "vis_mask", "q_ipt", "q_mask", "q_graph", "macro_ipt", "macro_mask",
+          "macro_graph", "macro_obj_loc", "micro_positive_obj", "micro_negative_obj",
+          "micro_obj_mask")
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def model():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from savqa_amd.AttModel_x3 import AttModel
+    m = AttModel(None, 512, 1024, 914, 40, 450, 49, 6, 8, 0.0, 0.0, 4, True, device="cuda",
+                 init=False)
+    m.train()
+    return m
+
+
+def load_hash(m):
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            p.copy_(torch.from_numpy(hashfill.param_value(n, tuple(p.shape))))
+
+
+def run(m, t, decMask):
+    empty = torch.empty((t["vis_fea"].shape[0], 0), device="cuda")
+    return m(*[t[k] for k in INPUTS], empty, empty, empty, empty, decMask=decMask, mcb=False)
+
+
+@pytest.mark.parametrize("case", ["full_b4", "full_b2_nodec"])
+def test_full_model_against_reference_golden(model, case):
+    from savqa_amd.loss import smoothed_loss
+    from savqa_amd.optim import Adam
+    g = np.load(os.path.join(GOLD, f"{case}.npz"))
+    load_hash(model)
+    t = {k: torch.from_numpy(g[k]).cuda() for k in INPUTS + ("answer",)}
+    dec = bool(g["decMask"])
+    lc, lv, ls, mil, rel0 = run(model, t, dec)
+    assert rel0 == 0
+    for name, out in (("logits_concat", lc), ("logits_vis", lv), ("logits_syb", ls)):
+        o = out.detach().cpu().numpy()
+        assert rel(o, g[name]) < 1e-3, name
+        assert (o.argmax(-1) == g[name].argmax(-1)).all(), name
+    assert abs(float(mil) - float(g["mil_nce_obj"])) < 1e-3 * max(1.0, abs(float(g["mil_nce_obj"])))
+    loss, lsm = smoothed_loss(lc, lv, ls, t["answer"], mil, with_milnce=True)
+    assert abs(float(loss) - float(g["loss"])) < 1e-4 * abs(float(g["loss"]))
+    opt = Adam(model, lr=1e-4)
+    opt.zero_grad()
+    loss.backward()
+    names = [str(n) for n in g["grad_names"]]
+    params = dict(model.named_parameters())
+    worst = []
+    for n in names:
+        gr = params[n].grad
+        assert gr is not None, n
+        flat = gr.reshape(-1).cpu().double().numpy()
+        ref = g[f"g:{n}:val"].astype(np.float64)
+        idx = g[f"g:{n}:idx"]
+        scale = max(np.abs(ref).max(), float(g[f"g:{n}:abssum"]) / flat.size, 1e-20)
+        err = np.abs(flat[idx] - ref).max() / scale
+        worst.append((err, n))
+        asum = float(g[f"g:{n}:abssum"])
+        assert abs(flat.sum() - float(g[f"g:{n}:sum"])) <= 1e-3 * max(asum, 1e-12) + 1e-9, n
+        if f"g:{n}:rows" in g.files:
+            rows = torch.from_numpy(g[f"g:{n}:rows"]).cuda()
+            rv = gr[rows].cpu().numpy()
+            assert rel(rv, g[f"g:{n}:rowval"]) < 1e-3, n
+    worst.sort(reverse=True)
+    assert worst[0][0] < 1e-3, worst[:5]
+    # two Adam steps, logits after each (same sequence as tools/make_golden.py)
+    opt.step()
+    for s in (1, 2):
+        lc, lv, ls, mil, _ = run(model, t, dec)
+        o = lc.detach().cpu().numpy()
+        assert rel(o, g[f"step{s}_logits_concat"]) < 1e-3, s
+        assert (o.argmax(-1) == g[f"step{s}_logits_concat"].argmax(-1)).all()
+        if s == 1:
+            loss, _ = smoothed_loss(lc, lv, ls, t["answer"], mil)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
