@@ -1,0 +1,215 @@
+#!/usr/bin/env python
+"""Throughput of the SA-VQA model_v=3 training step on MI355X (BASELINE.json metric).
+
+A step = forward + label-smoothed loss (+ MIL-NCE) + backward + Adam over one synthetic
+batch already resident in HBM (cfg 2: fp32, 256 samples/GPU, 36 regions x 2048-d,
+14-token questions, 59 scene-graph nodes, d=512, 8 heads, 6+6 layers per stack).
+N GPUs = one process per GPU (torch.distributed.run), weak scaling, RCCL all-reduce of
+the live gradients streamed out of the backward (savqa_amd.ddp).
+
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (fp32 MFMA
+GEMM, HIP-event timed) and the CPU oracle's throughput on the host as cpu_baseline.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "QA-samples/sec training (model_v=3, 36 regions × 2048-d) at 1/2/4/8 MI355X"
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec peak
+HBM_PEAK_GBS = 8000.0
+
+
+def train_flops_per_sample(Tv=50, Ts=73, Lq=14, Nv=36, Ns=59, d=512, L=6, C=914, Hm=1024, K=5):
+    """SURVEY.md 8(d) algorithmic count (fwd x 3)."""
+    def stack(T):
+        return (L * (22 * T * d * d + 4 * T * T * d) + L * (24 * d * d + 4 * T * d * d + 4 * T * d)
+                + 2 * Lq * 300 * 2048 + 2 * T * 2048 * d)
+    heads = 2 * (2 * d * d + d * C) + 4 * (d * d + d * C)
+    mil = 2 * Ns * 300 * Hm + 4 * Nv * K * 300 * Hm + 2 * Nv * 2048 * Hm + 6 * Nv * K * Hm \
+        + 2 * Ns * Hm * 2048
+    return 3.0 * (stack(Tv) + stack(Ts) + heads + mil)
+
+
+def cpu_baseline(seconds=15.0, B=4):
+    """Time the CPU oracle (oracle/savqa_oracle.py, the parity checker) on the host:
+    fwd + loss + bwd + Adam at the cfg-1 shape (B=4). Bounded sample."""
+    from oracle import hashfill
+    from oracle import savqa_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    gen = torch.Generator().manual_seed(0)
+    Nv, Lq, Ns, K = 36, 14, 59, 5
+    inp = {
+        "vis_fea": torch.randn(B, Nv, 2048, generator=gen).clamp_min(0),
+        "vis_mask": torch.ones(B, Nv, Nv, dtype=torch.int32),
+        "q_ipt": torch.randint(0, 400000, (B, Lq), generator=gen),
+        "q_mask": torch.ones(B, Lq, Lq, dtype=torch.int32),
+        "q_graph": (torch.rand(B, Lq, Lq, generator=gen) < 0.2).int(),
+        "macro_ipt": torch.randint(0, 400000, (B, Ns), generator=gen),
+        "macro_mask": torch.ones(B, Ns, Ns, dtype=torch.int32),
+        "macro_graph": (torch.rand(B, Ns, Ns, generator=gen) < 0.05).int(),
+        "macro_obj_loc": torch.arange(Nv).repeat(B, 1),
+        "micro_positive_obj": torch.randint(0, 400000, (B, Nv, K), generator=gen),
+        "micro_negative_obj": torch.randint(0, 400000, (B, Nv, K), generator=gen),
+        "micro_obj_mask": torch.ones(B, Nv, K, dtype=torch.int32),
+    }
+    answer = torch.randint(1, 914, (B,), generator=gen)
+    P = hashfill.HashParams(requires_grad=True)
+    state = {}
+
+    def step(i):
+        for p in P.values():
+            p.grad = None
+        lc, lv, ls, mil, _ = O.attmodel_forward(P, inp)
+        loss, _ = O.train_loss(lc, lv, ls, answer, mil)
+        loss.backward()
+        with torch.no_grad():
+            O.adam_step(P, {k: v.grad for k, v in P.items() if v.grad is not None}, state, i + 1)
+
+    step(0)  # materialise the lazily hash-filled parameters (setup, untimed)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step(n + 1)
+        n += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(B * n / dt, 3), "unit": "QA-samples/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle/savqa_oracle.py train step (fwd+loss+bwd+Adam), cfg-1 shape "
+                      f"B={B}, {n} steps in {dt:.1f}s, torch CPU {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="samples per GPU (cfg 2: 256)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import savqa_amd  # noqa: F401
+    from savqa_amd import ops
+    from savqa_amd.AttModel_x3 import AttModel
+    from savqa_amd.data import model_args, synthetic_batch
+    from savqa_amd.ddp import GradReducer
+    from savqa_amd.loss import smoothed_loss
+    from savqa_amd.optim import Adam
+    from savqa_amd.utils import init_params_
+
+    B = args.batch
+    model = AttModel(None, 512, 1024, 914, 40, 450, 49, 6, 8, 0.0, 0.0, 311, True, device=dev,
+                     init=False)
+    init_params_(model, seed=0)  # identical on every rank (same seed), like a broadcast
+    model.train()
+    opt = Adam(model, lr=1e-4)
+    reducer = GradReducer(model._arena) if world > 1 else None
+    if reducer:
+        model.attach_reducer(reducer)
+    batch = synthetic_batch(B, seed=1234 + rank, device=dev)
+    margs = model_args(batch)
+
+    def step():
+        if reducer:
+            reducer.begin()
+        lc, lv, ls, mil, _ = model(*margs, decMask=True, mcb=False)
+        loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil, with_milnce=True)
+        opt.zero_grad()
+        loss.backward()
+        if reducer:
+            opt.grad_scale = reducer.finish()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    final_loss = float(loss)
+
+    value = world * B * args.steps / elapsed
+    ms_step = elapsed / args.steps * 1e3
+    fl = train_flops_per_sample()
+
+    roof = None
+    if not args.no_roofline:
+        probe = ops.GemmProbe()
+        ops.set_gemm_probe(probe)
+        for _ in range(2):
+            step()
+        ops.set_gemm_probe(None)
+        agg = probe.summary()
+        var, (n, flops, ms) = max(agg.items(), key=lambda kv: kv[1][2])
+        achieved = (flops / n) / (ms / n * 1e-3) / 1e12
+        allfl = sum(v[1] for v in agg.values())
+        allms = sum(v[2] for v in agg.values())
+        roof = {"bound": "mfma", "kernel": var, "launches_per_step": n // 2,
+                "avg_launch_us": round(ms / n * 1e3, 2), "flops_per_launch": flops / n,
+                "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "all_gemm_tflops": round(allfl / (allms * 1e-3) / 1e12, 2),
+                "gemm_ms_per_step": round(allms / 2, 2)}
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_seconds)
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "QA-samples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (collate_fn tensor contract; random-init weights)",
+            "config": {"workload": "cfg2: model_v=3 train step (fwd+loss+bwd+Adam), fp32, "
+                                   "36 regions x 2048-d, 14 q-tokens, 59 nodes, d=512 h=8 L=6, "
+                                   "MIL-NCE only_obj topN=5 H=1024, 914 classes, decMask, "
+                                   "dropout 0",
+                       "per_gpu_batch": B, "global_batch": world * B,
+                       "parallelism": f"dp{world}"},
+            "model_tflops": round(value * fl / 1e12, 2),
+            "model_mfma_frac": round(value * fl / 1e12 / (FP32_MFMA_PEAK_TFLOPS * world), 4),
+            "loss": round(final_loss, 4),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

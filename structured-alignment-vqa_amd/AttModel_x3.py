@@ -201,8 +201,9 @@ class _AttModelFn(torch.autograd.Function):
 
         B = ctx.saved[1].B
         Cc = model.num_classes
+        red = model.__dict__.get("_reducer")
         model._engine.backward(ctx.saved, z(dlc, (B, Cc)), z(dlv, (B, Cc)), z(dls, (B, Cc)),
-                               z(dmil, ()))
+                               z(dmil, ()), on_region=red.region_done if red else None)
         ctx.saved = None
         return (None, None, None) + (None,) * len(_INPUT_NAMES)
 
@@ -251,6 +252,10 @@ class AttModel(nn.Module):
         object.__setattr__(self, "_arena", ParamArena(self, num_blocks, device=device))
         object.__setattr__(self, "_engine", ModelEngine(self._arena, num_blocks, hidden_size,
                                                         num_heads))
+
+    def attach_reducer(self, reducer):
+        """Stream the data-parallel gradient all-reduce out of the backward (ddp.GradReducer)."""
+        object.__setattr__(self, "_reducer", reducer)
 
     # parameters live in the arena: moving the module moves the arena
     def _apply(self, fn, recurse=True):

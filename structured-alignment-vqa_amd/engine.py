@@ -467,11 +467,29 @@ class ModelEngine:
         (lc, lv, ls), hs = heads_forward(self.head, sv.out, ss.out, d)
         return (lc, lv, ls, mil_val), (ms, sv, ss, hs)
 
-    def backward(self, saved, dlc, dlv, dls, dmil):
+    def region_bounds(self):
+        """Arena offsets at which the gradients of heads / vis stack / syb stack end."""
+        a, nb = self.arena, self.nb
+        return (a.offsets[f"att_vis_grid.dec_feed_forward_{nb - 1}.normalization.gamma"][0],
+                a.offsets[f"att_syb.dec_feed_forward_{nb - 1}.normalization.gamma"][0],
+                a.offsets["MIL_NCE.ipt_mlp.0.weight"][0])
+
+    def backward(self, saved, dlc, dlv, dls, dmil, on_region=None):
+        """Whole-model backward. on_region(n) is called whenever gradient elements
+        [0, n) of the arena are final (used to start the all-reduce early)."""
         self.grads()
         ms, sv, ss, hs = saved
         d, H = self.d, self.H
+        b_heads, b_vis, b_syb = self.region_bounds()
         df_vis, df_syb = heads_backward(self.head, self.ghead, hs, dlc, dlv, dls, d)
+        if on_region:
+            on_region(b_heads)
         stack_backward(self.vis, self.gvis, sv, df_vis, H, d, want_node_grad=False)
+        if on_region:
+            on_region(b_vis)
         dnode = stack_backward(self.syb, self.gsyb, ss, df_syb, H, d, want_node_grad=True)
+        if on_region:
+            on_region(b_syb)
         mil_backward(self.mil, self.gmil, ms, dnode, dmil)
+        if on_region:
+            on_region(self.arena.n_live)

@@ -36,6 +36,39 @@ def _f32(t: Optional[Tensor], name: str):
 
 
 # ------------------------------------------------------------------------------ GEMM
+class GemmProbe:
+    """Optional per-launch timing of savqa_gemm with HIP events on the launch stream
+    (bench.py's roofline measurement). Off unless a probe is installed."""
+
+    def __init__(self):
+        self.records = []  # (variant, flops, start_event, end_event)
+
+    @staticmethod
+    def variant(M, N, a_trans, b_trans, split):
+        big = ((M + 127) // 128) * ((N + 127) // 128) * split >= 192
+        tile = 128 if big else 64
+        return f"gemm_f32_kernel<{tile},{tile},{str(bool(a_trans)).lower()},{str(bool(b_trans)).lower()}>"
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for var, fl, e0, e1 in self.records:
+            ms = e0.elapsed_time(e1)
+            a = agg.setdefault(var, [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += fl
+            a[2] += ms
+        return agg
+
+
+_probe = None
+
+
+def set_gemm_probe(probe):
+    global _probe
+    _probe = probe
+
+
 def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
          ldc: int, a_trans=False, b_trans=False, a_rows=None, b_rows=None, c_rows=None,
          c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None, ldrv=0, rowvec_period=0,
@@ -58,7 +91,16 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
     d.rowscale = _p(rowscale)
     d.alpha, d.beta = float(alpha), float(beta)
     d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
+    if _probe is None:
+        call("savqa_gemm", _stream(), C.byref(d))
+        return
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
     call("savqa_gemm", _stream(), C.byref(d))
+    e1.record()
+    _probe.records.append((GemmProbe.variant(M, N, a_trans, b_trans, max(1, split_k)),
+                           2.0 * M * N * K, e0, e1))
 
 
 def linear(X: Tensor, W: Tensor, b: Optional[Tensor], out: Tensor, *, relu=False,
