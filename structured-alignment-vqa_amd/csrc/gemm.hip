@@ -32,17 +32,51 @@ struct TileLoader {
   static constexpr int LD = KCONTIG ? BM + 1 : BM + 4;
   static constexpr int ITERS = BM * GEMM_BK / 4 / GEMM_NT;  // float4 per thread
   float4 r[ITERS];
+  const float* rp[ITERS];  // FAST + KCONTIG: row pointers, resolved once per block
 
-  // rows (optional) gathers the operand's stored rows: m for KCONTIG, k otherwise.
-  __device__ __forceinline__ void load(const float* __restrict__ base, int64_t ld,
-                                       const int64_t* __restrict__ rows, int64_t mlim,
-                                       int64_t m0, int64_t k0, int64_t kend, bool vec, int tid) {
+  // FAST path (block-uniform): the whole tile is in range, the k range is a multiple of
+  // GEMM_BK and the operand is 16-B aligned -> branch-free float4 loads.
+  __device__ __forceinline__ void setup_fast(const float* __restrict__ base, int64_t ld,
+                                             const int64_t* __restrict__ rows, int64_t m0,
+                                             int tid) {
+    if (KCONTIG) {
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int idx = tid + it * GEMM_NT;
+        const int64_t m = m0 + (idx >> 3);
+        const int64_t rr = rows ? rows[m] : m;
+        rp[it] = base + rr * ld + (idx & 7) * 4;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load_fast(const float* __restrict__ base, int64_t ld,
+                                            int64_t m0, int64_t k0, int tid) {
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int idx = tid + it * GEMM_NT;
+      if (KCONTIG) {
+        r[it] = *reinterpret_cast<const float4*>(rp[it] + k0);
+      } else {
+        constexpr int PER_K = BM / 4;
+        const int kr = idx / PER_K;
+        const int mq = (idx % PER_K) * 4;
+        r[it] = *reinterpret_cast<const float4*>(base + (k0 + kr) * ld + m0 + mq);
+      }
+    }
+  }
+
+  // guarded path for edge tiles, k tails, unaligned operands and k-row gathers
+  __device__ __forceinline__ void load_slow(const float* __restrict__ base, int64_t ld,
+                                            const int64_t* __restrict__ rows, int64_t mlim,
+                                            int64_t m0, int64_t k0, int64_t kend, bool vec,
+                                            int tid) {
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
       const int idx = tid + it * GEMM_NT;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (KCONTIG) {
-        const int row = idx >> 3;          // BK/4 = 8 float4 per row
+        const int row = idx >> 3;
         const int kq = (idx & 7) * 4;
         const int64_t m = m0 + row;
         const int64_t k = k0 + kq;
@@ -103,20 +137,91 @@ struct TileLoader {
 };
 
 template <int BM, int BN, bool AT, bool BT>
-__global__ __launch_bounds__(GEMM_NT, 2) void gemm_f32_kernel(savqa_gemm_desc d, int tiles_m,
-                                                             int tiles_n, int64_t kchunk,
-                                                             int avec, int bvec) {
+struct GemmTile {
   using LA = TileLoader<BM, !AT>;
   using LB = TileLoader<BN, BT>;
-  constexpr int SA = GEMM_BK * LA::LD;
-  constexpr int SB = GEMM_BK * LB::LD;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (SA + SB)];
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int FM = WM / 32, FN = WN / 32;
+  static constexpr int SA = GEMM_BK * LA::LD;
+  static constexpr int SB = GEMM_BK * LB::LD;
+  static constexpr int WM = BM / 2, WN = BN / 2;
+  static constexpr int FM = WM / 32, FN = WN / 32;
+};
 
+template <int BM, int BN, bool AT, bool BT, bool FAST>
+__device__ __forceinline__ void gemm_mainloop(const savqa_gemm_desc& d, float* smem, int64_t m0,
+                                              int64_t n0, int64_t kbeg, int64_t kend, bool avec,
+                                              bool bvec,
+                                              f32x16 (&acc)[GemmTile<BM, BN, AT, BT>::FM]
+                                                           [GemmTile<BM, BN, AT, BT>::FN]) {
+  using GT = GemmTile<BM, BN, AT, BT>;
+  typename GT::LA la;
+  typename GT::LB lb;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntiles = kend > kbeg ? (int)((kend - kbeg + GEMM_BK - 1) / GEMM_BK) : 0;
+  if (ntiles == 0) return;
+  if (FAST) {
+    la.setup_fast(d.A, d.lda, d.a_rows, m0, tid);
+    lb.setup_fast(d.B, d.ldb, d.b_rows, n0, tid);
+    la.load_fast(d.A, d.lda, m0, kbeg, tid);
+    lb.load_fast(d.B, d.ldb, n0, kbeg, tid);
+  } else {
+    la.load_slow(d.A, d.lda, d.a_rows, d.M, m0, kbeg, kend, avec, tid);
+    lb.load_slow(d.B, d.ldb, d.b_rows, d.N, n0, kbeg, kend, bvec, tid);
+  }
+  la.store(smem, tid);
+  lb.store(smem + 2 * GT::SA, tid);
+  __syncthreads();
+
+  int cur = 0;
+  const int kl = lane >> 5;
+  const int il = lane & 31;
+  for (int tt = 0; tt < ntiles; ++tt) {
+    const bool more = tt + 1 < ntiles;
+    if (more) {
+      const int64_t kn = kbeg + (int64_t)(tt + 1) * GEMM_BK;
+      if (FAST) {
+        la.load_fast(d.A, d.lda, m0, kn, tid);
+        lb.load_fast(d.B, d.ldb, n0, kn, tid);
+      } else {
+        la.load_slow(d.A, d.lda, d.a_rows, d.M, m0, kn, kend, avec, tid);
+        lb.load_slow(d.B, d.ldb, d.b_rows, d.N, n0, kn, kend, bvec, tid);
+      }
+    }
+    const float* As = smem + cur * GT::SA + kl * GT::LA::LD + wm * GT::WM + il;
+    const float* Bs = smem + 2 * GT::SA + cur * GT::SB + kl * GT::LB::LD + wn * GT::WN + il;
+#pragma unroll
+    for (int kk = 0; kk < GEMM_BK; kk += 2) {
+      float a[GT::FM], b[GT::FN];
+#pragma unroll
+      for (int i = 0; i < GT::FM; ++i) a[i] = As[kk * GT::LA::LD + i * 32];
+#pragma unroll
+      for (int j = 0; j < GT::FN; ++j) b[j] = Bs[kk * GT::LB::LD + j * 32];
+#pragma unroll
+      for (int i = 0; i < GT::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < GT::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      la.store(smem + (cur ^ 1) * GT::SA, tid);
+      lb.store(smem + 2 * GT::SA + (cur ^ 1) * GT::SB, tid);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+
+template <int BM, int BN, bool AT, bool BT>
+__global__ __launch_bounds__(GEMM_NT, 2) void gemm_f32_kernel(savqa_gemm_desc d, int tiles_m,
+                                                             int tiles_n, int64_t kchunk,
+                                                             int avec, int bvec) {
+  using GT = GemmTile<BM, BN, AT, BT>;
+  constexpr int FM = GT::FM, FN = GT::FN, WM = GT::WM, WN = GT::WN;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (GT::SA + GT::SB)];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
 
   const int nblk = tiles_m * tiles_n;
@@ -128,8 +233,6 @@ __global__ __launch_bounds__(GEMM_NT, 2) void gemm_f32_kernel(savqa_gemm_desc d,
   const int64_t kbeg = (int64_t)blockIdx.y * kchunk;
   const int64_t kend = min(d.K, kbeg + kchunk);
 
-  LA la;
-  LB lb;
   f32x16 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -138,75 +241,54 @@ __global__ __launch_bounds__(GEMM_NT, 2) void gemm_f32_kernel(savqa_gemm_desc d,
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int ntiles = kend > kbeg ? (int)((kend - kbeg + GEMM_BK - 1) / GEMM_BK) : 0;
-  if (ntiles > 0) {
-    la.load(d.A, d.lda, d.a_rows, d.M, m0, kbeg, kend, avec, tid);
-    lb.load(d.B, d.ldb, d.b_rows, d.N, n0, kbeg, kend, bvec, tid);
-    la.store(smem, tid);
-    lb.store(smem + 2 * SA, tid);
-  }
-  __syncthreads();
-
-  int cur = 0;
-  for (int tt = 0; tt < ntiles; ++tt) {
-    const bool more = tt + 1 < ntiles;
-    if (more) {
-      const int64_t kn = kbeg + (int64_t)(tt + 1) * GEMM_BK;
-      la.load(d.A, d.lda, d.a_rows, d.M, m0, kn, kend, avec, tid);
-      lb.load(d.B, d.ldb, d.b_rows, d.N, n0, kn, kend, bvec, tid);
-    }
-    const float* As = smem + cur * SA;
-    const float* Bs = smem + 2 * SA + cur * SB;
-    const int kl = lane >> 5;
-    const int il = lane & 31;
-#pragma unroll
-    for (int kk = 0; kk < GEMM_BK; kk += 2) {
-      float a[FM], b[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = As[(kk + kl) * LA::LD + wm * WM + i * 32 + il];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = Bs[(kk + kl) * LB::LD + wn * WN + j * 32 + il];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-    if (more) {
-      la.store(smem + (cur ^ 1) * SA, tid);
-      lb.store(smem + 2 * SA + (cur ^ 1) * SB, tid);
-    }
-    __syncthreads();
-    cur ^= 1;
-  }
+  // block-uniform choice of the branch-free main loop
+  const bool a_kgather = AT && d.a_rows;
+  const bool b_kgather = !BT && d.b_rows;
+  const bool fast = (m0 + BM <= d.M) && (n0 + BN <= d.N) && ((kend - kbeg) % GEMM_BK == 0) &&
+                    avec && bvec && !a_kgather && !b_kgather;
+  if (fast)
+    gemm_mainloop<BM, BN, AT, BT, true>(d, smem, m0, n0, kbeg, kend, avec, bvec, acc);
+  else
+    gemm_mainloop<BM, BN, AT, BT, false>(d, smem, m0, n0, kbeg, kend, avec, bvec, acc);
 
   // ---------------------------------------------------------------- epilogue
   const bool first_split = blockIdx.y == 0;
   const bool atomic = d.atomic || gridDim.y > 1;
+  const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
+  const uint32_t cg = (uint32_t)d.c_group;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int64_t n = n0 + wn * WN + j * 32 + (lane & 31);
-      if (n >= d.N) continue;
-      float bias_n = 0.f;
-      if (d.bias && first_split) bias_n = d.bias[n];
+    for (int r = 0; r < 16; ++r) {
+      const int64_t m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (m >= d.M) continue;
+      int64_t cr;
+      if (ident) {
+        cr = m;
+      } else if (d.c_rows) {
+        cr = d.c_rows[m];
+      } else {
+        const uint32_t mu = (uint32_t)m;
+        cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
+      }
+      float* crow = d.C + cr * d.ldc;
+      const float rs = d.rowscale ? d.rowscale[m] : 1.f;
+      const int64_t mr = d.mask_arows ? d.a_rows[m] : m;
+      const int64_t pr = d.rowvec ? (int64_t)((uint32_t)m % (uint32_t)d.rowvec_period) : 0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m >= d.M) continue;
-        float v = acc[i][j][r] * d.alpha + bias_n;
-        if (first_split && d.rowvec) v += d.rowvec[(m % d.rowvec_period) * d.ldrv + n];
-        if (d.relu) v = fmaxf(v, 0.f);
-        if (d.rowscale) v *= d.rowscale[m];
-        if (d.mask) {
-          const int64_t mr = d.mask_arows ? d.a_rows[m] : m;
-          if (!(d.mask[mr * d.ldmask + n] > 0.f)) v = 0.f;
+      for (int j = 0; j < FN; ++j) {
+        const int64_t n = n0 + wn * WN + j * 32 + (lane & 31);
+        if (n >= d.N) continue;
+        float v = acc[i][j][r] * d.alpha;
+        if (first_split) {
+          if (d.bias) v += d.bias[n];
+          if (d.rowvec) v += d.rowvec[pr * d.ldrv + n];
         }
+        if (d.relu) v = fmaxf(v, 0.f);
+        v *= rs;
+        if (d.mask && !(d.mask[mr * d.ldmask + n] > 0.f)) v = 0.f;
         if (first_split && d.resid) v += d.resid[m * d.ldr + n];
-        const int64_t cr = d.c_rows ? d.c_rows[m]
-                                    : (m / d.c_group) * d.c_stride + (m % d.c_group) + d.c_offset;
-        float* cp = d.C + cr * d.ldc + n;
+        float* cp = crow + n;
         if (atomic) {
           atomicAdd(cp, v);
         } else if (d.beta != 0.f) {
@@ -259,8 +341,9 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   const int avec = (d.lda % 4 == 0) && aligned16(d.A);
   const int bvec = (d.ldb % 4 == 0) && aligned16(d.B);
   hipStream_t s = as_stream(stream);
+  // 128x128 tiles once there is enough parallelism (split-K counts), else 64x64
   const int64_t big_tiles = ((d.M + 127) / 128) * ((d.N + 127) / 128) * split;
-  if (big_tiles >= 192)
+  if (big_tiles >= 160)
     dispatch_layout<128, 128>(d, s, split, avec, bvec);
   else
     dispatch_layout<64, 64>(d, s, split, avec, bvec);

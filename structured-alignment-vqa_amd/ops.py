@@ -45,7 +45,7 @@ class GemmProbe:
 
     @staticmethod
     def variant(M, N, a_trans, b_trans, split):
-        big = ((M + 127) // 128) * ((N + 127) // 128) * split >= 192
+        big = ((M + 127) // 128) * ((N + 127) // 128) * split >= 160
         tile = 128 if big else 64
         return f"gemm_f32_kernel<{tile},{tile},{str(bool(a_trans)).lower()},{str(bool(b_trans)).lower()}>"
 
@@ -127,12 +127,10 @@ def linear_dx(dY: Tensor, W: Tensor, dX: Tensor, *, rows: int, a_rows=None, mask
 
 
 def _split_for(m_out: int, n_out: int, k: int) -> int:
+    """split-K factor for the dW GEMMs (reduction over all B*T rows): enough 128x128
+    tiles x splits to give every CU ~2 workgroups, each split >= 8 k-tiles of 32."""
     tiles = ((m_out + 127) // 128) * ((n_out + 127) // 128)
-    if tiles >= 192:
-        want = max(1, 512 // tiles)
-    else:
-        tiles64 = ((m_out + 63) // 64) * ((n_out + 63) // 64)
-        want = max(1, 512 // max(tiles64, 1))
+    want = max(1, -(-512 // tiles))
     return int(max(1, min(want, k // 256)))
 
 
