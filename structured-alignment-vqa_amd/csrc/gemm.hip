@@ -1,117 +1,104 @@
 // fp32 GEMM on gfx950 matrix cores (v_mfma_f32_32x32x2_f32: exact f32, 64 FLOP/clk/SIMD).
 //
 // Replaces every nn.Linear of the SA-VQA model_v=3 path and the two backward GEMMs of
-// each (dX = dY W, dW = dY^T X). One kernel template covers the three operand
-// layouts the path needs:
+// each (dX = dY W, dW = dY^T X). One kernel template covers the operand layouts:
 //   forward  C = X W^T        A [M][K] (a_trans=0), B [N][K] (b_trans=1)
 //   dX       C = dY W         A [M][K] (a_trans=0), B [K][N] (b_trans=0)
 //   dW      C += dY^T X       A [K][M] (a_trans=1), B [K][N] (b_trans=0), split-K + atomics
 // Fused epilogues: bias, periodic row vector (learned position table), residual,
-// ReLU, ReLU-backward mask, beta-accumulate, atomic scatter to indexed rows
+// ReLU, row scale, ReLU-backward mask, beta-accumulate, atomic scatter to indexed rows
 // (embedding-table gradient) -- see include/savqa.h for the exact formula.
 //
-// Tiling: 256 threads = 4 waves (2x2), block tile BMxBN (128x128 or 64x64), BK = 32,
-// LDS k-major [BK][BM+pad] so every MFMA operand read is 32 consecutive floats per
-// half-wave (conflict-free ds_read_b32). Global loads are float4 along the
-// contiguous dimension; register-staged double buffering with the LDS write after the
-// compute of the current tile (cdna_hip_programming.md T14), one barrier per k-tile.
+// Tiling: 256 threads = 4 waves (2x2), block tile BMxBN (128x128 or 64x64), BK 16/32.
+// Each operand tile keeps its global orientation in LDS, so every global->LDS move is a
+// float4 load + one ds_write_b128 (no transposition):
+//   ROW operand (k contiguous: X, W of the forward, dY of dX) -> LDS [m][BK+4]; the
+//     MFMA's 2-wide k slot is fed from ONE ds_read_b128 per 8 k: lane half q reads
+//     k = 8c+4q .. 8c+4q+3 and four successive MFMAs consume its 4 values (k order
+//     permuted consistently for A and B; +4-float row pad = conflict-free b128 reads);
+//   COL operand (m contiguous: W of dX, dY^T / X of dW) -> LDS [k][m+4], ds_read_b32 of
+//     32 consecutive floats per half-wave in the same permuted k order.
+// Interior tiles run a branch-free loop (row pointers resolved once per block, gathers
+// included); edge tiles, k tails and k-row gathers take a clamped, branch-free guarded
+// loader. One register-staged prefetch, LDS write after the compute (T14), one barrier
+// per k-tile, XCD-aware block order (T1).
 #include "common.h"
 
 namespace savqa {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f4 __attribute__((ext_vector_type(4)));  // native vector (HIP float4 copies
+                                                          // lower to memcpy and block SROA)
 
-constexpr int GEMM_BK = 32;
 constexpr int GEMM_NT = 256;
 
-template <int BM, bool KCONTIG>
-struct TileLoader {
-  // KCONTIG: the operand's k index is the contiguous one in global memory
-  //   (A stored [M][K], or B stored [N][K]) -> float4 along k, scalar transposed LDS writes.
-  // else: the operand's m/n index is contiguous ([K][M] / [K][N]) -> float4 along m/n.
-  static constexpr int LD = KCONTIG ? BM + 1 : BM + 4;
-  static constexpr int ITERS = BM * GEMM_BK / 4 / GEMM_NT;  // float4 per thread
-  float4 r[ITERS];
-  const float* rp[ITERS];  // FAST + KCONTIG: row pointers, resolved once per block
+template <int BMX, int BK, bool ROW>
+struct Operand {
+  static constexpr int LD = ROW ? BK + 4 : BMX + 4;
+  static constexpr int SIZE = ROW ? BMX * LD : BK * LD;
+  static constexpr int PER = ROW ? BK / 4 : BMX / 4;  // float4 per stored row
+  static constexpr int ITERS = BMX * BK / 4 / GEMM_NT;
+  static_assert(ITERS * GEMM_NT * 4 == BMX * BK, "tile not divisible by the block");
+  f4 r[ITERS];
+  const float* rp[ITERS];  // FAST path: per-float4 source pointers, resolved once per block
 
-  // FAST path (block-uniform): the whole tile is in range, the k range is a multiple of
-  // GEMM_BK and the operand is 16-B aligned -> branch-free float4 loads.
+  // ROW: stored row = m (tile row), contiguous col = k.  COL: stored row = k, col = m.
   __device__ __forceinline__ void setup_fast(const float* __restrict__ base, int64_t ld,
                                              const int64_t* __restrict__ rows, int64_t m0,
                                              int tid) {
-    if (KCONTIG) {
-#pragma unroll
-      for (int it = 0; it < ITERS; ++it) {
-        const int idx = tid + it * GEMM_NT;
-        const int64_t m = m0 + (idx >> 3);
-        const int64_t rr = rows ? rows[m] : m;
-        rp[it] = base + rr * ld + (idx & 7) * 4;
-      }
-    }
-  }
-
-  __device__ __forceinline__ void load_fast(const float* __restrict__ base, int64_t ld,
-                                            int64_t m0, int64_t k0, int tid) {
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
       const int idx = tid + it * GEMM_NT;
-      if (KCONTIG) {
-        r[it] = *reinterpret_cast<const float4*>(rp[it] + k0);
+      if constexpr (ROW) {
+        const int64_t m = m0 + idx / PER;
+        const int64_t rr = rows ? rows[m] : m;
+        rp[it] = base + rr * ld + (idx % PER) * 4;
       } else {
-        constexpr int PER_K = BM / 4;
-        const int kr = idx / PER_K;
-        const int mq = (idx % PER_K) * 4;
-        r[it] = *reinterpret_cast<const float4*>(base + (k0 + kr) * ld + m0 + mq);
+        rp[it] = base + (int64_t)(idx / PER) * ld + m0 + (idx % PER) * 4;
       }
     }
   }
 
-  // guarded path for edge tiles, k tails, unaligned operands and k-row gathers
+  // k0: first k of the tile. ROW advances along the row, COL by whole rows.
+  __device__ __forceinline__ void load_fast(int64_t ld, int64_t k0) {
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const float* p = ROW ? rp[it] + k0 : rp[it] + k0 * ld;
+      r[it] = *reinterpret_cast<const f4*>(p);
+    }
+  }
+
+  // guarded path: clamped addresses, out-of-range elements selected to 0 (branch-free)
   __device__ __forceinline__ void load_slow(const float* __restrict__ base, int64_t ld,
                                             const int64_t* __restrict__ rows, int64_t mlim,
-                                            int64_t m0, int64_t k0, int64_t kend, bool vec,
-                                            int tid) {
+                                            int64_t m0, int64_t k0, int64_t kend, int tid) {
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
       const int idx = tid + it * GEMM_NT;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (KCONTIG) {
-        const int row = idx >> 3;
-        const int kq = (idx & 7) * 4;
-        const int64_t m = m0 + row;
-        const int64_t k = k0 + kq;
-        if (m < mlim) {
-          const int64_t rr = rows ? rows[m] : m;
-          const float* p = base + rr * ld + k;
-          if (vec && k + 3 < kend) {
-            v = *reinterpret_cast<const float4*>(p);
-          } else {
-            if (k + 0 < kend) v.x = p[0];
-            if (k + 1 < kend) v.y = p[1];
-            if (k + 2 < kend) v.z = p[2];
-            if (k + 3 < kend) v.w = p[3];
-          }
-        }
+      int64_t row, col, rlim, clim;
+      if constexpr (ROW) {
+        row = m0 + idx / PER;
+        col = k0 + (idx % PER) * 4;
+        rlim = mlim;
+        clim = kend;
       } else {
-        constexpr int PER_K = BM / 4;
-        const int kr = idx / PER_K;
-        const int mq = (idx % PER_K) * 4;
-        const int64_t k = k0 + kr;
-        const int64_t m = m0 + mq;
-        if (k < kend) {
-          const int64_t kk = rows ? rows[k] : k;
-          const float* p = base + kk * ld + m;
-          if (vec && m + 3 < mlim) {
-            v = *reinterpret_cast<const float4*>(p);
-          } else {
-            if (m + 0 < mlim) v.x = p[0];
-            if (m + 1 < mlim) v.y = p[1];
-            if (m + 2 < mlim) v.z = p[2];
-            if (m + 3 < mlim) v.w = p[3];
-          }
-        }
+        row = k0 + idx / PER;
+        col = m0 + (idx % PER) * 4;
+        rlim = kend;
+        clim = mlim;
       }
-      r[it] = v;
+      const bool rok = row < rlim;
+      const int64_t rc = rok ? row : 0;
+      const int64_t rr = rows ? rows[rc] : rc;
+      const float* p = base + rr * ld;
+      float e[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = rok && (col + q < clim);
+        const float val = p[ok ? col + q : 0];
+        e[q] = ok ? val : 0.f;
+      }
+      r[it] = f4{e[0], e[1], e[2], e[3]};
     }
   }
 
@@ -119,107 +106,111 @@ struct TileLoader {
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
       const int idx = tid + it * GEMM_NT;
-      if (KCONTIG) {
-        const int row = idx >> 3;
-        const int kq = (idx & 7) * 4;
-        s[(kq + 0) * LD + row] = r[it].x;
-        s[(kq + 1) * LD + row] = r[it].y;
-        s[(kq + 2) * LD + row] = r[it].z;
-        s[(kq + 3) * LD + row] = r[it].w;
-      } else {
-        constexpr int PER_K = BM / 4;
-        const int kr = idx / PER_K;
-        const int mq = (idx % PER_K) * 4;
-        *reinterpret_cast<float4*>(&s[kr * LD + mq]) = r[it];
-      }
+      *reinterpret_cast<f4*>(&s[(idx / PER) * LD + (idx % PER) * 4]) = r[it];
+    }
+  }
+
+  // MFMA operand values of one 8-k chunk c for fragment rows [f*32, f*32+32) of this
+  // wave's sub-tile (wbase): v[j] feeds MFMA step j (k = 8c + 4*(lane>>5) + j).
+  static __device__ __forceinline__ void fetch(const float* __restrict__ s, int wbase, int f,
+                                               int c, int lane, float (&v)[4]) {
+    const int q = lane >> 5, i = lane & 31;
+    if constexpr (ROW) {
+      const f4 t = *reinterpret_cast<const f4*>(&s[(wbase + f * 32 + i) * LD + c * 8 + 4 * q]);
+      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = s[(c * 8 + 4 * q + j) * LD + wbase + f * 32 + i];
     }
   }
 };
 
-template <int BM, int BN, bool AT, bool BT>
-struct GemmTile {
-  using LA = TileLoader<BM, !AT>;
-  using LB = TileLoader<BN, BT>;
-  static constexpr int SA = GEMM_BK * LA::LD;
-  static constexpr int SB = GEMM_BK * LB::LD;
+template <int BM, int BN, int BK, bool AT, bool BT>
+struct GemmCfg {
+  using OA = Operand<BM, BK, !AT>;
+  using OB = Operand<BN, BK, BT>;
   static constexpr int WM = BM / 2, WN = BN / 2;
   static constexpr int FM = WM / 32, FN = WN / 32;
 };
 
-template <int BM, int BN, bool AT, bool BT, bool FAST>
-__device__ __forceinline__ void gemm_mainloop(const savqa_gemm_desc& d, float* smem, int64_t m0,
-                                              int64_t n0, int64_t kbeg, int64_t kend, bool avec,
-                                              bool bvec,
-                                              f32x16 (&acc)[GemmTile<BM, BN, AT, BT>::FM]
-                                                           [GemmTile<BM, BN, AT, BT>::FN]) {
-  using GT = GemmTile<BM, BN, AT, BT>;
-  typename GT::LA la;
-  typename GT::LB lb;
+template <int BM, int BN, int BK, bool AT, bool BT>
+__device__ __forceinline__ void gemm_compute_tile(
+    const float* __restrict__ As, const float* __restrict__ Bs, int wm, int wn, int lane,
+    f32x16 (&acc)[GemmCfg<BM, BN, BK, AT, BT>::FM][GemmCfg<BM, BN, BK, AT, BT>::FN]) {
+  using G = GemmCfg<BM, BN, BK, AT, BT>;
+#pragma unroll
+  for (int c = 0; c < BK / 8; ++c) {
+    float a[G::FM][4], b[G::FN][4];
+#pragma unroll
+    for (int i = 0; i < G::FM; ++i) G::OA::fetch(As, wm * G::WM, i, c, lane, a[i]);
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) G::OB::fetch(Bs, wn * G::WN, j, c, lane, b[j]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+  }
+}
+
+template <int BM, int BN, int BK, bool AT, bool BT, bool FAST>
+__device__ __forceinline__ void gemm_mainloop(
+    const savqa_gemm_desc& d, float* smem, int64_t m0, int64_t n0, int64_t kbeg, int64_t kend,
+    int ntiles,
+    f32x16 (&acc)[GemmCfg<BM, BN, BK, AT, BT>::FM][GemmCfg<BM, BN, BK, AT, BT>::FN]) {
+  using G = GemmCfg<BM, BN, BK, AT, BT>;
+  using OA = typename G::OA;
+  using OB = typename G::OB;
+  OA la;
+  OB lb;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int ntiles = kend > kbeg ? (int)((kend - kbeg + GEMM_BK - 1) / GEMM_BK) : 0;
-  if (ntiles == 0) return;
-  if (FAST) {
+  if constexpr (FAST) {
     la.setup_fast(d.A, d.lda, d.a_rows, m0, tid);
     lb.setup_fast(d.B, d.ldb, d.b_rows, n0, tid);
-    la.load_fast(d.A, d.lda, m0, kbeg, tid);
-    lb.load_fast(d.B, d.ldb, n0, kbeg, tid);
-  } else {
-    la.load_slow(d.A, d.lda, d.a_rows, d.M, m0, kbeg, kend, avec, tid);
-    lb.load_slow(d.B, d.ldb, d.b_rows, d.N, n0, kbeg, kend, bvec, tid);
   }
+#define SAVQA_GEMM_LOAD(k0)                                         \
+  do {                                                              \
+    if constexpr (FAST) {                                           \
+      la.load_fast(d.lda, (k0));                                    \
+      lb.load_fast(d.ldb, (k0));                                    \
+    } else {                                                        \
+      la.load_slow(d.A, d.lda, d.a_rows, d.M, m0, (k0), kend, tid); \
+      lb.load_slow(d.B, d.ldb, d.b_rows, d.N, n0, (k0), kend, tid); \
+    }                                                               \
+  } while (0)
+  SAVQA_GEMM_LOAD(kbeg);
   la.store(smem, tid);
-  lb.store(smem + 2 * GT::SA, tid);
+  lb.store(smem + 2 * OA::SIZE, tid);
   __syncthreads();
-
   int cur = 0;
-  const int kl = lane >> 5;
-  const int il = lane & 31;
   for (int tt = 0; tt < ntiles; ++tt) {
     const bool more = tt + 1 < ntiles;
+    if (more) SAVQA_GEMM_LOAD(kbeg + (int64_t)(tt + 1) * BK);
+    gemm_compute_tile<BM, BN, BK, AT, BT>(smem + cur * OA::SIZE,
+                                          smem + 2 * OA::SIZE + cur * OB::SIZE, wm, wn, lane,
+                                          acc);
     if (more) {
-      const int64_t kn = kbeg + (int64_t)(tt + 1) * GEMM_BK;
-      if (FAST) {
-        la.load_fast(d.A, d.lda, m0, kn, tid);
-        lb.load_fast(d.B, d.ldb, n0, kn, tid);
-      } else {
-        la.load_slow(d.A, d.lda, d.a_rows, d.M, m0, kn, kend, avec, tid);
-        lb.load_slow(d.B, d.ldb, d.b_rows, d.N, n0, kn, kend, bvec, tid);
-      }
-    }
-    const float* As = smem + cur * GT::SA + kl * GT::LA::LD + wm * GT::WM + il;
-    const float* Bs = smem + 2 * GT::SA + cur * GT::SB + kl * GT::LB::LD + wn * GT::WN + il;
-#pragma unroll
-    for (int kk = 0; kk < GEMM_BK; kk += 2) {
-      float a[GT::FM], b[GT::FN];
-#pragma unroll
-      for (int i = 0; i < GT::FM; ++i) a[i] = As[kk * GT::LA::LD + i * 32];
-#pragma unroll
-      for (int j = 0; j < GT::FN; ++j) b[j] = Bs[kk * GT::LB::LD + j * 32];
-#pragma unroll
-      for (int i = 0; i < GT::FM; ++i)
-#pragma unroll
-        for (int j = 0; j < GT::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-    if (more) {
-      la.store(smem + (cur ^ 1) * GT::SA, tid);
-      lb.store(smem + 2 * GT::SA + (cur ^ 1) * GT::SB, tid);
+      la.store(smem + (cur ^ 1) * OA::SIZE, tid);
+      lb.store(smem + 2 * OA::SIZE + (cur ^ 1) * OB::SIZE, tid);
     }
     __syncthreads();
     cur ^= 1;
   }
+#undef SAVQA_GEMM_LOAD
 }
 
-template <int BM, int BN, bool AT, bool BT>
-__global__ __launch_bounds__(GEMM_NT, 2) void gemm_f32_kernel(savqa_gemm_desc d, int tiles_m,
+template <int BM, int BN, int BK, bool AT, bool BT>
+__global__ __launch_bounds__(GEMM_NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_f32_kernel(savqa_gemm_desc d, int tiles_m,
                                                              int tiles_n, int64_t kchunk,
                                                              int avec, int bvec) {
-  using GT = GemmTile<BM, BN, AT, BT>;
-  constexpr int FM = GT::FM, FN = GT::FN, WM = GT::WM, WN = GT::WN;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (GT::SA + GT::SB)];
+  using G = GemmCfg<BM, BN, BK, AT, BT>;
+  constexpr int FM = G::FM, FN = G::FN, WM = G::WM, WN = G::WN;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (G::OA::SIZE + G::OB::SIZE)];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -244,12 +235,15 @@ __global__ __launch_bounds__(GEMM_NT, 2) void gemm_f32_kernel(savqa_gemm_desc d,
   // block-uniform choice of the branch-free main loop
   const bool a_kgather = AT && d.a_rows;
   const bool b_kgather = !BT && d.b_rows;
-  const bool fast = (m0 + BM <= d.M) && (n0 + BN <= d.N) && ((kend - kbeg) % GEMM_BK == 0) &&
-                    avec && bvec && !a_kgather && !b_kgather;
-  if (fast)
-    gemm_mainloop<BM, BN, AT, BT, true>(d, smem, m0, n0, kbeg, kend, avec, bvec, acc);
-  else
-    gemm_mainloop<BM, BN, AT, BT, false>(d, smem, m0, n0, kbeg, kend, avec, bvec, acc);
+  const bool fast = (m0 + BM <= d.M) && (n0 + BN <= d.N) && ((kend - kbeg) % BK == 0) && avec &&
+                    bvec && !a_kgather && !b_kgather;
+  const int ntiles = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
+  if (ntiles > 0) {
+    if (fast)
+      gemm_mainloop<BM, BN, BK, AT, BT, true>(d, smem, m0, n0, kbeg, kend, ntiles, acc);
+    else
+      gemm_mainloop<BM, BN, BK, AT, BT, false>(d, smem, m0, n0, kbeg, kend, ntiles, acc);
+  }
 
   // ---------------------------------------------------------------- epilogue
   const bool first_split = blockIdx.y == 0;
@@ -301,24 +295,24 @@ __global__ __launch_bounds__(GEMM_NT, 2) void gemm_f32_kernel(savqa_gemm_desc d,
   }
 }
 
-template <int BM, int BN, bool AT, bool BT>
+template <int BM, int BN, int BK, bool AT, bool BT>
 static void launch_gemm(const savqa_gemm_desc& d, hipStream_t s, int split, int avec, int bvec) {
   const int tm = (int)((d.M + BM - 1) / BM);
   const int tn = (int)((d.N + BN - 1) / BN);
   int64_t kchunk = (d.K + split - 1) / split;
-  kchunk = (kchunk + GEMM_BK - 1) / GEMM_BK * GEMM_BK;
-  const int nsplit = (int)((d.K + kchunk - 1) / kchunk);
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  const int nsplit = kchunk > 0 ? (int)((d.K + kchunk - 1) / kchunk) : 1;
   dim3 grid(tm * tn, nsplit > 0 ? nsplit : 1);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, AT, BT>), grid, dim3(GEMM_NT), 0, s, d, tm, tn,
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, AT, BT>), grid, dim3(GEMM_NT), 0, s, d, tm, tn,
                      kchunk, avec, bvec);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int BK>
 static void dispatch_layout(const savqa_gemm_desc& d, hipStream_t s, int split, int avec, int bvec) {
-  if (!d.a_trans && d.b_trans) launch_gemm<BM, BN, false, true>(d, s, split, avec, bvec);
-  else if (!d.a_trans && !d.b_trans) launch_gemm<BM, BN, false, false>(d, s, split, avec, bvec);
-  else if (d.a_trans && !d.b_trans) launch_gemm<BM, BN, true, false>(d, s, split, avec, bvec);
-  else launch_gemm<BM, BN, true, true>(d, s, split, avec, bvec);
+  if (!d.a_trans && d.b_trans) launch_gemm<BM, BN, BK, false, true>(d, s, split, avec, bvec);
+  else if (!d.a_trans && !d.b_trans) launch_gemm<BM, BN, BK, false, false>(d, s, split, avec, bvec);
+  else if (d.a_trans && !d.b_trans) launch_gemm<BM, BN, BK, true, false>(d, s, split, avec, bvec);
+  else launch_gemm<BM, BN, BK, true, true>(d, s, split, avec, bvec);
 }
 
 }  // namespace savqa
@@ -333,6 +327,7 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   if (d.M < 0 || d.N < 0 || d.K < 0) return fail(SAVQA_EINVAL, "savqa_gemm: negative dims");
   if (d.M == 0 || d.N == 0) return 0;
   if (!d.A || !d.B || !d.C) return fail(SAVQA_EINVAL, "savqa_gemm: null operand");
+  if (d.M >= (1LL << 31) || d.N >= (1LL << 31)) return fail(SAVQA_EUNSUP, "savqa_gemm: M/N >= 2^31");
   if (d.mask && d.mask_arows && (d.a_trans || !d.a_rows))
     return fail(SAVQA_EINVAL, "savqa_gemm: mask_arows needs a_trans=0 and a_rows");
   if (d.c_group <= 0) { d.c_group = d.M; d.c_stride = d.M; }
@@ -344,9 +339,9 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   // 128x128 tiles once there is enough parallelism (split-K counts), else 64x64
   const int64_t big_tiles = ((d.M + 127) / 128) * ((d.N + 127) / 128) * split;
   if (big_tiles >= 160)
-    dispatch_layout<128, 128>(d, s, split, avec, bvec);
+    dispatch_layout<128, 128, 32>(d, s, split, avec, bvec);
   else
-    dispatch_layout<64, 64>(d, s, split, avec, bvec);
+    dispatch_layout<64, 64, 32>(d, s, split, avec, bvec);
   return check_launch("savqa_gemm");
 }
 
