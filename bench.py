@@ -168,11 +168,15 @@ def main():
 
     roof = None
     if not args.no_roofline:
+        # per-kernel timing needs kernels that do not share the GPU: run the probe steps
+        # with both stacks on one stream (the timed region above overlaps them)
         probe = ops.GemmProbe()
+        model._engine.concurrent = False
         ops.set_gemm_probe(probe)
         for _ in range(2):
             step()
         ops.set_gemm_probe(None)
+        model._engine.concurrent = True
         agg = probe.summary()
         var, (n, flops, ms) = max(agg.items(), key=lambda kv: kv[1][2])
         achieved = (flops / n) / (ms / n * 1e-3) / 1e12

@@ -203,7 +203,7 @@ class _AttModelFn(torch.autograd.Function):
         Cc = model.num_classes
         red = model.__dict__.get("_reducer")
         model._engine.backward(ctx.saved, z(dlc, (B, Cc)), z(dlv, (B, Cc)), z(dls, (B, Cc)),
-                               z(dmil, ()), on_region=red.region_done if red else None)
+                               z(dmil, ()), on_range=red.reduce_range if red else None)
         ctx.saved = None
         return (None, None, None) + (None,) * len(_INPUT_NAMES)
 

@@ -203,25 +203,30 @@ __global__ __launch_bounds__(256) void gattn_bwd_kernel(AttnArgs a) {
   const int b = bh / a.H, h = bh % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int PLD = a.Tk + 1;
+  const int TQP = (a.Tq + ATT_RB - 1) / ATT_RB * ATT_RB;  // rows padded to the row block
   float* Ks = sm;
   float* Vs = Ks + a.Tk * ATT_KLD;
   float* Pst = Vs + a.Tk * ATT_KLD;          // [Tq][Tk+1]  P
   float* dSt = Pst + a.Tq * PLD;             // [Tq][Tk+1]  dS (pre-scale, masked)
-  float* Qs = dSt + a.Tq * PLD;              // [4][ATT_RB][64]
-  float* dOs = Qs + 4 * ATT_RB * ATT_DK;     // [4][ATT_RB][64]
-  float* qs = Qs + w * ATT_RB * ATT_DK;
-  float* dos = dOs + w * ATT_RB * ATT_DK;
+  float* Qs = dSt + a.Tq * PLD;              // [TQP][64]   Q_h rows (staged once)
+  float* dOs = Qs + TQP * ATT_DK;            // [TQP][64]   dO_h rows
   stage_kv(a, b, h, Ks, Vs);
+  for (int idx = threadIdx.x; idx < TQP * 16; idx += blockDim.x) {
+    const int i = idx >> 4, c4 = (idx & 15) * 4;
+    float4 qv = make_float4(0.f, 0.f, 0.f, 0.f), dv4 = qv;
+    if (i < a.Tq) {
+      const int64_t row = (int64_t)b * a.Tq + i;
+      qv = *reinterpret_cast<const float4*>(a.q + row * a.ldq + h * ATT_DK + c4);
+      dv4 = *reinterpret_cast<const float4*>(a.dout + row * a.lddo + h * ATT_DK + c4);
+    }
+    *reinterpret_cast<float4*>(&Qs[i * ATT_DK + c4]) = qv;
+    *reinterpret_cast<float4*>(&dOs[i * ATT_DK + c4]) = dv4;
+  }
   __syncthreads();
 
   for (int i0 = w * ATT_RB; i0 < a.Tq; i0 += 4 * ATT_RB) {
-#pragma unroll
-    for (int r = 0; r < ATT_RB; ++r) {
-      const int i = i0 + r < a.Tq ? i0 + r : a.Tq - 1;
-      const int64_t row = (int64_t)b * a.Tq + i;
-      qs[r * ATT_DK + lane] = a.q[row * a.ldq + h * ATT_DK + lane];
-      dos[r * ATT_DK + lane] = a.dout[row * a.lddo + h * ATT_DK + lane];
-    }
+    const float* qs = Qs + i0 * ATT_DK;
+    const float* dos = dOs + i0 * ATT_DK;
     __builtin_amdgcn_wave_barrier();
     float s[ATT_RB][KB], dp[ATT_RB][KB];
     row_dots<KB>(qs, Ks, a.Tk, lane, s);
@@ -289,9 +294,8 @@ __global__ __launch_bounds__(256) void gattn_bwd_kernel(AttnArgs a) {
     float dvv[4] = {0.f, 0.f, 0.f, 0.f}, dkk[4] = {0.f, 0.f, 0.f, 0.f};
     const int nj = min(4, a.Tk - j0);
     for (int i = 0; i < a.Tq; ++i) {
-      const int64_t row = (int64_t)b * a.Tq + i;
-      const float dov = a.dout[row * a.lddo + h * ATT_DK + lane];
-      const float qv = a.q[row * a.ldq + h * ATT_DK + lane];
+      const float dov = dOs[i * ATT_DK + lane];
+      const float qv = Qs[i * ATT_DK + lane];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         if (c < nj) {
@@ -316,7 +320,8 @@ static size_t fwd_lds(int Tk, int KB) {
   return sizeof(float) * ((size_t)2 * Tk * ATT_KLD + 4 * ATT_RB * KB * 64 + 4 * ATT_RB * ATT_DK);
 }
 static size_t bwd_lds(int Tq, int Tk) {
-  return sizeof(float) * ((size_t)2 * Tk * ATT_KLD + 2 * (size_t)Tq * (Tk + 1) + 8 * ATT_RB * ATT_DK);
+  const size_t tqp = (size_t)(Tq + ATT_RB - 1) / ATT_RB * ATT_RB;
+  return sizeof(float) * ((size_t)2 * Tk * ATT_KLD + 2 * (size_t)Tq * (Tk + 1) + 2 * tqp * ATT_DK);
 }
 constexpr size_t kMaxLds = 160 * 1024;
 

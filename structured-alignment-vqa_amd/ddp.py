@@ -6,9 +6,9 @@ and zero-filled). Here only the live range of the flat gradient arena is exchang
 (457M floats), as contiguous buckets, with RCCL (torch.distributed "nccl" = RCCL on
 ROCm) over xGMI:
 
-  * the arena orders live parameters by when the backward FINISHES them, so the
-    engine reports a monotonically growing "final" prefix of the gradient buffer
-    after the heads, each stack and the MIL-NCE part;
+  * the arena groups live parameters by the backward phase that FINISHES them, so the
+    engine reports final contiguous ranges (heads; visual stack; semantic stack +
+    MIL-NCE) on the stream that produced them;
   * every finished bucket is all-reduced asynchronously right away: RCCL's stream
     waits for the kernels that produced it and then runs beside the rest of the
     backward (overlap), exactly the dependency, nothing more;
@@ -30,33 +30,30 @@ class GradReducer:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.bucket = max(1, int(bucket_mb * (1 << 20) // 4))
-        self.launched = 0
         self.works: List = []
 
     def begin(self):
-        self.launched = 0
         self.works = []
 
-    def region_done(self, upto: int, final: bool = False):
-        """Gradient elements [0, upto) are final: all-reduce whole buckets of them."""
+    def reduce_range(self, start: int, end: int):
+        """Gradient elements [start, end) of the arena are final on the CURRENT stream:
+        all-reduce them in buckets; RCCL's stream waits for exactly that work."""
         if self.world <= 1:
             return
         g = self.arena.grad
-        upto = min(int(upto), g.numel())
-        while self.launched < upto:
-            end = min(self.launched + self.bucket, upto)
-            if end - self.launched < self.bucket and not final:
-                break  # partial bucket: wait for more finished gradients
-            view = g[self.launched:end]
-            self.works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group,
+        end = min(int(end), g.numel())
+        lo = int(start)
+        while lo < end:
+            hi = min(lo + self.bucket, end)
+            self.works.append(dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
                                               async_op=True))
-            self.launched = end
+            lo = hi
 
     def finish(self):
-        """Reduce what is left and make the current stream wait for every bucket."""
+        """Make the current stream wait for every bucket; returns the 1/world factor the
+        optimizer folds into its update (DDP averages)."""
         if self.world <= 1:
             return 1.0
-        self.region_done(self.arena.grad.numel(), final=True)
         for w in self.works:
             w.wait()
         self.works = []

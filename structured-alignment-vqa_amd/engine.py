@@ -445,7 +445,20 @@ class ModelEngine:
             self.ghead = HeadWeights(a, grad=True)
             self._gbound = g
 
+    concurrent = True  # False: run both stacks on the caller's stream (serial profiling)
+
+    def _streams(self, dev):
+        if not self.concurrent:
+            cur = torch.cuda.current_stream(dev)
+            return cur, cur
+        if getattr(self, "_side", None) is None or self._side[0].device != dev:
+            self._side = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+        return self._side
+
     def forward(self, inp: Dict[str, torch.Tensor], decMask: bool):
+        """The two stacks are independent until the heads (AttModel_x3.py:525-541), so the
+        visual stack and the MIL-NCE + semantic stack run on two HIP streams: one stack's
+        latency-bound decoder phase and GEMM tails overlap the other's big GEMMs."""
         d, H = self.d, self.H
         vis = inp["vis_fea"]
         dev = vis.device
@@ -453,17 +466,27 @@ class ModelEngine:
         Lq = inp["q_ipt"].shape[1]
         Ns = inp["macro_ipt"].shape[1]
         Tv, Ts = Nv + Lq, Ns + Lq
-        mil_val = _empty((), dev=dev)
-        cat_syb = _empty(B * Ts, Dv, dev=dev)
-        ms = mil_forward(self.mil, vis, inp["macro_ipt"], inp["macro_obj_loc"],
-                         inp["micro_positive_obj"], inp["micro_negative_obj"],
-                         inp["micro_obj_mask"], cat_syb, Ts, mil_val)
-        cat_vis = _empty(B * Tv, Dv, dev=dev)
-        ops.copy_rows(vis.reshape(B * Nv, Dv), B * Nv, Dv, Dv, cat_vis, Dv, Nv, Tv, 0)
-        sv = stack_forward(self.vis, cat_vis, B, Nv, Lq, inp["q_ipt"], inp["vis_mask"],
-                           inp["q_mask"], inp["q_graph"], None, decMask, H, d)
-        ss = stack_forward(self.syb, cat_syb, B, Ns, Lq, inp["q_ipt"], inp["macro_mask"],
-                           inp["q_mask"], inp["q_graph"], inp["macro_graph"], decMask, H, d)
+        main = torch.cuda.current_stream(dev)
+        s_vis, s_syb = self._streams(dev)
+        s_vis.wait_stream(main)
+        s_syb.wait_stream(main)
+        with torch.cuda.stream(s_syb):
+            mil_val = _empty((), dev=dev)
+            cat_syb = _empty(B * Ts, Dv, dev=dev)
+            ms = mil_forward(self.mil, vis, inp["macro_ipt"], inp["macro_obj_loc"],
+                             inp["micro_positive_obj"], inp["micro_negative_obj"],
+                             inp["micro_obj_mask"], cat_syb, Ts, mil_val)
+            ss = stack_forward(self.syb, cat_syb, B, Ns, Lq, inp["q_ipt"], inp["macro_mask"],
+                               inp["q_mask"], inp["q_graph"], inp["macro_graph"], decMask, H, d)
+        with torch.cuda.stream(s_vis):
+            cat_vis = _empty(B * Tv, Dv, dev=dev)
+            ops.copy_rows(vis.reshape(B * Nv, Dv), B * Nv, Dv, Dv, cat_vis, Dv, Nv, Tv, 0)
+            sv = stack_forward(self.vis, cat_vis, B, Nv, Lq, inp["q_ipt"], inp["vis_mask"],
+                               inp["q_mask"], inp["q_graph"], None, decMask, H, d)
+        main.wait_stream(s_vis)
+        main.wait_stream(s_syb)
+        for t in (sv.out, ss.out, mil_val):
+            t.record_stream(main)
         (lc, lv, ls), hs = heads_forward(self.head, sv.out, ss.out, d)
         return (lc, lv, ls, mil_val), (ms, sv, ss, hs)
 
@@ -474,22 +497,33 @@ class ModelEngine:
                 a.offsets[f"att_syb.dec_feed_forward_{nb - 1}.normalization.gamma"][0],
                 a.offsets["MIL_NCE.ipt_mlp.0.weight"][0])
 
-    def backward(self, saved, dlc, dlv, dls, dmil, on_region=None):
-        """Whole-model backward. on_region(n) is called whenever gradient elements
-        [0, n) of the arena are final (used to start the all-reduce early)."""
+    def backward(self, saved, dlc, dlv, dls, dmil, on_range=None):
+        """Whole-model backward (heads on the caller's stream, then the two stacks on their
+        own streams). on_range(start, end) is called, on the stream that produced them,
+        as soon as arena gradient elements [start, end) are final (all-reduce streaming)."""
         self.grads()
         ms, sv, ss, hs = saved
         d, H = self.d, self.H
+        dev = dlc.device
         b_heads, b_vis, b_syb = self.region_bounds()
+        main = torch.cuda.current_stream(dev)
         df_vis, df_syb = heads_backward(self.head, self.ghead, hs, dlc, dlv, dls, d)
-        if on_region:
-            on_region(b_heads)
-        stack_backward(self.vis, self.gvis, sv, df_vis, H, d, want_node_grad=False)
-        if on_region:
-            on_region(b_vis)
-        dnode = stack_backward(self.syb, self.gsyb, ss, df_syb, H, d, want_node_grad=True)
-        if on_region:
-            on_region(b_syb)
-        mil_backward(self.mil, self.gmil, ms, dnode, dmil)
-        if on_region:
-            on_region(self.arena.n_live)
+        if on_range:
+            on_range(0, b_heads)
+        s_vis, s_syb = self._streams(dev)
+        s_vis.wait_stream(main)
+        s_syb.wait_stream(main)
+        df_vis.record_stream(s_vis)
+        df_syb.record_stream(s_syb)
+        dmil.record_stream(s_syb)
+        with torch.cuda.stream(s_vis):
+            stack_backward(self.vis, self.gvis, sv, df_vis, H, d, want_node_grad=False)
+            if on_range:
+                on_range(b_heads, b_vis)
+        with torch.cuda.stream(s_syb):
+            dnode = stack_backward(self.syb, self.gsyb, ss, df_syb, H, d, want_node_grad=True)
+            mil_backward(self.mil, self.gmil, ms, dnode, dmil)
+            if on_range:
+                on_range(b_vis, self.arena.n_live)
+        main.wait_stream(s_vis)
+        main.wait_stream(s_syb)
