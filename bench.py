@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--serial", action="store_true",
+                    help="run both stacks on one stream (per-kernel profiling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,6 +125,8 @@ def main():
                      init=False)
     init_params_(model, seed=0)  # identical on every rank (same seed), like a broadcast
     model.train()
+    if args.serial:
+        model._engine.concurrent = False
     opt = Adam(model, lr=1e-4)
     reducer = GradReducer(model._arena) if world > 1 else None
     if reducer:
@@ -176,7 +180,7 @@ def main():
         for _ in range(2):
             step()
         ops.set_gemm_probe(None)
-        model._engine.concurrent = True
+        model._engine.concurrent = not args.serial
         agg = probe.summary()
         var, (n, flops, ms) = max(agg.items(), key=lambda kv: kv[1][2])
         achieved = (flops / n) / (ms / n * 1e-3) / 1e12

@@ -1,0 +1,182 @@
+"""Training-loop surface of models/main_itp_ddp_tar_super_node.py on the savqa engine.
+
+Same CLI flags (argparse main:430-500), same process model (one process per GPU:
+`mp.spawn(main, nprocs=ngpus)` main:517, or torchrun env vars), same step
+(forward → zero_grad → label-smoothed loss (+ -MIL-NCE) → backward → Adam, main:268-378),
+same per-epoch eval with accuracy counted on non-zero answers (main:42-142) and the
+3-float all_gather of metrics (main:383-400), same checkpoint naming with the DDP
+`module.` key prefix (main:425-428).
+
+Differences (hot path only): the model is savqa_amd.AttModel (HIP kernels), the
+gradient all-reduce is savqa_amd.ddp.GradReducer (RCCL, live gradients only, streamed
+out of the backward) instead of DistributedDataParallel(find_unused_parameters=True),
+Adam is the fused savqa_amd.optim.Adam, and the GQA tar data (absent offline) is
+replaced by savqa_amd.data.synthetic_batch unless a loader is plugged in.
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import logging
+import os
+
+import torch
+import torch.distributed as dist
+
+from .AttModel_x3 import AttModel
+from .data import model_args, synthetic_batch
+from .ddp import GradReducer
+from .loss import smoothed_loss
+from .optim import Adam
+from .utils import AverageMeter, add_module_prefix, init_params_
+
+
+def build_parser():
+    p = argparse.ArgumentParser()
+    p.add_argument('--data_dir_azure', type=str, default=os.environ.get('PT_DATA_DIR', './tmp'))
+    p.add_argument('--batch_size', type=int, default=256)
+    p.add_argument('--lr', type=float, default=0.0001)
+    p.add_argument('--output_dir', type=str, default=os.environ.get('PT_OUTPUT_DIR', './tmp'))
+    p.add_argument('--maxlen', type=int, default=300)
+    p.add_argument('--maxlen_q', type=int, default=50)
+    p.add_argument('--maxlen_v', type=int, default=49)
+    p.add_argument('--hidden_size', type=int, default=512)
+    p.add_argument('--hidden_size_mil', type=int, default=64)
+    p.add_argument('--num_blocks', type=int, default=6)
+    p.add_argument('--num_epochs', type=int, default=40)
+    p.add_argument('--num_heads', type=int, default=8)
+    p.add_argument('--dropout_rate', type=float, default=0.5)
+    p.add_argument('--dropout_rate_mcb', type=float, default=0.1)
+    p.add_argument('--topN', type=int, default=1)
+    p.add_argument('--num_classes', type=int, default=914)
+    p.add_argument('--num_relations', type=int, default=311)
+    for flag in ('with_smooth_labeling', 'with_MILNCE_loss', 'local_debug', 'decMask', 'mcb',
+                 'only_obj', 'pred_rel', 'with_loc', 'with_dec', 'with_bbox'):
+        p.add_argument(f'--{flag}', action='store_true')
+    p.add_argument('--log_steps', type=int, default=100)
+    p.add_argument('--model_v', type=int, default=3)
+    p.add_argument('--ngpus', type=int, default=-1)
+    p.add_argument('--num_nodes', type=int, default=1)
+    # synthetic-data shape (the GQA loader is out of scope)
+    p.add_argument('--steps_per_epoch', type=int, default=10)
+    p.add_argument('--num_regions', type=int, default=36)
+    p.add_argument('--num_nodes_sg', type=int, default=59)
+    p.add_argument('--q_len', type=int, default=14)
+    return p
+
+
+def evaluate(model, batches, with_mil, rank, args):
+    """main:42-142: loss meter + accuracy over non-zero answers."""
+    model.eval()
+    meter = AverageMeter()
+    cnt = torch.zeros((), device=torch.cuda.current_device())
+    correct = torch.zeros_like(cnt)
+    with torch.no_grad():
+        for batch in batches:
+            lc, lv, ls, mil, _ = model(*model_args(batch), decMask=args.decMask, mcb=args.mcb)
+            loss, lsm = smoothed_loss(lc, lv, ls, batch["answer"], mil, with_milnce=with_mil)
+            meter.update(float(loss), batch["answer"].shape[0])
+            valid = batch["answer"] != 0
+            correct += ((lsm.argmax(-1) == batch["answer"]) & valid).sum()
+            cnt += valid.sum()
+    model.train()
+    return meter.avg, float(correct), float(cnt)
+
+
+def main(gpu_rank, args):
+    rank = int(os.environ.get("RANK", gpu_rank))
+    local = int(os.environ.get("LOCAL_RANK", gpu_rank))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if args.world_size > 1 and not dist.is_initialized():
+        dist.init_process_group("nccl", rank=rank, world_size=args.world_size, device_id=dev)
+    if rank == 0:
+        logging.basicConfig(level=logging.INFO, format='%(asctime)s %(levelname)-8s %(message)s')
+    if args.model_v != 3:
+        raise NotImplementedError("only model_v=3 is on the savqa hot path")
+    model = AttModel(None, args.hidden_size, args.hidden_size_mil, args.num_classes, args.maxlen_q,
+                     args.maxlen, args.maxlen_v, args.num_blocks, args.num_heads, args.dropout_rate,
+                     args.dropout_rate_mcb, args.num_relations, args.only_obj, device=dev,
+                     init=False)
+    init_params_(model, seed=0)  # same seed on every rank = DDP's initial broadcast
+    model.train()
+    opt = Adam(model, lr=args.lr)
+    reducer = GradReducer(model._arena) if args.world_size > 1 else None
+    if reducer:
+        model.attach_reducer(reducer)
+    loss_meter, mil_meter = AverageMeter(), AverageMeter()
+
+    def batches(seed0):
+        for i in range(args.steps_per_epoch):
+            yield synthetic_batch(args.batch_size, Nv=args.num_regions, Lq=args.q_len,
+                                  Ns=args.num_nodes_sg, topN=args.topN,
+                                  num_classes=args.num_classes, seed=seed0 + i, device=dev)
+
+    for epoch in range(args.num_epochs):
+        for i, batch in enumerate(batches(1000 * epoch + 7919 * rank)):
+            if reducer:
+                reducer.begin()
+            lc, lv, ls, mil, _ = model(*model_args(batch), decMask=args.decMask, mcb=args.mcb)
+            opt.zero_grad()
+            loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil,
+                                    with_milnce=args.with_MILNCE_loss)
+            loss.backward()
+            if reducer:
+                opt.grad_scale = reducer.finish()
+            opt.step()
+            if (i + 1) % args.log_steps == 0 or i + 1 == args.steps_per_epoch:
+                loss_meter.update(float(loss), batch["answer"].shape[0])
+                mil_meter.update(-float(mil), batch["answer"].shape[0])
+                if rank == 0:
+                    logging.info('Time %s, Epoch [%d/%d], Step [%d/%d], Loss: %.5f, MIL NCE Loss: %.5f, '
+                                 'Avg Loss: %.5f', datetime.datetime.now(), epoch + 1, args.num_epochs,
+                                 i + 1, args.steps_per_epoch, float(loss), -float(mil), loss_meter.avg)
+        val_loss, corr, cnt = evaluate(model, batches(10 ** 6 + rank), args.with_MILNCE_loss, rank, args)
+        vals = torch.tensor([val_loss, corr, cnt], device=dev)
+        if args.world_size > 1:
+            gathered = [torch.zeros(3, device=dev) for _ in range(args.world_size)]
+            dist.all_gather(gathered, vals)
+            vals = torch.stack(gathered)
+        else:
+            vals = vals.unsqueeze(0)
+        if rank == 0:
+            acc = float(vals[:, 1].sum()) / max(float(vals[:, 2].sum()), 1.0)
+            logging.info('Epoch [%d/%d], Val Loss: %.5f, accuracy: %.4f', epoch + 1, args.num_epochs,
+                         float(vals[:, 0].mean()), acc)
+            out = os.path.join(args.data_dir_azure, args.output_dir)
+            os.makedirs(out, exist_ok=True)
+            sd = model.state_dict()
+            torch.save(add_module_prefix(sd) if args.world_size > 1 else sd,
+                       os.path.join(out, f'model_{epoch + 1}.pth'))
+    if args.world_size > 1:
+        dist.destroy_process_group()
+
+
+def cli(argv=None):
+    args = build_parser().parse_args(argv)
+    if "WORLD_SIZE" in os.environ:  # torchrun
+        args.world_size = int(os.environ["WORLD_SIZE"])
+        main(int(os.environ.get("LOCAL_RANK", 0)), args)
+        return
+    if args.ngpus == -1:
+        args.ngpus = torch.cuda.device_count()
+    args.world_size = args.ngpus * args.num_nodes
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    os.environ.setdefault('MASTER_PORT', '7787')
+    if args.local_debug or args.world_size <= 1:
+        args.world_size = 1
+        main(0, args)
+    else:
+        os.environ['WORLD_SIZE'] = str(args.world_size)
+        import torch.multiprocessing as mp
+        mp.spawn(_spawn_main, nprocs=args.ngpus, args=(args,))
+
+
+def _spawn_main(gpu_rank, args):
+    os.environ['RANK'] = str(gpu_rank)
+    os.environ['LOCAL_RANK'] = str(gpu_rank)
+    main(gpu_rank, args)
+
+
+if __name__ == "__main__":
+    cli()

@@ -1,0 +1,68 @@
+"""Data-parallel gradient exchange (savqa_amd.ddp.GradReducer) with world_size 2 on the
+gloo backend (CPU): ranged, bucketed, asynchronous all-reduce of the flat gradient arena
+and the 1/world factor folded into Adam -- i.e. what DDP's all-reduce does (main:203)."""
+import os
+import socket
+import types
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from savqa_amd.ddp import GradReducer
+    n = 10007
+    g = torch.arange(n, dtype=torch.float32) * (rank + 1)
+    arena = types.SimpleNamespace(grad=g.clone())
+    red = GradReducer(arena, bucket_mb=0.01)  # ~2.6k floats per bucket -> several buckets
+    red.begin()
+    red.reduce_range(0, 3000)        # "heads" range
+    red.reduce_range(3000, 7000)     # "visual stack"
+    red.reduce_range(7000, n)        # "semantic stack + MIL"
+    scale = red.finish()
+    expect = torch.arange(n, dtype=torch.float32) * sum(r + 1 for r in range(world))
+    q.put((rank, float((arena.grad - expect).abs().max()), scale, len(red.works)))
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, scale, nworks in res:
+        assert err == 0.0
+        assert scale == 0.5
+        assert nworks == 0
+
+
+def test_adam_grad_scale_matches_mean_of_grads():
+    """Adam(grad_scale=1/world) on summed grads == Adam on the mean (oracle restatement)."""
+    from oracle import savqa_oracle as O
+    g1, g2 = torch.randn(50), torch.randn(50)
+    p0 = torch.randn(50)
+    P = {"w": p0.clone()}
+    O.adam_step(P, {"w": (g1 + g2) / 2}, {}, 1)
+    # the fused kernel computes g' = g*grad_scale first; restate that order
+    P2 = {"w": p0.clone()}
+    O.adam_step(P2, {"w": (g1 + g2) * 0.5}, {}, 1)
+    assert torch.allclose(P["w"], P2["w"])
