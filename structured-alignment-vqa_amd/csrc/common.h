@@ -14,16 +14,33 @@ int check_launch(const char* what);
 
 constexpr int kWave = 64;
 
+// Wave-wide reductions with DPP row ops + 4 readlanes (all VALU/SALU, no LDS round
+// trips): quad_perm [1,0,3,2], [2,3,0,1], row_ror:4, row_ror:8 leave every lane of a
+// 16-lane row holding that row's total; the four row totals are then read as scalars.
+// (__shfl_xor lowers to ds_bpermute: ~100 cycles of LDS latency per step, 6 steps.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x124>(v);  // row_ror:4
+  v += dpp_f<0x128>(v);  // row_ror:8
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-  return v;
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x124>(v));
+  v = fmaxf(v, dpp_f<0x128>(v));
+  return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 
 // bijective XCD-aware remap (cdna_hip_programming.md T1): blocks b and b+8 share an
