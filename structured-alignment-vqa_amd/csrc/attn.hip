@@ -13,7 +13,9 @@
 // The encoder self-attention (Tq = Tk = T <= 100) and the decoder cross-attention
 // (Tq = 1, keys = encoder output) are the same kernel with different strides.
 //
-// Layout: one 256-thread workgroup (4 waves) per (b, h). K_h and V_h (Tk x 64 fp32)
+// Two kernel families. Tq >= 8 (encoder self-attention): the MFMA strip kernels below
+// (gattn_*_mfma_kernel). Tq < 8 (decoder cross-attention, Tq = 1): the lane-per-key
+// "row" kernels: one 256-thread workgroup (4 waves) per (b, h); K_h and V_h (Tk x 64 fp32)
 // are staged once into LDS with 68-float rows so a lane-per-key float4 read is
 // bank-conflict-free; each wave processes 4 query rows at a time (register blocking:
 // one K float4 read feeds 16 FMAs). Softmax / normalise use 64-lane shuffles.
@@ -316,6 +318,335 @@ __global__ __launch_bounds__(256) void gattn_bwd_kernel(AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// MFMA path (v_mfma_f32_16x16x4_f32, exact fp32 products). One workgroup per (b, h) with
+// one wave per 16-row query strip (nw = ceil(Tq/16) <= 8 waves); NJT = ceil(Tk/16) key
+// tiles. 16x16x4 operand maps: lane l supplies A[m = l&15][k = l>>4] and B[k = l>>4]
+// [n = l&15]; the accumulator holds D[4(l>>4) + r][l&15], r = 0..3. Inner products over
+// d take 4 consecutive d per lane (one b128 load) and consume them as 4 k-steps, so
+// lane group g covers d = 16c + 4g + t: the same permutation on A and B.
+//
+// Backward, phase 1 (per wave, registers only): S and dP strips (16 x 16*NJT), the row
+// softmax / graph / L1-normalise chain and its adjoint with 16-lane DPP row reductions
+// (an accumulator row lives in one 16-lane DPP row), then P and dS are written to LDS
+// transposed ([key][query], one b128 per lane per tile).
+// Phase 2 (after one barrier), output tiles round-robin over the waves:
+//   dV = P^T dO and dK = dS^T Q  (A = b128 rows of the transposed LDS images),
+//   dQ = dS K                     (A = 4 scalar LDS reads, conflict-free, see PLD).
+// The B operands (dO, Q, K columns) come straight from global memory (L1/L2 hits: the
+// workgroup just streamed the same rows in phase 1).
+// LDS: 2 * 16*NJT * (16*nw + 4) floats  (53.7 KB at T = 73, 2 workgroups / CU).
+// PLD = 16*nw + 4 makes both the b128 row reads (16 lanes -> 16 disjoint bank quads)
+// and the scalar column reads (4 lane groups at bank offsets 16g) conflict-free.
+using f4v = float __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v mfma16(float a, float b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// sum / max over the 16 lanes of a DPP row (every lane of the row gets the result)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x124>(v);
+  v += dpp_f<0x128>(v);
+  return v;
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x124>(v));
+  v = fmaxf(v, dpp_f<0x128>(v));
+  return v;
+}
+
+__device__ __forceinline__ f4v ld4(const float* p) { return *reinterpret_cast<const f4v*>(p); }
+
+// acc[jt] = X_strip . Y_tile(jt)^T over d = 64: X rows (i0 + col), Y rows (16 jt + col)
+template <int NJT>
+__device__ __forceinline__ void strip_dots(const f4v (&x)[4], const float* y, int64_t ldy,
+                                           int64_t ybase, int Tk, int col, int g,
+                                           f4v (&acc)[NJT]) {
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt) {
+    const int j = min(jt * 16 + col, Tk - 1);
+    const float* yr = y + (ybase + j) * ldy + 4 * g;
+    f4v yv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) yv[c] = ld4(yr + 16 * c);
+    f4v s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      s = mfma16(x[c].x, yv[c].x, s);
+      s = mfma16(x[c].y, yv[c].y, s);
+      s = mfma16(x[c].z, yv[c].z, s);
+      s = mfma16(x[c].w, yv[c].w, s);
+    }
+    acc[jt] = s;
+  }
+}
+
+// Forward row chain for accumulator row r of this lane (query i, keys 16 jt + col):
+// a = softmax, gg = graph, bm = a*gg, nrm = sum|bm| (all keys < Tk).
+template <int NJT>
+__device__ __forceinline__ float strip_row_forward(const f4v (&s)[NJT], int r, const float (&kf)[NJT],
+                                                   const float* grow, int Tk, int col,
+                                                   float (&aa)[NJT], float (&gg)[NJT],
+                                                   float (&bm)[NJT]) {
+  float x[NJT];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt) {
+    const int j = jt * 16 + col;
+    float v = -INFINITY;
+    if (j < Tk) v = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * 0.125f;
+    x[jt] = v;
+    mx = fmaxf(mx, v);
+  }
+  mx = row16_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt) {
+    const int j = jt * 16 + col;
+    const float e = j < Tk ? expf(x[jt] - mx) : 0.f;
+    x[jt] = e;
+    sum += e;
+  }
+  sum = row16_sum(sum);
+  float nrm = 0.f;
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt) {
+    const int j = jt * 16 + col;
+    aa[jt] = x[jt] / sum;
+    gg[jt] = j < Tk ? grow[j] : 0.f;
+    bm[jt] = gg[jt] * aa[jt];
+    nrm += fabsf(bm[jt]);
+  }
+  return row16_sum(nrm);
+}
+
+template <int NJT>
+__global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int bh = blockIdx.x;
+  const int b = bh / a.H, h = bh % a.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = w * 16;
+  constexpr int TK = NJT * 16;
+  constexpr int WLD = 20;                   // per-wave P^T image [TK][16 + 4]
+  float* Vs = sm;                           // [TK][ATT_KLD]
+  float* Pw = Vs + TK * ATT_KLD + w * TK * WLD;
+  // stage V (rows >= Tk zero)
+  for (int idx = threadIdx.x; idx < TK * 16; idx += blockDim.x) {
+    const int j = idx >> 4, c4 = (idx & 15) * 4;
+    f4v vv = {0.f, 0.f, 0.f, 0.f};
+    if (j < a.Tk) vv = ld4(a.v + ((int64_t)b * a.Tk + j) * a.ldv + h * ATT_DK + c4);
+    *reinterpret_cast<f4v*>(&Vs[j * ATT_KLD + c4]) = vv;
+  }
+  f4v qa[4];
+  {
+    const int iq = min(i0 + col, a.Tq - 1);
+    const float* qr = a.q + ((int64_t)b * a.Tq + iq) * a.ldq + h * ATT_DK + 4 * g;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) qa[c] = ld4(qr + 16 * c);
+  }
+  f4v s[NJT];
+  strip_dots<NJT>(qa, a.k + h * ATT_DK, a.ldk, (int64_t)b * a.Tk, a.Tk, col, g, s);
+  float kf[NJT];
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[(int64_t)b * a.Tk + min(jt * 16 + col, a.Tk - 1)];
+
+  f4v pv[NJT];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 4 * g + r;
+    const int ic = min(i, a.Tq - 1);
+    float aa[NJT], gg[NJT], bm[NJT];
+    const float nrm = strip_row_forward<NJT>(s, r, kf, a.G + ((int64_t)b * a.Tq + ic) * a.Tk, a.Tk,
+                                             col, aa, gg, bm);
+    const float sden = fmaxf(nrm, 1e-12f);
+    const float qf = a.qflag[(int64_t)b * a.Tq + ic];
+#pragma unroll
+    for (int jt = 0; jt < NJT; ++jt) {
+      const int j = jt * 16 + col;
+      const float n = bm[jt] / sden;
+      const bool ok = i < a.Tq && j < a.Tk;
+      if (a.att && ok) a.att[(((int64_t)h * a.B + b) * a.Tq + i) * a.Tk + j] = n;
+      pv[jt][r] = ok ? n * qf : 0.f;
+    }
+  }
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt)
+    *reinterpret_cast<f4v*>(&Pw[(jt * 16 + col) * WLD + 4 * g]) = pv[jt];
+  __syncthreads();  // V staged by all waves; P^T strip visible to this wave
+  // O strip = P V: A[m = i][k = j] = P^T[j][i], B[k = j][n = d] = V[j][d]
+  f4v o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int jc = 0; jc < NJT; ++jc) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = jc * 16 + 4 * g + t;
+      const float pa = Pw[j * WLD + col];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(pa, Vs[j * ATT_KLD + dt * 16 + col], o[dt]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 4 * g + r;
+    if (i < a.Tq) {
+      float* orow = a.o + ((int64_t)b * a.Tq + i) * a.ldo + h * ATT_DK + col;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) orow[dt * 16] = o[dt][r];
+    }
+  }
+}
+
+template <int NJT>
+__global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int bh = blockIdx.x;
+  const int b = bh / a.H, h = bh % a.H;
+  const int nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = w * 16;
+  constexpr int TK = NJT * 16;
+  const int PLD = 16 * nw + 4;
+  float* Pt = sm;             // [TK][PLD]  P^T
+  float* dSt = sm + TK * PLD; // [TK][PLD]  dS^T (scaled by 1/8, masked)
+  const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
+  const int hd = h * ATT_DK;
+
+  // ---- phase 1: strips
+  {
+    f4v qa[4], oa[4];
+    const int iq = min(i0 + col, a.Tq - 1);
+    const float* qr = a.q + (qb + iq) * a.ldq + hd + 4 * g;
+    const float* orr = a.dout + (qb + iq) * a.lddo + hd + 4 * g;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      qa[c] = ld4(qr + 16 * c);
+      oa[c] = ld4(orr + 16 * c);
+    }
+    f4v s[NJT], dp[NJT];
+    strip_dots<NJT>(qa, a.k + hd, a.ldk, kb, a.Tk, col, g, s);
+    strip_dots<NJT>(oa, a.v + hd, a.ldv, kb, a.Tk, col, g, dp);
+    float kf[NJT];
+#pragma unroll
+    for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[kb + min(jt * 16 + col, a.Tk - 1)];
+    f4v pv[NJT], dsv[NJT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * g + r;
+      const int ic = min(i, a.Tq - 1);
+      float aa[NJT], gg[NJT], bm[NJT];
+      const float nrm = strip_row_forward<NJT>(s, r, kf, a.G + (qb + ic) * a.Tk, a.Tk, col, aa, gg, bm);
+      const float sden = fmaxf(nrm, 1e-12f);
+      const float qf = a.qflag[qb + ic];
+      float dn[NJT], t1 = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        dn[jt] = dp[jt][r] * qf;
+        t1 += dn[jt] * bm[jt];
+      }
+      t1 = row16_sum(t1);
+      const float dnrm = nrm >= 1e-12f ? -t1 / (sden * sden) : 0.f;
+      float da[NJT], t2 = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        const float sg = bm[jt] > 0.f ? 1.f : (bm[jt] < 0.f ? -1.f : 0.f);
+        const float dbm = dn[jt] / sden + dnrm * sg;
+        da[jt] = dbm * gg[jt];
+        t2 += da[jt] * aa[jt];
+      }
+      t2 = row16_sum(t2);
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        const int j = jt * 16 + col;
+        const bool ok = i < a.Tq && j < a.Tk;
+        float ds = aa[jt] * (da[jt] - t2);
+        if (kf[jt] == 0.f) ds = 0.f;
+        dsv[jt][r] = ok ? ds * 0.125f : 0.f;
+        pv[jt][r] = ok ? bm[jt] / sden * qf : 0.f;
+      }
+    }
+#pragma unroll
+    for (int jt = 0; jt < NJT; ++jt) {
+      *reinterpret_cast<f4v*>(&Pt[(jt * 16 + col) * PLD + i0 + 4 * g]) = pv[jt];
+      *reinterpret_cast<f4v*>(&dSt[(jt * 16 + col) * PLD + i0 + 4 * g]) = dsv[jt];
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: output tiles. items [0, 4NJT): dV, [4NJT, 8NJT): dK, [8NJT, 8NJT + 4nw): dQ
+  const int nitems = 8 * NJT + 4 * nw;
+  for (int it = w; it < nitems; it += nw) {
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+    if (it < 8 * NJT) {
+      const bool isv = it < 4 * NJT;
+      const int t2 = isv ? it : it - 4 * NJT;
+      const int jt = t2 >> 2, dt = t2 & 3;
+      const float* img = isv ? Pt : dSt;
+      const float* src = isv ? a.dout : a.q;
+      const int64_t lds = isv ? a.lddo : a.ldq;
+      const float* arow = img + (jt * 16 + col) * PLD + 4 * g;
+      for (int ic = 0; ic < nw; ++ic) {
+        const f4v av = ld4(arow + ic * 16);
+        float bv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int i = min(ic * 16 + 4 * g + t, a.Tq - 1);
+          bv[t] = src[(qb + i) * lds + hd + dt * 16 + col];
+        }
+        acc = mfma16(av.x, bv[0], acc);
+        acc = mfma16(av.y, bv[1], acc);
+        acc = mfma16(av.z, bv[2], acc);
+        acc = mfma16(av.w, bv[3], acc);
+      }
+      // dV / dK rows j = 16 jt + 4g + r, ReLU mask of the saved V / K
+      const float* msrc = isv ? a.v : a.k;
+      const int64_t mld = isv ? a.ldv : a.ldk;
+      float* dst = isv ? a.dv : a.dk;
+      const int64_t dld = isv ? a.lddv : a.lddk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = jt * 16 + 4 * g + r;
+        if (j < a.Tk) {
+          const int d = hd + dt * 16 + col;
+          dst[(kb + j) * dld + d] = msrc[(kb + j) * mld + d] > 0.f ? acc[r] : 0.f;
+        }
+      }
+    } else {
+      const int t2 = it - 8 * NJT;
+      const int itile = t2 >> 2, dt = t2 & 3;
+#pragma unroll
+      for (int jc = 0; jc < NJT; ++jc) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = jc * 16 + 4 * g + t;
+          av[t] = dSt[j * PLD + itile * 16 + col];
+          bv[t] = a.k[(kb + min(j, a.Tk - 1)) * a.ldk + hd + dt * 16 + col];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc = mfma16(av[t], bv[t], acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = itile * 16 + 4 * g + r;
+        if (i < a.Tq) {
+          const int d = hd + dt * 16 + col;
+          a.dq[(qb + i) * a.lddq + d] = a.q[(qb + i) * a.ldq + d] > 0.f ? acc[r] : 0.f;
+        }
+      }
+    }
+  }
+}
+
 static size_t fwd_lds(int Tk, int KB) {
   return sizeof(float) * ((size_t)2 * Tk * ATT_KLD + 4 * ATT_RB * KB * 64 + 4 * ATT_RB * ATT_DK);
 }
@@ -332,7 +663,24 @@ static int validate(const AttnArgs& a, int64_t dk, const char* who) {
   const uintptr_t al = (uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v;
   if ((al & 15) || (a.ldk & 3) || (a.ldv & 3))
     return fail(SAVQA_EINVAL, std::string(who) + ": K/V must be 16-B aligned with ld % 4 == 0");
+  if (a.Tq > 128) return fail(SAVQA_EUNSUP, std::string(who) + ": Tq > 128 not supported yet");
+  if (a.ldq & 3 || ((uintptr_t)a.q & 15))
+    return fail(SAVQA_EINVAL, std::string(who) + ": Q must be 16-B aligned with ld % 4 == 0");
   return 0;
+}
+
+// Path choice: the MFMA strip kernels (default) or the row kernels (lane per key),
+// overridable with SAVQA_ATTN_PATH=rows|mfma for A/B timing.
+static bool use_mfma(const AttnArgs& a) {
+  static const int forced = [] {
+    const char* e = getenv("SAVQA_ATTN_PATH");
+    if (!e) return 0;
+    return std::string(e) == "rows" ? 1 : (std::string(e) == "mfma" ? 2 : 0);
+  }();
+  if (forced) return forced == 2;
+  // a single query row (the decoder cross-attention) would fill 1/16 of each MFMA tile:
+  // the lane-per-key kernels win there (76 vs 102 us bwd at B*H = 2048, Tk = 73)
+  return a.Tq >= 8;
 }
 
 }  // namespace savqa
@@ -350,7 +698,19 @@ extern "C" int savqa_gattn_fwd(void* stream, const float* q, int64_t ldq, const 
   a.o = o; a.ldo = ldo; a.att = att;
   if (int rc = validate(a, dk, "savqa_gattn_fwd")) return rc;
   hipStream_t s = as_stream(stream);
-  if (Tk <= 64) {
+  if (use_mfma(a)) {
+    const int njt = (int)((Tk + 15) / 16), nw = (int)((Tq + 15) / 16);
+    const size_t lds = sizeof(float) * ((size_t)njt * 16 * ATT_KLD + (size_t)nw * njt * 16 * 20);
+    switch (njt) {
+#define SAVQA_FWD_CASE(N)                                                                  \
+  case N:                                                                                  \
+    hipLaunchKernelGGL(gattn_fwd_mfma_kernel<N>, dim3(B * H), dim3(64 * nw), lds, s, a);   \
+    break;
+      SAVQA_FWD_CASE(1) SAVQA_FWD_CASE(2) SAVQA_FWD_CASE(3) SAVQA_FWD_CASE(4)
+      SAVQA_FWD_CASE(5) SAVQA_FWD_CASE(6) SAVQA_FWD_CASE(7) SAVQA_FWD_CASE(8)
+#undef SAVQA_FWD_CASE
+    }
+  } else if (Tk <= 64) {
     const size_t lds = fwd_lds((int)Tk, 1);
     hipLaunchKernelGGL(gattn_fwd_kernel<1>, dim3(B * H), dim3(256), lds, s, a);
   } else {
@@ -372,9 +732,25 @@ extern "C" int savqa_gattn_bwd(void* stream, const float* q, int64_t ldq, const 
   a.dout = dout; a.lddo = lddo; a.dq = dq; a.lddq = lddq; a.dk = dk_; a.lddk = lddk;
   a.dv = dv; a.lddv = lddv;
   if (int rc = validate(a, dk, "savqa_gattn_bwd")) return rc;
+  hipStream_t s = as_stream(stream);
+  if (use_mfma(a)) {
+    if ((a.ldq & 3) || (a.lddo & 3) || (((uintptr_t)a.dout) & 15))
+      return fail(SAVQA_EINVAL, "savqa_gattn_bwd: Q/dO must be 16-B aligned with ld % 4 == 0");
+    const int njt = (int)((Tk + 15) / 16), nw = (int)((Tq + 15) / 16);
+    const size_t lds = sizeof(float) * 2 * (size_t)njt * 16 * (16 * nw + 4);
+    switch (njt) {
+#define SAVQA_BWD_CASE(N)                                                                  \
+  case N:                                                                                  \
+    hipLaunchKernelGGL(gattn_bwd_mfma_kernel<N>, dim3(B * H), dim3(64 * nw), lds, s, a);   \
+    break;
+      SAVQA_BWD_CASE(1) SAVQA_BWD_CASE(2) SAVQA_BWD_CASE(3) SAVQA_BWD_CASE(4)
+      SAVQA_BWD_CASE(5) SAVQA_BWD_CASE(6) SAVQA_BWD_CASE(7) SAVQA_BWD_CASE(8)
+#undef SAVQA_BWD_CASE
+    }
+    return check_launch("savqa_gattn_bwd");
+  }
   const size_t lds = bwd_lds((int)Tq, (int)Tk);
   if (lds > kMaxLds) return fail(SAVQA_EUNSUP, "savqa_gattn_bwd: Tq*Tk too large for the LDS path");
-  hipStream_t s = as_stream(stream);
   if (Tk <= 64)
     hipLaunchKernelGGL(gattn_bwd_kernel<1>, dim3(B * H), dim3(256), lds, s, a);
   else

@@ -158,7 +158,10 @@ def _attn_ref(Q, K, V, G, kf, qf, h=8):
 
 
 @pytest.mark.parametrize("B,Tq,Tk,kind", [(3, 50, 50, "self"), (2, 73, 73, "self"),
-                                           (5, 1, 73, "cross"), (2, 20, 100, "self")])
+                                           (5, 1, 73, "cross"), (2, 20, 100, "self"),
+                                           (2, 128, 128, "self"), (3, 17, 33, "cross"),
+                                           (4, 1, 50, "cross"), (2, 16, 16, "self"),
+                                           (1, 5, 3, "cross"), (2, 100, 7, "cross")])
 def test_graph_attention_fwd_bwd(B, Tq, Tk, kind):
     O = ops()
     H, D = 8, 512
