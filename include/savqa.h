@@ -46,7 +46,11 @@ const char* savqa_last_error(void);
  *   v = (mask && !(mask[mr*ldmask+n] > 0)) ? 0 : v   mr = mask_arows ? a_rows[m] : m
  *   v += resid[m*ldr + n]
  *   C = atomic ? C + v (atomicAdd) : v + beta*C
- * split_k > 1 splits K across workgroups and forces atomic accumulation.
+ * split_k > 1 splits K across workgroups and forces atomic accumulation; split_k < 0
+ * (requires atomic=1) lets the library pick the split from the tile count and CU count.
+ * Non-atomic launches with a linear epilogue (relu=0, beta=0, C not aliasing resid) may
+ * split the last partial wave of tiles over K internally (zero-fill + atomics): results
+ * then differ from a single-pass launch only in fp32 summation order.
  * ------------------------------------------------------------------------ */
 typedef struct savqa_gemm_desc {
     int64_t M, N, K;
@@ -67,6 +71,10 @@ typedef struct savqa_gemm_desc {
 } savqa_gemm_desc;
 
 int savqa_gemm(void* stream, const savqa_gemm_desc* d);
+
+/* The launch plan savqa_gemm would use for *d (no launch): out[0] = tile (64|128),
+ * out[1] = split-K factor, out[2] = tail split factor (0: none), out[3] = workgroups. */
+int savqa_gemm_plan(const savqa_gemm_desc* d, int32_t* out);
 
 /* out[c] += sum_r X[r*ldx + c]  (bias gradients of every Linear above) */
 int savqa_colsum_acc(void* stream, const float* X, int64_t rows, int64_t cols, int64_t ldx, float* out);

@@ -42,6 +42,7 @@ class GemmDesc(C.Structure):
 _SIGS = {
     "savqa_version": [],
     "savqa_gemm": [c_p, C.POINTER(GemmDesc)],
+    "savqa_gemm_plan": [C.POINTER(GemmDesc), c_p],
     "savqa_colsum_acc": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
     "savqa_ln_fwd": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p],
     "savqa_ln_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p],

@@ -204,9 +204,16 @@ __device__ __forceinline__ void gemm_mainloop(
 #undef SAVQA_GEMM_LOAD
 }
 
+// Block -> (tile, k range). Blocks [0, full) own whole tiles (or split-K slices along
+// blockIdx.y); blocks [full, gridDim.x) are the "tail": tiles [tail_t0, T) each cut into
+// tail_f k-slices so the last partial wave of tiles spreads over every CU.
+struct GemmGrid {
+  int tiles_n, full, tail_t0, tail_f;
+  int64_t kchunk, tail_kchunk;
+};
+
 template <int BM, int BN, int BK, bool AT, bool BT>
-__global__ __launch_bounds__(GEMM_NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_f32_kernel(savqa_gemm_desc d, int tiles_m,
-                                                             int tiles_n, int64_t kchunk,
+__global__ __launch_bounds__(GEMM_NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_f32_kernel(savqa_gemm_desc d, GemmGrid gg,
                                                              int avec, int bvec) {
   using G = GemmCfg<BM, BN, BK, AT, BT>;
   constexpr int FM = G::FM, FN = G::FN, WM = G::WM, WN = G::WN;
@@ -215,14 +222,29 @@ __global__ __launch_bounds__(GEMM_NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
 
-  const int nblk = tiles_m * tiles_n;
-  const int t = xcd_remap(blockIdx.x, nblk);
-  const int tn = t % tiles_n;
-  const int tm = t / tiles_n;
+  const int bid = blockIdx.x;
+  int t;
+  int64_t kbeg, kend;
+  bool first_split, atomic;
+  if (bid < gg.full) {
+    t = xcd_remap(bid, gg.full);
+    kbeg = (int64_t)blockIdx.y * gg.kchunk;
+    kend = min(d.K, kbeg + gg.kchunk);
+    first_split = blockIdx.y == 0;
+    atomic = d.atomic || gridDim.y > 1;
+  } else {
+    const int u = bid - gg.full;
+    const int part = u % gg.tail_f;
+    t = gg.tail_t0 + u / gg.tail_f;
+    kbeg = (int64_t)part * gg.tail_kchunk;
+    kend = min(d.K, kbeg + gg.tail_kchunk);
+    first_split = part == 0;
+    atomic = true;
+  }
+  const int tn = t % gg.tiles_n;
+  const int tm = t / gg.tiles_n;
   const int64_t m0 = (int64_t)tm * BM;
   const int64_t n0 = (int64_t)tn * BN;
-  const int64_t kbeg = (int64_t)blockIdx.y * kchunk;
-  const int64_t kend = min(d.K, kbeg + kchunk);
 
   f32x16 acc[FM][FN];
 #pragma unroll
@@ -246,8 +268,6 @@ __global__ __launch_bounds__(GEMM_NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
   }
 
   // ---------------------------------------------------------------- epilogue
-  const bool first_split = blockIdx.y == 0;
-  const bool atomic = d.atomic || gridDim.y > 1;
   const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
   const uint32_t cg = (uint32_t)d.c_group;
 #pragma unroll
@@ -295,25 +315,40 @@ __global__ __launch_bounds__(GEMM_NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
   }
 }
 
-template <int BM, int BN, int BK, bool AT, bool BT>
-static void launch_gemm(const savqa_gemm_desc& d, hipStream_t s, int split, int avec, int bvec) {
-  const int tm = (int)((d.M + BM - 1) / BM);
-  const int tn = (int)((d.N + BN - 1) / BN);
-  int64_t kchunk = (d.K + split - 1) / split;
-  kchunk = (kchunk + BK - 1) / BK * BK;
-  const int nsplit = kchunk > 0 ? (int)((d.K + kchunk - 1) / kchunk) : 1;
-  dim3 grid(tm * tn, nsplit > 0 ? nsplit : 1);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, AT, BT>), grid, dim3(GEMM_NT), 0, s, d, tm, tn,
-                     kchunk, avec, bvec);
+static int slots_per_launch() {
+  // 2 workgroups per CU (launch bounds / LDS); the CU count of the current device
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 512;
+  if (!cached[dev]) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    cached[dev] = 2 * cus;
+  }
+  return cached[dev];
 }
 
-template <int BM, int BN, int BK>
-static void dispatch_layout(const savqa_gemm_desc& d, hipStream_t s, int split, int avec, int bvec) {
-  if (!d.a_trans && d.b_trans) launch_gemm<BM, BN, BK, false, true>(d, s, split, avec, bvec);
-  else if (!d.a_trans && !d.b_trans) launch_gemm<BM, BN, BK, false, false>(d, s, split, avec, bvec);
-  else if (d.a_trans && !d.b_trans) launch_gemm<BM, BN, BK, true, false>(d, s, split, avec, bvec);
-  else launch_gemm<BM, BN, BK, true, true>(d, s, split, avec, bvec);
+// split-K factor minimising  rounds(s) * (k-tiles per slice + per-block overhead)
+static int auto_split(int64_t tiles, int64_t K, int BK, int slots) {
+  const int64_t nch = (K + BK - 1) / BK;
+  int best = 1;
+  int64_t best_cost = INT64_MAX;
+  for (int s = 1; s <= 64 && (s == 1 || nch / s >= 8); ++s) {
+    const int64_t rounds = (tiles * s + slots - 1) / slots;
+    const int64_t cost = rounds * ((nch + s - 1) / s + 4);
+    if (cost < best_cost) { best_cost = cost; best = s; }
+  }
+  return best;
 }
+
+// Launch plan: tile size, split-K, tail split (shared by savqa_gemm / savqa_gemm_plan).
+struct GemmPlan {
+  int tile, split;
+  GemmGrid gg;
+  int grid_x, nsplit;
+  int64_t zero_row0;  // >= 0: rows [zero_row0, M) of C are zero-filled before the launch
+};
 
 }  // namespace savqa
 
@@ -321,27 +356,115 @@ using namespace savqa;
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
-  if (!dp) return fail(SAVQA_EINVAL, "savqa_gemm: null descriptor");
-  savqa_gemm_desc d = *dp;
+static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.M < 0 || d.N < 0 || d.K < 0) return fail(SAVQA_EINVAL, "savqa_gemm: negative dims");
-  if (d.M == 0 || d.N == 0) return 0;
-  if (!d.A || !d.B || !d.C) return fail(SAVQA_EINVAL, "savqa_gemm: null operand");
   if (d.M >= (1LL << 31) || d.N >= (1LL << 31)) return fail(SAVQA_EUNSUP, "savqa_gemm: M/N >= 2^31");
   if (d.mask && d.mask_arows && (d.a_trans || !d.a_rows))
     return fail(SAVQA_EINVAL, "savqa_gemm: mask_arows needs a_trans=0 and a_rows");
   if (d.c_group <= 0) { d.c_group = d.M; d.c_stride = d.M; }
   if (d.rowvec && d.rowvec_period <= 0) return fail(SAVQA_EINVAL, "savqa_gemm: rowvec_period");
+  if (d.split_k < 0 && !d.atomic) return fail(SAVQA_EINVAL, "savqa_gemm: auto split-K needs atomic=1");
+  constexpr int BK = 32;
+  const int slots = slots_per_launch();
+  const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
   int split = d.split_k > 1 ? d.split_k : 1;
+  if (d.split_k < 0) split = auto_split(tiles128, d.K, BK, slots);
+  // 128x128 tiles once there is enough parallelism (split-K counts), else 64x64
+  p.tile = tiles128 * split >= 160 ? 128 : 64;
+  const int tm = (int)((d.M + p.tile - 1) / p.tile);
+  const int tn = (int)((d.N + p.tile - 1) / p.tile);
+  const int T = tm * tn;
+  int64_t kchunk = (d.K + split - 1) / split;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  p.nsplit = kchunk > 0 ? (int)((d.K + kchunk - 1) / kchunk) : 1;
+  if (p.nsplit < 1) p.nsplit = 1;
+  p.split = p.nsplit;
+  p.gg.tiles_n = tn;
+  p.gg.kchunk = kchunk;
+  p.gg.full = T;
+  p.gg.tail_t0 = T;
+  p.gg.tail_f = 1;
+  p.gg.tail_kchunk = kchunk;
+  p.grid_x = T;
+  p.zero_row0 = -1;
+  // tail split: linear epilogue, identity row map, plain store, C not overlapping resid
+  const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
+  bool tail_ok = p.tile == 128 && !d.atomic && p.nsplit == 1 && !d.relu && d.beta == 0.f &&
+                 ident && d.ldc >= d.N;
+  if (tail_ok && d.resid) {
+    const char* c0 = (const char*)d.C;
+    const char* c1 = (const char*)(d.C + (d.M - 1) * d.ldc + d.N);
+    const char* r0 = (const char*)d.resid;
+    const char* r1 = (const char*)(d.resid + (d.M - 1) * d.ldr + d.N);
+    if (r0 < c1 && c0 < r1) tail_ok = false;
+  }
+  if (tail_ok && T > slots) {
+    const int64_t nch = (d.K + BK - 1) / BK;
+    int r = T % slots;
+    r = (r + tn - 1) / tn * tn;  // whole rows of tiles: one contiguous zero-fill
+    if (r > 0 && r < T) {
+      int f = slots / r;
+      if (f > nch / 4) f = (int)(nch / 4);
+      if (f >= 2) {
+        p.gg.full = T - r;
+        p.gg.tail_t0 = T - r;
+        p.gg.tail_f = f;
+        const int64_t tk = (d.K + f - 1) / f;
+        p.gg.tail_kchunk = (tk + BK - 1) / BK * BK;
+        p.grid_x = p.gg.full + r * f;
+        p.zero_row0 = (int64_t)(p.gg.tail_t0 / tn) * p.tile;
+      }
+    }
+  }
+  return 0;
+}
+
+template <int BM, int BN, int BK, bool AT, bool BT>
+static void launch_gemm(const savqa_gemm_desc& d, const GemmPlan& p, hipStream_t s, int avec,
+                        int bvec) {
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, AT, BT>), dim3(p.grid_x, p.nsplit), dim3(GEMM_NT),
+                     0, s, d, p.gg, avec, bvec);
+}
+
+template <int BM, int BN, int BK>
+static void dispatch_layout(const savqa_gemm_desc& d, const GemmPlan& p, hipStream_t s, int avec,
+                            int bvec) {
+  if (!d.a_trans && d.b_trans) launch_gemm<BM, BN, BK, false, true>(d, p, s, avec, bvec);
+  else if (!d.a_trans && !d.b_trans) launch_gemm<BM, BN, BK, false, false>(d, p, s, avec, bvec);
+  else if (d.a_trans && !d.b_trans) launch_gemm<BM, BN, BK, true, false>(d, p, s, avec, bvec);
+  else launch_gemm<BM, BN, BK, true, true>(d, p, s, avec, bvec);
+}
+
+extern "C" int savqa_gemm_plan(const savqa_gemm_desc* dp, int32_t* out) {
+  if (!dp || !out) return fail(SAVQA_EINVAL, "savqa_gemm_plan: null argument");
+  savqa_gemm_desc d = *dp;
+  GemmPlan p{};
+  if (int rc = plan_gemm(d, p)) return rc;
+  out[0] = p.tile;
+  out[1] = p.split;
+  out[2] = p.gg.tail_f > 1 ? p.gg.tail_f : 0;
+  out[3] = p.grid_x * p.nsplit;
+  return 0;
+}
+
+extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
+  if (!dp) return fail(SAVQA_EINVAL, "savqa_gemm: null descriptor");
+  savqa_gemm_desc d = *dp;
+  if (d.M == 0 || d.N == 0) return 0;
+  if (!d.A || !d.B || !d.C) return fail(SAVQA_EINVAL, "savqa_gemm: null operand");
+  GemmPlan p{};
+  if (int rc = plan_gemm(d, p)) return rc;
   const int avec = (d.lda % 4 == 0) && aligned16(d.A);
   const int bvec = (d.ldb % 4 == 0) && aligned16(d.B);
   hipStream_t s = as_stream(stream);
-  // 128x128 tiles once there is enough parallelism (split-K counts), else 64x64
-  const int64_t big_tiles = ((d.M + 127) / 128) * ((d.N + 127) / 128) * split;
-  if (big_tiles >= 160)
-    dispatch_layout<128, 128, 32>(d, s, split, avec, bvec);
+  if (p.zero_row0 >= 0 &&
+      hipMemset2DAsync(d.C + p.zero_row0 * d.ldc, d.ldc * sizeof(float), 0, d.N * sizeof(float),
+                       d.M - p.zero_row0, s) != hipSuccess)
+    return fail(SAVQA_EUNSUP, "savqa_gemm: tail zero-fill failed");
+  if (p.tile == 128)
+    dispatch_layout<128, 128, 32>(d, p, s, avec, bvec);
   else
-    dispatch_layout<64, 64, 32>(d, s, split, avec, bvec);
+    dispatch_layout<64, 64, 32>(d, p, s, avec, bvec);
   return check_launch("savqa_gemm");
 }
 

@@ -44,10 +44,11 @@ class GemmProbe:
         self.records = []  # (variant, flops, start_event, end_event)
 
     @staticmethod
-    def variant(M, N, a_trans, b_trans, split):
-        big = ((M + 127) // 128) * ((N + 127) // 128) * split >= 160
-        tile = 128 if big else 64
-        return f"gemm_f32_kernel<{tile},{tile},{str(bool(a_trans)).lower()},{str(bool(b_trans)).lower()}>"
+    def variant(d):
+        plan = (C.c_int32 * 4)()
+        call("savqa_gemm_plan", C.byref(d), C.cast(plan, C.c_void_p))
+        return (f"gemm_f32_kernel<{plan[0]},{plan[0]},{str(bool(d.a_trans)).lower()},"
+                f"{str(bool(d.b_trans)).lower()}>")
 
     def summary(self):
         torch.cuda.synchronize()
@@ -99,7 +100,7 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
     e0.record()
     call("savqa_gemm", _stream(), C.byref(d))
     e1.record()
-    _probe.records.append((GemmProbe.variant(M, N, a_trans, b_trans, max(1, split_k)),
+    _probe.records.append((GemmProbe.variant(d),
                            2.0 * M * N * K, e0, e1))
 
 
@@ -126,22 +127,13 @@ def linear_dx(dY: Tensor, W: Tensor, dX: Tensor, *, rows: int, a_rows=None, mask
          atomic=atomic, beta=beta)
 
 
-def _split_for(m_out: int, n_out: int, k: int) -> int:
-    """split-K factor for the dW GEMMs (reduction over all B*T rows): enough 128x128
-    tiles x splits to give every CU ~2 workgroups, each split >= 8 k-tiles of 32."""
-    tiles = ((m_out + 127) // 128) * ((n_out + 127) // 128)
-    want = max(1, -(-512 // tiles))
-    return int(max(1, min(want, k // 256)))
-
-
 def linear_dw(dY: Tensor, X: Tensor, dW: Tensor, db: Optional[Tensor], *, rows: int,
               x_rows=None, lddy=None, ldx=None):
     """dW += dY^T X ; db += colsum(dY)   (accumulating into the grad arena)."""
     N, K = dW.shape
-    split = _split_for(N, K, rows)
     gemm(dY, X, dW, N, K, rows, lda=lddy if lddy is not None else N,
          ldb=ldx if ldx is not None else K, ldc=K, a_trans=True, b_rows=x_rows, atomic=True,
-         split_k=split)
+         split_k=-1)  # library picks the split-K factor
     if db is not None:
         colsum_acc(dY, rows, N, lddy if lddy is not None else N, db)
 

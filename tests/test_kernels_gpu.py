@@ -93,6 +93,35 @@ def test_gemm_dx_dw(M, N, K):
     assert rel(dW2, dY.t() @ table[idx]) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(16640, 512, 512), (16600, 512, 2048), (18688, 512, 1536)])
+def test_gemm_tail_split(M, N, K):
+    """More 128x128 tiles than one wave of workgroups: the partial last wave is split
+    over K (zero-fill + atomics) when the epilogue is linear; relu/beta keep one pass."""
+    O = ops()
+    X, W, b = g(M, K, seed=30), g(N, K, seed=31), g(N, seed=32)
+    res = g(M, N, seed=33)
+    H = g(M, N, seed=34, relu=True)
+    out = torch.full((M, N), float("nan"), device=dev)
+    O.gemm(X, W, out, M, N, K, lda=K, ldb=K, ldc=N, b_trans=True, bias=b, resid=res, ldr=N,
+           mask=H, ldmask=N)
+    ref = (X.double() @ W.double().t() + b.double()) * (H > 0).double() + res.double()
+    tol = 1e-5  # fp32 accumulation over K <= 2048 against an fp64 reference
+    assert rel(out, ref) < tol
+    out2 = torch.full((M, N), float("nan"), device=dev)
+    O.linear(X, W, b, out2, relu=True)
+    assert rel(out2, torch.relu(X.double() @ W.double().t() + b.double())) < tol
+
+
+@pytest.mark.parametrize("N,K,rows", [(1536, 512, 18688), (6144, 512, 18688), (512, 2048, 12800)])
+def test_gemm_dw_auto_split(N, K, rows):
+    O = ops()
+    dY, X = g(rows, N, seed=35), g(rows, K, seed=36)
+    dW = g(N, K, seed=37)
+    dW0 = dW.clone()
+    O.linear_dw(dY, X, dW, None, rows=rows)
+    assert rel(dW, dW0.double() + dY.double().t() @ X.double()) < 1e-5
+
+
 def test_gemm_mask_arows_rowscale():
     O = ops()
     M, N, K = 50, 96, 64

@@ -51,9 +51,8 @@ def main():
             A = torch.randn(k, m, device=dev)
             X = torch.randn(k, n, device=dev)
             C = torch.zeros(m, n, device=dev)
-            split = ops._split_for(m, n, k)
             f = lambda: ops.gemm(A, X, C, m, n, k, lda=m, ldb=n, ldc=n, a_trans=True, atomic=True,
-                                 split_k=split)
+                                 split_k=-1)
             g = lambda: torch.mm(A.t(), X, out=C)
         t1 = timeit(f)
         t2 = timeit(g)
