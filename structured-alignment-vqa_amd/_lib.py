@@ -77,11 +77,14 @@ class SavqaError(RuntimeError):
     pass
 
 
-def load(path: str = LIB_PATH):
-    """Load libsavqa.so and bind every declared entry point (raises if absent)."""
+def load(path: str = None):
+    """Load libsavqa.so and bind every declared entry point (raises if absent).
+    SAVQA_LIB overrides the path (A/B timing of alternative builds of the same ABI)."""
     global _lib
     if _lib is not None:
         return _lib
+    if path is None:
+        path = os.environ.get("SAVQA_LIB", LIB_PATH)
     if not os.path.exists(path):
         raise SavqaError(f"libsavqa.so not built ({path}); run __graft_entry__.build() "
                          "or `make -C structured-alignment-vqa_amd/csrc`")

@@ -24,6 +24,13 @@
 // per k-tile, XCD-aware block order (T1).
 #include "common.h"
 
+#ifndef SAVQA_GEMM_OCC
+#define SAVQA_GEMM_OCC 2  // workgroups (= waves per SIMD) per CU
+#endif
+#ifndef SAVQA_GEMM_BK
+#define SAVQA_GEMM_BK 16  // k-tile; 16 beats 32 on the K=512 step shapes (shorter prologue)
+#endif
+
 namespace savqa {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -138,20 +145,28 @@ __device__ __forceinline__ void gemm_compute_tile(
     const float* __restrict__ As, const float* __restrict__ Bs, int wm, int wn, int lane,
     f32x16 (&acc)[GemmCfg<BM, BN, BK, AT, BT>::FM][GemmCfg<BM, BN, BK, AT, BT>::FN]) {
   using G = GemmCfg<BM, BN, BK, AT, BT>;
+  // operands of 8-k chunk c+1 are read from LDS while chunk c's MFMAs run
+  float a[2][G::FM][4], b[2][G::FN][4];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) G::OA::fetch(As, wm * G::WM, i, 0, lane, a[0][i]);
+#pragma unroll
+  for (int j = 0; j < G::FN; ++j) G::OB::fetch(Bs, wn * G::WN, j, 0, lane, b[0][j]);
 #pragma unroll
   for (int c = 0; c < BK / 8; ++c) {
-    float a[G::FM][4], b[G::FN][4];
+    const int cur = c & 1;
+    if (c + 1 < BK / 8) {
 #pragma unroll
-    for (int i = 0; i < G::FM; ++i) G::OA::fetch(As, wm * G::WM, i, c, lane, a[i]);
+      for (int i = 0; i < G::FM; ++i) G::OA::fetch(As, wm * G::WM, i, c + 1, lane, a[cur ^ 1][i]);
 #pragma unroll
-    for (int j = 0; j < G::FN; ++j) G::OB::fetch(Bs, wn * G::WN, j, c, lane, b[j]);
+      for (int j = 0; j < G::FN; ++j) G::OB::fetch(Bs, wn * G::WN, j, c + 1, lane, b[cur ^ 1][j]);
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int i = 0; i < G::FM; ++i)
 #pragma unroll
         for (int j = 0; j < G::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][i][s], b[cur][j][s], acc[i][j], 0, 0, 0);
   }
 }
 
@@ -213,7 +228,7 @@ struct GemmGrid {
 };
 
 template <int BM, int BN, int BK, bool AT, bool BT>
-__global__ __launch_bounds__(GEMM_NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_f32_kernel(savqa_gemm_desc d, GemmGrid gg,
+__global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_waves_per_eu(SAVQA_GEMM_OCC, SAVQA_GEMM_OCC))) void gemm_f32_kernel(savqa_gemm_desc d, GemmGrid gg,
                                                              int avec, int bvec) {
   using G = GemmCfg<BM, BN, BK, AT, BT>;
   constexpr int FM = G::FM, FN = G::FN, WM = G::WM, WN = G::WN;
@@ -324,7 +339,7 @@ static int slots_per_launch() {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
-    cached[dev] = 2 * cus;
+    cached[dev] = SAVQA_GEMM_OCC * cus;
   }
   return cached[dev];
 }
@@ -364,7 +379,7 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.c_group <= 0) { d.c_group = d.M; d.c_stride = d.M; }
   if (d.rowvec && d.rowvec_period <= 0) return fail(SAVQA_EINVAL, "savqa_gemm: rowvec_period");
   if (d.split_k < 0 && !d.atomic) return fail(SAVQA_EINVAL, "savqa_gemm: auto split-K needs atomic=1");
-  constexpr int BK = 32;
+  constexpr int BK = SAVQA_GEMM_BK;
   const int slots = slots_per_launch();
   const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
   int split = d.split_k > 1 ? d.split_k : 1;
@@ -462,7 +477,7 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
                        d.M - p.zero_row0, s) != hipSuccess)
     return fail(SAVQA_EUNSUP, "savqa_gemm: tail zero-fill failed");
   if (p.tile == 128)
-    dispatch_layout<128, 128, 32>(d, p, s, avec, bvec);
+    dispatch_layout<128, 128, SAVQA_GEMM_BK>(d, p, s, avec, bvec);
   else
     dispatch_layout<64, 64, 32>(d, p, s, avec, bvec);
   return check_launch("savqa_gemm");

@@ -33,6 +33,11 @@ def main():
              ("dx qkv", "NN", M, 512, 1536), ("dx kv", "NN", M, 512, 6144),
              ("dw qkv", "TN", 1536, 512, M), ("dw ffn1", "TN", 2048, 512, M),
              ("dw ffn2", "TN", 512, 2048, M), ("dw kv", "TN", 6144, 512, M)]
+    if len(sys.argv) > 1:  # custom shapes: LAYOUT:M:N:K ...
+        cases = []
+        for a in sys.argv[1:]:
+            lay, m, n, k = a.split(":")
+            cases.append((a, lay, int(m), int(n), int(k)))
     for name, lay, m, n, k in cases:
         fl = 2.0 * m * n * k
         if lay == "NT":
