@@ -68,6 +68,7 @@ typedef struct savqa_gemm_desc {
     const float* rowscale;
     float alpha, beta;
     int32_t relu, atomic, split_k, _pad2;
+    float* colsum_a;   /* optional, a_trans=1 only: colsum_a[m] += sum_k A(m,k) (bias grad) */
 } savqa_gemm_desc;
 
 int savqa_gemm(void* stream, const savqa_gemm_desc* d);

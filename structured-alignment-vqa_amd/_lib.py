@@ -35,6 +35,7 @@ class GemmDesc(C.Structure):
         ("rowscale", c_p),
         ("alpha", c_f), ("beta", c_f),
         ("relu", c_i32), ("atomic", c_i32), ("split_k", c_i32), ("_pad2", c_i32),
+        ("colsum_a", c_p),
     ]
 
 

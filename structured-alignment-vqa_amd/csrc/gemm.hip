@@ -109,6 +109,11 @@ struct Operand {
     }
   }
 
+  __device__ __forceinline__ void accum(f4 (&cs)[ITERS]) const {
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) cs[it] += r[it];
+  }
+
   __device__ __forceinline__ void store(float* __restrict__ s, int tid) const {
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
@@ -174,7 +179,8 @@ template <int BM, int BN, int BK, bool AT, bool BT, bool FAST>
 __device__ __forceinline__ void gemm_mainloop(
     const savqa_gemm_desc& d, float* smem, int64_t m0, int64_t n0, int64_t kbeg, int64_t kend,
     int ntiles,
-    f32x16 (&acc)[GemmCfg<BM, BN, BK, AT, BT>::FM][GemmCfg<BM, BN, BK, AT, BT>::FN]) {
+    f32x16 (&acc)[GemmCfg<BM, BN, BK, AT, BT>::FM][GemmCfg<BM, BN, BK, AT, BT>::FN],
+    bool do_cs, f4 (&cs)[GemmCfg<BM, BN, BK, AT, BT>::OA::ITERS]) {
   using G = GemmCfg<BM, BN, BK, AT, BT>;
   using OA = typename G::OA;
   using OB = typename G::OB;
@@ -199,6 +205,7 @@ __device__ __forceinline__ void gemm_mainloop(
     }                                                               \
   } while (0)
   SAVQA_GEMM_LOAD(kbeg);
+  if (do_cs) la.accum(cs);  // colsum_a: the staged A tile summed over its k rows
   la.store(smem, tid);
   lb.store(smem + 2 * OA::SIZE, tid);
   __syncthreads();
@@ -210,6 +217,7 @@ __device__ __forceinline__ void gemm_mainloop(
                                           smem + 2 * OA::SIZE + cur * OB::SIZE, wm, wn, lane,
                                           acc);
     if (more) {
+      if (do_cs) la.accum(cs);
       la.store(smem + (cur ^ 1) * OA::SIZE, tid);
       lb.store(smem + 2 * OA::SIZE + (cur ^ 1) * OB::SIZE, tid);
     }
@@ -275,11 +283,32 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
   const bool fast = (m0 + BM <= d.M) && (n0 + BN <= d.N) && ((kend - kbeg) % BK == 0) && avec &&
                     bvec && !a_kgather && !b_kgather;
   const int ntiles = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
+  // colsum_a (a_trans only): column tile 0 also sums its A tiles over k (bias gradient)
+  const bool do_cs = AT && d.colsum_a != nullptr && tn == 0;
+  f4 cs[G::OA::ITERS];
+#pragma unroll
+  for (int it = 0; it < G::OA::ITERS; ++it) cs[it] = f4{0.f, 0.f, 0.f, 0.f};
   if (ntiles > 0) {
     if (fast)
-      gemm_mainloop<BM, BN, BK, AT, BT, true>(d, smem, m0, n0, kbeg, kend, ntiles, acc);
+      gemm_mainloop<BM, BN, BK, AT, BT, true>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     else
-      gemm_mainloop<BM, BN, BK, AT, BT, false>(d, smem, m0, n0, kbeg, kend, ntiles, acc);
+      gemm_mainloop<BM, BN, BK, AT, BT, false>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+  }
+  if constexpr (AT) {
+    if (do_cs) {  // block-uniform; smem is free after the main loop's last barrier
+      constexpr int PER = G::OA::PER;
+      for (int i = threadIdx.x; i < BM; i += GEMM_NT) smem[i] = 0.f;
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < G::OA::ITERS; ++it) {
+        const int q = (threadIdx.x + it * GEMM_NT) % PER;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(&smem[4 * q + e], cs[it][e]);
+      }
+      __syncthreads();
+      for (int i = threadIdx.x; i < BM; i += GEMM_NT)
+        if (m0 + i < d.M) atomicAdd(&d.colsum_a[m0 + i], smem[i]);
+    }
   }
 
   // ---------------------------------------------------------------- epilogue
@@ -379,6 +408,7 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.c_group <= 0) { d.c_group = d.M; d.c_stride = d.M; }
   if (d.rowvec && d.rowvec_period <= 0) return fail(SAVQA_EINVAL, "savqa_gemm: rowvec_period");
   if (d.split_k < 0 && !d.atomic) return fail(SAVQA_EINVAL, "savqa_gemm: auto split-K needs atomic=1");
+  if (d.colsum_a && !d.a_trans) return fail(SAVQA_EINVAL, "savqa_gemm: colsum_a needs a_trans=1");
   constexpr int BK = SAVQA_GEMM_BK;
   const int slots = slots_per_launch();
   const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);

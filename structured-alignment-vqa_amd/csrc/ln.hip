@@ -83,10 +83,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-// Backward. Each wave walks rows with a grid stride, keeping its dgamma/dbeta
-// partial sums in registers; the 4 waves reduce through LDS and add once per
-// column per block.
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy,
+// Backward. 1024-thread workgroups (16 waves), one per CU: each wave walks rows with a
+// grid stride, keeping its dgamma/dbeta partial sums in registers; the 16 waves fold
+// them with LDS float atomics and the workgroup adds once per column to global memory
+// (256 global atomics per column instead of one per 4-row workgroup).
+constexpr int LN_BWD_WAVES = 16;
+__global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(const float* __restrict__ dy,
                                                      const float* __restrict__ z,
                                                      const float* __restrict__ mean_in,
                                                      const float* __restrict__ rden_in,
@@ -97,10 +99,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
                                                      float* __restrict__ dz,
                                                      float* __restrict__ dgamma,
                                                      float* __restrict__ dbeta) {
-  __shared__ float4 red[2][4][64 * LN_MAXV];
+  __shared__ float red[2][256 * LN_MAXV];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int nv = cols >> 8;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    red[0][c] = 0.f;
+    red[1][c] = 0.f;
+  }
   float4 dg[LN_MAXV], db[LN_MAXV], g[LN_MAXV];
 #pragma unroll
   for (int i = 0; i < LN_MAXV; ++i) {
@@ -109,17 +115,19 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
     if (i < nv) g[i] = reinterpret_cast<const float4*>(gamma)[lane + 64 * i];
   }
   const float invN = 1.f / (float)cols;
-  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += (int64_t)gridDim.x * 4) {
+  for (int64_t row = (int64_t)blockIdx.x * LN_BWD_WAVES + w; row < rows;
+       row += (int64_t)gridDim.x * LN_BWD_WAVES) {
     const float mean = mean_in[row], rden = rden_in[row], sd = std_in[row];
     const float4* dyr = reinterpret_cast<const float4*>(dy + row * cols);
     const float4* zr = reinterpret_cast<const float4*>(z + row * cols);
-    float4 gg[LN_MAXV], xc[LN_MAXV];
+    float4 gg[LN_MAXV], xc[LN_MAXV], ad[LN_MAXV];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int i = 0; i < LN_MAXV; ++i) {
       if (i < nv) {
         const float4 d4 = dyr[lane + 64 * i];
         const float4 z4 = zr[lane + 64 * i];
+        if (dz_add) ad[i] = reinterpret_cast<const float4*>(dz_add + row * cols)[lane + 64 * i];
         xc[i] = make_float4(z4.x - mean, z4.y - mean, z4.z - mean, z4.w - mean);
         gg[i] = make_float4(d4.x * g[i].x, d4.y * g[i].y, d4.z * g[i].z, d4.w * g[i].w);
         sg += (gg[i].x + gg[i].y) + (gg[i].z + gg[i].w);
@@ -143,33 +151,27 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
         o.z = (gg[i].z - mg) * rden - c * xc[i].z;
         o.w = (gg[i].w - mg) * rden - c * xc[i].w;
         if (dz_add) {
-          const float4 a = reinterpret_cast<const float4*>(dz_add + row * cols)[lane + 64 * i];
-          o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+          o.x += ad[i].x; o.y += ad[i].y; o.z += ad[i].z; o.w += ad[i].w;
         }
         reinterpret_cast<float4*>(dz + row * cols)[lane + 64 * i] = o;
       }
     }
   }
+  __syncthreads();  // red[] zeroed
 #pragma unroll
   for (int i = 0; i < LN_MAXV; ++i) {
-    red[0][w][lane + 64 * i] = dg[i];
-    red[1][w][lane + 64 * i] = db[i];
+    if (i < nv) {
+      const int c0 = 4 * (lane + 64 * i);
+      atomicAdd(&red[0][c0 + 0], dg[i].x); atomicAdd(&red[0][c0 + 1], dg[i].y);
+      atomicAdd(&red[0][c0 + 2], dg[i].z); atomicAdd(&red[0][c0 + 3], dg[i].w);
+      atomicAdd(&red[1][c0 + 0], db[i].x); atomicAdd(&red[1][c0 + 1], db[i].y);
+      atomicAdd(&red[1][c0 + 2], db[i].z); atomicAdd(&red[1][c0 + 3], db[i].w);
+    }
   }
   __syncthreads();
-  // 256 threads reduce the cols/4 float4 columns of both accumulators
-  for (int c4 = threadIdx.x; c4 < nv * 64; c4 += 256) {
-    float4 a = red[0][0][c4], b = red[1][0][c4];
-#pragma unroll
-    for (int ww = 1; ww < 4; ++ww) {
-      const float4 a2 = red[0][ww][c4], b2 = red[1][ww][c4];
-      a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
-      b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
-    }
-    // column index of float4 slot c4: lane + 64*i  ->  floats 4*c4 .. 4*c4+3
-    atomicAdd(&dgamma[4 * c4 + 0], a.x); atomicAdd(&dgamma[4 * c4 + 1], a.y);
-    atomicAdd(&dgamma[4 * c4 + 2], a.z); atomicAdd(&dgamma[4 * c4 + 3], a.w);
-    atomicAdd(&dbeta[4 * c4 + 0], b.x); atomicAdd(&dbeta[4 * c4 + 1], b.y);
-    atomicAdd(&dbeta[4 * c4 + 2], b.z); atomicAdd(&dbeta[4 * c4 + 3], b.w);
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    atomicAdd(&dgamma[c], red[0][c]);
+    atomicAdd(&dbeta[c], red[1][c]);
   }
 }
 
@@ -209,9 +211,9 @@ extern "C" int savqa_ln_bwd(void* stream, const float* dy, const float* z, const
   if (rows <= 0) return 0;
   if (cols % 256 != 0 || cols > 256 * LN_MAXV)
     return fail(SAVQA_EUNSUP, "savqa_ln_bwd: cols must be a multiple of 256 and <= 1024");
-  int64_t blocks = (rows + 3) / 4;
-  if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), dy, z, mean,
+  int64_t blocks = (rows + LN_BWD_WAVES - 1) / LN_BWD_WAVES;
+  if (blocks > 256) blocks = 256;
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(64 * LN_BWD_WAVES), 0, as_stream(stream), dy, z, mean,
                      rden, stdv, gamma, rows, (int)cols, dz_add, dz, dgamma, dbeta);
   return check_launch("savqa_ln_bwd");
 }

@@ -406,39 +406,60 @@ __global__ void scatter_rows_kernel(const float* __restrict__ g, const int64_t* 
 }
 
 // ------------------------------------------------------------------ Adam
+// torch.optim.Adam (foreach=False, amsgrad=False, maximize=False, weight_decay=0):
+// m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2; p -= (lr/bc1) m / (sqrt(v)/sqrt(bc2) + eps).
+// Streaming, 28 B/param: each thread moves 2 float4 of p, g, m, v per iteration with
+// non-temporal loads/stores (11 GB per step at the cfg-2 arena never fits in cache).
+typedef float adam_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void adam4(adam_f4& pp, adam_f4 gg, adam_f4& mm, adam_f4& vv, float b1,
+                                      float b2, float eps, float step_size, float sbc2, float gs) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float gx = gg[e] * gs;
+    mm[e] = mm[e] + (1.f - b1) * (gx - mm[e]);
+    vv[e] = b2 * vv[e] + (1.f - b2) * gx * gx;
+    const float den = sqrtf(vv[e]) / sbc2 + eps;
+    pp[e] = pp[e] - step_size * (mm[e] / den);
+  }
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    int64_t n, float lr, float b1, float b2,
                                                    float eps, float step_size, float sbc2,
                                                    float gs) {
+  (void)lr;
   const int64_t n4 = n / 4;
+  adam_f4* P = reinterpret_cast<adam_f4*>(p);
+  const adam_f4* Gv = reinterpret_cast<const adam_f4*>(g);
+  adam_f4* M = reinterpret_cast<adam_f4*>(m);
+  adam_f4* V = reinterpret_cast<adam_f4*>(v);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    float4 gg = reinterpret_cast<const float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-#define ADAM1(X)                                                      \
-  {                                                                   \
-    const float gx = gg.X * gs;                                       \
-    mm.X = mm.X + (1.f - b1) * (gx - mm.X);                           \
-    vv.X = b2 * vv.X + (1.f - b2) * gx * gx;                          \
-    const float den = sqrtf(vv.X) / sbc2 + eps;                       \
-    pp.X = pp.X - step_size * (mm.X / den);                           \
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const int64_t j = i + stride;
+    adam_f4 p0 = __builtin_nontemporal_load(P + i), p1 = __builtin_nontemporal_load(P + j);
+    const adam_f4 g0 = __builtin_nontemporal_load(Gv + i), g1 = __builtin_nontemporal_load(Gv + j);
+    adam_f4 m0 = __builtin_nontemporal_load(M + i), m1 = __builtin_nontemporal_load(M + j);
+    adam_f4 v0 = __builtin_nontemporal_load(V + i), v1 = __builtin_nontemporal_load(V + j);
+    adam4(p0, g0, m0, v0, b1, b2, eps, step_size, sbc2, gs);
+    adam4(p1, g1, m1, v1, b1, b2, eps, step_size, sbc2, gs);
+    __builtin_nontemporal_store(p0, P + i); __builtin_nontemporal_store(p1, P + j);
+    __builtin_nontemporal_store(m0, M + i); __builtin_nontemporal_store(m1, M + j);
+    __builtin_nontemporal_store(v0, V + i); __builtin_nontemporal_store(v1, V + j);
   }
-    ADAM1(x) ADAM1(y) ADAM1(z) ADAM1(w)
-#undef ADAM1
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
+  if (i < n4) {
+    adam_f4 p0 = P[i], m0 = M[i], v0 = V[i];
+    adam4(p0, Gv[i], m0, v0, b1, b2, eps, step_size, sbc2, gs);
+    P[i] = p0; M[i] = m0; V[i] = v0;
   }
   // scalar tail
-  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const float gx = g[i] * gs;
-    m[i] = m[i] + (1.f - b1) * (gx - m[i]);
-    v[i] = b2 * v[i] + (1.f - b2) * gx * gx;
-    const float den = sqrtf(v[i]) / sbc2 + eps;
-    p[i] = p[i] - step_size * (m[i] / den);
+  for (int64_t k = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    const float gx = g[k] * gs;
+    m[k] = m[k] + (1.f - b1) * (gx - m[k]);
+    v[k] = b2 * v[k] + (1.f - b2) * gx * gx;
+    const float den = sqrtf(v[k]) / sbc2 + eps;
+    p[k] = p[k] - step_size * (m[k] / den);
   }
 }
 

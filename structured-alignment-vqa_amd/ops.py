@@ -74,7 +74,7 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
          ldc: int, a_trans=False, b_trans=False, a_rows=None, b_rows=None, c_rows=None,
          c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None, ldrv=0, rowvec_period=0,
          resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False, rowscale=None, relu=False,
-         alpha=1.0, beta=0.0, atomic=False, split_k=1):
+         alpha=1.0, beta=0.0, atomic=False, split_k=1, colsum_a=None):
     """Generic fp32 MFMA GEMM with fused epilogue (see savqa_gemm in include/savqa.h)."""
     d = GemmDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
@@ -92,6 +92,7 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
     d.rowscale = _p(rowscale)
     d.alpha, d.beta = float(alpha), float(beta)
     d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
+    d.colsum_a = _p(colsum_a)
     if _probe is None:
         call("savqa_gemm", _stream(), C.byref(d))
         return
@@ -129,13 +130,12 @@ def linear_dx(dY: Tensor, W: Tensor, dX: Tensor, *, rows: int, a_rows=None, mask
 
 def linear_dw(dY: Tensor, X: Tensor, dW: Tensor, db: Optional[Tensor], *, rows: int,
               x_rows=None, lddy=None, ldx=None):
-    """dW += dY^T X ; db += colsum(dY)   (accumulating into the grad arena)."""
+    """dW += dY^T X ; db += colsum(dY)   (accumulating into the grad arena; the bias
+    gradient is summed by the same GEMM from its staged dY^T tiles)."""
     N, K = dW.shape
     gemm(dY, X, dW, N, K, rows, lda=lddy if lddy is not None else N,
          ldb=ldx if ldx is not None else K, ldc=K, a_trans=True, b_rows=x_rows, atomic=True,
-         split_k=-1)  # library picks the split-K factor
-    if db is not None:
-        colsum_acc(dY, rows, N, lddy if lddy is not None else N, db)
+         split_k=-1, colsum_a=db)  # library picks the split-K factor
 
 
 def colsum_acc(X: Tensor, rows: int, cols: int, ldx: int, out: Tensor):
