@@ -90,6 +90,21 @@ def cpu_baseline(seconds=15.0, B=4):
                       f"B={B}, {n} steps in {dt:.1f}s, torch CPU {threads} threads"}
 
 
+ROOFLINE_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                             "r01_bench_roofline.json")
+
+
+def committed_traffic(variant):
+    """HBM bytes per launch of `variant` from the committed PMC passes of this command
+    (tools/summarize_prof.py: 2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected), or None."""
+    try:
+        with open(ROOFLINE_JSON) as f:
+            t = json.load(f)["traffic"].get(variant)
+        return None if t is None else round(t["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -189,7 +204,8 @@ def main():
         roof = {"bound": "mfma", "kernel": var, "launches_per_step": n // 2,
                 "avg_launch_us": round(ms / n * 1e3, 2), "flops_per_launch": flops / n,
                 "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": committed_traffic(var),
                 "all_gemm_tflops": round(allfl / (allms * 1e-3) / 1e12, 2),
                 "gemm_ms_per_step": round(allms / 2, 2)}
 

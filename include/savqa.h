@@ -73,7 +73,7 @@ typedef struct savqa_gemm_desc {
 
 int savqa_gemm(void* stream, const savqa_gemm_desc* d);
 
-/* The launch plan savqa_gemm would use for *d (no launch): out[0] = tile (64|128),
+/* The launch plan savqa_gemm would use for *d (no launch): out[0] = tile (32: skinny kernel, 128),
  * out[1] = split-K factor, out[2] = tail split factor (0: none), out[3] = workgroups. */
 int savqa_gemm_plan(const savqa_gemm_desc* d, int32_t* out);
 

@@ -344,19 +344,23 @@ __device__ __forceinline__ f4v mfma16(float a, float b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// sum / max over the 16 lanes of a DPP row (every lane of the row gets the result)
+// sum / max over the 16 lanes of a DPP row. Butterfly partners (quad_perm [1,0,3,2],
+// [2,3,0,1], row_half_mirror, row_mirror) pair every lane with a lane holding the same
+// operand set, so all 16 lanes end with bitwise-identical totals (a row_ror ladder
+// leaves quads with different association orders: T=1 softmax would then give a != 1
+// in some lanes and break the reference's exact-zero Q/K gradients).
 __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_f<0xB1>(v);
   v += dpp_f<0x4E>(v);
-  v += dpp_f<0x124>(v);
-  v += dpp_f<0x128>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
   return v;
 }
 __device__ __forceinline__ float row16_max(float v) {
   v = fmaxf(v, dpp_f<0xB1>(v));
   v = fmaxf(v, dpp_f<0x4E>(v));
-  v = fmaxf(v, dpp_f<0x124>(v));
-  v = fmaxf(v, dpp_f<0x128>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
   return v;
 }
 
@@ -583,7 +587,11 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
   __syncthreads();
 
   // ---- phase 2: output tiles. items [0, 4NJT): dV, [4NJT, 8NJT): dK, [8NJT, 8NJT + 4nw): dQ
+#ifdef SAVQA_ATTN_SKIP_P2  // timing experiment only: phase 1 alone
+  const int nitems = 0;
+#else
   const int nitems = 8 * NJT + 4 * nw;
+#endif
   for (int it = w; it < nitems; it += nw) {
     f4v acc = {0.f, 0.f, 0.f, 0.f};
     if (it < 8 * NJT) {
@@ -647,6 +655,174 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Single-query path (T_q = 1: the decoder cross-attention, one query token per sample).
+// One wave per (b, h); 16 lanes per key row (lane = (key slot kk = lane>>4, float4 chunk
+// c = lane&15)), so every K/V load instruction reads 4 whole 256-B rows (coalesced) and
+// a 16-lane DPP row reduction finishes each dot product. NIT = ceil(Tk/4) rounded up to
+// a multiple of 8 (register arrays, compile-time indexed).
+__device__ __forceinline__ float rows4_max(float v) {  // one value per 16-lane row -> all
+  return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
+}
+__device__ __forceinline__ float rows4_sum(float v) {
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+}
+__device__ __forceinline__ f4v xrow_sum(f4v v) {  // sum over the 4 rows, lane c keeps col c
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] += __shfl_xor(v[e], 16);
+    v[e] += __shfl_xor(v[e], 32);
+  }
+  return v;
+}
+
+// s[it] (scaled, masked; -inf past Tk) and the forward chain for the single query of (b,h)
+template <int NIT>
+__device__ __forceinline__ void q1_forward(const AttnArgs& a, int b, int hd, int kk, int c,
+                                           const f4v q4, float (&s)[NIT], float (&aa)[NIT],
+                                           float (&gg)[NIT], float (&bm)[NIT], float& nrm) {
+  const int64_t kb = (int64_t)b * a.Tk;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    float x = -INFINITY;
+    if (4 * it < a.Tk) {
+      const int j = 4 * it + kk;
+      const f4v k4 = ld4(a.k + (kb + min(j, a.Tk - 1)) * a.ldk + hd + 4 * c);
+      const float d = row16_sum((q4.x * k4.x + q4.y * k4.y) + (q4.z * k4.z + q4.w * k4.w));
+      if (j < a.Tk) x = a.kflag[kb + j] == 0.f ? ATT_MASKED : d * 0.125f;
+    }
+    s[it] = x;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) mx = fmaxf(mx, s[it]);
+  mx = rows4_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const float e = 4 * it + kk < a.Tk ? expf(s[it] - mx) : 0.f;
+    aa[it] = e;
+    sum += e;
+  }
+  sum = rows4_sum(sum);
+  const float* grow = a.G + (int64_t)b * a.Tk;
+  float nr = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int j = 4 * it + kk;
+    aa[it] = aa[it] / sum;
+    gg[it] = j < a.Tk ? grow[j] : 0.f;
+    bm[it] = gg[it] * aa[it];
+    nr += fabsf(bm[it]);
+  }
+  nrm = rows4_sum(nr);
+}
+
+template <int NIT>
+__global__ __launch_bounds__(256) void gattn_fwd_q1_kernel(AttnArgs a) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bh = blockIdx.x * 4 + w;
+  if (bh >= a.B * a.H) return;  // wave-uniform
+  const int b = bh / a.H, h = bh % a.H, hd = h * ATT_DK;
+  const int kk = lane >> 4, c = lane & 15;
+  const f4v q4 = ld4(a.q + (int64_t)b * a.ldq + hd + 4 * c);
+  float s[NIT], aa[NIT], gg[NIT], bm[NIT], nrm;
+  q1_forward<NIT>(a, b, hd, kk, c, q4, s, aa, gg, bm, nrm);
+  const float sden = fmaxf(nrm, 1e-12f);
+  const float qf = a.qflag[b];
+  const int64_t kb = (int64_t)b * a.Tk;
+  f4v o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    if (4 * it < a.Tk) {
+      const int j = 4 * it + kk;
+      const float n = bm[it] / sden;
+      if (a.att && c == 0 && j < a.Tk) a.att[((int64_t)h * a.B + b) * a.Tk + j] = n;
+      const float pj = j < a.Tk ? n * qf : 0.f;
+      const f4v v4 = ld4(a.v + (kb + min(j, a.Tk - 1)) * a.ldv + hd + 4 * c);
+      o += pj * v4;
+    }
+  }
+  o = xrow_sum(o);
+  if (kk == 0) {
+    float* orow = a.o + (int64_t)b * a.ldo + hd + 4 * c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) orow[e] = o[e];
+  }
+}
+
+template <int NIT>
+__global__ __launch_bounds__(256) void gattn_bwd_q1_kernel(AttnArgs a) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bh = blockIdx.x * 4 + w;
+  if (bh >= a.B * a.H) return;
+  const int b = bh / a.H, h = bh % a.H, hd = h * ATT_DK;
+  const int kk = lane >> 4, c = lane & 15;
+  const int64_t kb = (int64_t)b * a.Tk;
+  const f4v q4 = ld4(a.q + (int64_t)b * a.ldq + hd + 4 * c);
+  const f4v do4 = ld4(a.dout + (int64_t)b * a.lddo + hd + 4 * c);
+  float s[NIT], aa[NIT], gg[NIT], bm[NIT], nrm;
+  q1_forward<NIT>(a, b, hd, kk, c, q4, s, aa, gg, bm, nrm);
+  const float sden = fmaxf(nrm, 1e-12f);
+  const float qf = a.qflag[b];
+  // dP_j = dO . V_j ; dN = dP * qf
+  float dn[NIT], t1 = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    float x = 0.f;
+    if (4 * it < a.Tk) {
+      const int j = 4 * it + kk;
+      const f4v v4 = ld4(a.v + (kb + min(j, a.Tk - 1)) * a.ldv + hd + 4 * c);
+      x = row16_sum((do4.x * v4.x + do4.y * v4.y) + (do4.z * v4.z + do4.w * v4.w)) * qf;
+      if (j >= a.Tk) x = 0.f;
+    }
+    dn[it] = x;
+    t1 += x * bm[it];
+  }
+  t1 = rows4_sum(t1);
+  const float dnrm = nrm >= 1e-12f ? -t1 / (sden * sden) : 0.f;
+  float t2 = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const float sg = bm[it] > 0.f ? 1.f : (bm[it] < 0.f ? -1.f : 0.f);
+    const float dbm = dn[it] / sden + dnrm * sg;
+    dn[it] = dbm * gg[it];  // da
+    t2 += dn[it] * aa[it];
+  }
+  t2 = rows4_sum(t2);
+  f4v dq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    if (4 * it < a.Tk) {
+      const int j = 4 * it + kk;
+      const bool ok = j < a.Tk;
+      float ds = aa[it] * (dn[it] - t2);
+      if (!ok || a.kflag[kb + min(j, a.Tk - 1)] == 0.f) ds = 0.f;
+      ds *= 0.125f;
+      const float pj = ok ? bm[it] / sden * qf : 0.f;
+      const int64_t row = kb + min(j, a.Tk - 1);
+      const f4v k4 = ld4(a.k + row * a.ldk + hd + 4 * c);
+      const f4v v4 = ld4(a.v + row * a.ldv + hd + 4 * c);
+      dq += ds * k4;
+      if (ok) {
+        float* dkr = a.dk + row * a.lddk + hd + 4 * c;
+        float* dvr = a.dv + row * a.lddv + hd + 4 * c;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          dkr[e] = k4[e] > 0.f ? ds * q4[e] : 0.f;
+          dvr[e] = v4[e] > 0.f ? pj * do4[e] : 0.f;
+        }
+      }
+    }
+  }
+  dq = xrow_sum(dq);
+  if (kk == 0) {
+    float* dqr = a.dq + (int64_t)b * a.lddq + hd + 4 * c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dqr[e] = q4[e] > 0.f ? dq[e] : 0.f;
+  }
+}
+
 static size_t fwd_lds(int Tk, int KB) {
   return sizeof(float) * ((size_t)2 * Tk * ATT_KLD + 4 * ATT_RB * KB * 64 + 4 * ATT_RB * ATT_DK);
 }
@@ -669,19 +845,23 @@ static int validate(const AttnArgs& a, int64_t dk, const char* who) {
   return 0;
 }
 
-// Path choice: the MFMA strip kernels (default) or the row kernels (lane per key),
-// overridable with SAVQA_ATTN_PATH=rows|mfma for A/B timing.
-static bool use_mfma(const AttnArgs& a) {
+// Path choice: 0 = row kernels (lane per key), 1 = MFMA strip kernels, 2 = single-query
+// kernels; overridable with SAVQA_ATTN_PATH=rows|mfma|q1 for A/B timing.
+static int attn_path(const AttnArgs& a) {
   static const int forced = [] {
     const char* e = getenv("SAVQA_ATTN_PATH");
-    if (!e) return 0;
-    return std::string(e) == "rows" ? 1 : (std::string(e) == "mfma" ? 2 : 0);
+    if (!e) return -1;
+    const std::string v(e);
+    return v == "rows" ? 0 : (v == "mfma" ? 1 : (v == "q1" ? 2 : -1));
   }();
-  if (forced) return forced == 2;
-  // a single query row (the decoder cross-attention) would fill 1/16 of each MFMA tile:
-  // the lane-per-key kernels win there (76 vs 102 us bwd at B*H = 2048, Tk = 73)
-  return a.Tq >= 8;
+  if (forced == 2) return a.Tq == 1 ? 2 : 1;
+  if (forced >= 0) return forced;
+  if (a.Tq == 1) return 2;
+  // a few query rows would fill <1/2 of each MFMA tile: lane-per-key kernels
+  return a.Tq >= 8 ? 1 : 0;
 }
+
+static int q1_nit(int Tk) { return ((Tk + 3) / 4 + 7) / 8 * 8; }
 
 }  // namespace savqa
 
@@ -698,7 +878,16 @@ extern "C" int savqa_gattn_fwd(void* stream, const float* q, int64_t ldq, const 
   a.o = o; a.ldo = ldo; a.att = att;
   if (int rc = validate(a, dk, "savqa_gattn_fwd")) return rc;
   hipStream_t s = as_stream(stream);
-  if (use_mfma(a)) {
+  const int path = attn_path(a);
+  if (path == 2) {
+    const dim3 g((unsigned)((B * H + 3) / 4));
+    switch (q1_nit((int)Tk)) {
+      case 8: hipLaunchKernelGGL(gattn_fwd_q1_kernel<8>, g, dim3(256), 0, s, a); break;
+      case 16: hipLaunchKernelGGL(gattn_fwd_q1_kernel<16>, g, dim3(256), 0, s, a); break;
+      case 24: hipLaunchKernelGGL(gattn_fwd_q1_kernel<24>, g, dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL(gattn_fwd_q1_kernel<32>, g, dim3(256), 0, s, a); break;
+    }
+  } else if (path == 1) {
     const int njt = (int)((Tk + 15) / 16), nw = (int)((Tq + 15) / 16);
     const size_t lds = sizeof(float) * ((size_t)njt * 16 * ATT_KLD + (size_t)nw * njt * 16 * 20);
     switch (njt) {
@@ -733,9 +922,20 @@ extern "C" int savqa_gattn_bwd(void* stream, const float* q, int64_t ldq, const 
   a.dv = dv; a.lddv = lddv;
   if (int rc = validate(a, dk, "savqa_gattn_bwd")) return rc;
   hipStream_t s = as_stream(stream);
-  if (use_mfma(a)) {
-    if ((a.ldq & 3) || (a.lddo & 3) || (((uintptr_t)a.dout) & 15))
-      return fail(SAVQA_EINVAL, "savqa_gattn_bwd: Q/dO must be 16-B aligned with ld % 4 == 0");
+  const int path = attn_path(a);
+  if (path >= 1 && ((a.ldq & 3) || (a.lddo & 3) || (((uintptr_t)a.dout) & 15)))
+    return fail(SAVQA_EINVAL, "savqa_gattn_bwd: Q/dO must be 16-B aligned with ld % 4 == 0");
+  if (path == 2) {
+    const dim3 g((unsigned)((B * H + 3) / 4));
+    switch (q1_nit((int)Tk)) {
+      case 8: hipLaunchKernelGGL(gattn_bwd_q1_kernel<8>, g, dim3(256), 0, s, a); break;
+      case 16: hipLaunchKernelGGL(gattn_bwd_q1_kernel<16>, g, dim3(256), 0, s, a); break;
+      case 24: hipLaunchKernelGGL(gattn_bwd_q1_kernel<24>, g, dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL(gattn_bwd_q1_kernel<32>, g, dim3(256), 0, s, a); break;
+    }
+    return check_launch("savqa_gattn_bwd");
+  }
+  if (path == 1) {
     const int njt = (int)((Tk + 15) / 16), nw = (int)((Tq + 15) / 16);
     const size_t lds = sizeof(float) * 2 * (size_t)njt * 16 * (16 * nw + 4);
     switch (njt) {

@@ -145,6 +145,52 @@ struct GemmCfg {
   static constexpr int FM = WM / 32, FN = WN / 32;
 };
 
+// Epilogue of one output element (include/savqa.h formula), split per row / element.
+struct EpiRow {
+  float* crow;
+  float rs;
+  int64_t mr, pr;
+};
+
+__device__ __forceinline__ EpiRow epi_row(const savqa_gemm_desc& d, int64_t m, bool ident) {
+  EpiRow e;
+  int64_t cr;
+  if (ident) {
+    cr = m;
+  } else if (d.c_rows) {
+    cr = d.c_rows[m];
+  } else {
+    const uint32_t mu = (uint32_t)m, cg = (uint32_t)d.c_group;
+    cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
+  }
+  e.crow = d.C + cr * d.ldc;
+  e.rs = d.rowscale ? d.rowscale[m] : 1.f;
+  e.mr = d.mask_arows ? d.a_rows[m] : m;
+  e.pr = d.rowvec ? (int64_t)((uint32_t)m % (uint32_t)d.rowvec_period) : 0;
+  return e;
+}
+
+__device__ __forceinline__ void epi_store(const savqa_gemm_desc& d, const EpiRow& e, int64_t m,
+                                          int64_t n, float acc, bool first_split, bool atomic) {
+  float v = acc * d.alpha;
+  if (first_split) {
+    if (d.bias) v += d.bias[n];
+    if (d.rowvec) v += d.rowvec[e.pr * d.ldrv + n];
+  }
+  if (d.relu) v = fmaxf(v, 0.f);
+  v *= e.rs;
+  if (d.mask && !(d.mask[e.mr * d.ldmask + n] > 0.f)) v = 0.f;
+  if (first_split && d.resid) v += d.resid[m * d.ldr + n];
+  float* cp = e.crow + n;
+  if (atomic) {
+    atomicAdd(cp, v);
+  } else if (d.beta != 0.f) {
+    *cp = v + d.beta * *cp;
+  } else {
+    *cp = v;
+  }
+}
+
 template <int BM, int BN, int BK, bool AT, bool BT>
 __device__ __forceinline__ void gemm_compute_tile(
     const float* __restrict__ As, const float* __restrict__ Bs, int wm, int wn, int lane,
@@ -165,6 +211,12 @@ __device__ __forceinline__ void gemm_compute_tile(
 #pragma unroll
       for (int j = 0; j < G::FN; ++j) G::OB::fetch(Bs, wn * G::WN, j, c + 1, lane, b[cur ^ 1][j]);
     }
+#ifdef SAVQA_GEMM_SGB
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+#ifdef SAVQA_GEMM_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -172,6 +224,12 @@ __device__ __forceinline__ void gemm_compute_tile(
 #pragma unroll
         for (int j = 0; j < G::FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][i][s], b[cur][j][s], acc[i][j], 0, 0, 0);
+#ifdef SAVQA_GEMM_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+#ifdef SAVQA_GEMM_SGB
+    __builtin_amdgcn_sched_barrier(0);
+#endif
   }
 }
 
@@ -313,47 +371,135 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 
   // ---------------------------------------------------------------- epilogue
   const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
-  const uint32_t cg = (uint32_t)d.c_group;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int64_t m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (m >= d.M) continue;
-      int64_t cr;
-      if (ident) {
-        cr = m;
-      } else if (d.c_rows) {
-        cr = d.c_rows[m];
-      } else {
-        const uint32_t mu = (uint32_t)m;
-        cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
-      }
-      float* crow = d.C + cr * d.ldc;
-      const float rs = d.rowscale ? d.rowscale[m] : 1.f;
-      const int64_t mr = d.mask_arows ? d.a_rows[m] : m;
-      const int64_t pr = d.rowvec ? (int64_t)((uint32_t)m % (uint32_t)d.rowvec_period) : 0;
+      const EpiRow er = epi_row(d, m, ident);
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int64_t n = n0 + wn * WN + j * 32 + (lane & 31);
         if (n >= d.N) continue;
-        float v = acc[i][j][r] * d.alpha;
-        if (first_split) {
-          if (d.bias) v += d.bias[n];
-          if (d.rowvec) v += d.rowvec[pr * d.ldrv + n];
-        }
-        if (d.relu) v = fmaxf(v, 0.f);
-        v *= rs;
-        if (d.mask && !(d.mask[mr * d.ldmask + n] > 0.f)) v = 0.f;
-        if (first_split && d.resid) v += d.resid[m * d.ldr + n];
-        float* cp = crow + n;
-        if (atomic) {
-          atomicAdd(cp, v);
-        } else if (d.beta != 0.f) {
-          *cp = v + d.beta * *cp;
-        } else {
-          *cp = v;
-        }
+        epi_store(d, er, m, n, acc[i][j][r], first_split, atomic);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Small-M / small-N GEMMs (the decoder and head Linears at M = B = 256 rows, their dW at
+// K = 256): one 32x32 output tile per 512-thread workgroup, the 8 waves split K eight ways
+// and fold their accumulators through LDS, so a 256x512x512 GEMM runs as 128 workgroups of
+// 8 short MFMA chains instead of 32 workgroups of one long one. Operands go straight from
+// global memory (L2) into MFMA registers: lane half q of an 8-k group takes k = 8g+4q+s,
+// s = 0..3 -- one b128 load on a k-contiguous operand, 4 coalesced scalars otherwise.
+constexpr int SK_WAVES = 8;
+
+template <bool KCONTIG>
+__device__ __forceinline__ void sk_load4(const float* __restrict__ P, int64_t ld,
+                                         const int64_t* __restrict__ rows, int64_t x, int64_t xlim,
+                                         int64_t k, int64_t kend, bool vec, float (&v)[4]) {
+  // KCONTIG: value(x, k) = P[r(x)*ld + k]; else value(x, k) = P[r(k)*ld + x]
+  if constexpr (KCONTIG) {
+    const bool xok = x < xlim;
+    const int64_t rx = xok ? (rows ? rows[x] : x) : 0;
+    const float* p = P + rx * ld;
+    if (vec && xok && k + 3 < kend) {
+      const f4 t = *reinterpret_cast<const f4*>(p + k);
+      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = xok && k + j < kend;
+        const float t = p[ok ? k + j : 0];
+        v[j] = ok ? t : 0.f;
+      }
+    }
+  } else {
+    const bool xok = x < xlim;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = xok && k + j < kend;
+      const int64_t kk = ok ? k + j : 0;
+      const int64_t rk = rows ? rows[kk] : kk;
+      const float t = P[rk * ld + (xok ? x : 0)];
+      v[j] = ok ? t : 0.f;
+    }
+  }
+}
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(savqa_gemm_desc d, int tiles_n,
+                                                                   int avec, int bvec) {
+  __shared__ float red[SK_WAVES][32][33];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t = blockIdx.x;
+  const int64_t m0 = (int64_t)(t / tiles_n) * 32, n0 = (int64_t)(t % tiles_n) * 32;
+  // this wave's k range, in whole 8-k groups
+  const int64_t ngrp = (d.K + 7) / 8;
+  const int64_t g0 = ngrp * w / SK_WAVES, g1 = ngrp * (w + 1) / SK_WAVES;
+  const int i = lane & 31, q = lane >> 5;
+  const int64_t am = m0 + i, bn = n0 + i;
+  const int64_t* arows = d.a_rows;  // !AT: gather on m; AT: gather on k
+  const int64_t* brows = d.b_rows;  // BT: gather on n; !BT: gather on k
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float cs = 0.f;  // colsum_a partial (AT): sum over this wave's k of A(m0 + i, k), half q
+  // software pipeline: the loads of group pair p+1 are in flight while pair p's MFMAs run
+  float a[2][2][4], b[2][2][4];
+  auto load_pair = [&](int64_t gg, float (&aa)[2][4], float (&bb)[2][4]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t k = (gg + u) * 8 + 4 * q;
+      const int64_t kl = gg + u < g1 ? d.K : 0;  // groups past this wave's range load zeros
+      sk_load4<!AT>(d.A, d.lda, arows, am, d.M, k, kl, avec, aa[u]);
+      sk_load4<BT>(d.B, d.ldb, brows, bn, d.N, k, kl, bvec, bb[u]);
+    }
+  };
+  auto mma_pair = [&](const float (&aa)[2][4], const float (&bb)[2][4]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      cs += (aa[u][0] + aa[u][1]) + (aa[u][2] + aa[u][3]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(aa[u][s], bb[u][s], acc, 0, 0, 0);
+    }
+  };
+  const int npair = (int)((g1 - g0 + 1) / 2);
+  if (npair > 0) load_pair(g0, a[0], b[0]);
+  for (int pi = 0; pi < npair; pi += 2) {  // buffers alternate with compile-time indices
+    if (pi + 1 < npair) load_pair(g0 + 2 * (pi + 1), a[1], b[1]);
+    mma_pair(a[0], b[0]);
+    if (pi + 1 >= npair) break;
+    if (pi + 2 < npair) load_pair(g0 + 2 * (pi + 2), a[0], b[0]);
+    mma_pair(a[1], b[1]);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[w][(r & 3) + 8 * (r >> 2) + 4 * q][i] = acc[r];
+  __syncthreads();
+  const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
+  for (int e = threadIdx.x; e < 32 * 32; e += 64 * SK_WAVES) {
+    const int r = e >> 5, c = e & 31;
+    const int64_t m = m0 + r, n = n0 + c;
+    if (m >= d.M || n >= d.N) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < SK_WAVES; ++ww) v += red[ww][r][c];
+    const EpiRow er = epi_row(d, m, ident);
+    epi_store(d, er, m, n, v, true, d.atomic != 0);
+  }
+  if constexpr (AT) {
+    if (d.colsum_a && n0 == 0) {
+      __syncthreads();
+      float* flat = &red[0][0][0];
+      flat[threadIdx.x] = cs;  // 64 * SK_WAVES partials: (wave, half q, i)
+      __syncthreads();
+      if (threadIdx.x < 32 && m0 + threadIdx.x < d.M) {
+        float sum = 0.f;
+        for (int j = 0; j < 2 * SK_WAVES; ++j) sum += flat[j * 32 + threadIdx.x];
+        atomicAdd(&d.colsum_a[m0 + threadIdx.x], sum);
       }
     }
   }
@@ -414,8 +560,19 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
   int split = d.split_k > 1 ? d.split_k : 1;
   if (d.split_k < 0) split = auto_split(tiles128, d.K, BK, slots);
-  // 128x128 tiles once there is enough parallelism (split-K counts), else 64x64
-  p.tile = tiles128 * split >= 160 ? 128 : 64;
+  // 128x128 tiles once there is enough parallelism (split-K counts), else the skinny
+  // kernel (32x32 tiles, K split over the 4 waves of a workgroup; no split-K launch)
+  if (tiles128 * split < 160) {
+    p.tile = 32;
+    p.split = 1;
+    p.nsplit = 1;
+    p.gg.tiles_n = (int)((d.N + 31) / 32);
+    p.grid_x = (int)((d.M + 31) / 32) * p.gg.tiles_n;
+    p.zero_row0 = -1;
+    p.gg.tail_f = 1;
+    return 0;
+  }
+  p.tile = 128;
   const int tm = (int)((d.M + p.tile - 1) / p.tile);
   const int tn = (int)((d.N + p.tile - 1) / p.tile);
   const int T = tm * tn;
@@ -506,10 +663,16 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
       hipMemset2DAsync(d.C + p.zero_row0 * d.ldc, d.ldc * sizeof(float), 0, d.N * sizeof(float),
                        d.M - p.zero_row0, s) != hipSuccess)
     return fail(SAVQA_EUNSUP, "savqa_gemm: tail zero-fill failed");
-  if (p.tile == 128)
+  if (p.tile == 128) {
     dispatch_layout<128, 128, SAVQA_GEMM_BK>(d, p, s, avec, bvec);
-  else
-    dispatch_layout<64, 64, 32>(d, p, s, avec, bvec);
+  } else {
+    const dim3 g(p.grid_x), b(64 * SK_WAVES);
+    const int tn = p.gg.tiles_n;
+    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, true>), g, b, 0, s, d, tn, avec, bvec);
+    else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, false>), g, b, 0, s, d, tn, avec, bvec);
+    else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<true, false>), g, b, 0, s, d, tn, avec, bvec);
+    else hipLaunchKernelGGL((gemm_skinny_kernel<true, true>), g, b, 0, s, d, tn, avec, bvec);
+  }
   return check_launch("savqa_gemm");
 }
 

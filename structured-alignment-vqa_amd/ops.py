@@ -47,8 +47,10 @@ class GemmProbe:
     def variant(d):
         plan = (C.c_int32 * 4)()
         call("savqa_gemm_plan", C.byref(d), C.cast(plan, C.c_void_p))
-        return (f"gemm_f32_kernel<{plan[0]},{plan[0]},{str(bool(d.a_trans)).lower()},"
-                f"{str(bool(d.b_trans)).lower()}>")
+        lay = f"{str(bool(d.a_trans)).lower()},{str(bool(d.b_trans)).lower()}"
+        if plan[0] == 32:
+            return f"gemm_skinny_kernel<{lay}>"
+        return f"gemm_f32_kernel<{plan[0]},{plan[0]},{lay}>"
 
     def summary(self):
         torch.cuda.synchronize()

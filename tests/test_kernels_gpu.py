@@ -122,6 +122,32 @@ def test_gemm_dw_auto_split(N, K, rows):
     assert rel(dW, dW0.double() + dY.double().t() @ X.double()) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(33, 65, 37), (256, 512, 2048), (256, 914, 1024), (1, 7, 3)])
+@pytest.mark.parametrize("at,bt", [(False, True), (False, False), (True, False), (True, True)])
+def test_gemm_skinny_layouts(M, N, K, at, bt):
+    """Few-tile problems run the skinny kernel (32x32 tiles, K split over 8 waves): every
+    operand layout, K tails, an m/n gather and the fused bias-gradient column sum."""
+    O = ops()
+    A = g(K, M, seed=40) if at else g(M, K, seed=40)
+    B = g(N, K, seed=41) if bt else g(K, N, seed=41)
+    Ar = A.t() if at else A
+    Br = B.t() if bt else B
+    bias = g(N, seed=42)
+    out = torch.full((M, N), float("nan"), device=dev)
+    cs = torch.zeros(M, device=dev) if at else None
+    O.gemm(A, B, out, M, N, K, lda=M if at else K, ldb=K if bt else N, ldc=N, a_trans=at,
+           b_trans=bt, bias=bias, relu=True, colsum_a=cs)
+    ref = torch.relu(Ar.double() @ Br.double() + bias.double())
+    assert rel(out, ref) < 1e-5
+    if at:
+        assert rel(cs, Ar.double().sum(1)) < 1e-5
+    if not at:  # gather rows of A through a_rows (embedding-style)
+        idx = torch.randint(0, M, (M,), generator=torch.Generator().manual_seed(43)).to(dev)
+        out2 = torch.empty(M, N, device=dev)
+        O.gemm(A, B, out2, M, N, K, lda=K, ldb=K if bt else N, ldc=N, b_trans=bt, a_rows=idx)
+        assert rel(out2, Ar.double()[idx] @ Br.double()) < 1e-5
+
+
 def test_gemm_mask_arows_rowscale():
     O = ops()
     M, N, K = 50, 96, 64
@@ -190,7 +216,9 @@ def _attn_ref(Q, K, V, G, kf, qf, h=8):
                                            (5, 1, 73, "cross"), (2, 20, 100, "self"),
                                            (2, 128, 128, "self"), (3, 17, 33, "cross"),
                                            (4, 1, 50, "cross"), (2, 16, 16, "self"),
-                                           (1, 5, 3, "cross"), (2, 100, 7, "cross")])
+                                           (1, 5, 3, "cross"), (2, 100, 7, "cross"),
+                                           (3, 1, 128, "cross"), (2, 1, 5, "cross"),
+                                           (2, 1, 3, "cross"), (3, 4, 33, "cross")])
 def test_graph_attention_fwd_bwd(B, Tq, Tk, kind):
     O = ops()
     H, D = 8, 512

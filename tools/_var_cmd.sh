@@ -1,6 +1,2 @@
 set -e
-S="NT:18688:2048:512 NT:18688:1536:512 NN:18688:512:2048 NN:18688:2048:512 TN:2048:512:18688 TN:6144:512:18688 NT:12800:2048:512 NT:4096:4096:4096"
-for v in o2bk32 o3bk16 o2bk16; do
-  echo "== $v" >> gpurun_out/var1.log
-  SAVQA_LIB=structured-alignment-vqa_amd/csrc/build/libsavqa_$v.so timeout -k 10 120 python tools/gemm_bench.py $S >> gpurun_out/var1.log 2>&1
-done
+SAVQA_LIB=structured-alignment-vqa_amd/csrc/build/libsavqa_skip2.so timeout -k 10 100 python tools/attn_bench.py > gpurun_out/at4.log 2>&1
