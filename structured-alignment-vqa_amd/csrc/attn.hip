@@ -330,11 +330,12 @@ __global__ __launch_bounds__(256) void gattn_bwd_kernel(AttnArgs a) {
 // softmax / graph / L1-normalise chain and its adjoint with 16-lane DPP row reductions
 // (an accumulator row lives in one 16-lane DPP row), then P and dS are written to LDS
 // transposed ([key][query], one b128 per lane per tile).
-// Phase 2 (after one barrier), output tiles round-robin over the waves:
+// Phase 2 (after one barrier), 16x16 output tiles in contiguous runs per wave:
 //   dV = P^T dO and dK = dS^T Q  (A = b128 rows of the transposed LDS images),
 //   dQ = dS K                     (A = 4 scalar LDS reads, conflict-free, see PLD).
-// The B operands (dO, Q, K columns) come straight from global memory (L1/L2 hits: the
-// workgroup just streamed the same rows in phase 1).
+// The B operands (dO, Q, K column blocks) come straight from global memory (L1/L2 hits:
+// the workgroup just streamed the same rows in phase 1) into registers, once per
+// (tensor, column block) group.
 // LDS: 2 * 16*NJT * (16*nw + 4) floats  (53.7 KB at T = 73, 2 workgroups / CU).
 // PLD = 16*nw + 4 makes both the b128 row reads (16 lanes -> 16 disjoint bank quads)
 // and the scalar column reads (4 lane groups at bank offsets 16g) conflict-free.
@@ -390,11 +391,49 @@ __device__ __forceinline__ void strip_dots(const f4v (&x)[4], const float* y, in
   }
 }
 
+// Same with Y staged in LDS ([TK][ATT_KLD], rows >= Tk zero): b128 reads, lanes 0-15 of a
+// read phase hit 16 disjoint bank quads (row stride 68 floats).
+template <int NJT>
+__device__ __forceinline__ void strip_dots_lds(const f4v (&x)[4], const float* Ys, int col, int g,
+                                               f4v (&acc)[NJT]) {
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt) {
+    const float* yr = Ys + (jt * 16 + col) * ATT_KLD + 4 * g;
+    f4v s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f4v yv = ld4(yr + 16 * c);
+      s = mfma16(x[c].x, yv.x, s);
+      s = mfma16(x[c].y, yv.y, s);
+      s = mfma16(x[c].z, yv.z, s);
+      s = mfma16(x[c].w, yv.w, s);
+    }
+    acc[jt] = s;
+  }
+}
+
+// Cooperative stage of K_h and V_h rows [0, TK) into LDS (zero rows past Tk): every
+// thread issues its b128 loads back to back, so the workgroup waits one latency.
+template <int TK>
+__device__ __forceinline__ void stage_kv_tiles(const AttnArgs& a, int b, int h, float* Ks, float* Vs) {
+  for (int idx = threadIdx.x; idx < TK * 16; idx += blockDim.x) {
+    const int j = idx >> 4, c4 = (idx & 15) * 4;
+    f4v kv = {0.f, 0.f, 0.f, 0.f}, vv = kv;
+    if (j < a.Tk) {
+      const int64_t row = (int64_t)b * a.Tk + j;
+      kv = ld4(a.k + row * a.ldk + h * ATT_DK + c4);
+      vv = ld4(a.v + row * a.ldv + h * ATT_DK + c4);
+    }
+    *reinterpret_cast<f4v*>(&Ks[j * ATT_KLD + c4]) = kv;
+    *reinterpret_cast<f4v*>(&Vs[j * ATT_KLD + c4]) = vv;
+  }
+}
+
 // Forward row chain for accumulator row r of this lane (query i, keys 16 jt + col):
 // a = softmax, gg = graph, bm = a*gg, nrm = sum|bm| (all keys < Tk).
 template <int NJT>
 __device__ __forceinline__ float strip_row_forward(const f4v (&s)[NJT], int r, const float (&kf)[NJT],
-                                                   const float* grow, int Tk, int col,
+                                                   const float (&gpre)[NJT], int Tk, int col,
                                                    float (&aa)[NJT], float (&gg)[NJT],
                                                    float (&bm)[NJT]) {
   float x[NJT];
@@ -422,11 +461,25 @@ __device__ __forceinline__ float strip_row_forward(const f4v (&s)[NJT], int r, c
   for (int jt = 0; jt < NJT; ++jt) {
     const int j = jt * 16 + col;
     aa[jt] = x[jt] / sum;
-    gg[jt] = j < Tk ? grow[j] : 0.f;
+    gg[jt] = j < Tk ? gpre[jt] : 0.f;
     bm[jt] = gg[jt] * aa[jt];
     nrm += fabsf(bm[jt]);
   }
   return row16_sum(nrm);
+}
+
+// graph values of this lane's 4 accumulator rows (queries i0+4g+r) x keys 16 jt + col,
+// loaded up front with clamped (branch-free) addresses so their latency overlaps the
+// MFMA strip products instead of serialising inside the row chain
+template <int NJT>
+__device__ __forceinline__ void preload_graph(const AttnArgs& a, int b, int i0, int g, int col,
+                                              float (&gp)[4][NJT]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float* grow = a.G + ((int64_t)b * a.Tq + min(i0 + 4 * g + r, a.Tq - 1)) * a.Tk;
+#pragma unroll
+    for (int jt = 0; jt < NJT; ++jt) gp[r][jt] = grow[min(jt * 16 + col, a.Tk - 1)];
+  }
 }
 
 template <int NJT>
@@ -439,15 +492,10 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgs a) {
   const int i0 = w * 16;
   constexpr int TK = NJT * 16;
   constexpr int WLD = 20;                   // per-wave P^T image [TK][16 + 4]
-  float* Vs = sm;                           // [TK][ATT_KLD]
+  float* Ks = sm;                           // [TK][ATT_KLD]
+  float* Vs = Ks + TK * ATT_KLD;            // [TK][ATT_KLD]
   float* Pw = Vs + TK * ATT_KLD + w * TK * WLD;
-  // stage V (rows >= Tk zero)
-  for (int idx = threadIdx.x; idx < TK * 16; idx += blockDim.x) {
-    const int j = idx >> 4, c4 = (idx & 15) * 4;
-    f4v vv = {0.f, 0.f, 0.f, 0.f};
-    if (j < a.Tk) vv = ld4(a.v + ((int64_t)b * a.Tk + j) * a.ldv + h * ATT_DK + c4);
-    *reinterpret_cast<f4v*>(&Vs[j * ATT_KLD + c4]) = vv;
-  }
+  stage_kv_tiles<TK>(a, b, h, Ks, Vs);
   f4v qa[4];
   {
     const int iq = min(i0 + col, a.Tq - 1);
@@ -455,11 +503,14 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgs a) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) qa[c] = ld4(qr + 16 * c);
   }
-  f4v s[NJT];
-  strip_dots<NJT>(qa, a.k + h * ATT_DK, a.ldk, (int64_t)b * a.Tk, a.Tk, col, g, s);
+  float gp[4][NJT];
+  preload_graph<NJT>(a, b, i0, g, col, gp);
   float kf[NJT];
 #pragma unroll
   for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[(int64_t)b * a.Tk + min(jt * 16 + col, a.Tk - 1)];
+  __syncthreads();  // K/V staged
+  f4v s[NJT];
+  strip_dots_lds<NJT>(qa, Ks, col, g, s);
 
   f4v pv[NJT];
 #pragma unroll
@@ -467,8 +518,7 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgs a) {
     const int i = i0 + 4 * g + r;
     const int ic = min(i, a.Tq - 1);
     float aa[NJT], gg[NJT], bm[NJT];
-    const float nrm = strip_row_forward<NJT>(s, r, kf, a.G + ((int64_t)b * a.Tq + ic) * a.Tk, a.Tk,
-                                             col, aa, gg, bm);
+    const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
     const float sden = fmaxf(nrm, 1e-12f);
     const float qf = a.qflag[(int64_t)b * a.Tq + ic];
 #pragma unroll
@@ -483,7 +533,7 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgs a) {
 #pragma unroll
   for (int jt = 0; jt < NJT; ++jt)
     *reinterpret_cast<f4v*>(&Pw[(jt * 16 + col) * WLD + 4 * g]) = pv[jt];
-  __syncthreads();  // V staged by all waves; P^T strip visible to this wave
+  __builtin_amdgcn_wave_barrier();  // this wave's P^T strip written (wave-private image)
   // O strip = P V: A[m = i][k = j] = P^T[j][i], B[k = j][n = d] = V[j][d]
   f4v o[4];
 #pragma unroll
@@ -520,11 +570,14 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
   const int i0 = w * 16;
   constexpr int TK = NJT * 16;
   const int PLD = 16 * nw + 4;
-  float* Pt = sm;             // [TK][PLD]  P^T
+  float* Pt = sm;             // [TK][PLD]  P^T                      (phase 2)
   float* dSt = sm + TK * PLD; // [TK][PLD]  dS^T (scaled by 1/8, masked)
+  float* Ks = sm;             // [TK][ATT_KLD] K_h, V_h staged for phase 1 (aliases Pt/dSt)
+  float* Vs = sm + TK * ATT_KLD;
   const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
   const int hd = h * ATT_DK;
 
+  stage_kv_tiles<TK>(a, b, h, Ks, Vs);
   // ---- phase 1: strips
   {
     f4v qa[4], oa[4];
@@ -536,19 +589,23 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
       qa[c] = ld4(qr + 16 * c);
       oa[c] = ld4(orr + 16 * c);
     }
-    f4v s[NJT], dp[NJT];
-    strip_dots<NJT>(qa, a.k + hd, a.ldk, kb, a.Tk, col, g, s);
-    strip_dots<NJT>(oa, a.v + hd, a.ldv, kb, a.Tk, col, g, dp);
+    float gp[4][NJT];
+    preload_graph<NJT>(a, b, i0, g, col, gp);
     float kf[NJT];
 #pragma unroll
     for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[kb + min(jt * 16 + col, a.Tk - 1)];
+    __syncthreads();  // K/V staged
+    f4v s[NJT], dp[NJT];
+    strip_dots_lds<NJT>(qa, Ks, col, g, s);
+    strip_dots_lds<NJT>(oa, Vs, col, g, dp);
+    __syncthreads();  // every wave is done with K/V: the region becomes P^T / dS^T
     f4v pv[NJT], dsv[NJT];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + 4 * g + r;
       const int ic = min(i, a.Tq - 1);
       float aa[NJT], gg[NJT], bm[NJT];
-      const float nrm = strip_row_forward<NJT>(s, r, kf, a.G + (qb + ic) * a.Tk, a.Tk, col, aa, gg, bm);
+      const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
       const float sden = fmaxf(nrm, 1e-12f);
       const float qf = a.qflag[qb + ic];
       float dn[NJT], t1 = 0.f;
@@ -586,70 +643,91 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
   }
   __syncthreads();
 
-  // ---- phase 2: output tiles. items [0, 4NJT): dV, [4NJT, 8NJT): dK, [8NJT, 8NJT + 4nw): dQ
+  // ---- phase 2: 16x16 output tiles, grouped (tensor, 16-column block dt):
+  //   groups [0,4): dV = P^T dO, [4,8): dK = dS^T Q  (NJT key tiles each, k = query),
+  //   groups [8,12): dQ = dS K                        (nw query tiles each, k = key).
+  // Each wave takes a CONTIGUOUS run of tiles, so consecutive tiles share the group's
+  // B column block (dO / Q / K[:, dt]), loaded once into registers per group.
 #ifdef SAVQA_ATTN_SKIP_P2  // timing experiment only: phase 1 alone
   const int nitems = 0;
 #else
   const int nitems = 8 * NJT + 4 * nw;
 #endif
-  for (int it = w; it < nitems; it += nw) {
-    f4v acc = {0.f, 0.f, 0.f, 0.f};
+  const int it0 = nitems * w / nw, it1 = nitems * (w + 1) / nw;
+  int cur = -1;
+  float bcol[8][4];  // B rows k = 16 kc + 4g + t of column dt*16 + col (kc < 8)
+  for (int it = it0; it < it1; ++it) {
+    int grp, tile;
     if (it < 8 * NJT) {
-      const bool isv = it < 4 * NJT;
-      const int t2 = isv ? it : it - 4 * NJT;
-      const int jt = t2 >> 2, dt = t2 & 3;
-      const float* img = isv ? Pt : dSt;
-      const float* src = isv ? a.dout : a.q;
-      const int64_t lds = isv ? a.lddo : a.ldq;
-      const float* arow = img + (jt * 16 + col) * PLD + 4 * g;
-      for (int ic = 0; ic < nw; ++ic) {
-        const f4v av = ld4(arow + ic * 16);
-        float bv[4];
+      grp = it / NJT;
+      tile = it - grp * NJT;
+    } else {
+      grp = 8 + (it - 8 * NJT) / nw;
+      tile = (it - 8 * NJT) % nw;
+    }
+    const int dt = grp & 3;
+    const int dcol = hd + dt * 16 + col;
+    if (grp != cur) {  // wave-uniform
+      cur = grp;
+      const float* src = grp < 4 ? a.dout : (grp < 8 ? a.q : a.k);
+      const int64_t ld = grp < 4 ? a.lddo : (grp < 8 ? a.ldq : a.ldk);
+      const int64_t base = grp < 8 ? qb : kb;
+      const int lim = grp < 8 ? a.Tq : a.Tk;
+      const int nk = grp < 8 ? nw : NJT;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int i = min(ic * 16 + 4 * g + t, a.Tq - 1);
-          bv[t] = src[(qb + i) * lds + hd + dt * 16 + col];
+      for (int kc = 0; kc < 8; ++kc) {
+        if (kc < nk) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            bcol[kc][t] = src[(base + min(kc * 16 + 4 * g + t, lim - 1)) * ld + dcol];
         }
-        acc = mfma16(av.x, bv[0], acc);
-        acc = mfma16(av.y, bv[1], acc);
-        acc = mfma16(av.z, bv[2], acc);
-        acc = mfma16(av.w, bv[3], acc);
       }
-      // dV / dK rows j = 16 jt + 4g + r, ReLU mask of the saved V / K
-      const float* msrc = isv ? a.v : a.k;
-      const int64_t mld = isv ? a.ldv : a.ldk;
+    }
+    // ReLU-mask values of this tile's 4 output rows, fetched before the MFMAs (clamped rows)
+    float mk[4];
+    {
+      const float* msrc = grp < 4 ? a.v : (grp < 8 ? a.k : a.q);
+      const int64_t mld = grp < 4 ? a.ldv : (grp < 8 ? a.ldk : a.ldq);
+      const int64_t base = grp < 8 ? kb : qb;
+      const int lim = grp < 8 ? a.Tk : a.Tq;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mk[r] = msrc[(base + min(tile * 16 + 4 * g + r, lim - 1)) * mld + dcol];
+    }
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+    if (grp < 8) {
+      const bool isv = grp < 4;
+      const float* arow = (isv ? Pt : dSt) + (tile * 16 + col) * PLD + 4 * g;
+#pragma unroll
+      for (int kc = 0; kc < 8; ++kc) {
+        if (kc < nw) {
+          const f4v av = ld4(arow + kc * 16);
+          acc = mfma16(av.x, bcol[kc][0], acc);
+          acc = mfma16(av.y, bcol[kc][1], acc);
+          acc = mfma16(av.z, bcol[kc][2], acc);
+          acc = mfma16(av.w, bcol[kc][3], acc);
+        }
+      }
+      // dV / dK rows j = 16 tile + 4g + r, ReLU mask of the saved V / K
       float* dst = isv ? a.dv : a.dk;
       const int64_t dld = isv ? a.lddv : a.lddk;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int j = jt * 16 + 4 * g + r;
-        if (j < a.Tk) {
-          const int d = hd + dt * 16 + col;
-          dst[(kb + j) * dld + d] = msrc[(kb + j) * mld + d] > 0.f ? acc[r] : 0.f;
-        }
+        const int j = tile * 16 + 4 * g + r;
+        if (j < a.Tk) dst[(kb + j) * dld + dcol] = mk[r] > 0.f ? acc[r] : 0.f;
       }
     } else {
-      const int t2 = it - 8 * NJT;
-      const int itile = t2 >> 2, dt = t2 & 3;
 #pragma unroll
-      for (int jc = 0; jc < NJT; ++jc) {
-        float av[4], bv[4];
+      for (int kc = 0; kc < NJT; ++kc) {
+        float av[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int j = jc * 16 + 4 * g + t;
-          av[t] = dSt[j * PLD + itile * 16 + col];
-          bv[t] = a.k[(kb + min(j, a.Tk - 1)) * a.ldk + hd + dt * 16 + col];
-        }
+        for (int t = 0; t < 4; ++t) av[t] = dSt[(kc * 16 + 4 * g + t) * PLD + tile * 16 + col];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc = mfma16(av[t], bv[t], acc);
+        for (int t = 0; t < 4; ++t) acc = mfma16(av[t], bcol[kc][t], acc);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int i = itile * 16 + 4 * g + r;
-        if (i < a.Tq) {
-          const int d = hd + dt * 16 + col;
-          a.dq[(qb + i) * a.lddq + d] = a.q[(qb + i) * a.ldq + d] > 0.f ? acc[r] : 0.f;
-        }
+        const int i = tile * 16 + 4 * g + r;
+        if (i < a.Tq) a.dq[(qb + i) * a.lddq + dcol] = mk[r] > 0.f ? acc[r] : 0.f;
       }
     }
   }
@@ -889,7 +967,7 @@ extern "C" int savqa_gattn_fwd(void* stream, const float* q, int64_t ldq, const 
     }
   } else if (path == 1) {
     const int njt = (int)((Tk + 15) / 16), nw = (int)((Tq + 15) / 16);
-    const size_t lds = sizeof(float) * ((size_t)njt * 16 * ATT_KLD + (size_t)nw * njt * 16 * 20);
+    const size_t lds = sizeof(float) * ((size_t)2 * njt * 16 * ATT_KLD + (size_t)nw * njt * 16 * 20);
     switch (njt) {
 #define SAVQA_FWD_CASE(N)                                                                  \
   case N:                                                                                  \
@@ -937,7 +1015,7 @@ extern "C" int savqa_gattn_bwd(void* stream, const float* q, int64_t ldq, const 
   }
   if (path == 1) {
     const int njt = (int)((Tk + 15) / 16), nw = (int)((Tq + 15) / 16);
-    const size_t lds = sizeof(float) * 2 * (size_t)njt * 16 * (16 * nw + 4);
+    const size_t lds = sizeof(float) * 2 * (size_t)njt * 16 * (size_t)std::max(16 * nw + 4, ATT_KLD);
     switch (njt) {
 #define SAVQA_BWD_CASE(N)                                                                  \
   case N:                                                                                  \
