@@ -51,6 +51,8 @@ const char* savqa_last_error(void);
  * Non-atomic launches with a linear epilogue (relu=0, beta=0, C not aliasing resid) may
  * split the last partial wave of tiles over K internally (zero-fill + atomics): results
  * then differ from a single-pass launch only in fp32 summation order.
+ * SAVQA_GEMM_SK=1 selects a stream-K launch instead (tiles cut between workgroups are
+ * combined in-launch in a fixed order; 64 MB library-owned workspace per stream).
  * ------------------------------------------------------------------------ */
 typedef struct savqa_gemm_desc {
     int64_t M, N, K;
@@ -74,7 +76,8 @@ typedef struct savqa_gemm_desc {
 int savqa_gemm(void* stream, const savqa_gemm_desc* d);
 
 /* The launch plan savqa_gemm would use for *d (no launch): out[0] = tile (32: skinny kernel, 128),
- * out[1] = split-K factor, out[2] = tail split factor (0: none), out[3] = workgroups. */
+ * out[1] = split-K factor (-1: stream-K launch), out[2] = tail split factor (0: none),
+ * out[3] = workgroups. */
 int savqa_gemm_plan(const savqa_gemm_desc* d, int32_t* out);
 
 /* out[c] += sum_r X[r*ldx + c]  (bias gradients of every Linear above) */

@@ -24,6 +24,10 @@
 // per k-tile, XCD-aware block order (T1).
 #include "common.h"
 
+#include <algorithm>
+#include <map>
+#include <mutex>
+
 #ifndef SAVQA_GEMM_OCC
 #define SAVQA_GEMM_OCC 2  // workgroups (= waves per SIMD) per CU
 #endif
@@ -389,6 +393,186 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 }
 
 // ---------------------------------------------------------------------------------------
+// Stream-K launch of the same 128x128 tile machinery (opt-in, see sk_enabled()).
+// The T x nch (tile, k-tile) iteration space is cut into G equal contiguous ranges, one per
+// workgroup (G = 2 per CU): no wave-quantisation tail, whatever T is. A workgroup walks its
+// range tile segment by tile segment; a segment covering a whole tile runs the normal
+// epilogue. A tile cut between workgroups is combined in-launch (cdna_hip_programming.md,
+// "In-launch split-K reduction"): each contributor stores its fp32 accumulator slab
+// (plain dwordx4) -> vmcnt(0) -> barrier -> lane 0 agent-scope release -> vmcnt(0) ->
+// relaxed agent fetch_add on the tile's ticket; the contributor drawing the last ticket
+// acquires (agent scope), sums every contributor's slab in workgroup order (deterministic
+// whichever arrives last), runs the full epilogue (any epilogue: ReLU included) and
+// resets the ticket. A workgroup has at most two cut segments (its first and its last),
+// so slabs are [G][2][BM*BN] floats, owned per stream by the library.
+struct SkGrid {
+  int tiles_n, nch, G;
+  int R;       // data-parallel rounds first: workgroup w owns whole tiles r*G + w, r < R
+  int64_t I0;  // = R * G * nch: start of the stream-K iteration range
+  int64_t I;   // stream-K iterations: (T - R*G) * nch
+  float* slabs;
+  int* cnt;    // per-tile tickets (zero between launches)
+};
+
+__device__ __forceinline__ int64_t sk_begin(int64_t w, const SkGrid& s) { return s.I0 + w * s.I / s.G; }
+__device__ __forceinline__ int64_t sk_owner(int64_t x, const SkGrid& s) {  // workgroup holding iteration x
+  return ((x - s.I0 + 1) * s.G - 1) / s.I;
+}
+
+template <int BM, int BN, int BK, bool AT, bool BT>
+__global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_waves_per_eu(SAVQA_GEMM_OCC, SAVQA_GEMM_OCC))) void gemm_sk_kernel(savqa_gemm_desc d, SkGrid sk,
+                                                             int avec, int bvec) {
+  using G = GemmCfg<BM, BN, BK, AT, BT>;
+  constexpr int FM = G::FM, FN = G::FN, WM = G::WM, WN = G::WN;
+  constexpr int NACC4 = FM * FN * 4;  // float4 groups of accumulators per thread
+  __shared__ __attribute__((aligned(16))) float smem[2 * (G::OA::SIZE + G::OB::SIZE)];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t w = xcd_remap(blockIdx.x, sk.G);  // neighbouring tiles share an XCD's L2
+  int64_t it = sk_begin(w, sk);
+  const int64_t it_end = sk_begin(w + 1, sk);
+  const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
+  const bool a_kgather = AT && d.a_rows;
+  const bool b_kgather = !BT && d.b_rows;
+  for (int r = 0;; ++r) {
+    // rounds r < R: the whole tile r*G + w; then this workgroup's stream-K range
+    int64_t tile, t0;
+    int kc0, kc1;
+    if (r < sk.R) {
+      tile = (int64_t)r * sk.G + w;
+      t0 = tile * sk.nch;
+      kc0 = 0;
+      kc1 = sk.nch;
+    } else {
+      if (it >= it_end) break;
+      tile = it / sk.nch;
+      t0 = tile * sk.nch;
+      kc0 = (int)(it - t0);
+      kc1 = (int)min((int64_t)sk.nch, it_end - t0);
+    }
+    const int tn = (int)(tile % sk.tiles_n);
+    const int tm = (int)(tile / sk.tiles_n);
+    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+    const int64_t kbeg = (int64_t)kc0 * BK, kend = min(d.K, (int64_t)kc1 * BK);
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const bool fast = (m0 + BM <= d.M) && (n0 + BN <= d.N) && ((kend - kbeg) % BK == 0) && avec &&
+                      bvec && !a_kgather && !b_kgather;
+    const int ntiles = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
+    const bool do_cs = AT && d.colsum_a != nullptr && tn == 0;
+    f4 cs[G::OA::ITERS];
+#pragma unroll
+    for (int q = 0; q < G::OA::ITERS; ++q) cs[q] = f4{0.f, 0.f, 0.f, 0.f};
+    if (ntiles > 0) {
+      if (fast)
+        gemm_mainloop<BM, BN, BK, AT, BT, true>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      else
+        gemm_mainloop<BM, BN, BK, AT, BT, false>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+    }
+    if constexpr (AT) {
+      if (do_cs) {  // this segment's share of the bias gradient (atomics: segments add up)
+        constexpr int PER = G::OA::PER;
+        for (int i = tid; i < BM; i += GEMM_NT) smem[i] = 0.f;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < G::OA::ITERS; ++q) {
+          const int qq = (tid + q * GEMM_NT) % PER;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) atomicAdd(&smem[4 * qq + e], cs[q][e]);
+        }
+        __syncthreads();
+        for (int i = tid; i < BM; i += GEMM_NT)
+          if (m0 + i < d.M) atomicAdd(&d.colsum_a[m0 + i], smem[i]);
+        __syncthreads();
+      }
+    }
+    bool epi = true;
+    if (!(kc0 == 0 && kc1 == sk.nch)) {
+      // ---- cut tile: publish this segment's slab, the last arriver combines
+      f4* slab = reinterpret_cast<f4*>(sk.slabs + (w * 2 + (kc0 != 0 ? 0 : 1)) * (int64_t)(BM * BN));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+            slab[((i * FN + j) * 4 + q) * GEMM_NT + tid] = v;
+          }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int64_t w0 = sk_owner(t0, sk), w1 = sk_owner(t0 + sk.nch - 1, sk);
+      int* flag = reinterpret_cast<int*>(smem);
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int ticket = __hip_atomic_fetch_add(&sk.cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = ticket == (int)(w1 - w0) ? 1 : 0;
+      }
+      __syncthreads();
+      epi = *flag != 0;
+      __syncthreads();  // the flag word is read before smem is reused
+      if (epi) {
+        if (tid == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int64_t wc = w0; wc <= w1; ++wc) {  // fixed order: deterministic sum
+          const int slot = sk_begin(wc, sk) > t0 ? 0 : 1;
+          const f4* sl = reinterpret_cast<const f4*>(sk.slabs + (wc * 2 + slot) * (int64_t)(BM * BN));
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const f4 v = sl[((i * FN + j) * 4 + q) * GEMM_NT + tid];
+                acc[i][j][4 * q] += v[0];
+                acc[i][j][4 * q + 1] += v[1];
+                acc[i][j][4 * q + 2] += v[2];
+                acc[i][j][4 * q + 3] += v[3];
+              }
+        }
+        if (tid == 0) sk.cnt[tile] = 0;  // ready for the next launch on this stream
+      }
+    }
+    if (epi) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (m >= d.M) continue;
+          const EpiRow er = epi_row(d, m, ident);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int64_t n = n0 + wn * WN + j * 32 + (lane & 31);
+            if (n >= d.N) continue;
+            epi_store(d, er, m, n, acc[i][j][r], true, d.atomic != 0);
+          }
+        }
+      }
+    }
+    if (r >= sk.R) it = t0 + kc1;
+  }
+  (void)NACC4;
+}
+
+// ---------------------------------------------------------------------------------------
 // Small-M / small-N GEMMs (the decoder and head Linears at M = B = 256 rows, their dW at
 // K = 256): one 32x32 output tile per 512-thread workgroup, the 8 waves split K eight ways
 // and fold their accumulators through LDS, so a 256x512x512 GEMM runs as 128 workgroups of
@@ -538,7 +722,60 @@ struct GemmPlan {
   GemmGrid gg;
   int grid_x, nsplit;
   int64_t zero_row0;  // >= 0: rows [zero_row0, M) of C are zero-filled before the launch
+  bool sk;            // stream-K launch (gemm_sk_kernel): G = grid_x workgroups
+  int64_t sk_iters, sk_tiles;
 };
+
+// Stream-K launch of the 128x128 path: opt-in (SAVQA_GEMM_SK=1). Measured on the step
+// shapes it loses 2-8% to the data-parallel launch (split-K / tail split) even where it
+// removes a 10-20% wave-quantisation tail: the persistent walk gives up the dynamic
+// block dispatch that staggers tiles, and in the training step the other HIP stream's
+// kernels already fill the data-parallel tail.
+static bool sk_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SAVQA_GEMM_SK");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// Per-(device, stream) stream-K workspace: accumulator slabs [G][2][128*128] fp32 and
+// per-tile tickets (zeroed once; each combining workgroup resets its ticket).
+struct SkWorkspace {
+  float* slabs = nullptr;
+  int* cnt = nullptr;
+  int64_t slab_floats = 0, ncnt = 0;
+};
+
+static int sk_workspace(hipStream_t s, int64_t slab_floats, int64_t ncnt, SkWorkspace& out) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, SkWorkspace> pool;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(SAVQA_EUNSUP, "savqa_gemm: hipGetDevice");
+  std::lock_guard<std::mutex> lk(mu);
+  SkWorkspace& w = pool[{dev, s}];
+  if (w.slab_floats < slab_floats || w.ncnt < ncnt) {
+    if (w.slabs || w.cnt) (void)hipStreamSynchronize(s);  // previous launches may still read them
+    if (w.slab_floats < slab_floats) {
+      if (w.slabs) (void)hipFree(w.slabs);
+      w.slabs = nullptr;
+      if (hipMalloc(&w.slabs, slab_floats * sizeof(float)) != hipSuccess)
+        return fail(SAVQA_EUNSUP, "savqa_gemm: stream-K slab allocation failed");
+      w.slab_floats = slab_floats;
+    }
+    if (w.ncnt < ncnt) {
+      if (w.cnt) (void)hipFree(w.cnt);
+      w.cnt = nullptr;
+      const int64_t n = std::max<int64_t>(ncnt, 4096);
+      if (hipMalloc(&w.cnt, n * sizeof(int)) != hipSuccess ||
+          hipMemsetAsync(w.cnt, 0, n * sizeof(int), s) != hipSuccess)
+        return fail(SAVQA_EUNSUP, "savqa_gemm: stream-K ticket allocation failed");
+      w.ncnt = n;
+    }
+  }
+  out = w;
+  return 0;
+}
 
 }  // namespace savqa
 
@@ -570,6 +807,21 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
     p.grid_x = (int)((d.M + 31) / 32) * p.gg.tiles_n;
     p.zero_row0 = -1;
     p.gg.tail_f = 1;
+    p.sk = false;
+    return 0;
+  }
+  p.sk = false;
+  if (sk_enabled()) {
+    p.tile = 128;
+    p.split = 1;
+    p.nsplit = 1;
+    p.gg.tiles_n = (int)((d.N + 127) / 128);
+    p.sk_tiles = tiles128;
+    p.sk_iters = tiles128 * ((d.K + BK - 1) / BK);
+    p.grid_x = (int)std::min<int64_t>(slots, std::max<int64_t>(p.sk_iters, 1));
+    p.zero_row0 = -1;
+    p.gg.tail_f = 1;
+    p.sk = true;
     return 0;
   }
   p.tile = 128;
@@ -643,7 +895,7 @@ extern "C" int savqa_gemm_plan(const savqa_gemm_desc* dp, int32_t* out) {
   GemmPlan p{};
   if (int rc = plan_gemm(d, p)) return rc;
   out[0] = p.tile;
-  out[1] = p.split;
+  out[1] = p.sk ? -1 : p.split;
   out[2] = p.gg.tail_f > 1 ? p.gg.tail_f : 0;
   out[3] = p.grid_x * p.nsplit;
   return 0;
@@ -663,7 +915,36 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
       hipMemset2DAsync(d.C + p.zero_row0 * d.ldc, d.ldc * sizeof(float), 0, d.N * sizeof(float),
                        d.M - p.zero_row0, s) != hipSuccess)
     return fail(SAVQA_EUNSUP, "savqa_gemm: tail zero-fill failed");
-  if (p.tile == 128) {
+  if (p.sk) {
+    if (d.K == 0) {  // empty reduction: the epilogue alone (bias, residual, ...) via the
+      GemmPlan q = p;  // data-parallel kernel
+      q.sk = false;
+      q.gg.kchunk = 0;
+      q.gg.full = (int)p.sk_tiles;
+      q.gg.tail_t0 = (int)p.sk_tiles;
+      q.grid_x = (int)p.sk_tiles;
+      dispatch_layout<128, 128, SAVQA_GEMM_BK>(d, q, s, avec, bvec);
+      return check_launch("savqa_gemm");
+    }
+    SkWorkspace ws;
+    if (int rc = sk_workspace(s, (int64_t)p.grid_x * 2 * 128 * 128, p.sk_tiles, ws)) return rc;
+    SkGrid sk;
+    sk.tiles_n = p.gg.tiles_n;
+    sk.nch = (int)((d.K + SAVQA_GEMM_BK - 1) / SAVQA_GEMM_BK);
+    sk.G = p.grid_x;
+    // whole-tile rounds while at least two rounds' worth remain; stream-K over the rest
+    sk.R = (int)std::max<int64_t>(0, p.sk_tiles / p.grid_x - 1);
+    sk.I0 = (int64_t)sk.R * p.grid_x * sk.nch;
+    sk.I = p.sk_iters - sk.I0;
+    sk.slabs = ws.slabs;
+    sk.cnt = ws.cnt;
+    const dim3 g(p.grid_x), b(GEMM_NT);
+    constexpr int BK = SAVQA_GEMM_BK;
+    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, false, true>), g, b, 0, s, d, sk, avec, bvec);
+    else if (!d.a_trans) hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, false, false>), g, b, 0, s, d, sk, avec, bvec);
+    else if (!d.b_trans) hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, true, false>), g, b, 0, s, d, sk, avec, bvec);
+    else hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, true, true>), g, b, 0, s, d, sk, avec, bvec);
+  } else if (p.tile == 128) {
     dispatch_layout<128, 128, SAVQA_GEMM_BK>(d, p, s, avec, bvec);
   } else {
     const dim3 g(p.grid_x), b(64 * SK_WAVES);
