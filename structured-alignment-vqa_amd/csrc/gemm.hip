@@ -43,6 +43,42 @@ typedef float f4 __attribute__((ext_vector_type(4)));  // native vector (HIP flo
 
 constexpr int GEMM_NT = 256;
 
+// MFMA shape of the 128x128 path (fp32 in, fp32 accumulate; same 64 FLOP/clk/SIMD):
+//   Mi32: v_mfma_f32_32x32x2_f32, 32-row fragments, 16 accumulator VGPRs per fragment;
+//   Mi16: v_mfma_f32_16x16x4_f32, 16-row fragments, 4 accumulator VGPRs per fragment
+//         (per FLOP it moves 40% fewer accumulator registers through the matrix core).
+// A fragment's operand lane (i, q) feeds k = KCH*c + 4q + j in MFMA step j (b128 trick).
+struct Mi32 {
+  static constexpr int FR = 32, KCH = 8, NACC = 16;
+  using Acc = f32x16;
+  static __device__ __forceinline__ Acc mma(float a, float b, Acc c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ int lane_i(int lane) { return lane & 31; }
+  static __device__ __forceinline__ int lane_q(int lane) { return lane >> 5; }
+  static __device__ __forceinline__ int row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+  static __device__ __forceinline__ int col(int lane) { return lane & 31; }
+};
+struct Mi16 {
+  static constexpr int FR = 16, KCH = 16, NACC = 4;
+  using Acc = f4;
+  static __device__ __forceinline__ Acc mma(float a, float b, Acc c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ int lane_i(int lane) { return lane & 15; }
+  static __device__ __forceinline__ int lane_q(int lane) { return lane >> 4; }
+  static __device__ __forceinline__ int row(int r, int lane) { return 4 * (lane >> 4) + r; }
+  static __device__ __forceinline__ int col(int lane) { return lane & 15; }
+};
+#ifndef SAVQA_GEMM_MI
+#define SAVQA_GEMM_MI 32
+#endif
+#if SAVQA_GEMM_MI == 16
+using GemmMi = Mi16;
+#else
+using GemmMi = Mi32;
+#endif
+
 template <int BMX, int BK, bool ROW>
 struct Operand {
   static constexpr int LD = ROW ? BK + 4 : BMX + 4;
@@ -126,17 +162,18 @@ struct Operand {
     }
   }
 
-  // MFMA operand values of one 8-k chunk c for fragment rows [f*32, f*32+32) of this
-  // wave's sub-tile (wbase): v[j] feeds MFMA step j (k = 8c + 4*(lane>>5) + j).
+  // MFMA operand values of k-chunk c (MI::KCH wide) for fragment rows [f*FR, f*FR+FR) of
+  // this wave's sub-tile (wbase): v[j] feeds MFMA step j (k = KCH*c + 4*q + j).
+  template <class MI>
   static __device__ __forceinline__ void fetch(const float* __restrict__ s, int wbase, int f,
                                                int c, int lane, float (&v)[4]) {
-    const int q = lane >> 5, i = lane & 31;
+    const int q = MI::lane_q(lane), i = MI::lane_i(lane);
     if constexpr (ROW) {
-      const f4 t = *reinterpret_cast<const f4*>(&s[(wbase + f * 32 + i) * LD + c * 8 + 4 * q]);
+      const f4 t = *reinterpret_cast<const f4*>(&s[(wbase + f * MI::FR + i) * LD + c * MI::KCH + 4 * q]);
       v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = s[(c * 8 + 4 * q + j) * LD + wbase + f * 32 + i];
+      for (int j = 0; j < 4; ++j) v[j] = s[(c * MI::KCH + 4 * q + j) * LD + wbase + f * MI::FR + i];
     }
   }
 };
@@ -145,8 +182,10 @@ template <int BM, int BN, int BK, bool AT, bool BT>
 struct GemmCfg {
   using OA = Operand<BM, BK, !AT>;
   using OB = Operand<BN, BK, BT>;
+  using MI = GemmMi;
+  using Acc = typename MI::Acc;
   static constexpr int WM = BM / 2, WN = BN / 2;
-  static constexpr int FM = WM / 32, FN = WN / 32;
+  static constexpr int FM = WM / MI::FR, FN = WN / MI::FR;
 };
 
 // Epilogue of one output element (include/savqa.h formula), split per row / element.
@@ -198,22 +237,24 @@ __device__ __forceinline__ void epi_store(const savqa_gemm_desc& d, const EpiRow
 template <int BM, int BN, int BK, bool AT, bool BT>
 __device__ __forceinline__ void gemm_compute_tile(
     const float* __restrict__ As, const float* __restrict__ Bs, int wm, int wn, int lane,
-    f32x16 (&acc)[GemmCfg<BM, BN, BK, AT, BT>::FM][GemmCfg<BM, BN, BK, AT, BT>::FN]) {
+    typename GemmCfg<BM, BN, BK, AT, BT>::Acc (&acc)[GemmCfg<BM, BN, BK, AT, BT>::FM][GemmCfg<BM, BN, BK, AT, BT>::FN]) {
   using G = GemmCfg<BM, BN, BK, AT, BT>;
-  // operands of 8-k chunk c+1 are read from LDS while chunk c's MFMAs run
+  using MI = typename G::MI;
+  constexpr int NC = BK / MI::KCH;
+  // operands of k-chunk c+1 are read from LDS while chunk c's MFMAs run
   float a[2][G::FM][4], b[2][G::FN][4];
 #pragma unroll
-  for (int i = 0; i < G::FM; ++i) G::OA::fetch(As, wm * G::WM, i, 0, lane, a[0][i]);
+  for (int i = 0; i < G::FM; ++i) G::OA::template fetch<MI>(As, wm * G::WM, i, 0, lane, a[0][i]);
 #pragma unroll
-  for (int j = 0; j < G::FN; ++j) G::OB::fetch(Bs, wn * G::WN, j, 0, lane, b[0][j]);
+  for (int j = 0; j < G::FN; ++j) G::OB::template fetch<MI>(Bs, wn * G::WN, j, 0, lane, b[0][j]);
 #pragma unroll
-  for (int c = 0; c < BK / 8; ++c) {
+  for (int c = 0; c < NC; ++c) {
     const int cur = c & 1;
-    if (c + 1 < BK / 8) {
+    if (c + 1 < NC) {
 #pragma unroll
-      for (int i = 0; i < G::FM; ++i) G::OA::fetch(As, wm * G::WM, i, c + 1, lane, a[cur ^ 1][i]);
+      for (int i = 0; i < G::FM; ++i) G::OA::template fetch<MI>(As, wm * G::WM, i, c + 1, lane, a[cur ^ 1][i]);
 #pragma unroll
-      for (int j = 0; j < G::FN; ++j) G::OB::fetch(Bs, wn * G::WN, j, c + 1, lane, b[cur ^ 1][j]);
+      for (int j = 0; j < G::FN; ++j) G::OB::template fetch<MI>(Bs, wn * G::WN, j, c + 1, lane, b[cur ^ 1][j]);
     }
 #ifdef SAVQA_GEMM_SGB
     __builtin_amdgcn_sched_barrier(0);
@@ -227,7 +268,7 @@ __device__ __forceinline__ void gemm_compute_tile(
       for (int i = 0; i < G::FM; ++i)
 #pragma unroll
         for (int j = 0; j < G::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][i][s], b[cur][j][s], acc[i][j], 0, 0, 0);
+          acc[i][j] = MI::mma(a[cur][i][s], b[cur][j][s], acc[i][j]);
 #ifdef SAVQA_GEMM_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -241,7 +282,7 @@ template <int BM, int BN, int BK, bool AT, bool BT, bool FAST>
 __device__ __forceinline__ void gemm_mainloop(
     const savqa_gemm_desc& d, float* smem, int64_t m0, int64_t n0, int64_t kbeg, int64_t kend,
     int ntiles,
-    f32x16 (&acc)[GemmCfg<BM, BN, BK, AT, BT>::FM][GemmCfg<BM, BN, BK, AT, BT>::FN],
+    typename GemmCfg<BM, BN, BK, AT, BT>::Acc (&acc)[GemmCfg<BM, BN, BK, AT, BT>::FM][GemmCfg<BM, BN, BK, AT, BT>::FN],
     bool do_cs, f4 (&cs)[GemmCfg<BM, BN, BK, AT, BT>::OA::ITERS]) {
   using G = GemmCfg<BM, BN, BK, AT, BT>;
   using OA = typename G::OA;
@@ -331,13 +372,14 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
   const int64_t m0 = (int64_t)tm * BM;
   const int64_t n0 = (int64_t)tn * BN;
 
-  f32x16 acc[FM][FN];
+  using MI = typename G::MI;
+  typename G::Acc acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < MI::NACC; ++r) acc[i][j][r] = 0.f;
 
   // block-uniform choice of the branch-free main loop
   const bool a_kgather = AT && d.a_rows;
@@ -378,13 +420,13 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    for (int r = 0; r < MI::NACC; ++r) {
+      const int64_t m = m0 + wm * WM + i * MI::FR + MI::row(r, lane);
       if (m >= d.M) continue;
       const EpiRow er = epi_row(d, m, ident);
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int64_t n = n0 + wn * WN + j * 32 + (lane & 31);
+        const int64_t n = n0 + wn * WN + j * MI::FR + MI::col(lane);
         if (n >= d.N) continue;
         epi_store(d, er, m, n, acc[i][j][r], first_split, atomic);
       }
@@ -424,7 +466,8 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
                                                              int avec, int bvec) {
   using G = GemmCfg<BM, BN, BK, AT, BT>;
   constexpr int FM = G::FM, FN = G::FN, WM = G::WM, WN = G::WN;
-  constexpr int NACC4 = FM * FN * 4;  // float4 groups of accumulators per thread
+  using MI = typename G::MI;
+  constexpr int NACC4 = FM * FN * MI::NACC / 4;  // float4 groups of accumulators per thread
   __shared__ __attribute__((aligned(16))) float smem[2 * (G::OA::SIZE + G::OB::SIZE)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -456,13 +499,13 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
     const int tm = (int)(tile / sk.tiles_n);
     const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
     const int64_t kbeg = (int64_t)kc0 * BK, kend = min(d.K, (int64_t)kc1 * BK);
-    f32x16 acc[FM][FN];
+    typename G::Acc acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int r = 0; r < MI::NACC; ++r) acc[i][j][r] = 0.f;
     const bool fast = (m0 + BM <= d.M) && (n0 + BN <= d.N) && ((kend - kbeg) % BK == 0) && avec &&
                       bvec && !a_kgather && !b_kgather;
     const int ntiles = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
@@ -502,9 +545,9 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 #pragma unroll
         for (int j = 0; j < FN; ++j)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < MI::NACC / 4; ++q) {
             const f4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-            slab[((i * FN + j) * 4 + q) * GEMM_NT + tid] = v;
+            slab[((i * FN + j) * (MI::NACC / 4) + q) * GEMM_NT + tid] = v;
           }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -530,7 +573,7 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 #pragma unroll
           for (int j = 0; j < FN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            for (int r = 0; r < MI::NACC; ++r) acc[i][j][r] = 0.f;
         for (int64_t wc = w0; wc <= w1; ++wc) {  // fixed order: deterministic sum
           const int slot = sk_begin(wc, sk) > t0 ? 0 : 1;
           const f4* sl = reinterpret_cast<const f4*>(sk.slabs + (wc * 2 + slot) * (int64_t)(BM * BN));
@@ -539,8 +582,8 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 #pragma unroll
             for (int j = 0; j < FN; ++j)
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const f4 v = sl[((i * FN + j) * 4 + q) * GEMM_NT + tid];
+              for (int q = 0; q < MI::NACC / 4; ++q) {
+                const f4 v = sl[((i * FN + j) * (MI::NACC / 4) + q) * GEMM_NT + tid];
                 acc[i][j][4 * q] += v[0];
                 acc[i][j][4 * q + 1] += v[1];
                 acc[i][j][4 * q + 2] += v[2];
@@ -554,13 +597,13 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        for (int r = 0; r < MI::NACC; ++r) {
+          const int64_t m = m0 + wm * WM + i * MI::FR + MI::row(r, lane);
           if (m >= d.M) continue;
           const EpiRow er = epi_row(d, m, ident);
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
-            const int64_t n = n0 + wn * WN + j * 32 + (lane & 31);
+            const int64_t n = n0 + wn * WN + j * MI::FR + MI::col(lane);
             if (n >= d.N) continue;
             epi_store(d, er, m, n, acc[i][j][r], true, d.atomic != 0);
           }
