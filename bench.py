@@ -3,7 +3,8 @@
 
 A step = forward + label-smoothed loss (+ MIL-NCE) + backward + Adam over one synthetic
 batch already resident in HBM (cfg 2: fp32, 256 samples/GPU, 36 regions x 2048-d,
-14-token questions, 59 scene-graph nodes, d=512, 8 heads, 6+6 layers per stack).
+14-token questions, 59 scene-graph nodes, d=512, 8 heads, 6+6 layers per stack, training
+dropout 0.5 = the reference's default, main_itp_ddp_tar_super_node.py:466, submit.py:98).
 N GPUs = one process per GPU (torch.distributed.run), weak scaling, RCCL all-reduce of
 the live gradients streamed out of the backward (savqa_amd.ddp).
 
@@ -40,7 +41,7 @@ def train_flops_per_sample(Tv=50, Ts=73, Lq=14, Nv=36, Ns=59, d=512, L=6, C=914,
     return 3.0 * (stack(Tv) + stack(Ts) + heads + mil)
 
 
-def cpu_baseline(seconds=15.0, B=4):
+def cpu_baseline(seconds=15.0, B=4, rate=0.5):
     """Time the CPU oracle (oracle/savqa_oracle.py, the parity checker) on the host:
     fwd + loss + bwd + Adam at the cfg-1 shape (B=4). Bounded sample."""
     from oracle import hashfill
@@ -70,7 +71,8 @@ def cpu_baseline(seconds=15.0, B=4):
     def step(i):
         for p in P.values():
             p.grad = None
-        lc, lv, ls, mil, _ = O.attmodel_forward(P, inp)
+        drop = (1000 + i, rate) if rate > 0 else None
+        lc, lv, ls, mil, _ = O.attmodel_forward(P, inp, drop=drop)
         loss, _ = O.train_loss(lc, lv, ls, answer, mil)
         loss.backward()
         with torch.no_grad():
@@ -87,7 +89,7 @@ def cpu_baseline(seconds=15.0, B=4):
     return {"value": round(B * n / dt, 3), "unit": "QA-samples/s", "cores": threads,
             "kind": "port",
             "sample": f"oracle/savqa_oracle.py train step (fwd+loss+bwd+Adam), cfg-1 shape "
-                      f"B={B}, {n} steps in {dt:.1f}s, torch CPU {threads} threads"}
+                      f"B={B}, dropout {rate}, {n} steps in {dt:.1f}s, torch CPU {threads} threads"}
 
 
 ROOFLINE_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
@@ -111,6 +113,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="samples per GPU (cfg 2: 256)")
+    ap.add_argument("--dropout", type=float, default=0.5,
+                    help="dropout_rate (reference training default 0.5, main:466)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
@@ -136,8 +140,8 @@ def main():
     from savqa_amd.utils import init_params_
 
     B = args.batch
-    model = AttModel(None, 512, 1024, 914, 40, 450, 49, 6, 8, 0.0, 0.0, 311, True, device=dev,
-                     init=False)
+    model = AttModel(None, 512, 1024, 914, 40, 450, 49, 6, 8, args.dropout, 0.1, 311, True,
+                     device=dev, init=False)
     init_params_(model, seed=0)  # identical on every rank (same seed), like a broadcast
     model.train()
     if args.serial:
@@ -212,7 +216,7 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.cpu_seconds)
+            cpu = cpu_baseline(args.cpu_seconds, rate=args.dropout)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "QA-samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
@@ -221,7 +225,7 @@ def main():
             "config": {"workload": "cfg2: model_v=3 train step (fwd+loss+bwd+Adam), fp32, "
                                    "36 regions x 2048-d, 14 q-tokens, 59 nodes, d=512 h=8 L=6, "
                                    "MIL-NCE only_obj topN=5 H=1024, 914 classes, decMask, "
-                                   "dropout 0",
+                                   f"dropout {args.dropout}",
                        "per_gpu_batch": B, "global_batch": world * B,
                        "parallelism": f"dp{world}"},
             "model_tflops": round(value * fl / 1e12, 2),

@@ -138,13 +138,42 @@ int savqa_graph_build(void* stream, const int32_t* node_mask, const int32_t* q_m
                       int64_t Lq, int32_t dec_mask_on, float* graph_diag, float* graph,
                       float* dec_mask);
 
-/* dec0[b,:] = emb[idx,:]*scale + pos[0,:]   (AttModel_x3.py:141-146, modules.py:40-43) */
+/* dec0[b,:] = D(emb[idx,:]*scale + pos[0,:])   (AttModel_x3.py:141-147, :267-274,
+ * modules.py:40-43); D = dec_dropout with keep mask savqa_dropout(site) when p > 0
+ * (element index b*d + c), identity when p == 0 (eval / dropout_rate 0). */
 int savqa_dec_init(void* stream, const float* emb, int64_t idx, float scale, const float* pos,
-                   int64_t B, int64_t d, float* out);
+                   int64_t B, int64_t d, uint64_t seed, int32_t site, float p, float* out);
 
-/* backward of savqa_dec_init: demb[idx,:] += scale*sum_b g[b,:]; dpos[0,:] += sum_b g[b,:] */
+/* backward of savqa_dec_init: with g' = D'(g): demb[idx,:] += scale*sum_b g'[b,:];
+ * dpos[0,:] += sum_b g'[b,:] */
 int savqa_dec_init_bwd(void* stream, const float* g, int64_t B, int64_t d, int64_t idx, float scale,
-                       float* demb, float* dpos);
+                       uint64_t seed, int32_t site, float p, float* demb, float* dpos);
+
+/* ------------------------------------------------------------------------
+ * Dropout (nn.Dropout(dropout_rate) sites of model_v=3: stack inputs
+ * AttModel_x3.py:71-72/:102 (vis: position-table dropout, then enc_dropout) and :227
+ * (syb enc_dropout); decoder inputs :147/:274 (savqa_dec_init); heads :482-500).
+ * Keep bit of element idx at dropout site `site` (>= 0) under step seed `seed`:
+ *   z = seed + site*0xD1B54A32D192ED03 + (idx+1)*0x9E3779B97F4A7C15   (mod 2^64)
+ *   z = (z ^ z>>30)*0xBF58476D1CE4E5B9; z = (z ^ z>>27)*0x94D049BB133111EB; z ^= z>>31
+ *   keep = (uint32)(z>>32) >= floor(p*2^32);  kept values are scaled by 1/(1-p).
+ * (torch's Philox stream is not reproducible outside torch; the backward regenerates
+ * masks from (seed, site, idx), so none are stored.) p == 1 drops everything.
+ * ------------------------------------------------------------------------ */
+/* out[i] = in[i]*keep(i)*scale (in == out allowed); forward and backward of nn.Dropout */
+int savqa_dropout(void* stream, const float* in, int64_t n, uint64_t seed, int32_t site, float p,
+                  float* out);
+
+/* out[b,t,c] = Dx(z[b,t,c] + Dp(pos[t,c])), idx = (b*T+t)*d + c; Dp = identity if
+ * site_pos < 0 (syb stack), else the vis stack's position-table dropout (:71-72). */
+int savqa_posadd_dropout(void* stream, const float* z, const float* pos, int64_t B, int64_t T,
+                         int64_t d, uint64_t seed, int32_t site_pos, int32_t site_x, float p,
+                         float* out);
+
+/* backward: dz = Dx'(g) (dz == g allowed); dpos[t,c] += sum_b Dp'(dz[b,t,c]) */
+int savqa_posadd_dropout_bwd(void* stream, const float* g, int64_t B, int64_t T, int64_t d,
+                             uint64_t seed, int32_t site_pos, int32_t site_x, float p, float* dz,
+                             float* dpos);
 
 /* out[t][c] += sum_b X[(b*T+t)*ldx + c]: gradient of the learned position tables
  * (syb_positional_encoding, AttModel_x3.py:100-101, :225-226; padding_idx=-1 row untouched

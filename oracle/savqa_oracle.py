@@ -23,11 +23,50 @@ from __future__ import annotations
 import math
 from typing import Dict
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
 PAD = 400000          # AttModel_x3.py:13
 PAD_NEG = -2 ** 32 + 1  # modules.py:261 (becomes -4294967296.0 in fp32)
+
+
+# --------------------------------------------------------------------------- dropout
+# nn.Dropout sites of model_v=3 (p = dropout_rate in training): torch draws masks from its
+# Philox stream, which no other implementation can reproduce, so parity with p > 0 uses
+# the build's documented counter-hash stream (include/savqa.h, "Dropout") on both sides:
+# everything except WHICH elements are dropped is then checked against this restatement.
+VIS_SITES = (1, 2, 3)    # vis position-table dropout (:71-72), enc_dropout (:102), dec (:147)
+SYB_SITES = (-1, 4, 5)   # syb: no position dropout (:178), enc_dropout (:227), dec (:274)
+HEAD_SITES = {"cls": 6, "cls_vis": 7, "cls_syb": 8}   # heads (:482-500)
+
+_K1, _K2 = np.uint64(0xD1B54A32D192ED03), np.uint64(0x9E3779B97F4A7C15)
+_M1, _M2 = np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB)
+
+
+def dropout_keep(seed: int, site: int, n: int, p: float) -> np.ndarray:
+    """Keep mask (bool[n]) of elements 0..n-1 at dropout site `site` (SplitMix64 of
+    counter seed + site*K1 + (idx+1)*K2, keep iff the high 32 bits >= floor(p*2^32))."""
+    with np.errstate(over="ignore"):
+        idx = np.arange(n, dtype=np.uint64)
+        z = np.uint64(seed) + np.uint64(site) * _K1 + (idx + np.uint64(1)) * _K2
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        z = z ^ (z >> np.uint64(31))
+    if p >= 1:
+        return np.zeros(n, dtype=bool)
+    thr = min(int(p * 4294967296.0), 0xFFFFFFFF) if p > 0 else 0
+    return (z >> np.uint64(32)) >= np.uint64(thr)
+
+
+def dropout(x, drop, site):
+    """nn.Dropout(p)(x) with the counter-hash mask; drop = (seed, p) or None (identity)."""
+    if drop is None or site < 0:
+        return x
+    seed, p = drop
+    keep = torch.from_numpy(dropout_keep(seed, site, x.numel(), p)).reshape(x.shape)
+    scale = 0.0 if p >= 1 else float(np.float32(1.0) / (np.float32(1.0) - np.float32(p)))
+    return x * keep.to(x.dtype) * scale
 
 
 # --------------------------------------------------------------------------- blocks
@@ -140,7 +179,8 @@ def build_graphs(node_mask, q_mask, q_graph, node_graph=None, decMask=True):
 
 
 # --------------------------------------------------------------------------- stacks
-def _encoder_decoder(P, pre, fea, graph_diag, graph, dec_mask, num_blocks=6, h=8):
+def _encoder_decoder(P, pre, fea, graph_diag, graph, dec_mask, num_blocks=6, h=8, drop=None,
+                     dec_site=-1):
     """Encoder schedule AttModel_x3.py:127-139 and decoder :141-154."""
     x = fea
     for i in range(num_blocks):
@@ -153,6 +193,7 @@ def _encoder_decoder(P, pre, fea, graph_diag, graph, dec_mask, num_blocks=6, h=8
     dec = F.embedding(dec_in, P[f"{pre}.dec_emb.lookup_table"], 0) * (d ** 0.5)  # modules.py:40-43
     dec = dec + F.embedding(torch.zeros((B, 1), dtype=torch.long),
                             P[f"{pre}.dec_positional_encoding.lookup_table"], -1)
+    dec = dropout(dec, drop, dec_site)                                       # dec_dropout
     for i in range(num_blocks):
         dec = causal_mha(P, f"{pre}.dec_self_attention_{i}", dec, dec, dec, h)
         dec = graph_mha(P, f"{pre}.dec_vanilla_attention_{i}", dec, x, x, dec_mask, h)
@@ -161,20 +202,22 @@ def _encoder_decoder(P, pre, fea, graph_diag, graph, dec_mask, num_blocks=6, h=8
 
 
 def vis_grid_forward(P, vis_fea, vis_mask, q_ipt, q_graph, q_mask, decMask=True,
-                     num_blocks=6, h=8, pre="att_vis_grid"):
+                     num_blocks=6, h=8, pre="att_vis_grid", drop=None):
     """AttModel_vis_grid.forward, AttModel_x3.py:91-156."""
     q = F.embedding(q_ipt, P[f"{pre}.syb_emb.weight"])
     q = linear(q, P, f"{pre}.syb_mlp.0", relu=True)
     fea = linear(torch.cat([vis_fea, q], dim=1), P, f"{pre}.syb_mlp2")
     T = fea.size(1)
     pos = torch.arange(T).unsqueeze(0).repeat(fea.size(0), 1)
-    fea = fea + F.embedding(pos, P[f"{pre}.syb_positional_encoding.0.lookup_table"], -1)
+    pe = F.embedding(pos, P[f"{pre}.syb_positional_encoding.0.lookup_table"], -1)
+    fea = fea + dropout(pe, drop, VIS_SITES[0])              # Sequential(embedding, Dropout)
+    fea = dropout(fea, drop, VIS_SITES[1])                   # enc_dropout (:102)
     gd, g, dm = build_graphs(vis_mask, q_mask, q_graph, None, decMask)
-    return _encoder_decoder(P, pre, fea, gd, g, dm, num_blocks, h)
+    return _encoder_decoder(P, pre, fea, gd, g, dm, num_blocks, h, drop, VIS_SITES[2])
 
 
 def syb_forward(P, syb_ipt, syb_mask, syb_graph, q_ipt, q_graph, q_mask, decMask=True,
-                num_blocks=6, h=8, pre="att_syb"):
+                num_blocks=6, h=8, pre="att_syb", drop=None):
     """AttModel_syb.forward, AttModel_x3.py:214-282."""
     q = F.embedding(q_ipt, P[f"{pre}.syb_emb.weight"])
     q = linear(q, P, f"{pre}.syb_mlp.0", relu=True)
@@ -182,8 +225,9 @@ def syb_forward(P, syb_ipt, syb_mask, syb_graph, q_ipt, q_graph, q_mask, decMask
     T = fea.size(1)
     pos = torch.arange(T).unsqueeze(0).repeat(fea.size(0), 1)
     fea = fea + F.embedding(pos, P[f"{pre}.syb_positional_encoding.lookup_table"], -1)
+    fea = dropout(fea, drop, SYB_SITES[1])                   # enc_dropout (:227)
     gd, g, dm = build_graphs(syb_mask, q_mask, q_graph, syb_graph, decMask)
-    return _encoder_decoder(P, pre, fea, gd, g, dm, num_blocks, h)
+    return _encoder_decoder(P, pre, fea, gd, g, dm, num_blocks, h, drop, SYB_SITES[2])
 
 
 def mil_nce_forward(P, vis_fea, macro_ipt, macro_obj_loc, pos_obj, neg_obj, obj_mask,
@@ -208,10 +252,11 @@ def mil_nce_forward(P, vis_fea, macro_ipt, macro_obj_loc, pos_obj, neg_obj, obj_
     return out, mil, 0
 
 
-def heads(P, fea_vis, fea_syb):
-    """AttModel.forward heads, AttModel_x3.py:531-541 (mcb=False, dropout p=0)."""
+def heads(P, fea_vis, fea_syb, drop=None):
+    """AttModel.forward heads, AttModel_x3.py:531-541 (mcb=False)."""
     def head(x, name):
-        return linear(linear(x, P, f"{name}.0", relu=True), P, f"{name}.3")
+        hdn = dropout(linear(x, P, f"{name}.0", relu=True), drop, HEAD_SITES[name])
+        return linear(hdn, P, f"{name}.3")
     logits_vis = head(fea_vis, "cls_vis").squeeze(1)
     logits_syb = head(fea_syb, "cls_syb").squeeze(1)
     fea = torch.cat((fea_syb.squeeze(1), fea_vis.squeeze(1)), 1)
@@ -219,16 +264,18 @@ def heads(P, fea_vis, fea_syb):
     return logits_concat, logits_vis, logits_syb
 
 
-def attmodel_forward(P, inp: Dict[str, torch.Tensor], decMask=True, num_blocks=6, h=8):
-    """AttModel.forward, AttModel_x3.py:512-542 (only_obj, mcb=False)."""
+def attmodel_forward(P, inp: Dict[str, torch.Tensor], decMask=True, num_blocks=6, h=8,
+                     drop=None):
+    """AttModel.forward, AttModel_x3.py:512-542 (only_obj, mcb=False); drop = (seed, p)
+    applies the training-mode dropout sites with the counter-hash masks."""
     new_macro, mil_obj, mil_rel = mil_nce_forward(
         P, inp["vis_fea"], inp["macro_ipt"], inp["macro_obj_loc"],
         inp["micro_positive_obj"], inp["micro_negative_obj"], inp["micro_obj_mask"])
     f_vis = vis_grid_forward(P, inp["vis_fea"], inp["vis_mask"], inp["q_ipt"], inp["q_graph"],
-                             inp["q_mask"], decMask, num_blocks, h)
+                             inp["q_mask"], decMask, num_blocks, h, drop=drop)
     f_syb = syb_forward(P, new_macro, inp["macro_mask"], inp["macro_graph"], inp["q_ipt"],
-                        inp["q_graph"], inp["q_mask"], decMask, num_blocks, h)
-    lc, lv, ls = heads(P, f_vis, f_syb)
+                        inp["q_graph"], inp["q_mask"], decMask, num_blocks, h, drop=drop)
+    lc, lv, ls = heads(P, f_vis, f_syb, drop)
     return lc, lv, ls, mil_obj, mil_rel
 
 

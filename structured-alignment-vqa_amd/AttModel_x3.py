@@ -184,9 +184,9 @@ class CompactBilinearPooling(nn.Module):
 
 class _AttModelFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, model, decMask, anchor, *tensors):
+    def forward(ctx, model, decMask, drop, anchor, *tensors):
         inp = dict(zip(_INPUT_NAMES, tensors))
-        (lc, lv, ls, mil), saved = model._engine.forward(inp, decMask)
+        (lc, lv, ls, mil), saved = model._engine.forward(inp, decMask, drop)
         ctx.model = model
         ctx.saved = saved
         return lc, lv, ls, mil
@@ -205,7 +205,7 @@ class _AttModelFn(torch.autograd.Function):
         model._engine.backward(ctx.saved, z(dlc, (B, Cc)), z(dlv, (B, Cc)), z(dls, (B, Cc)),
                                z(dmil, ()), on_range=red.reduce_range if red else None)
         ctx.saved = None
-        return (None, None, None) + (None,) * len(_INPUT_NAMES)
+        return (None, None, None, None) + (None,) * len(_INPUT_NAMES)
 
 
 _INPUT_NAMES = ("vis_fea", "vis_mask", "q_ipt", "q_mask", "q_graph", "macro_ipt", "macro_mask",
@@ -276,11 +276,13 @@ class AttModel(nn.Module):
         if not self.only_obj:
             raise NotImplementedError("MIL-NCE relation branch (only_obj=False) is the next scope "
                                       "row (SURVEY.md 8f); use only_obj=True")
+        drop = None
         if self.training and self.dropout_rate > 0:
-            raise NotImplementedError(
-                "dropout_rate > 0 in training mode is not implemented; the reference itself "
-                "cannot backpropagate it on torch>=2 (ReLU -> Dropout(inplace) in the heads, "
-                "AttModel_x3.py:482-500)")
+            # one 63-bit step seed per forward from torch's CPU generator (torch.manual_seed
+            # makes it reproducible); the backward regenerates the same masks from it
+            seed = int(torch.randint(0, 2 ** 63 - 1, (1,), dtype=torch.int64).item())
+            drop = (seed, float(self.dropout_rate))
+        object.__setattr__(self, "_last_dropout", drop)
         dev = self._arena.flat.device
         if dev.type != "cuda":
             raise RuntimeError("savqa AttModel runs on a HIP device: call model.cuda() first")
@@ -298,7 +300,7 @@ class AttModel(nn.Module):
                    i32(macro_mask), i32(macro_graph), i64(macro_obj_loc), i64(micro_positive_obj),
                    i64(micro_negative_obj), i32(micro_obj_mask))
         anchor = self._arena_anchor()
-        lc, lv, ls, mil = _AttModelFn.apply(self, bool(decMask), anchor, *tensors)
+        lc, lv, ls, mil = _AttModelFn.apply(self, bool(decMask), drop, anchor, *tensors)
         return lc, lv, ls, mil, 0
 
     def _arena_anchor(self):

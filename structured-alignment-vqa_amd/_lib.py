@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libsavqa.so")
 
 c_i64 = C.c_int64
 c_i32 = C.c_int32
+c_u64 = C.c_uint64
 c_f = C.c_float
 c_p = C.c_void_p
 
@@ -54,8 +55,12 @@ _SIGS = {
                         c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64,
                         c_p, c_i64],
     "savqa_graph_build": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p],
-    "savqa_dec_init": [c_p, c_p, c_i64, c_f, c_p, c_i64, c_i64, c_p],
-    "savqa_dec_init_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p],
+    "savqa_dec_init": [c_p, c_p, c_i64, c_f, c_p, c_i64, c_i64, c_u64, c_i32, c_f, c_p],
+    "savqa_dec_init_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_f, c_u64, c_i32, c_f, c_p, c_p],
+    "savqa_dropout": [c_p, c_p, c_i64, c_u64, c_i32, c_f, c_p],
+    "savqa_posadd_dropout": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_u64, c_i32, c_i32, c_f, c_p],
+    "savqa_posadd_dropout_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_u64, c_i32, c_i32, c_f, c_p,
+                                 c_p],
     "savqa_period_sum_acc": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p],
     "savqa_copy_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64],
     "savqa_mil_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_p],

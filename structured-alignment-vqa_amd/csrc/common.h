@@ -52,6 +52,42 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   return base + (bid >> 3);
 }
 
+// Dropout keep bits (nn.Dropout sites of the path, AttModel_x3.py:71-72, 102, 147, 227, 274,
+// 482-500). torch's Philox stream cannot be reproduced bit-for-bit, so the library defines
+// its own counter-based stream: element idx of dropout site `site` under step seed `seed`
+// is the SplitMix64 output for counter (seed + site*K1 + (idx+1)*K2). Stateless, so the
+// backward regenerates the forward's masks instead of storing them. Restated in
+// oracle/savqa_oracle.py:dropout_keep for the parity tests.
+__device__ __forceinline__ uint32_t drop_bits(uint64_t seed, uint32_t site, uint64_t idx) {
+  uint64_t z = seed + (uint64_t)site * 0xD1B54A32D192ED03ull + (idx + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+
+// keep iff bits >= thr, thr = floor(p * 2^32); kept values are scaled by 1/(1-p).
+struct DropParam {
+  uint64_t seed;
+  uint32_t thr;
+  float scale;
+  int drop_all;
+};
+
+inline DropParam make_drop(uint64_t seed, float p) {
+  DropParam d;
+  d.seed = seed;
+  d.drop_all = p >= 1.f;
+  const double t = (double)p * 4294967296.0;
+  d.thr = p <= 0.f ? 0u : (t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t);
+  d.scale = d.drop_all ? 0.f : 1.f / (1.f - p);
+  return d;
+}
+
+__device__ __forceinline__ float drop_mul(const DropParam& d, uint32_t site, uint64_t idx) {
+  return (!d.drop_all && drop_bits(d.seed, site, idx) >= d.thr) ? d.scale : 0.f;
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace savqa

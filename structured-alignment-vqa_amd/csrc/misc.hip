@@ -43,22 +43,25 @@ __global__ __launch_bounds__(256) void graph_build_kernel(
 // ------------------------------------------------------------------ decoder input
 __global__ void dec_init_kernel(const float* __restrict__ emb, int64_t idx, float scale,
                                 const float* __restrict__ pos, int64_t B, int64_t d,
-                                float* __restrict__ out) {
+                                DropParam dp, int32_t site, float* __restrict__ out) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= B * d) return;
   const int64_t c = t % d;
-  out[t] = emb[idx * d + c] * scale + pos[c];
+  float v = emb[idx * d + c] * scale + pos[c];
+  if (site >= 0) v *= drop_mul(dp, site, t);  // dec_dropout (AttModel_x3.py:147, :274)
+  out[t] = v;
 }
 
-// d emb[idx] += scale * sum_b g[b], d pos[0] += sum_b g[b]
+// d emb[idx] += scale * sum_b D'(g[b]), d pos[0] += sum_b D'(g[b])
 __global__ void dec_init_bwd_kernel(const float* __restrict__ g, int64_t B, int64_t d,
-                                    int64_t idx, float scale, float* __restrict__ demb,
-                                    float* __restrict__ dpos) {
+                                    int64_t idx, float scale, DropParam dp, int32_t site,
+                                    float* __restrict__ demb, float* __restrict__ dpos) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= d) return;
   float s = 0.f, ss = 0.f;
   for (int64_t b = 0; b < B; ++b) {
-    const float v = g[b * d + c];
+    float v = g[b * d + c];
+    if (site >= 0) v *= drop_mul(dp, site, b * d + c);
     s += v * scale;
     ss += v;
   }
@@ -481,19 +484,23 @@ extern "C" int savqa_graph_build(void* stream, const int32_t* node_mask, const i
 }
 
 extern "C" int savqa_dec_init(void* stream, const float* emb, int64_t idx, float scale,
-                              const float* pos, int64_t B, int64_t d, float* out) {
+                              const float* pos, int64_t B, int64_t d, uint64_t seed, int32_t site,
+                              float p, float* out) {
   const int64_t n = B * d;
   if (n <= 0) return 0;
+  if (p < 0.f || p > 1.f) return fail(SAVQA_EINVAL, "savqa_dec_init: p outside [0,1]");
   hipLaunchKernelGGL(dec_init_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), emb,
-                     idx, scale, pos, B, d, out);
+                     idx, scale, pos, B, d, make_drop(seed, p), p > 0.f ? site : -1, out);
   return check_launch("savqa_dec_init");
 }
 
 extern "C" int savqa_dec_init_bwd(void* stream, const float* g, int64_t B, int64_t d, int64_t idx,
-                                  float scale, float* demb, float* dpos) {
+                                  float scale, uint64_t seed, int32_t site, float p, float* demb,
+                                  float* dpos) {
   if (B <= 0 || d <= 0) return 0;
+  if (p < 0.f || p > 1.f) return fail(SAVQA_EINVAL, "savqa_dec_init_bwd: p outside [0,1]");
   hipLaunchKernelGGL(dec_init_bwd_kernel, dim3((d + 255) / 256), dim3(256), 0, as_stream(stream), g,
-                     B, d, idx, scale, demb, dpos);
+                     B, d, idx, scale, make_drop(seed, p), p > 0.f ? site : -1, demb, dpos);
   return check_launch("savqa_dec_init_bwd");
 }
 

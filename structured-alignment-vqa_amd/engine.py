@@ -122,6 +122,14 @@ class StackSaved:
     kv: torch.Tensor = None
     dec: List[dict] = field(default_factory=list)
     out: torch.Tensor = None
+    drop: Optional[tuple] = None
+    sites: tuple = (-1, 4, 5)
+
+
+# dropout sites (site ids of the library's counter-hash masks, include/savqa.h)
+VIS_SITES = (1, 2, 3)   # (position-table dropout :71-72, enc_dropout :102, dec_dropout :147)
+SYB_SITES = (-1, 4, 5)  # (none -- plain position table :178, enc_dropout :227, dec_dropout :274)
+HEAD_SITES = {"cls": 6, "cls_vis": 7, "cls_syb": 8}  # Dropout(inplace) in the heads :482-500
 
 
 def _ln_stats(rows, dev):
@@ -130,21 +138,26 @@ def _ln_stats(rows, dev):
 
 def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
                   q_ipt: torch.Tensor, node_mask, q_mask, q_graph, node_graph, decMask: bool,
-                  H: int, d: int) -> StackSaved:
+                  H: int, d: int, drop=None, sites=SYB_SITES) -> StackSaved:
     """AttModel_vis_grid.forward (:91-156) / AttModel_syb.forward (:214-282).
 
     `cat` is the [B*T, 2048] input buffer whose node rows [0, Nn) of every sample
-    are already filled by the caller; the question rows are produced here."""
+    are already filled by the caller; the question rows are produced here.
+    drop = (seed, p) applies the stack's nn.Dropout sites (training, p > 0)."""
     dev = cat.device
     T = Nn + Lq
     M = B * T
-    s = StackSaved(B=B, Nn=Nn, Lq=Lq, T=T, cat=cat)
+    s = StackSaved(B=B, Nn=Nn, Lq=Lq, T=T, cat=cat, drop=drop, sites=sites)
     s.q_flat = q_ipt.reshape(-1)
     # question tokens: relu(syb_emb[q] W^T + b) straight into rows [Nn, T) of cat
     ops.linear(W.E, W.Wq, W.bq, cat, relu=True, rows=B * Lq, a_rows=s.q_flat, c_group=Lq,
                c_stride=T, c_offset=Nn, ldo=cat.shape[1])
     s.x0 = _empty(M, d, dev=dev)
-    ops.linear(cat, W.Win, W.bin, s.x0, rowvec=W.pos, rowvec_period=T)
+    if drop is None:
+        ops.linear(cat, W.Win, W.bin, s.x0, rowvec=W.pos, rowvec_period=T)
+    else:
+        ops.linear(cat, W.Win, W.bin, s.x0)
+        ops.posadd_dropout(s.x0, W.pos, B, T, d, drop, sites[0], sites[1], s.x0)
     flag = _empty(M, dev=dev)
     ops.rowflag(s.x0, M, d, d, flag)
     s.gdiag, s.graph = _empty(B, T, T, dev=dev), _empty(B, T, T, dev=dev)
@@ -179,7 +192,7 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
     s.kv = _empty(M, 2 * nb * d, dev=dev)
     ops.linear(x, W.Wkv, W.bkv, s.kv, relu=True)
     dec = _empty(B, d, dev=dev)
-    ops.dec_init(W.dec_emb, 2, math.sqrt(d), W.dec_pos, B, d, dec)
+    ops.dec_init(W.dec_emb, 2, math.sqrt(d), W.dec_pos, B, d, dec, drop=drop, site=sites[2])
     fdec = _empty(B, dev=dev)
     ops.rowflag(dec, B, d, d, fdec)
     for i, L in enumerate(W.dec):
@@ -257,7 +270,8 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         dprev = _empty(B, d, dev=dev)
         ops.linear_dx(dvp, L["Wv"], dprev, rows=B, resid=dzs)
         ddec = dprev
-    ops.dec_init_bwd(ddec, B, d, 2, math.sqrt(d), G.dec_emb, G.dec_pos)
+    ops.dec_init_bwd(ddec, B, d, 2, math.sqrt(d), G.dec_emb, G.dec_pos, drop=s.drop,
+                     site=s.sites[2])
     # all decoder K/V projections at once
     ops.linear_dw(dkv, s.x6, G.Wkv, G.bkv, rows=M)
     dx = _empty(M, d, dev=dev)
@@ -286,7 +300,10 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         ops.linear_dx(dqkv, L["Wqkv"], dxn, rows=M, resid=dz1)
         dx = dxn
     # input projection, position table, question-token MLP and embedding table
-    ops.period_sum_acc(dx, B, T, d, d, G.pos)
+    if s.drop is None:
+        ops.period_sum_acc(dx, B, T, d, d, G.pos)
+    else:  # dx <- enc_dropout'(dx); dpos += sum_b pos_dropout'(dx)
+        ops.posadd_dropout_bwd(dx, B, T, d, s.drop, s.sites[0], s.sites[1], dx, G.pos)
     ops.linear_dw(dx, s.cat, G.Win, G.bin, rows=M)
     qrows = _rows_index(B, T, Nn, Lq, dev)
     dq = _empty(B * Lq, W.Win.shape[1], dev=dev)
@@ -375,19 +392,22 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
 
 
 # ----------------------------------------------------------------------------- heads
-def heads_forward(Wh: HeadWeights, f_vis, f_syb, d: int):
-    """AttModel.forward heads, AttModel_x3.py:531-541 (mcb=False)."""
+def heads_forward(Wh: HeadWeights, f_vis, f_syb, d: int, drop=None):
+    """AttModel.forward heads, AttModel_x3.py:531-541 (mcb=False): Linear -> ReLU ->
+    Dropout(inplace) -> Linear."""
     dev = f_vis.device
     B = f_vis.shape[0]
     fcat = _empty(B, 2 * d, dev=dev)
     ops.copy_rows(f_syb, B, d, d, fcat, 2 * d)
     ops.copy_rows(f_vis, B, d, d, fcat[:, d:], 2 * d)
-    saved = {"fcat": fcat, "f_vis": f_vis, "f_syb": f_syb}
+    saved = {"fcat": fcat, "f_vis": f_vis, "f_syb": f_syb, "drop": drop}
     outs = []
     for name, x in (("cls", fcat), ("cls_vis", f_vis), ("cls_syb", f_syb)):
         W0, b0, W3, b3 = Wh.h[name]
         h = _empty(B, W0.shape[0], dev=dev)
         ops.linear(x, W0, b0, h, relu=True)
+        if drop is not None:
+            ops.dropout(h, h.numel(), drop, HEAD_SITES[name], h)
         lo = _empty(B, W3.shape[0], dev=dev)
         ops.linear(h, W3, b3, lo)
         saved[name] = h
@@ -406,7 +426,9 @@ def heads_backward(Wh: HeadWeights, Gh: HeadWeights, saved, dlc, dlv, dls, d: in
         h = saved[name]
         ops.linear_dw(dlo, h, gW3, gb3, rows=B)
         dh = _empty(B, W0.shape[0], dev=dev)
-        ops.linear_dx(dlo, W3, dh, rows=B, mask=h, ldmask=W0.shape[0])
+        ops.linear_dx(dlo, W3, dh, rows=B, mask=h, ldmask=W0.shape[0])  # h > 0: relu & kept
+        if saved["drop"] is not None:
+            ops.dropout(dh, dh.numel(), saved["drop"], HEAD_SITES[name], dh)
         ops.linear_dw(dh, x, gW0, gb0, rows=B)
         dx[name] = dh
     dfcat = _empty(B, 2 * d, dev=dev)
@@ -455,10 +477,11 @@ class ModelEngine:
             self._side = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
         return self._side
 
-    def forward(self, inp: Dict[str, torch.Tensor], decMask: bool):
+    def forward(self, inp: Dict[str, torch.Tensor], decMask: bool, drop=None):
         """The two stacks are independent until the heads (AttModel_x3.py:525-541), so the
         visual stack and the MIL-NCE + semantic stack run on two HIP streams: one stack's
-        latency-bound decoder phase and GEMM tails overlap the other's big GEMMs."""
+        latency-bound decoder phase and GEMM tails overlap the other's big GEMMs.
+        drop = (seed, p): training-mode dropout (None in eval or at p = 0)."""
         d, H = self.d, self.H
         vis = inp["vis_fea"]
         dev = vis.device
@@ -477,17 +500,19 @@ class ModelEngine:
                              inp["micro_positive_obj"], inp["micro_negative_obj"],
                              inp["micro_obj_mask"], cat_syb, Ts, mil_val)
             ss = stack_forward(self.syb, cat_syb, B, Ns, Lq, inp["q_ipt"], inp["macro_mask"],
-                               inp["q_mask"], inp["q_graph"], inp["macro_graph"], decMask, H, d)
+                               inp["q_mask"], inp["q_graph"], inp["macro_graph"], decMask, H, d,
+                               drop, SYB_SITES)
         with torch.cuda.stream(s_vis):
             cat_vis = _empty(B * Tv, Dv, dev=dev)
             ops.copy_rows(vis.reshape(B * Nv, Dv), B * Nv, Dv, Dv, cat_vis, Dv, Nv, Tv, 0)
             sv = stack_forward(self.vis, cat_vis, B, Nv, Lq, inp["q_ipt"], inp["vis_mask"],
-                               inp["q_mask"], inp["q_graph"], None, decMask, H, d)
+                               inp["q_mask"], inp["q_graph"], None, decMask, H, d, drop,
+                               VIS_SITES)
         main.wait_stream(s_vis)
         main.wait_stream(s_syb)
         for t in (sv.out, ss.out, mil_val):
             t.record_stream(main)
-        (lc, lv, ls), hs = heads_forward(self.head, sv.out, ss.out, d)
+        (lc, lv, ls), hs = heads_forward(self.head, sv.out, ss.out, d, drop)
         return (lc, lv, ls, mil_val), (ms, sv, ss, hs)
 
     def region_bounds(self):

@@ -183,12 +183,35 @@ def graph_build(node_mask, q_mask, q_graph, node_graph, B, Nn, Lq, dec_on, gdiag
          B, Nn, Lq, int(bool(dec_on)), _p(gdiag), _p(graph), _p(dec_mask))
 
 
-def dec_init(emb, idx, scale, pos, B, d, out):
-    call("savqa_dec_init", _stream(), _p(emb), int(idx), float(scale), _p(pos), B, d, _p(out))
+def dec_init(emb, idx, scale, pos, B, d, out, drop=None, site=-1):
+    seed, p = drop if drop is not None else (0, 0.0)
+    call("savqa_dec_init", _stream(), _p(emb), int(idx), float(scale), _p(pos), B, d, int(seed),
+         int(site), float(p), _p(out))
 
 
-def dec_init_bwd(g, B, d, idx, scale, demb, dpos):
-    call("savqa_dec_init_bwd", _stream(), _p(g), B, d, int(idx), float(scale), _p(demb), _p(dpos))
+def dec_init_bwd(g, B, d, idx, scale, demb, dpos, drop=None, site=-1):
+    seed, p = drop if drop is not None else (0, 0.0)
+    call("savqa_dec_init_bwd", _stream(), _p(g), B, d, int(idx), float(scale), int(seed),
+         int(site), float(p), _p(demb), _p(dpos))
+
+
+# ------------------------------------------------------------------------------ dropout
+def dropout(inp, n, drop, site, out):
+    """out = nn.Dropout(p)(inp) with the library's counter-hash masks; drop = (seed, p)."""
+    seed, p = drop
+    call("savqa_dropout", _stream(), _p(inp), int(n), int(seed), int(site), float(p), _p(out))
+
+
+def posadd_dropout(z, pos, B, T, d, drop, site_pos, site_x, out):
+    seed, p = drop
+    call("savqa_posadd_dropout", _stream(), _p(z), _p(pos), B, T, d, int(seed), int(site_pos),
+         int(site_x), float(p), _p(out))
+
+
+def posadd_dropout_bwd(g, B, T, d, drop, site_pos, site_x, dz, dpos):
+    seed, p = drop
+    call("savqa_posadd_dropout_bwd", _stream(), _p(g), B, T, d, int(seed), int(site_pos),
+         int(site_x), float(p), _p(dz), _p(dpos))
 
 
 def period_sum_acc(X, B, T, Cc, ldx, out):
