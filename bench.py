@@ -125,10 +125,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SAVQA_DIST_BACKEND", "nccl") != "nccl":  # rehearsal: ranks share GPUs
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL ("nccl" on ROCm) over xGMI; SAVQA_DIST_BACKEND=gloo only to rehearse the
+        # N>1 code path with several ranks on one GPU (RCCL refuses duplicate devices)
+        backend = os.environ.get("SAVQA_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     import savqa_amd  # noqa: F401
     from savqa_amd import ops
@@ -160,9 +165,7 @@ def main():
         loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil, with_milnce=True)
         opt.zero_grad()
         loss.backward()
-        if reducer:
-            opt.grad_scale = reducer.finish()
-        opt.step()
+        opt.step(reducer=reducer)
         return loss
 
     for _ in range(args.warmup):

@@ -25,36 +25,76 @@ import torch.distributed as dist
 
 
 class GradReducer:
+    """Bucketed, streamed all-reduce of the live gradient range of a ParamArena.
+
+    reduce_range(lo, hi) declares arena gradient elements [lo, hi) final on the CURRENT
+    stream. Contiguous declarations from one stream are coalesced, and every full bucket
+    (bucket_mb) is all-reduced asynchronously at once; flush=True (end of a backward
+    phase) also sends the remainder. drain() returns the (work, lo, hi) list so the
+    optimizer can update each bucket as soon as ITS all-reduce lands (Adam of the early
+    buckets overlaps the all-reduce of the last ones)."""
+
     def __init__(self, arena, bucket_mb: float = 64.0, group=None):
         self.arena = arena
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.bucket = max(1, int(bucket_mb * (1 << 20) // 4))
         self.works: List = []
+        self.pending = {}
 
     def begin(self):
         self.works = []
+        self.pending = {}
 
-    def reduce_range(self, start: int, end: int):
-        """Gradient elements [start, end) of the arena are final on the CURRENT stream:
-        all-reduce them in buckets; RCCL's stream waits for exactly that work."""
+    @staticmethod
+    def _stream_key():
+        return torch.cuda.current_stream().cuda_stream if torch.cuda.is_available() else 0
+
+    def _issue(self, lo: int, hi: int):
+        g = self.arena.grad
+        w = dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self.works.append((w, lo, hi))
+
+    def reduce_range(self, start: int, end: int, flush: bool = False):
         if self.world <= 1:
             return
-        g = self.arena.grad
-        end = min(int(end), g.numel())
-        lo = int(start)
-        while lo < end:
-            hi = min(lo + self.bucket, end)
-            self.works.append(dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
-                                              async_op=True))
+        end = min(int(end), self.arena.grad.numel())
+        start = int(start)
+        key = self._stream_key()
+        lo, hi = self.pending.get(key, (start, start))
+        if hi != start:          # not contiguous with this stream's pending range
+            if hi > lo:
+                self._issue(lo, hi)
+            lo = start
+        hi = max(end, start)
+        while hi - lo >= self.bucket:
+            self._issue(lo, lo + self.bucket)
+            lo += self.bucket
+        if flush and hi > lo:
+            self._issue(lo, hi)
             lo = hi
+        self.pending[key] = (lo, hi)
+
+    def _flush_all(self):
+        # called on the stream that joined every producer stream (engine.backward ends
+        # with main.wait_stream(...)), so the remainders are final there as well
+        for lo, hi in self.pending.values():
+            if hi > lo:
+                self._issue(lo, hi)
+        self.pending = {}
+
+    def drain(self):
+        """Issue what is pending; return ([(work, lo, hi)...] in issue order, 1/world)."""
+        if self.world <= 1:
+            return [], 1.0
+        self._flush_all()
+        works, self.works = self.works, []
+        return works, 1.0 / self.world
 
     def finish(self):
         """Make the current stream wait for every bucket; returns the 1/world factor the
         optimizer folds into its update (DDP averages)."""
-        if self.world <= 1:
-            return 1.0
-        for w in self.works:
+        works, scale = self.drain()
+        for w, _, _ in works:
             w.wait()
-        self.works = []
-        return 1.0 / self.world
+        return scale

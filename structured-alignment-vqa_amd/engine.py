@@ -229,11 +229,14 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
 
 
 def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.Tensor, H: int,
-                   d: int, want_node_grad: bool) -> Optional[torch.Tensor]:
+                   d: int, want_node_grad: bool, mark=None) -> Optional[torch.Tensor]:
     """Backward of stack_forward; accumulates parameter grads into G (arena views).
 
     Returns d(pre-activation of the node rows of cat) [B*Nn, 2048] when want_node_grad
-    (the syb stack feeds it to the MIL-NCE backward), else None."""
+    (the syb stack feeds it to the MIL-NCE backward), else None.
+    mark(name) declares every arena gradient before parameter `name` final (the arena is
+    in backward-completion order), so the all-reduce streams out layer by layer."""
+    mark = mark or (lambda name: None)
     dev = dout.device
     B, T, Nn, Lq = s.B, s.T, s.Nn, s.Lq
     M = B * T
@@ -270,6 +273,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         dprev = _empty(B, d, dev=dev)
         ops.linear_dx(dvp, L["Wv"], dprev, rows=B, resid=dzs)
         ddec = dprev
+        mark(f"dec_feed_forward_{i - 1}.normalization.gamma" if i > 0 else "dec_emb.lookup_table")
     ops.dec_init_bwd(ddec, B, d, 2, math.sqrt(d), G.dec_emb, G.dec_pos, drop=s.drop,
                      site=s.sites[2])
     # all decoder K/V projections at once
@@ -277,6 +281,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
     dx = _empty(M, d, dev=dev)
     ops.linear_dx(dkv, W.Wkv, dx, rows=M)
     del dkv
+    mark(f"enc_feed_forward_{len(W.enc) - 1}.normalization.gamma")
     for i in reversed(range(len(W.enc))):
         L, Lg, e = W.enc[i], G.enc[i], s.enc[i]
         Gm = s.gdiag if i < 2 else s.graph
@@ -299,6 +304,8 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         dxn = _empty(M, d, dev=dev)
         ops.linear_dx(dqkv, L["Wqkv"], dxn, rows=M, resid=dz1)
         dx = dxn
+        if i > 0:
+            mark(f"enc_feed_forward_{i - 1}.normalization.gamma")
     # input projection, position table, question-token MLP and embedding table
     if s.drop is None:
         ops.period_sum_acc(dx, B, T, d, d, G.pos)
@@ -525,7 +532,8 @@ class ModelEngine:
     def backward(self, saved, dlc, dlv, dls, dmil, on_range=None):
         """Whole-model backward (heads on the caller's stream, then the two stacks on their
         own streams). on_range(start, end) is called, on the stream that produced them,
-        as soon as arena gradient elements [start, end) are final (all-reduce streaming)."""
+        as soon as arena gradient elements [start, end) are final (all-reduce streaming);
+        a third argument True marks the end of a backward phase (flush the bucket)."""
         self.grads()
         ms, sv, ss, hs = saved
         d, H = self.d, self.H
@@ -534,7 +542,22 @@ class ModelEngine:
         main = torch.cuda.current_stream(dev)
         df_vis, df_syb = heads_backward(self.head, self.ghead, hs, dlc, dlv, dls, d)
         if on_range:
-            on_range(0, b_heads)
+            on_range(0, b_heads, True)
+        offs = self.arena.offsets
+
+        class Marker:
+            """Declares consecutive arena ranges [lo, end) final, per backward phase."""
+
+            def __init__(self, pre, lo):
+                self.pre, self.lo = pre, lo
+
+            def __call__(self, name):
+                self.upto(offs[f"{self.pre}.{name}"][0])
+
+            def upto(self, end, flush=False):
+                if on_range and (end > self.lo or flush):
+                    on_range(self.lo, max(end, self.lo), flush)
+                self.lo = max(self.lo, end)
         s_vis, s_syb = self._streams(dev)
         s_vis.wait_stream(main)
         s_syb.wait_stream(main)
@@ -542,13 +565,15 @@ class ModelEngine:
         df_syb.record_stream(s_syb)
         dmil.record_stream(s_syb)
         with torch.cuda.stream(s_vis):
-            stack_backward(self.vis, self.gvis, sv, df_vis, H, d, want_node_grad=False)
-            if on_range:
-                on_range(b_heads, b_vis)
+            mk = Marker("att_vis_grid", b_heads)
+            stack_backward(self.vis, self.gvis, sv, df_vis, H, d, want_node_grad=False, mark=mk)
+            mk.upto(b_vis, flush=True)
         with torch.cuda.stream(s_syb):
-            dnode = stack_backward(self.syb, self.gsyb, ss, df_syb, H, d, want_node_grad=True)
+            mk = Marker("att_syb", b_vis)
+            dnode = stack_backward(self.syb, self.gsyb, ss, df_syb, H, d, want_node_grad=True,
+                                   mark=mk)
+            mk.upto(b_syb, flush=True)
             mil_backward(self.mil, self.gmil, ms, dnode, dmil)
-            if on_range:
-                on_range(b_vis, self.arena.n_live)
+            mk.upto(self.arena.n_live, flush=True)
         main.wait_stream(s_vis)
         main.wait_stream(s_syb)

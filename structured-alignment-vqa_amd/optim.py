@@ -26,7 +26,9 @@ class Adam(torch.optim.Optimizer):
         self.grad_scale = 1.0
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, reducer=None):
+        """reducer (ddp.GradReducer): update bucket by bucket as each all-reduce lands,
+        with the reducer's 1/world factor; otherwise one launch over the live range."""
         loss = closure() if closure is not None else None
         a = self.arena
         g = a.grad
@@ -39,8 +41,25 @@ class Adam(torch.optim.Optimizer):
         grp = self.param_groups[0]
         b1, b2 = grp["betas"]
         t = self.step_count
-        ops.adam(a.flat[:a.n_live], g, self.m, self.v, a.n_live, grp["lr"], b1, b2, grp["eps"],
-                 1 - b1 ** t, 1 - b2 ** t, self.grad_scale)
+        bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+        ranges = [(None, 0, a.n_live)]
+        scale = self.grad_scale
+        if reducer is not None and reducer.world > 1:
+            works, scale = reducer.drain()
+            covered = sorted((lo, hi) for _, lo, hi in works)
+            pos = 0
+            for lo, hi in covered:
+                pos = hi if lo == pos else -1
+            if pos == a.n_live:
+                ranges = works
+            else:  # declarations did not tile the live range: wait for all, one launch
+                for w, _, _ in works:
+                    w.wait()
+        for w, lo, hi in ranges:
+            if w is not None:
+                w.wait()   # this stream waits for this bucket's all-reduce only
+            ops.adam(a.flat[lo:hi], g[lo:hi], self.m[lo:hi], self.v[lo:hi], hi - lo, grp["lr"], b1,
+                     b2, grp["eps"], bc1, bc2, scale)
         return loss
 
     def zero_grad(self, set_to_none: bool = False):

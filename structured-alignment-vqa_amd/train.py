@@ -121,9 +121,7 @@ def main(gpu_rank, args):
             loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil,
                                     with_milnce=args.with_MILNCE_loss)
             loss.backward()
-            if reducer:
-                opt.grad_scale = reducer.finish()
-            opt.step()
+            opt.step(reducer=reducer)
             if (i + 1) % args.log_steps == 0 or i + 1 == args.steps_per_epoch:
                 loss_meter.update(float(loss), batch["answer"].shape[0])
                 mil_meter.update(-float(mil), batch["answer"].shape[0])

@@ -27,14 +27,22 @@ def _worker(rank, world, port, q):
     n = 10007
     g = torch.arange(n, dtype=torch.float32) * (rank + 1)
     arena = types.SimpleNamespace(grad=g.clone())
-    red = GradReducer(arena, bucket_mb=0.01)  # ~2.6k floats per bucket -> several buckets
+    red = GradReducer(arena, bucket_mb=0.01)  # 2621 floats per bucket
     red.begin()
-    red.reduce_range(0, 3000)        # "heads" range
-    red.reduce_range(3000, 7000)     # "visual stack"
-    red.reduce_range(7000, n)        # "semantic stack + MIL"
-    scale = red.finish()
+    red.reduce_range(0, 3000, True)     # "heads" phase (flushed)
+    # "visual stack", declared layer by layer: coalesced into full buckets
+    for lo in range(3000, 7000, 500):
+        red.reduce_range(lo, lo + 500)
+    red.reduce_range(7000, 7000, True)  # empty declaration that only flushes
+    red.reduce_range(7000, 9000)        # "semantic stack": remainder left pending ...
+    red.reduce_range(9000, n)           # ... and extended
+    works, scale = red.drain()          # drain flushes what is pending
+    spans = [(lo, hi) for _, lo, hi in works]
+    for w, _, _ in works:
+        w.wait()
     expect = torch.arange(n, dtype=torch.float32) * sum(r + 1 for r in range(world))
-    q.put((rank, float((arena.grad - expect).abs().max()), scale, len(red.works)))
+    # finish() on an empty reducer is a no-op returning the 1/world factor
+    q.put((rank, float((arena.grad - expect).abs().max()), scale, spans, red.finish()))
     dist.destroy_process_group()
 
 
@@ -49,10 +57,17 @@ def test_grad_reducer_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, err, scale, nworks in res:
+    for rank, err, scale, spans, scale2 in res:
         assert err == 0.0
-        assert scale == 0.5
-        assert nworks == 0
+        assert scale == 0.5 and scale2 == 0.5
+        # buckets tile [0, n) exactly, none larger than the bucket size
+        assert spans[0] == (0, 2621) and spans[1] == (2621, 3000)
+        pos = 0
+        for lo, hi in sorted(spans):
+            assert lo == pos and 0 < hi - lo <= 2621
+            pos = hi
+        assert pos == 10007
+        assert spans[2] == (3000, 5621)   # full bucket issued during the layer loop
 
 
 def test_adam_grad_scale_matches_mean_of_grads():
