@@ -128,6 +128,25 @@ int savqa_gattn_bwd(void* stream, const float* q, int64_t ldq, const float* k, i
                     const float* dout, int64_t lddo, float* dq, int64_t lddq, float* dk_, int64_t lddk,
                     float* dv, int64_t lddv);
 
+/* Key-tiled variant of the same operator for long sequences (any Tq, Tk; used for
+ * Tk > 128: cfg 4's 449-token stacks, super-node relation graphs up to T = 1600).
+ * Keys stream through LDS in tiles of 64 with per-row online statistics; nothing of
+ * size Tq x Tk is materialised. stats: caller-owned [B*H*Tq][4] fp32 (m, Z, W, delta),
+ * written by the forward (m, Z, W) and the backward (delta = sum_j n_ij dN_ij); keep it
+ * from the forward to the backward. att (return_att) is not available on this path. */
+int savqa_gattn_fwd_flash(void* stream, const float* q, int64_t ldq, const float* k, int64_t ldk,
+                          const float* v, int64_t ldv, const float* G, const float* kflag,
+                          const float* qflag, int64_t B, int64_t Tq, int64_t Tk, int64_t H,
+                          int64_t dk, float* o, int64_t ldo, float* stats);
+
+/* Backward of savqa_gattn_fwd_flash: dQ (workgroup per query tile; its first sweep also
+ * writes delta), then dK/dV (workgroup per key tile), ReLU-masked like savqa_gattn_bwd. */
+int savqa_gattn_bwd_flash(void* stream, const float* q, int64_t ldq, const float* k, int64_t ldk,
+                          const float* v, int64_t ldv, const float* G, const float* kflag,
+                          const float* qflag, int64_t B, int64_t Tq, int64_t Tk, int64_t H,
+                          int64_t dk, const float* dout, int64_t lddo, float* stats, float* dq, int64_t lddq, float* dk_, int64_t lddk,
+                          float* dv, int64_t lddv);
+
 /* ------------------------------------------------------------------------
  * Graph construction, AttModel_x3.py:103-122 (vis, node_graph == NULL) and
  * :229-247 (syb): graph_diag, graph (== graph_cross, aliased in the reference),

@@ -54,6 +54,11 @@ _SIGS = {
     "savqa_gattn_bwd": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
                         c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64,
                         c_p, c_i64],
+    "savqa_gattn_fwd_flash": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
+                              c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p],
+    "savqa_gattn_bwd_flash": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
+                              c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p,
+                              c_p, c_i64, c_p, c_i64, c_p, c_i64],
     "savqa_graph_build": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p],
     "savqa_dec_init": [c_p, c_p, c_i64, c_f, c_p, c_i64, c_i64, c_u64, c_i32, c_f, c_p],
     "savqa_dec_init_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_f, c_u64, c_i32, c_f, c_p, c_p],

@@ -1,0 +1,79 @@
+// Shared pieces of the graph-attention kernels (attn.hip: T <= 128 full-row kernels,
+// attn_flash.hip: key-tiled kernels for long sequences). gfx950 only.
+#pragma once
+#include "common.h"
+
+namespace savqa {
+
+constexpr int ATT_DK = 64;
+constexpr int ATT_KLD = 68;  // padded K/V row (floats), 16-B aligned
+constexpr int ATT_RB = 4;    // query rows per wave per pass
+constexpr float ATT_MASKED = -4294967296.0f;  // fp32(-2**32 + 1)
+
+struct AttnArgs {
+  const float* q; int64_t ldq;
+  const float* k; int64_t ldk;
+  const float* v; int64_t ldv;
+  const float* G;
+  const float* kflag;
+  const float* qflag;
+  int B, Tq, Tk, H;
+  float* o; int64_t ldo;
+  float* att;
+  // backward
+  const float* dout; int64_t lddo;
+  float* dq; int64_t lddq;
+  float* dk; int64_t lddk;
+  float* dv; int64_t lddv;
+};
+
+using f4v = float __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v mfma16(float a, float b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// sum / max over the 16 lanes of a DPP row. Butterfly partners (quad_perm [1,0,3,2],
+// [2,3,0,1], row_half_mirror, row_mirror) pair every lane with a lane holding the same
+// operand set, so all 16 lanes end with bitwise-identical totals (a row_ror ladder
+// leaves quads with different association orders: T=1 softmax would then give a != 1
+// in some lanes and break the reference's exact-zero Q/K gradients).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  return v;
+}
+
+__device__ __forceinline__ f4v ld4(const float* p) { return *reinterpret_cast<const f4v*>(p); }
+
+// Same with Y staged in LDS ([TK][ATT_KLD], rows >= Tk zero): b128 reads, lanes 0-15 of a
+// read phase hit 16 disjoint bank quads (row stride 68 floats).
+template <int NJT>
+__device__ __forceinline__ void strip_dots_lds(const f4v (&x)[4], const float* Ys, int col, int g,
+                                               f4v (&acc)[NJT]) {
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt) {
+    const float* yr = Ys + (jt * 16 + col) * ATT_KLD + 4 * g;
+    f4v s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f4v yv = ld4(yr + 16 * c);
+      s = mfma16(x[c].x, yv.x, s);
+      s = mfma16(x[c].y, yv.y, s);
+      s = mfma16(x[c].z, yv.z, s);
+      s = mfma16(x[c].w, yv.w, s);
+    }
+    acc[jt] = s;
+  }
+}
+
+}  // namespace savqa

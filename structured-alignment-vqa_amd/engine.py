@@ -171,8 +171,14 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
         qkv = _empty(M, 3 * d, dev=dev)
         ops.linear(x, L["Wqkv"], L["bqkv"], qkv, relu=True)
         o = _empty(M, d, dev=dev)
-        ops.gattn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag, flag, B, T, T,
-                      H, o, d)
+        if ops.use_flash(T, T):  # key-tiled path: keeps the per-row statistics
+            ast = _empty(B * H * T * 4, dev=dev)
+            ops.gattn_fwd_flash(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag, flag,
+                                B, T, T, H, o, d, ast)
+            e.update(ast=ast)
+        else:
+            ops.gattn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag, flag, B,
+                          T, T, H, o, d)
         z1, y1 = _empty(M, d, dev=dev), _empty(M, d, dev=dev)
         st1 = _ln_stats(M, dev)
         ops.ln_fwd(o, L["g1"], L["b1"], y1, *st1, r=x, z_out=z1)
@@ -207,8 +213,14 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
         ops.linear(d1, L["Wqc"], L["bqc"], qc, relu=True)
         oc = _empty(B, d, dev=dev)
         kvi = s.kv[:, 2 * i * d:]
-        ops.gattn_fwd(qc, d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6, f1, B, 1, T, H,
-                      oc, d)
+        if ops.use_flash(1, T):
+            ast = _empty(B * H * 4, dev=dev)
+            ops.gattn_fwd_flash(qc, d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6, f1, B,
+                                1, T, H, oc, d, ast)
+            e.update(ast=ast)
+        else:
+            ops.gattn_fwd(qc, d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6, f1, B, 1,
+                          T, H, oc, d)
         zc, d2 = _empty(B, d, dev=dev), _empty(B, d, dev=dev)
         stc = _ln_stats(B, dev)
         ops.ln_fwd(oc, L["gc"], L["bc"], d2, *stc, r=d1, z_out=zc)
@@ -259,8 +271,14 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         ops.ln_bwd(dd2, e["zc"], *e["stc"], L["gc"], dzc, Lg["gc"], Lg["bc"])
         dqc = _empty(B, d, dev=dev)
         kvi, dkvi = s.kv[:, 2 * i * d:], dkv[:, 2 * i * d:]
-        ops.gattn_bwd(e["qc"], d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6, e["f1"], B,
-                      1, T, H, dzc, d, dqc, d, dkvi, 2 * nb * d, dkvi[:, d:], 2 * nb * d)
+        if "ast" in e:
+            ops.gattn_bwd_flash(e["qc"], d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6,
+                                e["f1"], B, 1, T, H, dzc, d, e["ast"], dqc, d, dkvi,
+                                2 * nb * d, dkvi[:, d:], 2 * nb * d)
+        else:
+            ops.gattn_bwd(e["qc"], d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6,
+                          e["f1"], B, 1, T, H, dzc, d, dqc, d, dkvi, 2 * nb * d, dkvi[:, d:],
+                          2 * nb * d)
         ops.linear_dw(dqc, e["d1"], Lg["Wqc"], Lg["bqc"], rows=B)
         dd1 = _empty(B, d, dev=dev)
         ops.linear_dx(dqc, L["Wqc"], dd1, rows=B, resid=dzc)
@@ -298,8 +316,14 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         ops.ln_bwd(dy1, e["z1"], *e["st1"], L["g1"], dz1, Lg["g1"], Lg["b1"])
         dqkv = _empty(M, 3 * d, dev=dev)
         qkv = e["qkv"]
-        ops.gattn_bwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, Gm, e["flag"], e["flag"],
-                      B, T, T, H, dz1, d, dqkv, 3 * d, dqkv[:, d:], 3 * d, dqkv[:, 2 * d:], 3 * d)
+        if "ast" in e:
+            ops.gattn_bwd_flash(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, Gm, e["flag"],
+                                e["flag"], B, T, T, H, dz1, d, e["ast"], dqkv, 3 * d,
+                                dqkv[:, d:], 3 * d, dqkv[:, 2 * d:], 3 * d)
+        else:
+            ops.gattn_bwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, Gm, e["flag"],
+                          e["flag"], B, T, T, H, dz1, d, dqkv, 3 * d, dqkv[:, d:], 3 * d,
+                          dqkv[:, 2 * d:], 3 * d)
         ops.linear_dw(dqkv, e["x"], Lg["Wqkv"], Lg["bqkv"], rows=M)
         dxn = _empty(M, d, dev=dev)
         ops.linear_dx(dqkv, L["Wqkv"], dxn, rows=M, resid=dz1)

@@ -136,12 +136,21 @@ class _MHAFn(torch.autograd.Function):
         G = graph.to(torch.float32).contiguous()
         o = _empty(B * Tq, d, dev=dev)
         att = _empty(H * B, Tq, Tk, dev=dev) if want_att else None
-        ops.gattn_fwd(Q, d, K, d, V, d, G, kf, qf, B, Tq, Tk, H, o, d, att)
+        flash = ops.use_flash(Tq, Tk)
+        if flash:
+            if want_att:
+                raise NotImplementedError("return_att=True needs T <= 128 (full-row kernels)")
+            ast = _empty(B * H * Tq * 4, dev=dev)
+            ops.gattn_fwd_flash(Q, d, K, d, V, d, G, kf, qf, B, Tq, Tk, H, o, d, ast)
+        else:
+            ast = o.new_empty(0)
+            ops.gattn_fwd(Q, d, K, d, V, d, G, kf, qf, B, Tq, Tk, H, o, d, att)
         z, y = _empty(B * Tq, d, dev=dev), _empty(B * Tq, d, dev=dev)
         st = tuple(_empty(B * Tq, dev=dev) for _ in range(3))
         ln = mod.normalization
         ops.ln_fwd(o, ln.gamma, ln.beta, y, *st, r=q2, z_out=z, eps=ln.epsilon)
-        ctx.save_for_backward(q2, k2, v2, Q, K, V, kf, qf, G, z, *st)
+        ctx.save_for_backward(q2, k2, v2, Q, K, V, kf, qf, G, z, *st, ast)
+        ctx.flash = flash
         ctx.mod, ctx.shape = mod, (B, Tq, Tk)
         ctx.same_kv = keys is values
         ctx.same_qk = queries is keys
@@ -153,7 +162,7 @@ class _MHAFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy, *rest):
-        q2, k2, v2, Q, K, V, kf, qf, G, z, m, r, s = ctx.saved_tensors
+        q2, k2, v2, Q, K, V, kf, qf, G, z, m, r, s, ast = ctx.saved_tensors
         mod = ctx.mod
         d, H = mod.num_units, mod.num_heads
         B, Tq, Tk = ctx.shape
@@ -162,7 +171,11 @@ class _MHAFn(torch.autograd.Function):
         dz = _empty(B * Tq, d, dev=dev)
         ops.ln_bwd(gy.contiguous(), z, m, r, s, ln.gamma, dz, _acc(ln.gamma), _acc(ln.beta))
         dQ, dK, dV = _empty(B * Tq, d, dev=dev), _empty(B * Tk, d, dev=dev), _empty(B * Tk, d, dev=dev)
-        ops.gattn_bwd(Q, d, K, d, V, d, G, kf, qf, B, Tq, Tk, H, dz, d, dQ, d, dK, d, dV, d)
+        if ctx.flash:
+            ops.gattn_bwd_flash(Q, d, K, d, V, d, G, kf, qf, B, Tq, Tk, H, dz, d, ast, dQ, d,
+                                dK, d, dV, d)
+        else:
+            ops.gattn_bwd(Q, d, K, d, V, d, G, kf, qf, B, Tq, Tk, H, dz, d, dQ, d, dK, d, dV, d)
         dq = _empty(B * Tq, d, dev=dev)
         dk = _empty(B * Tk, d, dev=dev)
         dv = _empty(B * Tk, d, dev=dev)

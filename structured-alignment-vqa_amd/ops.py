@@ -177,6 +177,29 @@ def gattn_bwd(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout, lddo,
          _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo, _p(dq), lddq, _p(dk_), lddk, _p(dv), lddv)
 
 
+def gattn_fwd_flash(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, o, ldo, stats, dk=64):
+    call("savqa_gattn_fwd_flash", _stream(), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G), _p(kflag),
+         _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(stats))
+
+
+def gattn_bwd_flash(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout, lddo,
+                    stats, dq, lddq, dk_, lddk, dv, lddv, dk=64):
+    call("savqa_gattn_bwd_flash", _stream(), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G), _p(kflag),
+         _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo, _p(stats), _p(dq), lddq, _p(dk_), lddk,
+         _p(dv), lddv)
+
+
+FULL_ROW_MAX_T = 128  # attn.hip's full-row kernels; longer sequences use the key-tiled path
+
+
+def use_flash(Tq: int, Tk: int) -> bool:
+    """Key-tiled attention beyond the full-row kernels' limit (SAVQA_ATTN_FLASH=1 forces it)."""
+    import os
+    if os.environ.get("SAVQA_ATTN_FLASH", "0") == "1":
+        return True
+    return Tk > FULL_ROW_MAX_T or Tq > FULL_ROW_MAX_T
+
+
 # ------------------------------------------------------------------------------ misc
 def graph_build(node_mask, q_mask, q_graph, node_graph, B, Nn, Lq, dec_on, gdiag, graph, dec_mask):
     call("savqa_graph_build", _stream(), _p(node_mask), _p(q_mask), _p(q_graph), _p(node_graph),
