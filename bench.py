@@ -27,6 +27,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "QA-samples/sec training (model_v=3, 36 regions × 2048-d) at 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -92,6 +93,22 @@ def cpu_baseline(seconds=15.0, B=4, rate=0.5):
                       f"B={B}, dropout {rate}, {n} steps in {dt:.1f}s, torch CPU {threads} threads"}
 
 
+WORKLOADS = {
+    "cfg2": dict(d=512, H=8, Nv=36, Ns=59, batch=256,
+                 desc="cfg2: model_v=3 train step (fwd+loss+bwd+Adam), fp32, 36 regions x 2048-d, "
+                      "14 q-tokens, 59 nodes, d=512 h=8 L=6, MIL-NCE only_obj topN=5 H=1024, "
+                      "914 classes, decMask"),
+    "cfg3": dict(d=512, H=8, Nv=36, Ns=59, batch=512, prec="bf16",
+                 desc="cfg3: model_v=3 train step, bf16 GEMM products (fp32 accumulation, fp32 "
+                      "master weights / LN / softmax / loss / Adam), 36 regions x 2048-d, "
+                      "14 q-tokens, 59 nodes, d=512 h=8 L=6, MIL-NCE only_obj topN=5 H=1024, "
+                      "914 classes, decMask"),
+    "cfg4": dict(d=1024, H=16, Nv=100, Ns=435, batch=32,
+                 desc="cfg4: model_v=3 train step, fp32, 100 regions x 2048-d, 14 q-tokens, "
+                      "435-node scene graph (T_vis=114, T_syb=449), d=1024 h=16 (h=12 does not "
+                      "divide d=1024) L=6, MIL-NCE only_obj topN=5 H=1024, 914 classes, decMask"),
+}
+
 ROOFLINE_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                              "r01_bench_roofline.json")
 
@@ -112,7 +129,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="samples per GPU (cfg 2: 256)")
+    ap.add_argument("--batch", type=int, default=None, help="samples per GPU (cfg2: 256)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2",
+                    help="cfg2 = BASELINE config 2 (fp32, 256/GPU: the metric's workload); cfg3 = "
+                         "config 3 (bf16 GEMM products, 512/GPU); cfg4 = the 100-region / 435-node "
+                         "scene-graph stress shape (d=1024, 16 heads, T_syb=449)")
     ap.add_argument("--dropout", type=float, default=0.5,
                     help="dropout_rate (reference training default 0.5, main:466)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -144,9 +165,11 @@ def main():
     from savqa_amd.optim import Adam
     from savqa_amd.utils import init_params_
 
-    B = args.batch
-    model = AttModel(None, 512, 1024, 914, 40, 450, 49, 6, 8, args.dropout, 0.1, 311, True,
-                     device=dev, init=False)
+    W = WORKLOADS[args.workload]
+    B = args.batch or W["batch"]
+    d, H, Nv, Ns = W["d"], W["H"], W["Nv"], W["Ns"]
+    model = AttModel(None, d, 1024, 914, 40, 450, 49, 6, H, args.dropout, 0.1, 311, True,
+                     device=dev, init=False, gemm_precision=W.get("prec", "fp32"))
     init_params_(model, seed=0)  # identical on every rank (same seed), like a broadcast
     model.train()
     if args.serial:
@@ -155,7 +178,7 @@ def main():
     reducer = GradReducer(model._arena) if world > 1 else None
     if reducer:
         model.attach_reducer(reducer)
-    batch = synthetic_batch(B, seed=1234 + rank, device=dev)
+    batch = synthetic_batch(B, Nv=Nv, Ns=Ns, seed=1234 + rank, device=dev)
     margs = model_args(batch)
 
     def step():
@@ -190,7 +213,8 @@ def main():
 
     value = world * B * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
-    fl = train_flops_per_sample()
+    fl = train_flops_per_sample(Tv=Nv + 14, Ts=Ns + 14, Nv=Nv, Ns=Ns, d=d)
+    peak = BF16_MFMA_PEAK_TFLOPS if W.get("prec") == "bf16" else FP32_MFMA_PEAK_TFLOPS
 
     roof = None
     if not args.no_roofline:
@@ -210,29 +234,27 @@ def main():
         allms = sum(v[2] for v in agg.values())
         roof = {"bound": "mfma", "kernel": var, "launches_per_step": n // 2,
                 "avg_launch_us": round(ms / n * 1e3, 2), "flops_per_launch": flops / n,
-                "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4),
                 "traffic": committed_traffic(var),
                 "all_gemm_tflops": round(allfl / (allms * 1e-3) / 1e12, 2),
                 "gemm_ms_per_step": round(allms / 2, 2)}
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.workload == "cfg2":
             cpu = cpu_baseline(args.cpu_seconds, rate=args.dropout)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "QA-samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16 (GEMM products; fp32 accumulate)" if W.get("prec") == "bf16" else "fp32",
             "data": "synthetic (collate_fn tensor contract; random-init weights)",
-            "config": {"workload": "cfg2: model_v=3 train step (fwd+loss+bwd+Adam), fp32, "
-                                   "36 regions x 2048-d, 14 q-tokens, 59 nodes, d=512 h=8 L=6, "
-                                   "MIL-NCE only_obj topN=5 H=1024, 914 classes, decMask, "
-                                   f"dropout {args.dropout}",
+            "config": {"workload": W["desc"] + f", dropout {args.dropout}",
                        "per_gpu_batch": B, "global_batch": world * B,
                        "parallelism": f"dp{world}"},
             "model_tflops": round(value * fl / 1e12, 2),
-            "model_mfma_frac": round(value * fl / 1e12 / (FP32_MFMA_PEAK_TFLOPS * world), 4),
+            "model_mfma_frac": round(value * fl / 1e12 / (peak * world), 4),
             "loss": round(final_loss, 4),
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -218,7 +218,7 @@ class AttModel(nn.Module):
 
     def __init__(self, glove, hidden_size, hidden_size_mil, num_classes, maxlen_q, maxlen, maxlen_v,
                  num_blocks, num_heads, dropout_rate, dropout_rate_mcb, num_relations, only_obj,
-                 device=None, init=True):
+                 device=None, init=True, gemm_precision="fp32"):
         super().__init__()
         self.only_obj = only_obj
         self.num_classes = num_classes
@@ -250,8 +250,11 @@ class AttModel(nn.Module):
         self.label_smoothing = label_smoothing()
         # flatten every parameter into the arena (state_dict keys unchanged)
         object.__setattr__(self, "_arena", ParamArena(self, num_blocks, device=device))
+        # gemm_precision: "fp32" (default, exact fp32 products), "bf16" (BASELINE cfg 3:
+        # bf16 MFMA products, fp32 accumulation / master weights / everything else) or
+        # "bf16x3" (three bf16 MFMAs per product, ~2^-16 relative)
         object.__setattr__(self, "_engine", ModelEngine(self._arena, num_blocks, hidden_size,
-                                                        num_heads))
+                                                        num_heads, gemm_precision))
 
     def attach_reducer(self, reducer):
         """Stream the data-parallel gradient all-reduce out of the backward (ddp.GradReducer)."""

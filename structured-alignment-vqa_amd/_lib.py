@@ -22,7 +22,7 @@ c_p = C.c_void_p
 class GemmDesc(C.Structure):
     _fields_ = [
         ("M", c_i64), ("N", c_i64), ("K", c_i64),
-        ("A", c_p), ("lda", c_i64), ("a_trans", c_i32), ("_pad0", c_i32),
+        ("A", c_p), ("lda", c_i64), ("a_trans", c_i32), ("prec", c_i32),
         ("a_rows", c_p),
         ("B", c_p), ("ldb", c_i64), ("b_trans", c_i32), ("_pad1", c_i32),
         ("b_rows", c_p),

@@ -22,7 +22,7 @@
 // included); edge tiles, k tails and k-row gathers take a clamped, branch-free guarded
 // loader. One register-staged prefetch, LDS write after the compute (T14), one barrier
 // per k-tile, XCD-aware block order (T1).
-#include "common.h"
+#include "gemm_common.h"
 
 #include <algorithm>
 #include <map>
@@ -36,12 +36,6 @@
 #endif
 
 namespace savqa {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f4 __attribute__((ext_vector_type(4)));  // native vector (HIP float4 copies
-                                                          // lower to memcpy and block SROA)
-
-constexpr int GEMM_NT = 256;
 
 // MFMA shape of the 128x128 path (fp32 in, fp32 accumulate; same 64 FLOP/clk/SIMD):
 //   Mi32: v_mfma_f32_32x32x2_f32, 32-row fragments, 16 accumulator VGPRs per fragment;
@@ -188,52 +182,6 @@ struct GemmCfg {
   static constexpr int FM = WM / MI::FR, FN = WN / MI::FR;
 };
 
-// Epilogue of one output element (include/savqa.h formula), split per row / element.
-struct EpiRow {
-  float* crow;
-  float rs;
-  int64_t mr, pr;
-};
-
-__device__ __forceinline__ EpiRow epi_row(const savqa_gemm_desc& d, int64_t m, bool ident) {
-  EpiRow e;
-  int64_t cr;
-  if (ident) {
-    cr = m;
-  } else if (d.c_rows) {
-    cr = d.c_rows[m];
-  } else {
-    const uint32_t mu = (uint32_t)m, cg = (uint32_t)d.c_group;
-    cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
-  }
-  e.crow = d.C + cr * d.ldc;
-  e.rs = d.rowscale ? d.rowscale[m] : 1.f;
-  e.mr = d.mask_arows ? d.a_rows[m] : m;
-  e.pr = d.rowvec ? (int64_t)((uint32_t)m % (uint32_t)d.rowvec_period) : 0;
-  return e;
-}
-
-__device__ __forceinline__ void epi_store(const savqa_gemm_desc& d, const EpiRow& e, int64_t m,
-                                          int64_t n, float acc, bool first_split, bool atomic) {
-  float v = acc * d.alpha;
-  if (first_split) {
-    if (d.bias) v += d.bias[n];
-    if (d.rowvec) v += d.rowvec[e.pr * d.ldrv + n];
-  }
-  if (d.relu) v = fmaxf(v, 0.f);
-  v *= e.rs;
-  if (d.mask && !(d.mask[e.mr * d.ldmask + n] > 0.f)) v = 0.f;
-  if (first_split && d.resid) v += d.resid[m * d.ldr + n];
-  float* cp = e.crow + n;
-  if (atomic) {
-    atomicAdd(cp, v);
-  } else if (d.beta != 0.f) {
-    *cp = v + d.beta * *cp;
-  } else {
-    *cp = v;
-  }
-}
-
 template <int BM, int BN, int BK, bool AT, bool BT>
 __device__ __forceinline__ void gemm_compute_tile(
     const float* __restrict__ As, const float* __restrict__ Bs, int wm, int wn, int lane,
@@ -329,14 +277,6 @@ __device__ __forceinline__ void gemm_mainloop(
   }
 #undef SAVQA_GEMM_LOAD
 }
-
-// Block -> (tile, k range). Blocks [0, full) own whole tiles (or split-K slices along
-// blockIdx.y); blocks [full, gridDim.x) are the "tail": tiles [tail_t0, T) each cut into
-// tail_f k-slices so the last partial wave of tiles spreads over every CU.
-struct GemmGrid {
-  int tiles_n, full, tail_t0, tail_f;
-  int64_t kchunk, tail_kchunk;
-};
 
 template <int BM, int BN, int BK, bool AT, bool BT>
 __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_waves_per_eu(SAVQA_GEMM_OCC, SAVQA_GEMM_OCC))) void gemm_f32_kernel(savqa_gemm_desc d, GemmGrid gg,
@@ -835,7 +775,9 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.rowvec && d.rowvec_period <= 0) return fail(SAVQA_EINVAL, "savqa_gemm: rowvec_period");
   if (d.split_k < 0 && !d.atomic) return fail(SAVQA_EINVAL, "savqa_gemm: auto split-K needs atomic=1");
   if (d.colsum_a && !d.a_trans) return fail(SAVQA_EINVAL, "savqa_gemm: colsum_a needs a_trans=1");
-  constexpr int BK = SAVQA_GEMM_BK;
+  if (d.prec != 0 && d.prec != 1 && d.prec != 3)
+    return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32), 1 (bf16) or 3 (3xbf16)");
+  const int BK = d.prec ? 32 : SAVQA_GEMM_BK;  // gemm_bf16_kernel k-tile: 32
   const int slots = slots_per_launch();
   const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
   int split = d.split_k > 1 ? d.split_k : 1;
@@ -854,7 +796,7 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
     return 0;
   }
   p.sk = false;
-  if (sk_enabled()) {
+  if (sk_enabled() && d.prec == 0) {
     p.tile = 128;
     p.split = 1;
     p.nsplit = 1;
@@ -987,6 +929,8 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
     else if (!d.a_trans) hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, false, false>), g, b, 0, s, d, sk, avec, bvec);
     else if (!d.b_trans) hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, true, false>), g, b, 0, s, d, sk, avec, bvec);
     else hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, true, true>), g, b, 0, s, d, sk, avec, bvec);
+  } else if (p.tile == 128 && d.prec != 0) {
+    savqa_launch_gemm_bf16(d, p.gg, p.grid_x, p.nsplit, s, avec, bvec);
   } else if (p.tile == 128) {
     dispatch_layout<128, 128, SAVQA_GEMM_BK>(d, p, s, avec, bvec);
   } else {

@@ -475,8 +475,9 @@ def heads_backward(Wh: HeadWeights, Gh: HeadWeights, saved, dlc, dlv, dls, d: in
 class ModelEngine:
     """Binds arena views once; runs the whole-model forward / backward."""
 
-    def __init__(self, arena, num_blocks: int, hidden: int, heads: int):
+    def __init__(self, arena, num_blocks: int, hidden: int, heads: int, gemm_precision="fp32"):
         self.arena = arena
+        self.gemm_precision = gemm_precision  # products of the 128x128 GEMMs (ops.PREC)
         self.nb, self.d, self.H = num_blocks, hidden, heads
         self.rebind()
 
@@ -509,6 +510,10 @@ class ModelEngine:
         return self._side
 
     def forward(self, inp: Dict[str, torch.Tensor], decMask: bool, drop=None):
+        with ops.gemm_precision(self.gemm_precision):
+            return self._forward(inp, decMask, drop)
+
+    def _forward(self, inp: Dict[str, torch.Tensor], decMask: bool, drop=None):
         """The two stacks are independent until the heads (AttModel_x3.py:525-541), so the
         visual stack and the MIL-NCE + semantic stack run on two HIP streams: one stack's
         latency-bound decoder phase and GEMM tails overlap the other's big GEMMs.
@@ -554,6 +559,10 @@ class ModelEngine:
                 a.offsets["MIL_NCE.ipt_mlp.0.weight"][0])
 
     def backward(self, saved, dlc, dlv, dls, dmil, on_range=None):
+        with ops.gemm_precision(self.gemm_precision):
+            return self._backward(saved, dlc, dlv, dls, dmil, on_range)
+
+    def _backward(self, saved, dlc, dlv, dls, dmil, on_range=None):
         """Whole-model backward (heads on the caller's stream, then the two stacks on their
         own streams). on_range(start, end) is called, on the stream that produced them,
         as soon as arena gradient elements [start, end) are final (all-reduce streaming);

@@ -50,6 +50,8 @@ class GemmProbe:
         lay = f"{str(bool(d.a_trans)).lower()},{str(bool(d.b_trans)).lower()}"
         if plan[0] == 32:
             return f"gemm_skinny_kernel<{lay}>"
+        if d.prec:
+            return f"gemm_bf16_kernel<{lay},{d.prec}>"
         return f"gemm_f32_kernel<{plan[0]},{plan[0]},{lay}>"
 
     def summary(self):
@@ -66,6 +68,31 @@ class GemmProbe:
 
 _probe = None
 
+# Product precision of the 128x128-tile GEMMs (savqa_gemm_desc.prec): 0 = fp32 MFMA (exact
+# fp32, the default), 1 = bf16 MFMA with fp32 accumulation (BASELINE cfg 3), 3 = 3xbf16
+# split products. Set per model (AttModel(..., gemm_precision=...)) via gemm_precision().
+PREC = {"fp32": 0, "bf16": 1, "bf16x3": 3}
+_prec = 0
+
+
+class gemm_precision:
+    """Context manager: GEMMs launched inside use the given product precision."""
+
+    def __init__(self, name: str):
+        if name not in PREC:
+            raise ValueError(f"gemm precision must be one of {sorted(PREC)}")
+        self.p = PREC[name]
+
+    def __enter__(self):
+        global _prec
+        self.old, _prec = _prec, self.p
+        return self
+
+    def __exit__(self, *exc):
+        global _prec
+        _prec = self.old
+        return False
+
 
 def set_gemm_probe(probe):
     global _probe
@@ -76,9 +103,10 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
          ldc: int, a_trans=False, b_trans=False, a_rows=None, b_rows=None, c_rows=None,
          c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None, ldrv=0, rowvec_period=0,
          resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False, rowscale=None, relu=False,
-         alpha=1.0, beta=0.0, atomic=False, split_k=1, colsum_a=None):
-    """Generic fp32 MFMA GEMM with fused epilogue (see savqa_gemm in include/savqa.h)."""
+         alpha=1.0, beta=0.0, atomic=False, split_k=1, colsum_a=None, prec=None):
+    """Generic MFMA GEMM with fused epilogue (see savqa_gemm in include/savqa.h)."""
     d = GemmDesc()
+    d.prec = _prec if prec is None else int(prec)
     d.M, d.N, d.K = int(M), int(N), int(K)
     d.A, d.lda, d.a_trans = _p(A), int(lda), int(bool(a_trans))
     d.a_rows = _p(a_rows)

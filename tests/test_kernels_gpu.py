@@ -377,3 +377,40 @@ def test_gemm_stream_k_path():
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("prec,tol", [(1, 2e-2), (3, 1e-4)])
+@pytest.mark.parametrize("lay", ["NT", "NN", "TN"])
+@pytest.mark.parametrize("M,N,K", [(2048, 2048, 512), (4100, 1280, 520), (2100, 1536, 96)])
+def test_gemm_bf16_paths(prec, tol, lay, M, N, K):
+    """bf16 (prec 1, BASELINE cfg 3) and 3xbf16 (prec 3) MFMA GEMMs against fp64, with the
+    same epilogues as the fp32 path (bias+ReLU forward, residual dX, split-K dW with the
+    bias-gradient column sums), including edge tiles and k tails."""
+    O = ops()
+    if lay == "NT":
+        X, W, b = g(M, K, seed=70), g(N, K, seed=71), g(N, seed=72)
+        res = g(M, N, seed=73)
+        out = torch.empty(M, N, device=dev)
+        O.gemm(X, W, out, M, N, K, lda=K, ldb=K, ldc=N, b_trans=True, bias=b, relu=True,
+               resid=res, ldr=N, prec=prec)
+        ref = torch.relu(X.double() @ W.double().t() + b.double()) + res.double()
+        scale = (X.double().abs() @ W.double().abs().t()).max()
+    elif lay == "NN":
+        A, W = g(M, K, seed=74), g(K, N, seed=75)
+        out = torch.empty(M, N, device=dev)
+        O.gemm(A, W, out, M, N, K, lda=K, ldb=N, ldc=N, prec=prec)
+        ref = A.double() @ W.double()
+        scale = (A.double().abs() @ W.double().abs()).max()
+    else:
+        A, X = g(K, M, seed=76), g(K, N, seed=77)
+        out = torch.zeros(M, N, device=dev)
+        cs = torch.zeros(M, device=dev)
+        O.gemm(A, X, out, M, N, K, lda=M, ldb=N, ldc=N, a_trans=True, atomic=True, split_k=-1,
+               colsum_a=cs, prec=prec)
+        ref = A.double().t() @ X.double()
+        scale = (A.double().abs().t() @ X.double().abs()).max()
+        assert rel(cs, A.double().sum(0)) < 1e-5  # column sums stay fp32
+    err = float((out.double() - ref).abs().max() / scale)
+    assert err < tol, err
+    if prec == 3:  # 3xbf16 is not plain bf16: at least 100x closer to fp64
+        assert err < 1e-4

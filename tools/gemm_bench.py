@@ -26,6 +26,7 @@ def timeit(fn, iters=10):
 
 
 def main():
+    prec = ops.PREC[os.environ.get("SAVQA_BENCH_PREC", "fp32")]
     M = 18688
     cases = [("fwd qkv", "NT", M, 1536, 512), ("fwd ffn1", "NT", M, 2048, 512),
              ("fwd ffn2", "NT", M, 512, 2048), ("fwd kv_all", "NT", M, 6144, 512),
@@ -44,22 +45,32 @@ def main():
             A = torch.randn(m, k, device=dev)
             W = torch.randn(n, k, device=dev)
             C = torch.empty(m, n, device=dev)
-            f = lambda: ops.gemm(A, W, C, m, n, k, lda=k, ldb=k, ldc=n, b_trans=True)
+            f = lambda: ops.gemm(A, W, C, m, n, k, lda=k, ldb=k, ldc=n, b_trans=True, prec=prec)
             g = lambda: torch.mm(A, W.t(), out=C)
         elif lay == "NN":
             A = torch.randn(m, k, device=dev)
             W = torch.randn(k, n, device=dev)
             C = torch.empty(m, n, device=dev)
-            f = lambda: ops.gemm(A, W, C, m, n, k, lda=k, ldb=n, ldc=n)
+            f = lambda: ops.gemm(A, W, C, m, n, k, lda=k, ldb=n, ldc=n, prec=prec)
             g = lambda: torch.mm(A, W, out=C)
         else:
             A = torch.randn(k, m, device=dev)
             X = torch.randn(k, n, device=dev)
             C = torch.zeros(m, n, device=dev)
             f = lambda: ops.gemm(A, X, C, m, n, k, lda=m, ldb=n, ldc=n, a_trans=True, atomic=True,
-                                 split_k=-1)
+                                 split_k=-1, prec=prec)
             g = lambda: torch.mm(A.t(), X, out=C)
         t1 = timeit(f)
+        if prec:  # yardstick: torch's bf16 GEMM on bf16 copies
+            A16 = A.bfloat16()
+            B16 = (W if lay != "TN" else X).bfloat16()
+            C16 = C.bfloat16()
+            if lay == "NT":
+                g = lambda: torch.mm(A16, B16.t(), out=C16)
+            elif lay == "NN":
+                g = lambda: torch.mm(A16, B16, out=C16)
+            else:
+                g = lambda: torch.mm(A16.t(), B16, out=C16)
         t2 = timeit(g)
         print(f"{name:10s} {lay} {m:6d}x{n:5d}x{k:6d}  savqa {t1*1e6:8.1f}us {fl/t1/1e12:6.1f} TF   "
               f"torch {t2*1e6:8.1f}us {fl/t2/1e12:6.1f} TF", flush=True)
