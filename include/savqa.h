@@ -101,7 +101,9 @@ int savqa_ln_fwd(void* stream, const float* x, const float* xscale, const float*
                  const float* gamma, const float* beta, float eps,
                  float* z_out, float* y, float* mean, float* rden, float* stdv, float* flag);
 
-/* Backward of the above: dz = dLN/dz (+ dz_add), dgamma += ..., dbeta += ... */
+/* Backward of the above: dz = dLN/dz (+ dz_add), dgamma += ..., dbeta += ...
+ * (column sums land in a library-owned 128 KB per-stream slot workspace first -- see
+ * ln.hip -- and a second tiny kernel on the same stream folds them into dgamma/dbeta) */
 int savqa_ln_bwd(void* stream, const float* dy, const float* z, const float* mean,
                  const float* rden, const float* stdv, const float* gamma,
                  int64_t rows, int64_t cols, const float* dz_add, float* dz,

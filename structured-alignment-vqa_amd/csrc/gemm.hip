@@ -278,6 +278,28 @@ __device__ __forceinline__ void gemm_mainloop(
 #undef SAVQA_GEMM_LOAD
 }
 
+// colsum_a fold (bias gradient of a dW GEMM): every thread's staged-A partials share one
+// column group q = tid % PER (GEMM_NT is a multiple of PER); rows of threads write plain
+// LDS rows and one thread per column sums them (LDS float atomics serialise: ~us per block)
+template <int PER, int ITERS, int BM>
+__device__ __forceinline__ void cs_fold(const f4 (&cs)[ITERS], float* smem, int64_t m0,
+                                        const savqa_gemm_desc& d) {
+  static_assert(GEMM_NT % PER == 0 && 4 * PER == BM, "colsum layout");
+  constexpr int ROWS = GEMM_NT / PER;
+  f4 t = cs[0];
+#pragma unroll
+  for (int it = 1; it < ITERS; ++it) t += cs[it];
+  __syncthreads();
+  *reinterpret_cast<f4*>(&smem[(threadIdx.x / PER) * BM + 4 * (threadIdx.x % PER)]) = t;
+  __syncthreads();
+  for (int i = threadIdx.x; i < BM; i += GEMM_NT) {
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) v += smem[r * BM + i];
+    if (m0 + i < d.M) atomicAdd(&d.colsum_a[m0 + i], v);
+  }
+}
+
 template <int BM, int BN, int BK, bool AT, bool BT>
 __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_waves_per_eu(SAVQA_GEMM_OCC, SAVQA_GEMM_OCC))) void gemm_f32_kernel(savqa_gemm_desc d, GemmGrid gg,
                                                              int avec, int bvec) {
@@ -340,18 +362,7 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
   }
   if constexpr (AT) {
     if (do_cs) {  // block-uniform; smem is free after the main loop's last barrier
-      constexpr int PER = G::OA::PER;
-      for (int i = threadIdx.x; i < BM; i += GEMM_NT) smem[i] = 0.f;
-      __syncthreads();
-#pragma unroll
-      for (int it = 0; it < G::OA::ITERS; ++it) {
-        const int q = (threadIdx.x + it * GEMM_NT) % PER;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) atomicAdd(&smem[4 * q + e], cs[it][e]);
-      }
-      __syncthreads();
-      for (int i = threadIdx.x; i < BM; i += GEMM_NT)
-        if (m0 + i < d.M) atomicAdd(&d.colsum_a[m0 + i], smem[i]);
+      cs_fold<G::OA::PER, G::OA::ITERS, BM>(cs, smem, m0, d);
     }
   }
 
@@ -461,18 +472,7 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
     }
     if constexpr (AT) {
       if (do_cs) {  // this segment's share of the bias gradient (atomics: segments add up)
-        constexpr int PER = G::OA::PER;
-        for (int i = tid; i < BM; i += GEMM_NT) smem[i] = 0.f;
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < G::OA::ITERS; ++q) {
-          const int qq = (tid + q * GEMM_NT) % PER;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) atomicAdd(&smem[4 * qq + e], cs[q][e]);
-        }
-        __syncthreads();
-        for (int i = tid; i < BM; i += GEMM_NT)
-          if (m0 + i < d.M) atomicAdd(&d.colsum_a[m0 + i], smem[i]);
+        cs_fold<G::OA::PER, G::OA::ITERS, BM>(cs, smem, m0, d);
         __syncthreads();
       }
     }

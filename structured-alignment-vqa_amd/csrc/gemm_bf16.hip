@@ -269,15 +269,17 @@ __global__ __launch_bounds__(GEMM_NT, 2) void gemm_bf16_kernel(savqa_gemm_desc d
   }
   if constexpr (AT) {
     if (do_cs) {  // block-uniform; smem is free after the main loop's last barrier
+      // thread rows tid/32 hold partials of columns 4*(tid%32)..+3: plain LDS rows, then
+      // one thread per column (no LDS float atomics)
       float* red = reinterpret_cast<float*>(smem);
-      for (int i = threadIdx.x; i < BF_BM; i += GEMM_NT) red[i] = 0.f;
+      *reinterpret_cast<f4*>(&red[(threadIdx.x / 32) * BF_BM + 4 * (threadIdx.x % 32)]) = cs;
       __syncthreads();
-      const int g = threadIdx.x % 32;
+      for (int i = threadIdx.x; i < BF_BM; i += GEMM_NT) {
+        float v = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(&red[4 * g + e], cs[e]);
-      __syncthreads();
-      for (int i = threadIdx.x; i < BF_BM; i += GEMM_NT)
-        if (m0 + i < d.M) atomicAdd(&d.colsum_a[m0 + i], red[i]);
+        for (int r = 0; r < GEMM_NT / 32; ++r) v += red[r * BF_BM + i];
+        if (m0 + i < d.M) atomicAdd(&d.colsum_a[m0 + i], v);
+      }
     }
   }
   // epilogue: the 32x32 accumulator layout of every v_mfma_f32_32x32x* form

@@ -8,6 +8,9 @@
 // query mask (modules.py:257, :289), so that mask never re-reads the activations.
 #include "common.h"
 
+#include <map>
+#include <mutex>
+
 namespace savqa {
 
 constexpr int LN_MAXV = 4;  // float4 per lane -> cols <= 1024
@@ -83,11 +86,84 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-// Backward. 1024-thread workgroups (16 waves), one per CU: each wave walks rows with a
-// grid stride, keeping its dgamma/dbeta partial sums in registers; the 16 waves fold
-// them with LDS float atomics and the workgroup adds once per column to global memory
-// (256 global atomics per column instead of one per 4-row workgroup).
-constexpr int LN_BWD_WAVES = 16;
+// Backward. 512-thread workgroups (8 waves), two per CU: each wave walks rows with a
+// grid stride, keeping its dgamma/dbeta partial sums in registers; the 8 waves fold
+// them through per-wave LDS rows and the workgroup adds once per column into one of
+// LN_SLOTS partial copies (a library workspace: 512 adders on ONE address serialise in L2
+// and cost ~35 us per launch; 32 per address run at the chip's atomic rate), which
+// ln_bwd_reduce_kernel then folds into dgamma/dbeta (and re-zeroes). NV (float4 per
+// lane = cols/256) is a template parameter, and the row loop is software-pipelined two
+// deep: the loads of row r+stride are in flight while row r is reduced and written
+// (one row's loads in flight per wave left every wave waiting on HBM latency).
+constexpr int LN_BWD_WAVES = 8;
+constexpr int LN_SLOTS = 16;
+
+template <int NV, bool ADD>
+struct LnBwdRow {
+  float4 d[NV], z[NV], a[ADD ? NV : 1];
+  float mean, rden, sd;
+};
+
+template <int NV, bool ADD>
+__device__ __forceinline__ void ln_bwd_fetch(LnBwdRow<NV, ADD>& b, int64_t row, int lane, int cols,
+                                             const float* __restrict__ dy,
+                                             const float* __restrict__ z,
+                                             const float* __restrict__ dz_add,
+                                             const float* __restrict__ mean_in,
+                                             const float* __restrict__ rden_in,
+                                             const float* __restrict__ std_in) {
+  const float4* dyr = reinterpret_cast<const float4*>(dy + row * cols);
+  const float4* zr = reinterpret_cast<const float4*>(z + row * cols);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    b.d[i] = dyr[lane + 64 * i];
+    b.z[i] = zr[lane + 64 * i];
+    if constexpr (ADD) b.a[i] = reinterpret_cast<const float4*>(dz_add + row * cols)[lane + 64 * i];
+  }
+  b.mean = mean_in[row];
+  b.rden = rden_in[row];
+  b.sd = std_in[row];
+}
+
+template <int NV, bool ADD>
+__device__ __forceinline__ void ln_bwd_row(const LnBwdRow<NV, ADD>& b, int64_t row, int lane, int cols,
+                                           float invN, const float4 (&g)[NV], float4 (&dg)[NV],
+                                           float4 (&db)[NV], const float* __restrict__ dz_add,
+                                           float* __restrict__ dz) {
+  float4 gg[NV], xc[NV];
+  float sg = 0.f, sgx = 0.f;
+  const float mean = b.mean, rden = b.rden;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float4 d4 = b.d[i], z4 = b.z[i];
+    xc[i] = make_float4(z4.x - mean, z4.y - mean, z4.z - mean, z4.w - mean);
+    gg[i] = make_float4(d4.x * g[i].x, d4.y * g[i].y, d4.z * g[i].z, d4.w * g[i].w);
+    sg += (gg[i].x + gg[i].y) + (gg[i].z + gg[i].w);
+    sgx += (gg[i].x * xc[i].x + gg[i].y * xc[i].y) + (gg[i].z * xc[i].z + gg[i].w * xc[i].w);
+    dg[i].x += d4.x * xc[i].x * rden; dg[i].y += d4.y * xc[i].y * rden;
+    dg[i].z += d4.z * xc[i].z * rden; dg[i].w += d4.w * xc[i].w * rden;
+    db[i].x += d4.x; db[i].y += d4.y; db[i].z += d4.z; db[i].w += d4.w;
+  }
+  sg = wave_sum(sg);
+  sgx = wave_sum(sgx);
+  const float mg = sg * invN;
+  // d std / dz_k = xc_k / ((N-1) std); guard std == 0 (constant row)
+  const float c = b.sd > 0.f ? sgx * rden * rden / ((float)(cols - 1) * b.sd) : 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float4 o;
+    o.x = (gg[i].x - mg) * rden - c * xc[i].x;
+    o.y = (gg[i].y - mg) * rden - c * xc[i].y;
+    o.z = (gg[i].z - mg) * rden - c * xc[i].z;
+    o.w = (gg[i].w - mg) * rden - c * xc[i].w;
+    if constexpr (ADD) {
+      o.x += b.a[i].x; o.y += b.a[i].y; o.z += b.a[i].z; o.w += b.a[i].w;
+    }
+    reinterpret_cast<float4*>(dz + row * cols)[lane + 64 * i] = o;
+  }
+}
+
+template <int NV, bool ADD>
 __global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(const float* __restrict__ dy,
                                                      const float* __restrict__ z,
                                                      const float* __restrict__ mean_in,
@@ -97,82 +173,88 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(const float* 
                                                      int64_t rows, int cols,
                                                      const float* __restrict__ dz_add,
                                                      float* __restrict__ dz,
-                                                     float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta) {
-  __shared__ float red[2][256 * LN_MAXV];
+                                                     float* __restrict__ ws) {
+  __shared__ float red[LN_BWD_WAVES][2][256 * NV];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  const int nv = cols >> 8;
-  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
-    red[0][c] = 0.f;
-    red[1][c] = 0.f;
-  }
-  float4 dg[LN_MAXV], db[LN_MAXV], g[LN_MAXV];
+  float4 dg[NV], db[NV], g[NV];
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < NV; ++i) {
     dg[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     db[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < nv) g[i] = reinterpret_cast<const float4*>(gamma)[lane + 64 * i];
+    g[i] = reinterpret_cast<const float4*>(gamma)[lane + 64 * i];
   }
   const float invN = 1.f / (float)cols;
-  for (int64_t row = (int64_t)blockIdx.x * LN_BWD_WAVES + w; row < rows;
-       row += (int64_t)gridDim.x * LN_BWD_WAVES) {
-    const float mean = mean_in[row], rden = rden_in[row], sd = std_in[row];
-    const float4* dyr = reinterpret_cast<const float4*>(dy + row * cols);
-    const float4* zr = reinterpret_cast<const float4*>(z + row * cols);
-    float4 gg[LN_MAXV], xc[LN_MAXV], ad[LN_MAXV];
-    float sg = 0.f, sgx = 0.f;
-#pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-      if (i < nv) {
-        const float4 d4 = dyr[lane + 64 * i];
-        const float4 z4 = zr[lane + 64 * i];
-        if (dz_add) ad[i] = reinterpret_cast<const float4*>(dz_add + row * cols)[lane + 64 * i];
-        xc[i] = make_float4(z4.x - mean, z4.y - mean, z4.z - mean, z4.w - mean);
-        gg[i] = make_float4(d4.x * g[i].x, d4.y * g[i].y, d4.z * g[i].z, d4.w * g[i].w);
-        sg += (gg[i].x + gg[i].y) + (gg[i].z + gg[i].w);
-        sgx += (gg[i].x * xc[i].x + gg[i].y * xc[i].y) + (gg[i].z * xc[i].z + gg[i].w * xc[i].w);
-        dg[i].x += d4.x * xc[i].x * rden; dg[i].y += d4.y * xc[i].y * rden;
-        dg[i].z += d4.z * xc[i].z * rden; dg[i].w += d4.w * xc[i].w * rden;
-        db[i].x += d4.x; db[i].y += d4.y; db[i].z += d4.z; db[i].w += d4.w;
-      }
-    }
-    sg = wave_sum(sg);
-    sgx = wave_sum(sgx);
-    const float mg = sg * invN;
-    // d std / dz_k = xc_k / ((N-1) std); guard std == 0 (constant row)
-    const float c = sd > 0.f ? sgx * rden * rden / ((float)(cols - 1) * sd) : 0.f;
-#pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-      if (i < nv) {
-        float4 o;
-        o.x = (gg[i].x - mg) * rden - c * xc[i].x;
-        o.y = (gg[i].y - mg) * rden - c * xc[i].y;
-        o.z = (gg[i].z - mg) * rden - c * xc[i].z;
-        o.w = (gg[i].w - mg) * rden - c * xc[i].w;
-        if (dz_add) {
-          o.x += ad[i].x; o.y += ad[i].y; o.z += ad[i].z; o.w += ad[i].w;
-        }
-        reinterpret_cast<float4*>(dz + row * cols)[lane + 64 * i] = o;
-      }
-    }
+  const int64_t stride = (int64_t)gridDim.x * LN_BWD_WAVES;
+  int64_t row = (int64_t)blockIdx.x * LN_BWD_WAVES + w;
+  LnBwdRow<NV, ADD> b0, b1;
+  if (row < rows) ln_bwd_fetch<NV, ADD>(b0, row, lane, cols, dy, z, dz_add, mean_in, rden_in, std_in);
+  while (row < rows) {
+    const int64_t r1 = row + stride;
+    if (r1 < rows) ln_bwd_fetch<NV, ADD>(b1, r1, lane, cols, dy, z, dz_add, mean_in, rden_in, std_in);
+    ln_bwd_row<NV, ADD>(b0, row, lane, cols, invN, g, dg, db, dz_add, dz);
+    if (r1 >= rows) break;
+    const int64_t r2 = r1 + stride;
+    if (r2 < rows) ln_bwd_fetch<NV, ADD>(b0, r2, lane, cols, dy, z, dz_add, mean_in, rden_in, std_in);
+    ln_bwd_row<NV, ADD>(b1, r1, lane, cols, invN, g, dg, db, dz_add, dz);
+    row = r2;
   }
-  __syncthreads();  // red[] zeroed
+  // fold the 8 waves' partials: plain per-wave LDS rows, then one thread per column
+  // (ds_add_f32 folding cost ~20 us per launch: LDS float atomics serialise)
+  __syncthreads();
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
-    if (i < nv) {
-      const int c0 = 4 * (lane + 64 * i);
-      atomicAdd(&red[0][c0 + 0], dg[i].x); atomicAdd(&red[0][c0 + 1], dg[i].y);
-      atomicAdd(&red[0][c0 + 2], dg[i].z); atomicAdd(&red[0][c0 + 3], dg[i].w);
-      atomicAdd(&red[1][c0 + 0], db[i].x); atomicAdd(&red[1][c0 + 1], db[i].y);
-      atomicAdd(&red[1][c0 + 2], db[i].z); atomicAdd(&red[1][c0 + 3], db[i].w);
-    }
+  for (int i = 0; i < NV; ++i) {
+    reinterpret_cast<float4*>(&red[w][0][0])[lane + 64 * i] = dg[i];
+    reinterpret_cast<float4*>(&red[w][1][0])[lane + 64 * i] = db[i];
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
-    atomicAdd(&dgamma[c], red[0][c]);
-    atomicAdd(&dbeta[c], red[1][c]);
+  float* slot = ws + (blockIdx.x % LN_SLOTS) * 2 * cols;
+  for (int c = threadIdx.x; c < 2 * cols; c += blockDim.x) {
+    const int a = c >= cols, cc = c - a * cols;
+    float t = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < LN_BWD_WAVES; ++ww) t += red[ww][a][cc];
+    atomicAdd(&slot[c], t);
   }
+}
+
+// dgamma[c] += sum_s ws[s][0][c]; dbeta[c] += sum_s ws[s][1][c]; the slots are re-zeroed
+__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(float* __restrict__ ws, int cols,
+                                                            float* __restrict__ dgamma,
+                                                            float* __restrict__ dbeta) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * cols) return;
+  float sacc = 0.f;
+#pragma unroll
+  for (int k = 0; k < LN_SLOTS; ++k) {
+    sacc += ws[k * 2 * cols + t];
+    ws[k * 2 * cols + t] = 0.f;
+  }
+  if (t < cols) {
+    if (dgamma) dgamma[t] += sacc;
+  } else if (dbeta) {
+    dbeta[t - cols] += sacc;
+  }
+}
+
+// per-(device, stream) zeroed slot workspace [LN_SLOTS][2][1024] (each stream's launches
+// are ordered, so one workspace per stream is race-free)
+static float* ln_workspace(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, float*> pool;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  float*& w = pool[{dev, s}];
+  if (!w) {
+    const size_t bytes = sizeof(float) * LN_SLOTS * 2 * 256 * LN_MAXV;
+    if (hipMalloc(&w, bytes) != hipSuccess) {
+      w = nullptr;
+      return nullptr;
+    }
+    if (hipMemsetAsync(w, 0, bytes, s) != hipSuccess) return nullptr;
+  }
+  return w;
 }
 
 __global__ __launch_bounds__(256) void rowflag_kernel(const float* __restrict__ X, int64_t rows,
@@ -212,9 +294,27 @@ extern "C" int savqa_ln_bwd(void* stream, const float* dy, const float* z, const
   if (cols % 256 != 0 || cols > 256 * LN_MAXV)
     return fail(SAVQA_EUNSUP, "savqa_ln_bwd: cols must be a multiple of 256 and <= 1024");
   int64_t blocks = (rows + LN_BWD_WAVES - 1) / LN_BWD_WAVES;
-  if (blocks > 256) blocks = 256;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(64 * LN_BWD_WAVES), 0, as_stream(stream), dy, z, mean,
-                     rden, stdv, gamma, rows, (int)cols, dz_add, dz, dgamma, dbeta);
+  if (blocks > 512) blocks = 512;
+  const dim3 g((unsigned)blocks), b(64 * LN_BWD_WAVES);
+  hipStream_t st = as_stream(stream);
+  float* ws = ln_workspace(st);
+  if (!ws) return fail(SAVQA_EUNSUP, "savqa_ln_bwd: workspace allocation failed");
+  switch (cols / 256) {
+#define SAVQA_LNB(NV)                                                                        \
+  case NV:                                                                                   \
+    if (dz_add)                                                                              \
+      hipLaunchKernelGGL((ln_bwd_kernel<NV, true>), g, b, 0, st, dy, z, mean, rden, stdv,    \
+                         gamma, rows, (int)cols, dz_add, dz, ws);                            \
+    else                                                                                     \
+      hipLaunchKernelGGL((ln_bwd_kernel<NV, false>), g, b, 0, st, dy, z, mean, rden, stdv,   \
+                         gamma, rows, (int)cols, dz_add, dz, ws);                            \
+    break;
+    SAVQA_LNB(1) SAVQA_LNB(2) SAVQA_LNB(3) SAVQA_LNB(4)
+#undef SAVQA_LNB
+  }
+  if (int rc = check_launch("savqa_ln_bwd")) return rc;
+  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((unsigned)((2 * cols + 255) / 256)), dim3(256), 0, st,
+                     ws, (int)cols, dgamma, dbeta);
   return check_launch("savqa_ln_bwd");
 }
 
