@@ -231,8 +231,9 @@ def syb_forward(P, syb_ipt, syb_mask, syb_graph, q_ipt, q_graph, q_mask, decMask
 
 
 def mil_nce_forward(P, vis_fea, macro_ipt, macro_obj_loc, pos_obj, neg_obj, obj_mask,
-                    pre="MIL_NCE", eps=1e-6):
-    """MIL_NCE.forward only_obj branch, AttModel_x3.py:338-380 and :441."""
+                    pre="MIL_NCE", eps=1e-6, rel=None):
+    """MIL_NCE.forward, AttModel_x3.py:338-441: the only_obj branch (:338-380), plus the
+    relation branch (:382-437) when rel = (pos_rel, neg_rel, pos_rel_loc, neg_rel_loc)."""
     E = P[f"{pre}.syb_emb.weight"]
     macro = linear(F.embedding(macro_ipt, E), P, f"{pre}.marco_mlp.0", relu=True).detach()
     Pf = linear(F.embedding(pos_obj, E), P, f"{pre}.syb_mlp.0", relu=True)   # (B,Nv,K,H)
@@ -248,8 +249,46 @@ def mil_nce_forward(P, vis_fea, macro_ipt, macro_obj_loc, pos_obj, neg_obj, obj_
     obj = torch.sum(w * Pf, dim=2)                                            # (B,Nv,H)
     valid = (macro_obj_loc >= 0).nonzero()                                    # :377-380
     macro[valid[:, 0], macro_obj_loc[valid[:, 0], valid[:, 1]].long(), :] = obj[valid[:, 0], valid[:, 1], :]
+    mil_rel = 0
+    if rel is not None:
+        macro, mil_rel = mil_nce_relations(P, macro, obj, *rel, pre=pre, eps=eps)
     out = linear(macro, P, f"{pre}.ipt_mlp.0", relu=True)
-    return out, mil, 0
+    return out, mil, mil_rel
+
+
+def mil_nce_relations(P, macro, obj, pos_rel, neg_rel, pos_loc, neg_loc, pre="MIL_NCE", eps=1e-6):
+    """Relation branch of MIL_NCE.forward, AttModel_x3.py:382-437.
+
+    loc rows: [obj_i, obj_j, rel_category, macro_rel_loc, micro_rel_loc] (negatives have
+    the first four); rows with macro_rel_loc < 0 are padding. bilinear(b, r, i, j) =
+    obj[b,i]^T R[r] obj[b,j] (the einsum pair at :398-401, only at the listed entries).
+    The softmax over ALL positives of the batch (:420) is indexed by the per-sample
+    micro_rel_loc (:426-436), exactly as the reference does."""
+    E = P[f"{pre}.syb_emb.weight"]
+    R = P[f"{pre}.R"]
+    relf = linear(F.embedding(pos_rel, E), P, f"{pre}.syb_mlp.0", relu=True)  # (B, maxrel, H)
+
+    def bilinear(loc):
+        v = (loc[:, :, 3] >= 0).nonzero()
+        b, k = v[:, 0], v[:, 1]
+        xi = obj[b, loc[b, k, 0]]
+        xj = obj[b, loc[b, k, 1]]
+        Rr = R[loc[b, k, 2]]
+        return torch.einsum("pl,plk,pk->p", xi, Rr, xj), v
+
+    sp, vpos = bilinear(pos_loc)
+    sn, _ = bilinear(neg_loc)
+    mil_rel = torch.logsumexp(sp.clamp(min=eps), dim=0) - torch.logsumexp(
+        torch.cat((sp.clamp(min=eps), sn.clamp(min=eps)), dim=0), dim=0)
+    b, k = vpos[:, 0], vpos[:, 1]
+    macro = macro.clone()
+    macro[b, pos_loc[b, k, 3]] = 0                                            # :418
+    w = F.softmax(sp, dim=0)                                                  # :420
+    for bb, kk in vpos.tolist():                                              # :421-436
+        m4 = int(pos_loc[bb, kk, 4])
+        r3 = int(pos_loc[bb, kk, 3])
+        macro[bb, r3] = macro[bb, r3] + w[m4] * relf[bb, m4]
+    return macro, mil_rel
 
 
 def heads(P, fea_vis, fea_syb, drop=None):
@@ -265,12 +304,14 @@ def heads(P, fea_vis, fea_syb, drop=None):
 
 
 def attmodel_forward(P, inp: Dict[str, torch.Tensor], decMask=True, num_blocks=6, h=8,
-                     drop=None):
+                     drop=None, only_obj=True):
     """AttModel.forward, AttModel_x3.py:512-542 (only_obj, mcb=False); drop = (seed, p)
     applies the training-mode dropout sites with the counter-hash masks."""
+    rel = None if only_obj else (inp["micro_positive_rel"], inp["micro_negative_rel"],
+                                 inp["micro_positive_rel_loc"], inp["micro_negative_rel_loc"])
     new_macro, mil_obj, mil_rel = mil_nce_forward(
         P, inp["vis_fea"], inp["macro_ipt"], inp["macro_obj_loc"],
-        inp["micro_positive_obj"], inp["micro_negative_obj"], inp["micro_obj_mask"])
+        inp["micro_positive_obj"], inp["micro_negative_obj"], inp["micro_obj_mask"], rel=rel)
     f_vis = vis_grid_forward(P, inp["vis_fea"], inp["vis_mask"], inp["q_ipt"], inp["q_graph"],
                              inp["q_mask"], decMask, num_blocks, h, drop=drop)
     f_syb = syb_forward(P, new_macro, inp["macro_mask"], inp["macro_graph"], inp["q_ipt"],
@@ -281,8 +322,9 @@ def attmodel_forward(P, inp: Dict[str, torch.Tensor], decMask=True, num_blocks=6
 
 # --------------------------------------------------------------------------- loss / optim
 def train_loss(logits_concat, logits_vis, logits_syb, answer, mil_nce_obj,
-               with_milnce=True, epsilon=0.1):
-    """main_itp_ddp_tar_super_node.py:335-361 with label_smoothing modules.py:461-463."""
+               with_milnce=True, epsilon=0.1, mil_nce_rel=0):
+    """main_itp_ddp_tar_super_node.py:326-361 with label_smoothing modules.py:461-463
+    (mil_nce_loss = -mil_nce_obj - mil_nce_rel when the relation branch runs)."""
     lsm = (F.log_softmax(logits_vis, -1) + F.log_softmax(logits_syb, -1)
            + F.log_softmax(logits_concat, -1)) / 3
     oh = torch.zeros_like(logits_concat)
@@ -290,7 +332,7 @@ def train_loss(logits_concat, logits_vis, logits_syb, answer, mil_nce_obj,
     oh = (1 - epsilon) * oh + epsilon / oh.size(-1)
     loss = (-(oh * lsm).sum(-1)).mean()
     if with_milnce:
-        loss = loss + (-mil_nce_obj)
+        loss = loss + (-mil_nce_obj - mil_nce_rel)
     return loss, lsm
 
 

@@ -145,3 +145,40 @@ def test_full_model_forward_loss_grads(case):
     # params that get no grad in the reference get none here either
     with_grad = {k for k, v in P.items() if v.grad is not None and k in P.shapes}
     assert with_grad == set(names)
+
+
+REL_INPUTS = ("vis_fea", "vis_mask", "q_ipt", "q_mask", "q_graph", "macro_ipt", "macro_mask",
+              "macro_graph", "macro_obj_loc", "micro_positive_obj", "micro_negative_obj",
+              "micro_obj_mask", "micro_positive_rel", "micro_negative_rel",
+              "micro_positive_rel_loc", "micro_negative_rel_loc", "answer")
+
+
+@pytest.mark.slow
+def test_relation_branch_full_model():
+    """MIL-NCE relation branch (only_obj=False, AttModel_x3.py:382-437) end to end: logits,
+    mil_nce_obj, mil_nce_rel, loss and every trained gradient (R included) against the
+    reference run on a super-node batch (tests/golden/full_rel_b2.npz)."""
+    g = np.load(os.path.join(GOLD, "full_rel_b2.npz"))
+    P = hashfill.HashParams(requires_grad=True, num_relations=int(g["num_relations"]))
+    inp = {k: torch.from_numpy(g[k]) for k in REL_INPUTS}
+    lc, lv, ls, mil, mil_rel = O.attmodel_forward(P, inp, decMask=True, only_obj=False)
+    assert rel_err(lc.detach(), g["logits_concat"]) < 1e-5
+    assert rel_err(ls.detach(), g["logits_syb"]) < 1e-5
+    assert abs(float(mil_rel) - float(g["mil_nce_rel"])) < 1e-5 * max(1, abs(float(g["mil_nce_rel"])))
+    loss, _ = O.train_loss(lc, lv, ls, inp["answer"], mil, mil_nce_rel=mil_rel)
+    assert abs(float(loss) - float(g["loss"])) < 1e-5 * abs(float(g["loss"]))
+    loss.backward()
+    names = [str(n) for n in g["grad_names"]]
+    assert "MIL_NCE.R" in names
+    for n in names:
+        gr = P[n].grad
+        assert gr is not None, n
+        flat = gr.reshape(-1)
+        idx = torch.from_numpy(g[f"g:{n}:idx"])
+        ref = g[f"g:{n}:val"]
+        scale = max(float(g[f"g:{n}:abssum"]) / flat.numel() * 50, np.abs(ref).max(), 1e-12)
+        assert np.abs(flat[idx].detach().numpy() - ref).max() <= 2e-4 * scale, n
+        assert abs(float(flat.double().sum()) - float(g[f"g:{n}:sum"])) <= \
+            1e-4 * max(float(g[f"g:{n}:abssum"]), 1e-9), n
+    used = torch.from_numpy(g["R_used"])
+    assert rel_err(P["MIL_NCE.R"].grad[used, :4].detach(), g["R_grad_used"]) < 1e-4

@@ -68,7 +68,7 @@ def fill_params(model):
             pass
 
 
-def ref_loss(lc, lv, ls, answer, mil_obj, eps=0.1):
+def ref_loss(lc, lv, ls, answer, mil_obj, eps=0.1, mil_rel=0):
     # main_itp_ddp_tar_super_node.py:335-361 (with_smooth_labeling, with_MILNCE_loss)
     lsm = (F.log_softmax(lv, -1) + F.log_softmax(ls, -1) + F.log_softmax(lc, -1)) / 3
     oh = torch.zeros((lc.size(0), lc.size(1)))
@@ -76,7 +76,7 @@ def ref_loss(lc, lv, ls, answer, mil_obj, eps=0.1):
     oh = ((1 - eps) * oh) + (eps / oh.size(-1))
     loss = -(oh * lsm).sum(-1)
     loss = loss.mean()
-    loss = loss + (-mil_obj)
+    loss = loss + (-mil_obj - mil_rel)  # main:326-329 (mil_rel = 0 when only_obj)
     return loss
 
 
@@ -152,6 +152,55 @@ def full_model_cases(modules_mod, att_mod):
                 opt.step()
         np.savez_compressed(os.path.join(OUT, f"{cname}.npz"), **out)
         print("wrote", cname, "loss", float(out["loss"]))
+    del model
+
+
+def relation_cases(att_mod):
+    """Full model with the MIL-NCE relation branch (only_obj=False, AttModel_x3.py:382-437)
+    on a super-node batch (oracle/cases.make_relation_inputs)."""
+    nrel = 7
+    glove = types.SimpleNamespace(vectors=torch.zeros(8, 300))
+    with torch.no_grad():
+        model = att_mod.AttModel(glove, CFG["hidden"], CFG["hidden_mil"], CFG["num_classes"],
+                                 CFG["maxlen_q"], CFG["maxlen"], CFG["maxlen_v"], CFG["num_blocks"], CFG["heads"],
+                                 0.0, 0.0, nrel, False)
+    model.train()
+    fill_params(model)
+    inp = cases.make_relation_inputs(2, [5, 4], [7, 5], nrel, tag="relcase")
+    t = to_t(inp)
+    lc, lv, ls, mil, mil_rel = model(
+        t["vis_fea"], t["vis_mask"], t["q_ipt"], t["q_mask"], t["q_graph"], t["macro_ipt"],
+        t["macro_mask"], t["macro_graph"], t["macro_obj_loc"], t["micro_positive_obj"],
+        t["micro_negative_obj"], t["micro_obj_mask"], t["micro_positive_rel"],
+        t["micro_negative_rel"], t["micro_positive_rel_loc"], t["micro_negative_rel_loc"],
+        decMask=True, mcb=False)
+    loss = ref_loss(lc, lv, ls, t["answer"], mil, mil_rel=mil_rel)
+    model.zero_grad()
+    loss.backward()
+    out = dict(inp)
+    out.update(logits_concat=lc.detach().numpy(), logits_vis=lv.detach().numpy(),
+               logits_syb=ls.detach().numpy(), mil_nce_obj=np.float32(mil.item()),
+               mil_nce_rel=np.float32(mil_rel.item()), loss=np.float32(loss.item()),
+               num_relations=np.int32(nrel), num_blocks=np.int32(CFG["num_blocks"]))
+    gnames = []
+    for name, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        gnames.append(name)
+        d = grad_digest(name, p.grad)
+        out[f"g:{name}:sum"] = np.float64(d["sum"])
+        out[f"g:{name}:abssum"] = np.float64(d["abssum"])
+        out[f"g:{name}:idx"] = d["idx"]
+        out[f"g:{name}:val"] = d["val"]
+    # R: the used categories' slices in full (sparse gradient)
+    used = np.unique(np.concatenate([inp["micro_positive_rel_loc"][..., 2].ravel(),
+                                     inp["micro_negative_rel_loc"][..., 2].ravel()]))
+    used = used[used >= 0]
+    out["R_used"] = used
+    out["R_grad_used"] = model.MIL_NCE.R.grad[torch.from_numpy(used), :4].numpy()  # 4 rows each
+    out["grad_names"] = np.array(gnames)
+    np.savez_compressed(os.path.join(OUT, "full_rel_b2.npz"), **out)
+    print("wrote full_rel_b2 loss", float(out["loss"]), "mil_rel", float(out["mil_nce_rel"]))
     del model
 
 
@@ -246,6 +295,8 @@ def main():
         block_cases(modules_mod)
     if "full" in which:
         full_model_cases(modules_mod, att_mod)
+    if "rel" in which:
+        relation_cases(att_mod)
 
 
 if __name__ == "__main__":
