@@ -176,6 +176,45 @@ int savqa_dec_init_bwd(void* stream, const float* g, int64_t B, int64_t d, int64
                        uint64_t seed, int32_t site, float p, float* demb, float* dpos);
 
 /* ------------------------------------------------------------------------
+ * MIL-NCE relation branch (only_obj = False), AttModel_x3.py:382-437. Slot tables are
+ * the loader's loc tensors (int64 [B][L][5] positives: obj_i, obj_j, rel_category,
+ * macro_rel_loc, micro_rel_loc; [B][L][4] negatives; macro_rel_loc < 0 = padding).
+ * obj = new_obj_fea [B*Nv][H]; R = MIL_NCE.R [nrel][H][H]; relf = relu(syb_mlp(syb_emb
+ * (micro_positive_rel))) [B*Lp][H]; macro = new_macro_ipt [B*Ns][H].
+ * ------------------------------------------------------------------------ */
+/* val[slot] = obj[b,i]^T R[r] obj[b,j] for every listed entry (0 on padding) */
+int savqa_rel_bilinear_fwd(void* stream, const int64_t* loc, int32_t loc_w, int64_t B, int64_t L,
+                           const float* obj, int64_t Nv, int64_t H, const float* R, float* val);
+/* dobj += (R x_j) dval, (R^T x_i) dval;  dR[r] += dval x_i x_j^T (atomics; dR may be NULL) */
+int savqa_rel_bilinear_bwd(void* stream, const int64_t* loc, int32_t loc_w, int64_t B, int64_t L,
+                           const float* obj, int64_t Nv, int64_t H, const float* R,
+                           const float* dval, float* dobj, float* dR);
+/* mil_rel = LSE(max(sp,eps)) - LSE(max(sp,eps) ++ max(sn,eps)) over valid entries (:405-406);
+ * cidx[c] = slot of the c-th valid positive (b-major), wsm = softmax over them (:420),
+ * st[0..4] = (P, m1, Z1, m2, Z2) for the backward. One workgroup. */
+int savqa_rel_loss_fwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp, const float* sp,
+                       const int64_t* neg_loc, int64_t Ln, const float* sn, float eps, int32_t* cidx,
+                       float* wsm, float* st, float* mil_rel);
+/* macro[b, loc3] = 0 for valid positives, then in order += wsm[loc4] * relf[b, loc4] (:418-436) */
+int savqa_rel_macro_fwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp,
+                        const int32_t* cidx, const float* st, const float* wsm, const float* relf,
+                        int64_t Ns, int64_t H, float* macro);
+/* backward of the update: dwsm[loc4] += dmacro[b,loc3].relf[b,loc4], drelf[b,loc4] +=
+ * wsm[loc4] dmacro[b,loc3] (both zero-initialised by the caller), then dmacro rows loc3 := 0 */
+int savqa_rel_macro_bwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp,
+                        const int32_t* cidx, const float* st, const float* wsm, const float* relf,
+                        int64_t Ns, int64_t H, float* dmacro, float* dwsm, float* drelf);
+/* dsp / dsn per slot from dmil (device scalar) through both logsumexps and the softmax path */
+int savqa_rel_loss_bwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp, const float* sp,
+                       const int64_t* neg_loc, int64_t Ln, const float* sn, float eps,
+                       const int32_t* cidx, const float* wsm, const float* dwsm, const float* st,
+                       const float* dmil, float* dsp, float* dsn);
+
+/* out = a*x + b*y over n floats (combining the MIL-NCE terms of the loss) */
+int savqa_axpby(void* stream, const float* x, const float* y, int64_t n, float a, float b,
+                float* out);
+
+/* ------------------------------------------------------------------------
  * Dropout (nn.Dropout(dropout_rate) sites of model_v=3: stack inputs
  * AttModel_x3.py:71-72/:102 (vis: position-table dropout, then enc_dropout) and :227
  * (syb enc_dropout); decoder inputs :147/:274 (savqa_dec_init); heads :482-500).

@@ -185,14 +185,19 @@ class CompactBilinearPooling(nn.Module):
 class _AttModelFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, model, decMask, drop, anchor, *tensors):
-        inp = dict(zip(_INPUT_NAMES, tensors))
-        (lc, lv, ls, mil), saved = model._engine.forward(inp, decMask, drop)
+        inp = dict(zip(_INPUT_NAMES + _REL_NAMES, tensors))
+        (lc, lv, ls, mil, mil_rel), saved = model._engine.forward(inp, decMask, drop)
         ctx.model = model
         ctx.saved = saved
-        return lc, lv, ls, mil
+        ctx.ntensors = len(tensors)
+        ctx.rel = mil_rel is not None
+        if mil_rel is None:
+            mil_rel = torch.zeros((), device=mil.device)
+            ctx.mark_non_differentiable(mil_rel)
+        return lc, lv, ls, mil, mil_rel
 
     @staticmethod
-    def backward(ctx, dlc, dlv, dls, dmil):
+    def backward(ctx, dlc, dlv, dls, dmil, dmil_rel):
         model = ctx.model
         dev = model._arena.flat.device
 
@@ -203,14 +208,16 @@ class _AttModelFn(torch.autograd.Function):
         Cc = model.num_classes
         red = model.__dict__.get("_reducer")
         model._engine.backward(ctx.saved, z(dlc, (B, Cc)), z(dlv, (B, Cc)), z(dls, (B, Cc)),
-                               z(dmil, ()), on_range=red.reduce_range if red else None)
+                               z(dmil, ()), on_range=red.reduce_range if red else None,
+                               dmil_rel=z(dmil_rel, ()) if ctx.rel else None)
         ctx.saved = None
-        return (None, None, None, None) + (None,) * len(_INPUT_NAMES)
+        return (None, None, None, None) + (None,) * ctx.ntensors
 
 
 _INPUT_NAMES = ("vis_fea", "vis_mask", "q_ipt", "q_mask", "q_graph", "macro_ipt", "macro_mask",
                 "macro_graph", "macro_obj_loc", "micro_positive_obj", "micro_negative_obj",
                 "micro_obj_mask")
+_REL_NAMES = ("micro_positive_rel", "micro_positive_rel_loc", "micro_negative_rel_loc")
 
 
 class AttModel(nn.Module):
@@ -276,9 +283,6 @@ class AttModel(nn.Module):
                 micro_negative_rel_loc, decMask=True, mcb=False):
         if mcb:
             raise NotImplementedError("mcb=True needs torch.rfft (removed in torch>=1.8); out of scope")
-        if not self.only_obj:
-            raise NotImplementedError("MIL-NCE relation branch (only_obj=False) is the next scope "
-                                      "row (SURVEY.md 8f); use only_obj=True")
         drop = None
         if self.training and self.dropout_rate > 0:
             # one 63-bit step seed per forward from torch's CPU generator (torch.manual_seed
@@ -302,9 +306,12 @@ class AttModel(nn.Module):
         tensors = (f32(vis_fea), i32(vis_mask), i64(q_ipt), i32(q_mask), i32(q_graph), i64(macro_ipt),
                    i32(macro_mask), i32(macro_graph), i64(macro_obj_loc), i64(micro_positive_obj),
                    i64(micro_negative_obj), i32(micro_obj_mask))
+        if not self.only_obj:  # relation branch inputs (micro_negative_rel ids are unused, :391)
+            tensors = tensors + (i64(micro_positive_rel), i64(micro_positive_rel_loc),
+                                 i64(micro_negative_rel_loc))
         anchor = self._arena_anchor()
-        lc, lv, ls, mil = _AttModelFn.apply(self, bool(decMask), drop, anchor, *tensors)
-        return lc, lv, ls, mil, 0
+        lc, lv, ls, mil, mil_rel = _AttModelFn.apply(self, bool(decMask), drop, anchor, *tensors)
+        return lc, lv, ls, mil, (mil_rel if not self.only_obj else 0)
 
     def _arena_anchor(self):
         # any parameter that requires grad links the autograd node into the graph

@@ -59,6 +59,16 @@ _SIGS = {
     "savqa_gattn_bwd_flash": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
                               c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p,
                               c_p, c_i64, c_p, c_i64, c_p, c_i64],
+    "savqa_rel_bilinear_fwd": [c_p, c_p, c_i32, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p],
+    "savqa_rel_bilinear_bwd": [c_p, c_p, c_i32, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_p,
+                               c_p],
+    "savqa_rel_loss_fwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p, c_p],
+    "savqa_rel_macro_fwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p],
+    "savqa_rel_macro_bwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p,
+                            c_p],
+    "savqa_rel_loss_bwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p, c_p,
+                           c_p, c_p, c_p],
+    "savqa_axpby": [c_p, c_p, c_p, c_i64, c_f, c_f, c_p],
     "savqa_graph_build": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p],
     "savqa_dec_init": [c_p, c_p, c_i64, c_f, c_p, c_i64, c_i64, c_u64, c_i32, c_f, c_p],
     "savqa_dec_init_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_f, c_u64, c_i32, c_f, c_p, c_p],

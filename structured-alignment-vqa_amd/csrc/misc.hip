@@ -613,6 +613,22 @@ extern "C" int savqa_rowscale_mask(void* stream, const float* in, const float* r
   return check_launch("savqa_rowscale_mask");
 }
 
+namespace savqa {
+__global__ void axpby_kernel(const float* __restrict__ x, const float* __restrict__ y, int64_t n,
+                             float a, float b, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a * x[i] + b * y[i];
+}
+}  // namespace savqa
+
+extern "C" int savqa_axpby(void* stream, const float* x, const float* y, int64_t n, float a,
+                           float b, float* out) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(axpby_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), x, y, n, a, b, out);
+  return check_launch("savqa_axpby");
+}
+
 extern "C" int savqa_affine(void* stream, const float* in, int64_t n, float a, float b, float* out) {
   if (n <= 0) return 0;
   int64_t blocks = (n + 255) / 256;

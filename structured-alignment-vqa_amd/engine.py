@@ -88,6 +88,8 @@ class MilWeights:
     def __init__(self, arena, grad=False):
         v = arena.gview if grad else arena.view
         m = "MIL_NCE"
+        live = f"{m}.R" in arena.live_names
+        self.R = v(f"{m}.R") if (live or not grad) else None  # relation branch only
         self.E = v(f"{m}.syb_emb.weight")
         self.Ws, self.bs = v(f"{m}.syb_mlp.0.weight"), v(f"{m}.syb_mlp.0.bias")
         self.Wv, self.bv = v(f"{m}.vis_mlp.0.weight"), v(f"{m}.vis_mlp.0.bias")
@@ -368,12 +370,16 @@ class MilSaved:
     Nf: torch.Tensor = None
     vv: torch.Tensor = None
     macro: torch.Tensor = None
+    obj: torch.Tensor = None
+    rel: Optional[dict] = None
 
 
 def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb, T_syb: int,
-                mil_out: torch.Tensor, eps: float = 1e-6) -> MilSaved:
-    """MIL_NCE.forward only_obj branch (AttModel_x3.py:352-380, :441). Writes
-    relu(new_macro W_ipt^T + b) into the node rows of the syb stack's cat buffer."""
+                mil_out: torch.Tensor, eps: float = 1e-6, rel=None,
+                mil_rel_out: Optional[torch.Tensor] = None) -> MilSaved:
+    """MIL_NCE.forward (AttModel_x3.py:352-441): the only_obj branch, plus the relation
+    branch (:382-437) when rel = (pos_rel [B,Lp], pos_loc [B,Lp,5], neg_loc [B,Ln,4]).
+    Writes relu(new_macro W_ipt^T + b) into the node rows of the syb stack's cat buffer."""
     dev = vis_fea.device
     B, Nv, Dv = vis_fea.shape
     Ns = macro_ipt.shape[1]
@@ -393,24 +399,71 @@ def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb
     ws = _empty(B * Nv, dev=dev)
     ops.mil_fwd(s.Pf, s.Nf, s.vv, omask, B * Nv, K, Hm, eps, obj, ws, mil_out)
     ops.index_put_rows(s.loc, B, Nv, Ns, Hm, obj, s.macro)
+    s.obj = obj
+    if rel is not None:
+        s.rel = _rel_forward(W, s, rel, Ns, Hm, eps, mil_rel_out)
     ops.linear(s.macro, W.Wipt, W.bipt, cat_syb, relu=True, rows=B * Ns, c_group=Ns,
                c_stride=T_syb, c_offset=0, ldo=cat_syb.shape[1])
     return s
 
 
+def _rel_forward(W: MilWeights, s: MilSaved, rel, Ns: int, Hm: int, eps: float, mil_rel_out):
+    """Relation branch, AttModel_x3.py:382-437 (csrc/rel.hip): rel features, the listed
+    bilinear entries x_i^T R_r x_j, the two logsumexps + softmax, the ordered macro update."""
+    pos_rel, pos_loc, neg_loc = rel
+    dev = s.macro.device
+    B, Lp = pos_rel.shape
+    Ln = neg_loc.shape[1]
+    r = dict(pos_rel=pos_rel.reshape(-1), pos_loc=pos_loc, neg_loc=neg_loc, Lp=Lp, Ln=Ln)
+    relf = _empty(B * Lp, Hm, dev=dev)
+    ops.linear(W.E, W.Ws, W.bs, relf, relu=True, a_rows=r["pos_rel"])
+    sp, sn = _empty(B * Lp, dev=dev), _empty(B * Ln, dev=dev)
+    ops.rel_bilinear_fwd(pos_loc, B, Lp, s.obj, s.Nv, Hm, W.R, sp)
+    ops.rel_bilinear_fwd(neg_loc, B, Ln, s.obj, s.Nv, Hm, W.R, sn)
+    cidx = torch.empty(max(B * Lp, 1), dtype=torch.int32, device=dev)
+    wsm, st = _empty(max(B * Lp, 1), dev=dev), _empty(8, dev=dev)
+    ops.rel_loss_fwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cidx, wsm, st, mil_rel_out)
+    ops.rel_macro_fwd(pos_loc, B, Lp, cidx, st, wsm, relf, Ns, Hm, s.macro)
+    r.update(relf=relf, sp=sp, sn=sn, cidx=cidx, wsm=wsm, st=st)
+    return r
+
+
 def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torch.Tensor],
-                 dmil: torch.Tensor, eps: float = 1e-6):
+                 dmil: torch.Tensor, eps: float = 1e-6, dmil_rel: Optional[torch.Tensor] = None):
     dev = dmil.device
     B, Nv, Ns, K = s.B, s.Nv, s.Ns, s.K
     Hm = W.Ws.shape[0]
+    rel = s.rel
     dobj = None
     if dnode is not None:
         ops.linear_dw(dnode, s.macro, G.Wipt, G.bipt, rows=B * Ns)
         dmacro = _empty(B * Ns, Hm, dev=dev)
         ops.linear_dx(dnode, W.Wipt, dmacro, rows=B * Ns)
+        if rel is not None:  # relation rows: grads to the softmax weights and rel features,
+            Lp = rel["Lp"]    # and the overwritten previous contents get none
+            rel["dwsm"] = torch.zeros(max(B * Lp, 1), device=dev)
+            rel["drelf"] = torch.zeros(B * Lp, Hm, device=dev)
+            ops.rel_macro_bwd(rel["pos_loc"], B, Lp, rel["cidx"], rel["st"], rel["wsm"],
+                              rel["relf"], Ns, Hm, dmacro, rel["dwsm"], rel["drelf"])
         dobj = _empty(B * Nv, Hm, dev=dev)
         ops.index_get_rows(s.loc, B, Nv, Ns, Hm, dmacro, dobj)
         del dmacro
+    if rel is not None:
+        Lp, Ln = rel["Lp"], rel["Ln"]
+        if dobj is None:
+            dobj = torch.zeros(B * Nv, Hm, device=dev)
+        if "dwsm" not in rel:
+            rel["dwsm"] = torch.zeros(max(B * Lp, 1), device=dev)
+            rel["drelf"] = torch.zeros(B * Lp, Hm, device=dev)
+        dsp, dsn = _empty(B * Lp, dev=dev), _empty(B * Ln, dev=dev)
+        ops.rel_loss_bwd(rel["pos_loc"], B, Lp, rel["sp"], rel["neg_loc"], Ln, rel["sn"], eps,
+                         rel["cidx"], rel["wsm"], rel["dwsm"], rel["st"], dmil_rel, dsp, dsn)
+        ops.rel_bilinear_bwd(rel["pos_loc"], B, Lp, s.obj, Nv, Hm, W.R, dsp, dobj, G.R)
+        ops.rel_bilinear_bwd(rel["neg_loc"], B, Ln, s.obj, Nv, Hm, W.R, dsn, dobj, G.R)
+        drelf = rel["drelf"]
+        ops.rowscale_mask(drelf, None, rel["relf"], B * Lp, Hm, drelf)  # ReLU of syb_mlp
+        ops.linear_dw(drelf, W.E, G.Ws, G.bs, rows=B * Lp, x_rows=rel["pos_rel"])
+        ops.linear_dx(drelf, W.Ws, G.E, rows=B * Lp, c_rows=rel["pos_rel"], atomic=True)
     dPf, dNf = torch.empty_like(s.Pf), torch.empty_like(s.Nf)
     dvv = torch.empty_like(s.vv)
     ops.mil_bwd(s.Pf, s.Nf, s.vv, s.mask, B * Nv, K, Hm, eps, dobj, dmil, dPf, dNf, dvv)
@@ -532,9 +585,15 @@ class ModelEngine:
         with torch.cuda.stream(s_syb):
             mil_val = _empty((), dev=dev)
             cat_syb = _empty(B * Ts, Dv, dev=dev)
+            rel, mil_rel = None, None
+            if "micro_positive_rel_loc" in inp:
+                rel = (inp["micro_positive_rel"], inp["micro_positive_rel_loc"],
+                       inp["micro_negative_rel_loc"])
+                mil_rel = _empty((), dev=dev)
             ms = mil_forward(self.mil, vis, inp["macro_ipt"], inp["macro_obj_loc"],
                              inp["micro_positive_obj"], inp["micro_negative_obj"],
-                             inp["micro_obj_mask"], cat_syb, Ts, mil_val)
+                             inp["micro_obj_mask"], cat_syb, Ts, mil_val, rel=rel,
+                             mil_rel_out=mil_rel)
             ss = stack_forward(self.syb, cat_syb, B, Ns, Lq, inp["q_ipt"], inp["macro_mask"],
                                inp["q_mask"], inp["q_graph"], inp["macro_graph"], decMask, H, d,
                                drop, SYB_SITES)
@@ -546,10 +605,10 @@ class ModelEngine:
                                VIS_SITES)
         main.wait_stream(s_vis)
         main.wait_stream(s_syb)
-        for t in (sv.out, ss.out, mil_val):
+        for t in (sv.out, ss.out, mil_val) + ((mil_rel,) if mil_rel is not None else ()):
             t.record_stream(main)
         (lc, lv, ls), hs = heads_forward(self.head, sv.out, ss.out, d, drop)
-        return (lc, lv, ls, mil_val), (ms, sv, ss, hs)
+        return (lc, lv, ls, mil_val, mil_rel), (ms, sv, ss, hs)
 
     def region_bounds(self):
         """Arena offsets at which the gradients of heads / vis stack / syb stack end."""
@@ -558,11 +617,11 @@ class ModelEngine:
                 a.offsets[f"att_syb.dec_feed_forward_{nb - 1}.normalization.gamma"][0],
                 a.offsets["MIL_NCE.ipt_mlp.0.weight"][0])
 
-    def backward(self, saved, dlc, dlv, dls, dmil, on_range=None):
+    def backward(self, saved, dlc, dlv, dls, dmil, on_range=None, dmil_rel=None):
         with ops.gemm_precision(self.gemm_precision):
-            return self._backward(saved, dlc, dlv, dls, dmil, on_range)
+            return self._backward(saved, dlc, dlv, dls, dmil, on_range, dmil_rel)
 
-    def _backward(self, saved, dlc, dlv, dls, dmil, on_range=None):
+    def _backward(self, saved, dlc, dlv, dls, dmil, on_range=None, dmil_rel=None):
         """Whole-model backward (heads on the caller's stream, then the two stacks on their
         own streams). on_range(start, end) is called, on the stream that produced them,
         as soon as arena gradient elements [start, end) are final (all-reduce streaming);
@@ -597,6 +656,8 @@ class ModelEngine:
         df_vis.record_stream(s_vis)
         df_syb.record_stream(s_syb)
         dmil.record_stream(s_syb)
+        if dmil_rel is not None:
+            dmil_rel.record_stream(s_syb)
         with torch.cuda.stream(s_vis):
             mk = Marker("att_vis_grid", b_heads)
             stack_backward(self.vis, self.gvis, sv, df_vis, H, d, want_node_grad=False, mark=mk)
@@ -606,7 +667,7 @@ class ModelEngine:
             dnode = stack_backward(self.syb, self.gsyb, ss, df_syb, H, d, want_node_grad=True,
                                    mark=mk)
             mk.upto(b_syb, flush=True)
-            mil_backward(self.mil, self.gmil, ms, dnode, dmil)
+            mil_backward(self.mil, self.gmil, ms, dnode, dmil, dmil_rel=dmil_rel)
             mk.upto(self.arena.n_live, flush=True)
         main.wait_stream(s_vis)
         main.wait_stream(s_syb)

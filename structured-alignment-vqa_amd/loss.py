@@ -44,8 +44,26 @@ class _LossFn(torch.autograd.Function):
         return out[0], out[1], out[2], None, dmil, None, None
 
 
+class _Sum2Fn(torch.autograd.Function):
+    """mil_nce_obj + mil_nce_rel on the device (main:326-329: loss += -obj - rel)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        out = torch.empty((), dtype=torch.float32, device=a.device)
+        ops.axpby(a.contiguous(), b.contiguous(), 1, 1.0, 1.0, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
 def smoothed_loss(logits_concat, logits_vis, logits_syb, answer, mil_nce_obj=None,
-                  with_milnce=True, epsilon=0.1):
-    """Returns (loss, lsm). lsm is the averaged log-softmax the reference uses for accuracy."""
-    return _LossFn.apply(logits_concat, logits_vis, logits_syb, answer, mil_nce_obj,
-                         bool(with_milnce and mil_nce_obj is not None), float(epsilon))
+                  with_milnce=True, epsilon=0.1, mil_nce_rel=None):
+    """Returns (loss, lsm). lsm is the averaged log-softmax the reference uses for accuracy.
+    mil_nce_rel (relation branch, a tensor) is subtracted too, as main:326-329 does."""
+    mil = mil_nce_obj
+    if mil is not None and torch.is_tensor(mil_nce_rel):
+        mil = _Sum2Fn.apply(mil_nce_obj, mil_nce_rel)
+    return _LossFn.apply(logits_concat, logits_vis, logits_syb, answer, mil,
+                         bool(with_milnce and mil is not None), float(epsilon))

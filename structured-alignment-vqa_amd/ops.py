@@ -320,6 +320,41 @@ def scatter_rows(g, idx, rows, cols, scale, padding_idx, dtable):
          int(padding_idx), _p(dtable))
 
 
+# ------------------------------------------------------------------------------ relations
+def rel_bilinear_fwd(loc, B, L, obj, Nv, H, R, val):
+    call("savqa_rel_bilinear_fwd", _stream(), _p(loc), int(loc.shape[-1]), B, L, _p(obj), Nv, H,
+         _p(R), _p(val))
+
+
+def rel_bilinear_bwd(loc, B, L, obj, Nv, H, R, dval, dobj, dR):
+    call("savqa_rel_bilinear_bwd", _stream(), _p(loc), int(loc.shape[-1]), B, L, _p(obj), Nv, H,
+         _p(R), _p(dval), _p(dobj), _p(dR))
+
+
+def rel_loss_fwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cidx, wsm, st, mil_rel):
+    call("savqa_rel_loss_fwd", _stream(), _p(pos_loc), B, Lp, _p(sp), _p(neg_loc), Ln, _p(sn),
+         float(eps), _p(cidx), _p(wsm), _p(st), _p(mil_rel))
+
+
+def rel_macro_fwd(pos_loc, B, Lp, cidx, st, wsm, relf, Ns, H, macro):
+    call("savqa_rel_macro_fwd", _stream(), _p(pos_loc), B, Lp, _p(cidx), _p(st), _p(wsm), _p(relf),
+         Ns, H, _p(macro))
+
+
+def rel_macro_bwd(pos_loc, B, Lp, cidx, st, wsm, relf, Ns, H, dmacro, dwsm, drelf):
+    call("savqa_rel_macro_bwd", _stream(), _p(pos_loc), B, Lp, _p(cidx), _p(st), _p(wsm),
+         _p(relf), Ns, H, _p(dmacro), _p(dwsm), _p(drelf))
+
+
+def rel_loss_bwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cidx, wsm, dwsm, st, dmil, dsp, dsn):
+    call("savqa_rel_loss_bwd", _stream(), _p(pos_loc), B, Lp, _p(sp), _p(neg_loc), Ln, _p(sn),
+         float(eps), _p(cidx), _p(wsm), _p(dwsm), _p(st), _p(dmil), _p(dsp), _p(dsn))
+
+
+def axpby(x, y, n, a, b, out):
+    call("savqa_axpby", _stream(), _p(x), _p(y), int(n), float(a), float(b), _p(out))
+
+
 def adam(p, g, m, v, n, lr, beta1, beta2, eps, bc1, bc2, grad_scale=1.0):
     call("savqa_adam", _stream(), _p(p), _p(g), _p(m), _p(v), int(n), float(lr), float(beta1),
          float(beta2), float(eps), float(bc1), float(bc2), float(grad_scale))

@@ -25,8 +25,10 @@ import torch.nn as nn
 ALIGN = 64
 
 
-def _live_order(num_blocks: int) -> List[str]:
-    """Live parameter names in backward-completion order (see module docstring)."""
+def _live_order(num_blocks: int, only_obj: bool = True) -> List[str]:
+    """Live parameter names in backward-completion order (see module docstring). With the
+    relation branch (only_obj=False) MIL_NCE.R receives a gradient too (AttModel_x3.py:
+    393-401) and joins the live range, last."""
     out: List[str] = []
     for head in ("cls", "cls_vis", "cls_syb"):
         out += [f"{head}.3.weight", f"{head}.3.bias", f"{head}.0.weight", f"{head}.0.bias"]
@@ -66,6 +68,8 @@ def _live_order(num_blocks: int) -> List[str]:
     out += [f"{m}.ipt_mlp.0.weight", f"{m}.ipt_mlp.0.bias", f"{m}.syb_mlp.0.weight",
             f"{m}.syb_mlp.0.bias", f"{m}.vis_mlp.0.weight", f"{m}.vis_mlp.0.bias",
             f"{m}.syb_emb.weight"]
+    if not only_obj:
+        out.append(f"{m}.R")
     return out
 
 
@@ -74,8 +78,9 @@ class ParamArena:
 
     def __init__(self, model: nn.Module, num_blocks: int, device=None):
         named = OrderedDict(model.named_parameters())
-        live = [n for n in _live_order(num_blocks) if n in named]
-        missing = set(_live_order(num_blocks)) - set(named)
+        order = _live_order(num_blocks, bool(getattr(model, "only_obj", True)))
+        live = [n for n in order if n in named]
+        missing = set(order) - set(named)
         if missing:
             raise RuntimeError(f"ParamArena: model lacks live params {sorted(missing)[:4]}")
         dead = [n for n in named if n not in set(live)]

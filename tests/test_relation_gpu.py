@@ -1,0 +1,72 @@
+"""MIL-NCE relation branch (only_obj=False, AttModel_x3.py:382-437) on the HIP path against
+the reference's own outputs on a super-node batch (tests/golden/full_rel_b2.npz, produced by
+tools/make_golden.py running the reference): logits, mil_nce_obj, mil_nce_rel, loss and the
+gradients of every trained parameter, MIL_NCE.R included (north-star tolerance 1e-3)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import hashfill
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+INPUTS = ("vis_fea", "vis_mask", "q_ipt", "q_mask", "q_graph", "macro_ipt", "macro_mask",
+          "macro_graph", "macro_obj_loc", "micro_positive_obj", "micro_negative_obj",
+          "micro_obj_mask", "micro_positive_rel", "micro_negative_rel", "micro_positive_rel_loc",
+          "micro_negative_rel_loc")
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def test_relation_branch_against_reference_golden():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    torch.backends.cuda.matmul.allow_tf32 = False
+    from savqa_amd.AttModel_x3 import AttModel
+    from savqa_amd.loss import smoothed_loss
+    from savqa_amd.optim import Adam
+    g = np.load(os.path.join(GOLD, "full_rel_b2.npz"))
+    m = AttModel(None, 512, 1024, 914, 40, 450, 49, int(g["num_blocks"]), 8, 0.0, 0.0,
+                 int(g["num_relations"]), False, device="cuda", init=False)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            p.copy_(torch.from_numpy(hashfill.param_value(n, tuple(p.shape))))
+    m.train()
+    assert "MIL_NCE.R" in m._arena.live_names
+    t = {k: torch.from_numpy(g[k]).cuda() for k in INPUTS + ("answer",)}
+    lc, lv, ls, mil, mil_rel = m(*[t[k] for k in INPUTS], decMask=True, mcb=False)
+    for name, out in (("logits_concat", lc), ("logits_vis", lv), ("logits_syb", ls)):
+        o = out.detach().cpu().numpy()
+        assert rel(o, g[name]) < 1e-3, name
+        assert (o.argmax(-1) == g[name].argmax(-1)).all(), name
+    assert abs(float(mil) - float(g["mil_nce_obj"])) < 1e-3 * max(1.0, abs(float(g["mil_nce_obj"])))
+    assert abs(float(mil_rel) - float(g["mil_nce_rel"])) < 1e-3 * max(1.0, abs(float(g["mil_nce_rel"])))
+    loss, _ = smoothed_loss(lc, lv, ls, t["answer"], mil, mil_nce_rel=mil_rel)
+    assert abs(float(loss) - float(g["loss"])) < 1e-4 * abs(float(g["loss"]))
+    opt = Adam(m, lr=1e-4)
+    opt.zero_grad()
+    loss.backward()
+    params = dict(m.named_parameters())
+    worst = []
+    for n in [str(x) for x in g["grad_names"]]:
+        gr = params[n].grad
+        assert gr is not None, n
+        flat = gr.reshape(-1).cpu().double().numpy()
+        ref = g[f"g:{n}:val"].astype(np.float64)
+        idx = g[f"g:{n}:idx"]
+        scale = max(np.abs(ref).max(), float(g[f"g:{n}:abssum"]) / flat.size, 1e-20)
+        worst.append((np.abs(flat[idx] - ref).max() / scale, n))
+        asum = float(g[f"g:{n}:abssum"])
+        assert abs(flat.sum() - float(g[f"g:{n}:sum"])) <= 1e-3 * max(asum, 1e-12) + 1e-9, n
+    worst.sort(reverse=True)
+    assert worst[0][0] < 1e-3, worst[:5]
+    used = torch.from_numpy(g["R_used"]).cuda()
+    assert rel(params["MIL_NCE.R"].grad[used, :4].cpu().numpy(), g["R_grad_used"]) < 1e-3
+    opt.step()
+    torch.cuda.synchronize()
