@@ -182,13 +182,15 @@ int savqa_dec_init_bwd(void* stream, const float* g, int64_t B, int64_t d, int64
  * obj = new_obj_fea [B*Nv][H]; R = MIL_NCE.R [nrel][H][H]; relf = relu(syb_mlp(syb_emb
  * (micro_positive_rel))) [B*Lp][H]; macro = new_macro_ipt [B*Ns][H].
  * ------------------------------------------------------------------------ */
-/* val[slot] = obj[b,i]^T R[r] obj[b,j] for every listed entry (0 on padding) */
-int savqa_rel_bilinear_fwd(void* stream, const int64_t* loc, int32_t loc_w, int64_t B, int64_t L,
-                           const float* obj, int64_t Nv, int64_t H, const float* R, float* val);
-/* dobj += (R x_j) dval, (R^T x_i) dval;  dR[r] += dval x_i x_j^T (atomics; dR may be NULL) */
-int savqa_rel_bilinear_bwd(void* stream, const int64_t* loc, int32_t loc_w, int64_t B, int64_t L,
-                           const float* obj, int64_t Nv, int64_t H, const float* R,
-                           const float* dval, float* dobj, float* dR);
+/* val[slot] = obj[b,i] . V[b*Nv + j][r*H : r*H + H] for every listed entry (0 on padding),
+ * where V = obj Rmat^T is computed by savqa_gemm (Rmat = R as [nrel*H][H]): x_i^T R_r x_j */
+int savqa_rel_entries_fwd(void* stream, const int64_t* loc, int32_t loc_w, int64_t B, int64_t L,
+                          const float* obj, int64_t Nv, int64_t H, const float* V, int64_t ldv,
+                          float* val);
+/* dobj[b,i] += dval V[(b,j)][rH:]; dV[(b,j)][rH:] += dval obj[b,i]  (atomics) */
+int savqa_rel_entries_bwd(void* stream, const int64_t* loc, int32_t loc_w, int64_t B, int64_t L,
+                          const float* obj, int64_t Nv, int64_t H, const float* V, int64_t ldv,
+                          const float* dval, float* dobj, float* dV);
 /* mil_rel = LSE(max(sp,eps)) - LSE(max(sp,eps) ++ max(sn,eps)) over valid entries (:405-406);
  * cidx[c] = slot of the c-th valid positive (b-major), wsm = softmax over them (:420),
  * st[0..4] = (P, m1, Z1, m2, Z2) for the backward. One workgroup. */

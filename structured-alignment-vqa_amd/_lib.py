@@ -59,9 +59,9 @@ _SIGS = {
     "savqa_gattn_bwd_flash": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
                               c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p,
                               c_p, c_i64, c_p, c_i64, c_p, c_i64],
-    "savqa_rel_bilinear_fwd": [c_p, c_p, c_i32, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p],
-    "savqa_rel_bilinear_bwd": [c_p, c_p, c_i32, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_p,
-                               c_p],
+    "savqa_rel_entries_fwd": [c_p, c_p, c_i32, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p],
+    "savqa_rel_entries_bwd": [c_p, c_p, c_i32, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p,
+                              c_p, c_p],
     "savqa_rel_loss_fwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p, c_p],
     "savqa_rel_macro_fwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p],
     "savqa_rel_macro_bwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p,

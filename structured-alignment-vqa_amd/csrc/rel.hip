@@ -5,10 +5,11 @@
 //   positive [b][k] = [obj_i, obj_j, rel_category, macro_rel_loc, micro_rel_loc], negative
 //   [b][k] = [obj_i, obj_j, rel_category, macro_rel_loc]; macro_rel_loc < 0 = padding.
 // The reference evaluates x_i^T R_r x_j for ALL (b, r, i, j) (an N x #rel x H x H einsum,
-// :393-401) and then gathers the listed entries; here only the listed entries are
-// computed: one workgroup per slot streams R_r once (row l: t_l = R_r[l,:] . x_j, the
-// bilinear value is sum_l x_i[l] t_l), and the backward streams it once more for
-// dx_i (+= g t), dx_j (+= g R_r^T x_i) and dR_r (+= g x_i x_j^T, atomics).
+// :393-401, materialising R repeated N times) and then gathers the listed entries. Here
+// the caller runs ONE MFMA GEMM V = X_all Rmat^T (X_all = the batch's object rows,
+// Rmat = R viewed as [nrel*H][H]: V[(b,j)][r*H+l] = (R_r x_j)_l), every listed entry is a
+// contiguous 4*H-byte dot (rel_entries_*), and the backward is the entries' scatter into
+// dV plus two more GEMMs (dR += dV^T X_all, dX_all += dV Rmat).
 // The scalar chain (two logsumexps over the batch's positives / negatives, the softmax
 // over the positives, :405-420) and the ordered macro-node update (:418-436: zero the
 // relation nodes, then add softmax[micro_rel_loc] * rel_feature[micro_rel_loc] entry by
@@ -27,75 +28,52 @@ __device__ __forceinline__ bool slot_valid(const RelSlots& s, int slot) {
   return s.loc[(int64_t)slot * s.W + 3] >= 0;
 }
 
-// val[slot] = x_i^T R_r x_j (0 for padding slots). Block = 256 threads; waves walk rows l.
-__global__ __launch_bounds__(256) void rel_bilinear_fwd_kernel(RelSlots s, const float* __restrict__ obj,
-                                                              int Nv, int H,
-                                                              const float* __restrict__ R,
-                                                              float* __restrict__ val) {
-  __shared__ float part[4];
-  const int slot = blockIdx.x;
+// Bilinear entries through the dense product V = X R^T-stacked (csrc: a GEMM by the caller):
+//   V[(b,j)][r*H + l] = sum_k obj[b,j][k] R[r][l][k] = (R_r x_j)_l,  ldv = nrel*H
+// so an entry is one contiguous dot: val = sum_l x_i[l] V[(b,j)][r*H + l]. One wave per slot.
+__global__ __launch_bounds__(256) void rel_entries_fwd_kernel(RelSlots s, const float* __restrict__ obj,
+                                                             int Nv, int H,
+                                                             const float* __restrict__ V,
+                                                             int64_t ldv, float* __restrict__ val) {
+  const int lane = threadIdx.x & 63;
+  const int slot = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (slot >= s.B * s.L) return;
   const int64_t* lr = s.loc + (int64_t)slot * s.W;
   if (lr[3] < 0) {
-    if (threadIdx.x == 0) val[slot] = 0.f;
+    if (lane == 0) val[slot] = 0.f;
     return;
   }
   const int b = slot / s.L;
   const float* xi = obj + ((int64_t)b * Nv + lr[0]) * H;
-  const float* xj = obj + ((int64_t)b * Nv + lr[1]) * H;
-  const float* Rr = R + lr[2] * (int64_t)H * H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float* vr = V + ((int64_t)b * Nv + lr[1]) * ldv + lr[2] * (int64_t)H;
   float acc = 0.f;
-  for (int l = w; l < H; l += 4) {
-    const float* row = Rr + (int64_t)l * H;
-    float t = 0.f;
-    for (int k = lane; k < H; k += 64) t += row[k] * xj[k];
-    acc += xi[l] * t;  // lane partials of t_l, scaled: summed over lanes below
-  }
+  for (int l = lane; l < H; l += 64) acc += xi[l] * vr[l];
   acc = wave_sum(acc);
-  if (lane == 0) part[w] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) val[slot] = (part[0] + part[1]) + (part[2] + part[3]);
+  if (lane == 0) val[slot] = acc;
 }
 
-// backward of one slot with upstream g = dval[slot]
-__global__ __launch_bounds__(256) void rel_bilinear_bwd_kernel(RelSlots s, const float* __restrict__ obj,
-                                                              int Nv, int H,
-                                                              const float* __restrict__ R,
-                                                              const float* __restrict__ dval,
-                                                              float* __restrict__ dobj,
-                                                              float* __restrict__ dR) {
-  extern __shared__ float sx[];  // [4][H] per-wave partials of R^T x_i
-  const int slot = blockIdx.x;
+// backward of one entry with g = dval[slot]: dobj[b,i] += g V[(b,j)][rH:], dV[(b,j)][rH:] += g x_i
+__global__ __launch_bounds__(256) void rel_entries_bwd_kernel(RelSlots s, const float* __restrict__ obj,
+                                                             int Nv, int H,
+                                                             const float* __restrict__ V,
+                                                             int64_t ldv,
+                                                             const float* __restrict__ dval,
+                                                             float* __restrict__ dobj,
+                                                             float* __restrict__ dV) {
+  const int lane = threadIdx.x & 63;
+  const int slot = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (slot >= s.B * s.L) return;
   const int64_t* lr = s.loc + (int64_t)slot * s.W;
   if (lr[3] < 0) return;
   const float g = dval[slot];
   if (g == 0.f) return;
   const int b = slot / s.L;
-  const int64_t ri = (int64_t)b * Nv + lr[0], rj = (int64_t)b * Nv + lr[1];
+  const int64_t ri = (int64_t)b * Nv + lr[0];
   const float* xi = obj + ri * H;
-  const float* xj = obj + rj * H;
-  const float* Rr = R + lr[2] * (int64_t)H * H;
-  float* dRr = dR ? dR + lr[2] * (int64_t)H * H : nullptr;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int k = threadIdx.x; k < 4 * H; k += blockDim.x) sx[k] = 0.f;
-  __syncthreads();
-  for (int l = w; l < H; l += 4) {
-    const float* row = Rr + (int64_t)l * H;
-    const float xil = xi[l];
-    float t = 0.f;
-    for (int k = lane; k < H; k += 64) {
-      const float rv = row[k];
-      t += rv * xj[k];
-      sx[w * H + k] += xil * rv;  // this wave's (R^T x_i)_k partial
-      if (dRr) atomicAdd(&dRr[(int64_t)l * H + k], g * xil * xj[k]);
-    }
-    t = wave_sum(t);
-    if (lane == 0) atomicAdd(&dobj[ri * H + l], g * t);
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < H; k += blockDim.x) {
-    const float v = (sx[k] + sx[H + k]) + (sx[2 * H + k] + sx[3 * H + k]);
-    atomicAdd(&dobj[rj * H + k], g * v);
+  const int64_t vo = ((int64_t)b * Nv + lr[1]) * ldv + lr[2] * (int64_t)H;
+  for (int l = lane; l < H; l += 64) {
+    atomicAdd(&dobj[ri * H + l], g * V[vo + l]);
+    atomicAdd(&dV[vo + l], g * xi[l]);
   }
 }
 
@@ -292,29 +270,27 @@ static int rel_check(const RelSlots& s, const char* who) {
   return 0;
 }
 
-extern "C" int savqa_rel_bilinear_fwd(void* stream, const int64_t* loc, int32_t loc_w, int64_t B,
-                                      int64_t L, const float* obj, int64_t Nv, int64_t H,
-                                      const float* R, float* val) {
+extern "C" int savqa_rel_entries_fwd(void* stream, const int64_t* loc, int32_t loc_w, int64_t B,
+                                     int64_t L, const float* obj, int64_t Nv, int64_t H,
+                                     const float* V, int64_t ldv, float* val) {
   RelSlots s{loc, loc_w, (int)B, (int)L};
   if (B * L == 0) return 0;
-  if (int rc = rel_check(s, "savqa_rel_bilinear_fwd")) return rc;
-  hipLaunchKernelGGL(rel_bilinear_fwd_kernel, dim3((unsigned)(B * L)), dim3(256), 0,
-                     as_stream(stream), s, obj, (int)Nv, (int)H, R, val);
-  return check_launch("savqa_rel_bilinear_fwd");
+  if (int rc = rel_check(s, "savqa_rel_entries_fwd")) return rc;
+  hipLaunchKernelGGL(rel_entries_fwd_kernel, dim3((unsigned)((B * L + 3) / 4)), dim3(256), 0,
+                     as_stream(stream), s, obj, (int)Nv, (int)H, V, ldv, val);
+  return check_launch("savqa_rel_entries_fwd");
 }
 
-extern "C" int savqa_rel_bilinear_bwd(void* stream, const int64_t* loc, int32_t loc_w, int64_t B,
-                                      int64_t L, const float* obj, int64_t Nv, int64_t H,
-                                      const float* R, const float* dval, float* dobj, float* dR) {
+extern "C" int savqa_rel_entries_bwd(void* stream, const int64_t* loc, int32_t loc_w, int64_t B,
+                                     int64_t L, const float* obj, int64_t Nv, int64_t H,
+                                     const float* V, int64_t ldv, const float* dval, float* dobj,
+                                     float* dV) {
   RelSlots s{loc, loc_w, (int)B, (int)L};
   if (B * L == 0) return 0;
-  if (int rc = rel_check(s, "savqa_rel_bilinear_bwd")) return rc;
-  if (4 * H * sizeof(float) > 64 * 1024)
-    return fail(SAVQA_EUNSUP, "savqa_rel_bilinear_bwd: H > 4096");
-  hipLaunchKernelGGL(rel_bilinear_bwd_kernel, dim3((unsigned)(B * L)), dim3(256),
-                     4 * H * sizeof(float), as_stream(stream), s, obj, (int)Nv, (int)H, R, dval, dobj,
-                     dR);
-  return check_launch("savqa_rel_bilinear_bwd");
+  if (int rc = rel_check(s, "savqa_rel_entries_bwd")) return rc;
+  hipLaunchKernelGGL(rel_entries_bwd_kernel, dim3((unsigned)((B * L + 3) / 4)), dim3(256), 0,
+                     as_stream(stream), s, obj, (int)Nv, (int)H, V, ldv, dval, dobj, dV);
+  return check_launch("savqa_rel_entries_bwd");
 }
 
 extern "C" int savqa_rel_loss_fwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp,

@@ -417,14 +417,19 @@ def _rel_forward(W: MilWeights, s: MilSaved, rel, Ns: int, Hm: int, eps: float, 
     r = dict(pos_rel=pos_rel.reshape(-1), pos_loc=pos_loc, neg_loc=neg_loc, Lp=Lp, Ln=Ln)
     relf = _empty(B * Lp, Hm, dev=dev)
     ops.linear(W.E, W.Ws, W.bs, relf, relu=True, a_rows=r["pos_rel"])
+    # V[(b,j)][r*H + l] = (R_r x_j)_l for every object row and category: one GEMM
+    nrel = W.R.shape[0]
+    Rmat = W.R.reshape(nrel * Hm, Hm)
+    V = _empty(B * s.Nv, nrel * Hm, dev=dev)
+    ops.gemm(s.obj, Rmat, V, B * s.Nv, nrel * Hm, Hm, lda=Hm, ldb=Hm, ldc=nrel * Hm, b_trans=True)
     sp, sn = _empty(B * Lp, dev=dev), _empty(B * Ln, dev=dev)
-    ops.rel_bilinear_fwd(pos_loc, B, Lp, s.obj, s.Nv, Hm, W.R, sp)
-    ops.rel_bilinear_fwd(neg_loc, B, Ln, s.obj, s.Nv, Hm, W.R, sn)
+    ops.rel_entries_fwd(pos_loc, B, Lp, s.obj, s.Nv, Hm, V, nrel * Hm, sp)
+    ops.rel_entries_fwd(neg_loc, B, Ln, s.obj, s.Nv, Hm, V, nrel * Hm, sn)
     cidx = torch.empty(max(B * Lp, 1), dtype=torch.int32, device=dev)
     wsm, st = _empty(max(B * Lp, 1), dev=dev), _empty(8, dev=dev)
     ops.rel_loss_fwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cidx, wsm, st, mil_rel_out)
     ops.rel_macro_fwd(pos_loc, B, Lp, cidx, st, wsm, relf, Ns, Hm, s.macro)
-    r.update(relf=relf, sp=sp, sn=sn, cidx=cidx, wsm=wsm, st=st)
+    r.update(relf=relf, sp=sp, sn=sn, cidx=cidx, wsm=wsm, st=st, V=V, nrel=nrel)
     return r
 
 
@@ -458,8 +463,16 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
         dsp, dsn = _empty(B * Lp, dev=dev), _empty(B * Ln, dev=dev)
         ops.rel_loss_bwd(rel["pos_loc"], B, Lp, rel["sp"], rel["neg_loc"], Ln, rel["sn"], eps,
                          rel["cidx"], rel["wsm"], rel["dwsm"], rel["st"], dmil_rel, dsp, dsn)
-        ops.rel_bilinear_bwd(rel["pos_loc"], B, Lp, s.obj, Nv, Hm, W.R, dsp, dobj, G.R)
-        ops.rel_bilinear_bwd(rel["neg_loc"], B, Ln, s.obj, Nv, Hm, W.R, dsn, dobj, G.R)
+        nrel, V = rel["nrel"], rel["V"]
+        dV = torch.zeros_like(V)
+        ops.rel_entries_bwd(rel["pos_loc"], B, Lp, s.obj, Nv, Hm, V, nrel * Hm, dsp, dobj, dV)
+        ops.rel_entries_bwd(rel["neg_loc"], B, Ln, s.obj, Nv, Hm, V, nrel * Hm, dsn, dobj, dV)
+        Rmat, dRmat = W.R.reshape(nrel * Hm, Hm), G.R.reshape(nrel * Hm, Hm)
+        # dR += dV^T X_all ; dX_all += dV Rmat
+        ops.linear_dw(dV, s.obj, dRmat, None, rows=B * Nv)
+        ops.gemm(dV, Rmat, dobj, B * Nv, Hm, nrel * Hm, lda=nrel * Hm, ldb=Hm, ldc=Hm, atomic=True,
+                 split_k=-1)
+        del dV
         drelf = rel["drelf"]
         ops.rowscale_mask(drelf, None, rel["relf"], B * Lp, Hm, drelf)  # ReLU of syb_mlp
         ops.linear_dw(drelf, W.E, G.Ws, G.bs, rows=B * Lp, x_rows=rel["pos_rel"])

@@ -321,14 +321,14 @@ def scatter_rows(g, idx, rows, cols, scale, padding_idx, dtable):
 
 
 # ------------------------------------------------------------------------------ relations
-def rel_bilinear_fwd(loc, B, L, obj, Nv, H, R, val):
-    call("savqa_rel_bilinear_fwd", _stream(), _p(loc), int(loc.shape[-1]), B, L, _p(obj), Nv, H,
-         _p(R), _p(val))
+def rel_entries_fwd(loc, B, L, obj, Nv, H, V, ldv, val):
+    call("savqa_rel_entries_fwd", _stream(), _p(loc), int(loc.shape[-1]), B, L, _p(obj), Nv, H,
+         _p(V), int(ldv), _p(val))
 
 
-def rel_bilinear_bwd(loc, B, L, obj, Nv, H, R, dval, dobj, dR):
-    call("savqa_rel_bilinear_bwd", _stream(), _p(loc), int(loc.shape[-1]), B, L, _p(obj), Nv, H,
-         _p(R), _p(dval), _p(dobj), _p(dR))
+def rel_entries_bwd(loc, B, L, obj, Nv, H, V, ldv, dval, dobj, dV):
+    call("savqa_rel_entries_bwd", _stream(), _p(loc), int(loc.shape[-1]), B, L, _p(obj), Nv, H,
+         _p(V), int(ldv), _p(dval), _p(dobj), _p(dV))
 
 
 def rel_loss_fwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cidx, wsm, st, mil_rel):
