@@ -103,6 +103,12 @@ WORKLOADS = {
                       "master weights / LN / softmax / loss / Adam), 36 regions x 2048-d, "
                       "14 q-tokens, 59 nodes, d=512 h=8 L=6, MIL-NCE only_obj topN=5 H=1024, "
                       "914 classes, decMask"),
+    "rel": dict(d=512, H=8, Nv=36, Ns=36 + 4 + 36 * 35, batch=4, rel=True, maxlen=1600,
+                desc="relation mode (only_obj=False, submit.py:76 'with relations'): model_v=3 "
+                     "train step, fp32, 36 regions, super-node graph of 1300 nodes (36 objects, "
+                     "4 attributes, 1260 relation nodes: T_syb=1314), 31,500 positive + 31,500 "
+                     "negative relation entries per sample, 311 relation categories (R: "
+                     "311x1024x1024), d=512 h=8 L=6, H_mil=1024, topN=5, decMask"),
     "cfg4": dict(d=1024, H=16, Nv=100, Ns=435, batch=32,
                  desc="cfg4: model_v=3 train step, fp32, 100 regions x 2048-d, 14 q-tokens, "
                       "435-node scene graph (T_vis=114, T_syb=449), d=1024 h=16 (h=12 does not "
@@ -168,8 +174,9 @@ def main():
     W = WORKLOADS[args.workload]
     B = args.batch or W["batch"]
     d, H, Nv, Ns = W["d"], W["H"], W["Nv"], W["Ns"]
-    model = AttModel(None, d, 1024, 914, 40, 450, 49, 6, H, args.dropout, 0.1, 311, True,
-                     device=dev, init=False, gemm_precision=W.get("prec", "fp32"))
+    model = AttModel(None, d, 1024, 914, 40, W.get("maxlen", 450), 49, 6, H, args.dropout, 0.1, 311,
+                     not W.get("rel", False), device=dev, init=False,
+                     gemm_precision=W.get("prec", "fp32"))
     init_params_(model, seed=0)  # identical on every rank (same seed), like a broadcast
     model.train()
     if args.serial:
@@ -178,14 +185,20 @@ def main():
     reducer = GradReducer(model._arena) if world > 1 else None
     if reducer:
         model.attach_reducer(reducer)
-    batch = synthetic_batch(B, Nv=Nv, Ns=Ns, seed=1234 + rank, device=dev)
-    margs = model_args(batch)
+    if W.get("rel"):
+        from savqa_amd.data import model_args_rel, synthetic_relation_batch
+        batch = synthetic_relation_batch(B, Nv=Nv, seed=1234 + rank, device=dev)
+        margs = model_args_rel(batch)
+    else:
+        batch = synthetic_batch(B, Nv=Nv, Ns=Ns, seed=1234 + rank, device=dev)
+        margs = model_args(batch)
 
     def step():
         if reducer:
             reducer.begin()
-        lc, lv, ls, mil, _ = model(*margs, decMask=True, mcb=False)
-        loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil, with_milnce=True)
+        lc, lv, ls, mil, mil_rel = model(*margs, decMask=True, mcb=False)
+        loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil, with_milnce=True,
+                                mil_nce_rel=mil_rel)
         opt.zero_grad()
         loss.backward()
         opt.step(reducer=reducer)

@@ -192,24 +192,26 @@ int savqa_rel_entries_bwd(void* stream, const int64_t* loc, int32_t loc_w, int64
                           const float* obj, int64_t Nv, int64_t H, const float* V, int64_t ldv,
                           const float* dval, float* dobj, float* dV);
 /* mil_rel = LSE(max(sp,eps)) - LSE(max(sp,eps) ++ max(sn,eps)) over valid entries (:405-406);
- * cidx[c] = slot of the c-th valid positive (b-major), wsm = softmax over them (:420),
- * st[0..4] = (P, m1, Z1, m2, Z2) for the backward. One workgroup. */
+ * valid entries must be a prefix of each sample's slots (collate pads the tail); cum[b] =
+ * valid positives of samples < b (int32 [B+1]); wsm[cum[b]+k] = softmax over the batch's
+ * valid positives (:420); st (16 floats) = (P, m1, Z1, m2, Z2, err, mr, Zr, ...) for the
+ * backward; err = 1 and mil_rel = NaN if the prefix layout is violated. */
 int savqa_rel_loss_fwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp, const float* sp,
-                       const int64_t* neg_loc, int64_t Ln, const float* sn, float eps, int32_t* cidx,
+                       const int64_t* neg_loc, int64_t Ln, const float* sn, float eps, int32_t* cum,
                        float* wsm, float* st, float* mil_rel);
-/* macro[b, loc3] = 0 for valid positives, then in order += wsm[loc4] * relf[b, loc4] (:418-436) */
-int savqa_rel_macro_fwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp,
-                        const int32_t* cidx, const float* st, const float* wsm, const float* relf,
-                        int64_t Ns, int64_t H, float* macro);
+/* macro[b, loc3] = sum over the node's (consecutive) entries, in order, of
+ * wsm[loc4] * relf[b, loc4]  (:418-436: zero, then the reference's accumulation loop) */
+int savqa_rel_macro_fwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp, const float* st,
+                        const float* wsm, const float* relf, int64_t Ns, int64_t H, float* macro);
 /* backward of the update: dwsm[loc4] += dmacro[b,loc3].relf[b,loc4], drelf[b,loc4] +=
  * wsm[loc4] dmacro[b,loc3] (both zero-initialised by the caller), then dmacro rows loc3 := 0 */
-int savqa_rel_macro_bwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp,
-                        const int32_t* cidx, const float* st, const float* wsm, const float* relf,
-                        int64_t Ns, int64_t H, float* dmacro, float* dwsm, float* drelf);
+int savqa_rel_macro_bwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp, const float* st,
+                        const float* wsm, const float* relf, int64_t Ns, int64_t H, float* dmacro,
+                        float* dwsm, float* drelf);
 /* dsp / dsn per slot from dmil (device scalar) through both logsumexps and the softmax path */
 int savqa_rel_loss_bwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp, const float* sp,
                        const int64_t* neg_loc, int64_t Ln, const float* sn, float eps,
-                       const int32_t* cidx, const float* wsm, const float* dwsm, const float* st,
+                       const int32_t* cum, const float* wsm, const float* dwsm, float* st,
                        const float* dmil, float* dsp, float* dsn);
 
 /* out = a*x + b*y over n floats (combining the MIL-NCE terms of the loss) */

@@ -63,9 +63,8 @@ _SIGS = {
     "savqa_rel_entries_bwd": [c_p, c_p, c_i32, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p,
                               c_p, c_p],
     "savqa_rel_loss_fwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p, c_p],
-    "savqa_rel_macro_fwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p],
-    "savqa_rel_macro_bwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p,
-                            c_p],
+    "savqa_rel_macro_fwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_i64, c_p],
+    "savqa_rel_macro_bwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p],
     "savqa_rel_loss_bwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p, c_p,
                            c_p, c_p, c_p],
     "savqa_axpby": [c_p, c_p, c_p, c_i64, c_f, c_f, c_p],

@@ -77,125 +77,168 @@ __global__ __launch_bounds__(256) void rel_entries_bwd_kernel(RelSlots s, const 
   }
 }
 
-// Scalar chain, one workgroup. Writes: cidx[c] = slot of the c-th valid positive (the
-// reference's nonzero() order: b-major, then k), wsm[c] = softmax over the valid positives
-// (:420), st[0..5] = (P, m1, Z1, m2, Z2, mx/Zsm packed below), mil_rel.
-//   mil_rel = LSE_c(max(sp_c, eps)) - LSE(max(sp, eps) ++ max(sn, eps))   (:405-406)
-__global__ __launch_bounds__(256) void rel_loss_fwd_kernel(RelSlots sp_s, const float* __restrict__ sp,
-                                                          RelSlots sn_s, const float* __restrict__ sn,
-                                                          float eps, int* __restrict__ cidx,
-                                                          float* __restrict__ wsm,
-                                                          float* __restrict__ st,
-                                                          float* __restrict__ mil_rel) {
-  __shared__ float red[4];
-  __shared__ int count;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int S = sp_s.B * sp_s.L, Sn = sn_s.B * sn_s.L;
-  if (tid == 0) {  // ordered compaction (S is small: slots = B x max_rel_len)
-    int c = 0;
-    for (int slot = 0; slot < S; ++slot)
-      if (slot_valid(sp_s, slot)) cidx[c++] = slot;
-    count = c;
-  }
+// Scalar chain (:405-420). Valid entries of a sample must be a prefix of its slots (the
+// collate fills rows from 0 and pads the tail, :445-449), so the reference's nonzero()
+// order gives the c-th valid positive as slot (b, c - cum[b]): no compaction pass is
+// needed. One 1024-thread workgroup:
+//   cum[b] = valid positives of samples < b; wsm[cum[b] + k] = softmax over all valid
+//   positives (:420); st = (P, m1, Z1, m2, Z2, err, mr, Zr) with
+//   mil_rel = (m1 + log Z1) - (m2 + log Z2)  the two clamped logsumexps (:405-406);
+//   err = 1 (and mil_rel = NaN) if some sample's valid slots are not a prefix.
+constexpr int REL_LOSS_NT = 1024;
+constexpr int REL_MAXB = 64;
+
+__device__ __forceinline__ float blk_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_max(v);
+  if (lane == 0) red[w] = v;
   __syncthreads();
-  const int P = count;
-  auto block_max = [&](float v) {
-    v = wave_max(v);
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    const float r = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    __syncthreads();
-    return r;
-  };
-  auto block_sum = [&](float v) {
-    v = wave_sum(v);
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    const float r = (red[0] + red[1]) + (red[2] + red[3]);
-    __syncthreads();
-    return r;
-  };
-  // LSE over clamped positives, and over clamped positives ++ clamped negatives
-  float m1 = -INFINITY, mn = -INFINITY, mr = -INFINITY;
-  for (int c = tid; c < P; c += blockDim.x) {
-    m1 = fmaxf(m1, fmaxf(sp[cidx[c]], eps));
-    mr = fmaxf(mr, sp[cidx[c]]);
+  float r = red[0];
+  for (int k = 1; k < (int)(blockDim.x >> 6); ++k) r = fmaxf(r, red[k]);
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ float blk_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_sum(v);
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) r += red[k];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(REL_LOSS_NT) void rel_loss_fwd_kernel(
+    RelSlots sp_s, const float* __restrict__ sp, RelSlots sn_s, const float* __restrict__ sn,
+    float eps, int* __restrict__ cum, float* __restrict__ wsm, float* __restrict__ st,
+    float* __restrict__ mil_rel) {
+  __shared__ float red[REL_LOSS_NT / 64];
+  __shared__ int cnt[REL_MAXB], kmax[REL_MAXB], cs[REL_MAXB + 1];
+  const int tid = threadIdx.x;
+  const int B = sp_s.B, L = sp_s.L, S = B * L, Sn = sn_s.B * sn_s.L;
+  for (int b = tid; b < B; b += blockDim.x) cnt[b] = kmax[b] = 0;
+  __syncthreads();
+  float m1 = -INFINITY, mr = -INFINITY, mn = -INFINITY;
+  for (int slot = tid; slot < S; slot += blockDim.x) {
+    if (slot_valid(sp_s, slot)) {
+      const int b = slot / L, k = slot - b * L;
+      atomicAdd(&cnt[b], 1);
+      atomicMax(&kmax[b], k + 1);
+      const float v = sp[slot];
+      m1 = fmaxf(m1, fmaxf(v, eps));
+      mr = fmaxf(mr, v);
+    }
   }
   for (int slot = tid; slot < Sn; slot += blockDim.x)
     if (slot_valid(sn_s, slot)) mn = fmaxf(mn, fmaxf(sn[slot], eps));
-  m1 = block_max(m1);
-  mr = block_max(mr);
-  const float m2 = fmaxf(m1, block_max(mn));
+  m1 = blk_max(m1, red);  // (its barriers also publish cnt / kmax)
+  mr = blk_max(mr, red);
+  const float m2 = fmaxf(m1, blk_max(mn, red));
+  if (tid == 0) {
+    int c = 0, err = 0;
+    for (int b = 0; b < B; ++b) {
+      cs[b] = c;
+      c += cnt[b];
+      err |= kmax[b] != cnt[b];
+    }
+    cs[B] = c;
+    st[5] = (float)err;
+  }
+  __syncthreads();
   float z1 = 0.f, z2 = 0.f, zr = 0.f;
-  for (int c = tid; c < P; c += blockDim.x) {
-    const float v = fmaxf(sp[cidx[c]], eps);
-    z1 += expf(v - m1);
-    z2 += expf(v - m2);
-    zr += expf(sp[cidx[c]] - mr);
+  for (int slot = tid; slot < S; slot += blockDim.x) {
+    if (slot_valid(sp_s, slot)) {
+      const float v = sp[slot], vc = fmaxf(v, eps);
+      z1 += expf(vc - m1);
+      z2 += expf(vc - m2);
+      zr += expf(v - mr);
+    }
   }
   for (int slot = tid; slot < Sn; slot += blockDim.x)
     if (slot_valid(sn_s, slot)) z2 += expf(fmaxf(sn[slot], eps) - m2);
-  z1 = block_sum(z1);
-  z2 = block_sum(z2);
-  zr = block_sum(zr);
-  for (int c = tid; c < P; c += blockDim.x) wsm[c] = expf(sp[cidx[c]] - mr) / zr;
+  z1 = blk_sum(z1, red);
+  z2 = blk_sum(z2, red);
+  zr = blk_sum(zr, red);
+  for (int slot = tid; slot < S; slot += blockDim.x) {
+    if (slot_valid(sp_s, slot)) {
+      const int b = slot / L;
+      wsm[cs[b] + (slot - b * L)] = expf(sp[slot] - mr) / zr;
+    }
+  }
+  for (int b = tid; b <= B; b += blockDim.x) cum[b] = cs[b];
   if (tid == 0) {
+    const int P = cs[B];
     st[0] = (float)P;
     st[1] = m1;
     st[2] = z1;
     st[3] = m2;
     st[4] = z2;
-    *mil_rel = P > 0 ? (m1 + logf(z1)) - (m2 + logf(z2)) : NAN;
+    st[6] = mr;
+    st[7] = zr;
+    *mil_rel = (P > 0 && st[5] == 0.f) ? (m1 + logf(z1)) - (m2 + logf(z2)) : NAN;
   }
 }
 
-// Ordered macro-node update (:418, :421-436): rows macro[b, loc3] of every valid positive
-// are zeroed, then, entry by entry, macro[b, loc3] += wsm[loc4] * relf[b, loc4].
-// One workgroup: threads over columns, entries in the reference's order.
-__global__ __launch_bounds__(256) void rel_macro_fwd_kernel(RelSlots s, const int* __restrict__ cidx,
-                                                           const float* __restrict__ st,
+// Macro-node update (:418-436), one wave per run: the entries of one relation node
+// (same sample, same macro_rel_loc) are consecutive slots (the loader appends a pair's
+// entries together and each pair owns one relation node, :208-237), so the node's row
+// is  0 + w[m4_1] f_1 + w[m4_2] f_2 + ...  accumulated in the reference's order in
+// registers and written once (the zeroing of :418 is the accumulator's initial 0).
+__global__ __launch_bounds__(256) void rel_macro_fwd_kernel(RelSlots s, const float* __restrict__ st,
                                                            const float* __restrict__ wsm,
                                                            const float* __restrict__ relf, int Ns,
                                                            int H, float* __restrict__ macro) {
+  const int lane = threadIdx.x & 63;
+  const int slot = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (slot >= s.B * s.L) return;
+  const int b = slot / s.L, k0 = slot - b * s.L;
+  const int64_t* lr = s.loc + (int64_t)slot * s.W;
+  const int64_t r3 = lr[3];
+  if (r3 < 0) return;
+  if (k0 > 0 && s.loc[(int64_t)(slot - 1) * s.W + 3] == r3) return;  // not a run start
   const int P = (int)st[0];
-  for (int c = 0; c < P; ++c) {
-    const int slot = cidx[c];
-    const int64_t* lr = s.loc + (int64_t)slot * s.W;
-    float* row = macro + ((int64_t)(slot / s.L) * Ns + lr[3]) * H;
-    for (int h = threadIdx.x; h < H; h += blockDim.x) row[h] = 0.f;
+  constexpr int HV = 16;  // columns per lane (H <= 1024)
+  float acc[HV];
+#pragma unroll
+  for (int t = 0; t < HV; ++t) acc[t] = 0.f;
+  for (int k = k0; k < s.L; ++k) {
+    const int64_t* e = s.loc + ((int64_t)b * s.L + k) * s.W;
+    if (e[3] != r3) break;
+    const int64_t m4 = e[4];
+    if (m4 >= P) continue;  // (the reference would index out of range)
+    const float wv = wsm[m4];
+    const float* src = relf + ((int64_t)b * s.L + m4) * H;
+#pragma unroll
+    for (int t = 0; t < HV; ++t) {
+      const int h = lane + 64 * t;
+      if (h < H) acc[t] += wv * src[h];
+    }
   }
-  __syncthreads();
-  for (int c = 0; c < P; ++c) {
-    const int slot = cidx[c];
-    const int64_t* lr = s.loc + (int64_t)slot * s.W;
-    const int b = slot / s.L;
-    float* row = macro + ((int64_t)b * Ns + lr[3]) * H;
-    if (lr[4] >= P) continue;  // (the reference would index out of range)
-    const float wv = wsm[lr[4]];
-    const float* src = relf + ((int64_t)b * s.L + lr[4]) * H;
-    for (int h = threadIdx.x; h < H; h += blockDim.x) row[h] += wv * src[h];
+  float* row = macro + ((int64_t)b * Ns + r3) * H;
+#pragma unroll
+  for (int t = 0; t < HV; ++t) {
+    const int h = lane + 64 * t;
+    if (h < H) row[h] = acc[t];
   }
 }
 
 // Backward of the update, one wave per entry: dwsm[loc4] += dmacro[b,loc3] . relf[b,loc4],
 // drelf[b,loc4] += wsm[loc4] * dmacro[b,loc3]. (The zeroing of the relation rows' previous
 // contents is applied by rel_zero_rows_kernel after this kernel has read dmacro.)
-__global__ __launch_bounds__(256) void rel_macro_bwd_kernel(RelSlots s, const int* __restrict__ cidx,
-                                                           const float* __restrict__ st,
+__global__ __launch_bounds__(256) void rel_macro_bwd_kernel(RelSlots s, const float* __restrict__ st,
                                                            const float* __restrict__ wsm,
                                                            const float* __restrict__ relf, int Ns,
                                                            int H, const float* __restrict__ dmacro,
                                                            float* __restrict__ dwsm,
                                                            float* __restrict__ drelf) {
-  const int P = (int)st[0];
   const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (c >= P) return;
-  const int slot = cidx[c];
+  const int slot = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (slot >= s.B * s.L) return;
   const int64_t* lr = s.loc + (int64_t)slot * s.W;
+  if (lr[3] < 0 || lr[4] >= (int64_t)st[0]) return;
   const int b = slot / s.L;
   const float* drow = dmacro + ((int64_t)b * Ns + lr[3]) * H;
-  if (lr[4] >= P) return;
   const int64_t fr = ((int64_t)b * s.L + lr[4]) * H;
   const float wv = wsm[lr[4]];
   float dot = 0.f;
@@ -207,56 +250,60 @@ __global__ __launch_bounds__(256) void rel_macro_bwd_kernel(RelSlots s, const in
   if (lane == 0) atomicAdd(&dwsm[lr[4]], dot);
 }
 
-__global__ __launch_bounds__(256) void rel_zero_rows_kernel(RelSlots s, const int* __restrict__ cidx,
-                                                           const float* __restrict__ st, int Ns,
-                                                           int H, float* __restrict__ dmacro) {
-  const int P = (int)st[0];
-  for (int c = blockIdx.x; c < P; c += gridDim.x) {
-    const int slot = cidx[c];
-    const int64_t* lr = s.loc + (int64_t)slot * s.W;
-    float* row = dmacro + ((int64_t)(slot / s.L) * Ns + lr[3]) * H;
-    for (int h = threadIdx.x; h < H; h += blockDim.x) row[h] = 0.f;
-  }
+__global__ __launch_bounds__(256) void rel_zero_rows_kernel(RelSlots s, int Ns, int H,
+                                                           float* __restrict__ dmacro) {
+  const int lane = threadIdx.x & 63;
+  const int slot = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (slot >= s.B * s.L) return;
+  const int64_t* lr = s.loc + (int64_t)slot * s.W;
+  if (lr[3] < 0) return;
+  float* row = dmacro + ((int64_t)(slot / s.L) * Ns + lr[3]) * H;
+  for (int h = lane; h < H; h += 64) row[h] = 0.f;
 }
 
-// Scalar-chain backward (one workgroup): dsp / dsn per slot from
-//   d mil_rel (through both clamped logsumexps; clamp passes gradient where x >= eps)
-//   + the softmax path: dsp[cidx[c]] += wsm[c] (dwsm[c] - sum_c' wsm[c'] dwsm[c'])
+// st[8] = sum_c wsm[c] dwsm[c]  (softmax-path adjoint), one workgroup
+__global__ __launch_bounds__(REL_LOSS_NT) void rel_wdot_kernel(const float* __restrict__ wsm,
+                                                              const float* __restrict__ dwsm,
+                                                              float* __restrict__ st) {
+  __shared__ float red[REL_LOSS_NT / 64];
+  const int P = (int)st[0];
+  float t = 0.f;
+  for (int c = threadIdx.x; c < P; c += blockDim.x) t += wsm[c] * dwsm[c];
+  t = blk_sum(t, red);
+  if (threadIdx.x == 0) st[8] = t;
+}
+
+// dsp / dsn per slot (parallel): d mil_rel through both clamped logsumexps (clamp passes
+// gradient where x >= eps) + the softmax path wsm[c] (dwsm[c] - st[8])
 __global__ __launch_bounds__(256) void rel_loss_bwd_kernel(RelSlots sp_s, const float* __restrict__ sp,
                                                           RelSlots sn_s, const float* __restrict__ sn,
-                                                          float eps, const int* __restrict__ cidx,
+                                                          float eps, const int* __restrict__ cum,
                                                           const float* __restrict__ wsm,
                                                           const float* __restrict__ dwsm,
                                                           const float* __restrict__ st,
                                                           const float* __restrict__ dmil,
                                                           float* __restrict__ dsp,
                                                           float* __restrict__ dsn) {
-  __shared__ float red[4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int P = (int)st[0];
-  const float m1 = st[1], z1 = st[2], m2 = st[3], z2 = st[4];
-  const float g = dmil ? *dmil : 0.f;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int S = sp_s.B * sp_s.L, Sn = sn_s.B * sn_s.L;
-  for (int slot = tid; slot < S; slot += blockDim.x) dsp[slot] = 0.f;
-  for (int slot = tid; slot < Sn; slot += blockDim.x) {
+  const float m1 = st[1], z1 = st[2], m2 = st[3], z2 = st[4], wd = st[8];
+  const float g = dmil ? *dmil : 0.f;
+  if (t < S) {
+    const int slot = (int)t;
+    float d = 0.f;
+    if (slot_valid(sp_s, slot)) {
+      const float v = sp[slot];
+      if (v >= eps) d = g * (expf(v - m1) / z1 - expf(v - m2) / z2);
+      const int b = slot / sp_s.L;
+      const int c = cum[b] + (slot - b * sp_s.L);
+      d += wsm[c] * (dwsm[c] - wd);
+    }
+    dsp[slot] = d;
+  } else if (t < S + Sn) {
+    const int slot = (int)(t - S);
     float d = 0.f;
     if (slot_valid(sn_s, slot) && sn[slot] >= eps) d = -g * expf(sn[slot] - m2) / z2;
     dsn[slot] = d;
-  }
-  float t = 0.f;
-  for (int c = tid; c < P; c += blockDim.x) t += wsm[c] * dwsm[c];
-  t = wave_sum(t);
-  if (lane == 0) red[w] = t;
-  __syncthreads();
-  const float wd = (red[0] + red[1]) + (red[2] + red[3]);
-  __syncthreads();  // dsp zeroed before the scattered writes below
-  for (int c = tid; c < P; c += blockDim.x) {
-    const int slot = cidx[c];
-    const float v = sp[slot];
-    float d = 0.f;
-    if (v >= eps) d = g * (expf(v - m1) / z1 - expf(v - m2) / z2);
-    d += wsm[c] * (dwsm[c] - wd);
-    dsp[slot] = d;
   }
 }
 
@@ -295,51 +342,60 @@ extern "C" int savqa_rel_entries_bwd(void* stream, const int64_t* loc, int32_t l
 
 extern "C" int savqa_rel_loss_fwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp,
                                   const float* sp, const int64_t* neg_loc, int64_t Ln,
-                                  const float* sn, float eps, int32_t* cidx, float* wsm, float* st,
+                                  const float* sn, float eps, int32_t* cum, float* wsm, float* st,
                                   float* mil_rel) {
   RelSlots a{pos_loc, 5, (int)B, (int)Lp}, n{neg_loc, 4, (int)B, (int)Ln};
   if (int rc = rel_check(a, "savqa_rel_loss_fwd")) return rc;
   if (int rc = rel_check(n, "savqa_rel_loss_fwd")) return rc;
-  hipLaunchKernelGGL(rel_loss_fwd_kernel, dim3(1), dim3(256), 0, as_stream(stream), a, sp, n, sn, eps,
-                     cidx, wsm, st, mil_rel);
+  if (B > REL_MAXB) return fail(SAVQA_EUNSUP, "savqa_rel_loss_fwd: batch > 64");
+  hipLaunchKernelGGL(rel_loss_fwd_kernel, dim3(1), dim3(REL_LOSS_NT), 0, as_stream(stream), a, sp, n,
+                     sn, eps, cum, wsm, st, mil_rel);
   return check_launch("savqa_rel_loss_fwd");
 }
 
 extern "C" int savqa_rel_macro_fwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp,
-                                   const int32_t* cidx, const float* st, const float* wsm,
-                                   const float* relf, int64_t Ns, int64_t H, float* macro) {
+                                   const float* st, const float* wsm, const float* relf, int64_t Ns,
+                                   int64_t H, float* macro) {
   RelSlots a{pos_loc, 5, (int)B, (int)Lp};
   if (int rc = rel_check(a, "savqa_rel_macro_fwd")) return rc;
-  hipLaunchKernelGGL(rel_macro_fwd_kernel, dim3(1), dim3(256), 0, as_stream(stream), a, cidx, st, wsm,
-                     relf, (int)Ns, (int)H, macro);
+  if (H > 1024) return fail(SAVQA_EUNSUP, "savqa_rel_macro_fwd: H > 1024");
+  const int64_t S = B * Lp;
+  if (S == 0) return 0;
+  hipLaunchKernelGGL(rel_macro_fwd_kernel, dim3((unsigned)((S + 3) / 4)), dim3(256), 0,
+                     as_stream(stream), a, st, wsm, relf, (int)Ns, (int)H, macro);
   return check_launch("savqa_rel_macro_fwd");
 }
 
 extern "C" int savqa_rel_macro_bwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp,
-                                   const int32_t* cidx, const float* st, const float* wsm,
-                                   const float* relf, int64_t Ns, int64_t H, float* dmacro,
-                                   float* dwsm, float* drelf) {
+                                   const float* st, const float* wsm, const float* relf, int64_t Ns,
+                                   int64_t H, float* dmacro, float* dwsm, float* drelf) {
   RelSlots a{pos_loc, 5, (int)B, (int)Lp};
   if (int rc = rel_check(a, "savqa_rel_macro_bwd")) return rc;
   const int64_t S = B * Lp;
   if (S == 0) return 0;
-  hipLaunchKernelGGL(rel_macro_bwd_kernel, dim3((unsigned)((S + 3) / 4)), dim3(256), 0,
-                     as_stream(stream), a, cidx, st, wsm, relf, (int)Ns, (int)H, dmacro, dwsm, drelf);
+  const dim3 g((unsigned)((S + 3) / 4));
+  hipLaunchKernelGGL(rel_macro_bwd_kernel, g, dim3(256), 0, as_stream(stream), a, st, wsm, relf,
+                     (int)Ns, (int)H, dmacro, dwsm, drelf);
   if (int rc = check_launch("savqa_rel_macro_bwd")) return rc;
-  hipLaunchKernelGGL(rel_zero_rows_kernel, dim3(64), dim3(256), 0, as_stream(stream), a, cidx, st,
-                     (int)Ns, (int)H, dmacro);
+  hipLaunchKernelGGL(rel_zero_rows_kernel, g, dim3(256), 0, as_stream(stream), a, (int)Ns, (int)H,
+                     dmacro);
   return check_launch("savqa_rel_macro_bwd(zero)");
 }
 
 extern "C" int savqa_rel_loss_bwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp,
                                   const float* sp, const int64_t* neg_loc, int64_t Ln,
-                                  const float* sn, float eps, const int32_t* cidx, const float* wsm,
-                                  const float* dwsm, const float* st, const float* dmil, float* dsp,
+                                  const float* sn, float eps, const int32_t* cum, const float* wsm,
+                                  const float* dwsm, float* st, const float* dmil, float* dsp,
                                   float* dsn) {
   RelSlots a{pos_loc, 5, (int)B, (int)Lp}, n{neg_loc, 4, (int)B, (int)Ln};
   if (int rc = rel_check(a, "savqa_rel_loss_bwd")) return rc;
   if (int rc = rel_check(n, "savqa_rel_loss_bwd")) return rc;
-  hipLaunchKernelGGL(rel_loss_bwd_kernel, dim3(1), dim3(256), 0, as_stream(stream), a, sp, n, sn, eps,
-                     cidx, wsm, dwsm, st, dmil, dsp, dsn);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(rel_wdot_kernel, dim3(1), dim3(REL_LOSS_NT), 0, s, wsm, dwsm, st);
+  if (int rc = check_launch("savqa_rel_loss_bwd(wdot)")) return rc;
+  const int64_t n_all = B * Lp + B * Ln;
+  if (n_all == 0) return 0;
+  hipLaunchKernelGGL(rel_loss_bwd_kernel, dim3((unsigned)((n_all + 255) / 256)), dim3(256), 0, s, a,
+                     sp, n, sn, eps, cum, wsm, dwsm, st, dmil, dsp, dsn);
   return check_launch("savqa_rel_loss_bwd");
 }

@@ -51,3 +51,57 @@ def model_args(batch):
     B = batch["vis_fea"].shape[0]
     empty = torch.empty((B, 0), device=batch["vis_fea"].device)
     return [batch[k] for k in MODEL_INPUTS] + [empty, empty, empty, empty]
+
+
+REL_INPUTS = ("micro_positive_rel", "micro_negative_rel", "micro_positive_rel_loc",
+              "micro_negative_rel_loc")
+
+
+def model_args_rel(batch):
+    """Positional args of AttModel.forward with the relation tensors (only_obj=False)."""
+    return [batch[k] for k in MODEL_INPUTS] + [batch[k] for k in REL_INPUTS]
+
+
+def synthetic_relation_batch(B: int, Nv: int = 36, Lq: int = 14, topN: int = 5,
+                             num_relations: int = 311, n_attr: int = 4, num_classes: int = 914,
+                             seed: int = 1234, device="cuda"):
+    """Super-node batch with the relation tensors of the relation loader
+    (dataloader/data_loader_itp_bbox_super_node.py:150-252, collate :366-497), synthetic:
+    macro nodes = Nv objects, n_attr attribute nodes, one relation node per ordered object
+    pair (Nv*(Nv-1)); edges obj<->attr and obj_i -> rel(i,j) -> obj_j (:165-206); every pair
+    contributes topN*topN positive entries [i, j, category, macro_rel_loc, running counter]
+    (:215-237) and as many negatives [i, j, category', macro_rel_loc] (:241-246).
+    At Nv = 36: T_syb = 36 + 4 + 1260 + Lq = 1314 tokens, 31,500 entries per sample."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    Ns = Nv + n_attr + Nv * (Nv - 1)
+    pairs = [(i, j) for i in range(Nv) for j in range(Nv) if i != j]
+    K = topN * topN
+    L = len(pairs) * K
+    pi = np.repeat(np.array([p[0] for p in pairs]), K)
+    pj = np.repeat(np.array([p[1] for p in pairs]), K)
+    ploc = np.repeat(Nv + n_attr + np.arange(len(pairs)), K)
+    pos_loc = np.zeros((B, L, 5), np.int64)
+    neg_loc = np.zeros((B, L, 4), np.int64)
+    graph = np.zeros((B, Ns, Ns), np.int32)
+    for b in range(B):
+        cat = rng.integers(0, num_relations, L)
+        ncat = (cat + rng.integers(1, max(num_relations, 2), L)) % max(num_relations, 1)
+        pos_loc[b] = np.stack([pi, pj, cat, ploc, np.arange(L)], 1)
+        neg_loc[b] = np.stack([pi, pj, ncat, ploc], 1)
+        attr = Nv + rng.integers(0, n_attr, Nv)
+        graph[b, np.arange(Nv), attr] = 1
+        graph[b, attr, np.arange(Nv)] = 1
+        q = Nv + n_attr + np.arange(len(pairs))
+        graph[b, [p[0] for p in pairs], q] = 1
+        graph[b, q, [p[1] for p in pairs]] = 1
+    batch = synthetic_batch(B, Nv=Nv, Lq=Lq, Ns=Ns, topN=topN, num_classes=num_classes,
+                            seed=seed, device=device)
+    dev = batch["vis_fea"].device
+    batch["macro_graph"] = torch.from_numpy(graph).to(dev)
+    g = torch.Generator(device=dev).manual_seed(seed + 1)
+    batch["micro_positive_rel"] = torch.randint(0, PAD, (B, L), generator=g, device=dev)
+    batch["micro_negative_rel"] = torch.randint(0, PAD, (B, L), generator=g, device=dev)
+    batch["micro_positive_rel_loc"] = torch.from_numpy(pos_loc).to(dev)
+    batch["micro_negative_rel_loc"] = torch.from_numpy(neg_loc).to(dev)
+    return batch

@@ -425,11 +425,11 @@ def _rel_forward(W: MilWeights, s: MilSaved, rel, Ns: int, Hm: int, eps: float, 
     sp, sn = _empty(B * Lp, dev=dev), _empty(B * Ln, dev=dev)
     ops.rel_entries_fwd(pos_loc, B, Lp, s.obj, s.Nv, Hm, V, nrel * Hm, sp)
     ops.rel_entries_fwd(neg_loc, B, Ln, s.obj, s.Nv, Hm, V, nrel * Hm, sn)
-    cidx = torch.empty(max(B * Lp, 1), dtype=torch.int32, device=dev)
-    wsm, st = _empty(max(B * Lp, 1), dev=dev), _empty(8, dev=dev)
-    ops.rel_loss_fwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cidx, wsm, st, mil_rel_out)
-    ops.rel_macro_fwd(pos_loc, B, Lp, cidx, st, wsm, relf, Ns, Hm, s.macro)
-    r.update(relf=relf, sp=sp, sn=sn, cidx=cidx, wsm=wsm, st=st, V=V, nrel=nrel)
+    cum = torch.empty(B + 1, dtype=torch.int32, device=dev)
+    wsm, st = _empty(max(B * Lp, 1), dev=dev), torch.zeros(16, device=dev)
+    ops.rel_loss_fwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cum, wsm, st, mil_rel_out)
+    ops.rel_macro_fwd(pos_loc, B, Lp, st, wsm, relf, Ns, Hm, s.macro)
+    r.update(relf=relf, sp=sp, sn=sn, cum=cum, wsm=wsm, st=st, V=V, nrel=nrel)
     return r
 
 
@@ -448,8 +448,8 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
             Lp = rel["Lp"]    # and the overwritten previous contents get none
             rel["dwsm"] = torch.zeros(max(B * Lp, 1), device=dev)
             rel["drelf"] = torch.zeros(B * Lp, Hm, device=dev)
-            ops.rel_macro_bwd(rel["pos_loc"], B, Lp, rel["cidx"], rel["st"], rel["wsm"],
-                              rel["relf"], Ns, Hm, dmacro, rel["dwsm"], rel["drelf"])
+            ops.rel_macro_bwd(rel["pos_loc"], B, Lp, rel["st"], rel["wsm"], rel["relf"], Ns, Hm,
+                              dmacro, rel["dwsm"], rel["drelf"])
         dobj = _empty(B * Nv, Hm, dev=dev)
         ops.index_get_rows(s.loc, B, Nv, Ns, Hm, dmacro, dobj)
         del dmacro
@@ -462,7 +462,7 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
             rel["drelf"] = torch.zeros(B * Lp, Hm, device=dev)
         dsp, dsn = _empty(B * Lp, dev=dev), _empty(B * Ln, dev=dev)
         ops.rel_loss_bwd(rel["pos_loc"], B, Lp, rel["sp"], rel["neg_loc"], Ln, rel["sn"], eps,
-                         rel["cidx"], rel["wsm"], rel["dwsm"], rel["st"], dmil_rel, dsp, dsn)
+                         rel["cum"], rel["wsm"], rel["dwsm"], rel["st"], dmil_rel, dsp, dsn)
         nrel, V = rel["nrel"], rel["V"]
         dV = torch.zeros_like(V)
         ops.rel_entries_bwd(rel["pos_loc"], B, Lp, s.obj, Nv, Hm, V, nrel * Hm, dsp, dobj, dV)

@@ -331,24 +331,24 @@ def rel_entries_bwd(loc, B, L, obj, Nv, H, V, ldv, dval, dobj, dV):
          _p(V), int(ldv), _p(dval), _p(dobj), _p(dV))
 
 
-def rel_loss_fwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cidx, wsm, st, mil_rel):
+def rel_loss_fwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cum, wsm, st, mil_rel):
     call("savqa_rel_loss_fwd", _stream(), _p(pos_loc), B, Lp, _p(sp), _p(neg_loc), Ln, _p(sn),
-         float(eps), _p(cidx), _p(wsm), _p(st), _p(mil_rel))
+         float(eps), _p(cum), _p(wsm), _p(st), _p(mil_rel))
 
 
-def rel_macro_fwd(pos_loc, B, Lp, cidx, st, wsm, relf, Ns, H, macro):
-    call("savqa_rel_macro_fwd", _stream(), _p(pos_loc), B, Lp, _p(cidx), _p(st), _p(wsm), _p(relf),
-         Ns, H, _p(macro))
+def rel_macro_fwd(pos_loc, B, Lp, st, wsm, relf, Ns, H, macro):
+    call("savqa_rel_macro_fwd", _stream(), _p(pos_loc), B, Lp, _p(st), _p(wsm), _p(relf), Ns, H,
+         _p(macro))
 
 
-def rel_macro_bwd(pos_loc, B, Lp, cidx, st, wsm, relf, Ns, H, dmacro, dwsm, drelf):
-    call("savqa_rel_macro_bwd", _stream(), _p(pos_loc), B, Lp, _p(cidx), _p(st), _p(wsm),
-         _p(relf), Ns, H, _p(dmacro), _p(dwsm), _p(drelf))
+def rel_macro_bwd(pos_loc, B, Lp, st, wsm, relf, Ns, H, dmacro, dwsm, drelf):
+    call("savqa_rel_macro_bwd", _stream(), _p(pos_loc), B, Lp, _p(st), _p(wsm), _p(relf), Ns, H,
+         _p(dmacro), _p(dwsm), _p(drelf))
 
 
-def rel_loss_bwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cidx, wsm, dwsm, st, dmil, dsp, dsn):
+def rel_loss_bwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cum, wsm, dwsm, st, dmil, dsp, dsn):
     call("savqa_rel_loss_bwd", _stream(), _p(pos_loc), B, Lp, _p(sp), _p(neg_loc), Ln, _p(sn),
-         float(eps), _p(cidx), _p(wsm), _p(dwsm), _p(st), _p(dmil), _p(dsp), _p(dsn))
+         float(eps), _p(cum), _p(wsm), _p(dwsm), _p(st), _p(dmil), _p(dsp), _p(dsn))
 
 
 def axpby(x, y, n, a, b, out):
