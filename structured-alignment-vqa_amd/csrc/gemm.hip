@@ -20,7 +20,8 @@
 //     32 consecutive floats per half-wave in the same permuted k order.
 // Interior tiles run a branch-free loop (row pointers resolved once per block, gathers
 // included); edge tiles, k tails and k-row gathers take a clamped, branch-free guarded
-// loader. One register-staged prefetch, LDS write after the compute (T14), one barrier
+// loader. One register-staged prefetch, LDS write after the barrier (forward, dX) or
+// after the compute (dW) -- see gemm_t14 --, one barrier
 // per k-tile, XCD-aware block order (T1).
 #include "gemm_common.h"
 
@@ -226,6 +227,18 @@ __device__ __forceinline__ void gemm_compute_tile(
   }
 }
 
+// k-loop order. Measured (tools/gemm_bench.py, cfg-2 shapes): storing the staged tile
+// right after the barrier (T14) is +1-4% on the k-contiguous-A layouts (forward, dX) and
+// -1..-4% on dW (A = dY^T, m-contiguous), so dW keeps the store-after-compute order.
+// SAVQA_GEMM_T14=0/2 forces the old / new order everywhere (A/B builds).
+#ifndef SAVQA_GEMM_T14
+#define SAVQA_GEMM_T14 1
+#endif
+template <bool AT>
+__host__ __device__ constexpr bool gemm_t14() {
+  return SAVQA_GEMM_T14 == 2 || (SAVQA_GEMM_T14 == 1 && !AT);
+}
+
 template <int BM, int BN, int BK, bool AT, bool BT, bool FAST>
 __device__ __forceinline__ void gemm_mainloop(
     const savqa_gemm_desc& d, float* smem, int64_t m0, int64_t n0, int64_t kbeg, int64_t kend,
@@ -259,6 +272,25 @@ __device__ __forceinline__ void gemm_mainloop(
   if (do_cs) la.accum(cs);  // colsum_a: the staged A tile summed over its k rows
   la.store(smem, tid);
   lb.store(smem + 2 * OA::SIZE, tid);
+  if constexpr (gemm_t14<AT>()) {
+  // write-after-barrier order: per k-tile  barrier -> store tile t+1 (its loads landed
+  // during compute t-1) -> issue loads of t+2 -> compute t
+  if (ntiles > 1) SAVQA_GEMM_LOAD(kbeg + BK);
+  for (int tt = 0; tt < ntiles; ++tt) {
+    __syncthreads();
+    const int cur = tt & 1;
+    if (tt + 1 < ntiles) {
+      if (do_cs) la.accum(cs);
+      la.store(smem + (cur ^ 1) * OA::SIZE, tid);
+      lb.store(smem + 2 * OA::SIZE + (cur ^ 1) * OB::SIZE, tid);
+      if (tt + 2 < ntiles) SAVQA_GEMM_LOAD(kbeg + (int64_t)(tt + 2) * BK);
+    }
+    gemm_compute_tile<BM, BN, BK, AT, BT>(smem + cur * OA::SIZE,
+                                          smem + 2 * OA::SIZE + cur * OB::SIZE, wm, wn, lane,
+                                          acc);
+  }
+  __syncthreads();  // the caller's epilogue helpers reuse smem
+  } else {
   __syncthreads();
   int cur = 0;
   for (int tt = 0; tt < ntiles; ++tt) {
@@ -274,6 +306,7 @@ __device__ __forceinline__ void gemm_mainloop(
     }
     __syncthreads();
     cur ^= 1;
+  }
   }
 #undef SAVQA_GEMM_LOAD
 }

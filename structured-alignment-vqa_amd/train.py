@@ -24,7 +24,7 @@ import torch
 import torch.distributed as dist
 
 from .AttModel_x3 import AttModel
-from .data import model_args, synthetic_batch
+from .data import model_args, model_args_rel, synthetic_batch, synthetic_relation_batch
 from .ddp import GradReducer
 from .loss import smoothed_loss
 from .optim import Adam
@@ -65,6 +65,14 @@ def build_parser():
     return p
 
 
+def run_model(model, batch, args):
+    """main:318-329: forward + the MIL-NCE terms the loss subtracts (relation term only
+    when only_obj is off)."""
+    inputs = model_args(batch) if args.only_obj else model_args_rel(batch)
+    lc, lv, ls, mil, mil_rel = model(*inputs, decMask=args.decMask, mcb=args.mcb)
+    return lc, lv, ls, mil, (None if args.only_obj else mil_rel)
+
+
 def evaluate(model, batches, with_mil, rank, args):
     """main:42-142: loss meter + accuracy over non-zero answers."""
     model.eval()
@@ -73,8 +81,9 @@ def evaluate(model, batches, with_mil, rank, args):
     correct = torch.zeros_like(cnt)
     with torch.no_grad():
         for batch in batches:
-            lc, lv, ls, mil, _ = model(*model_args(batch), decMask=args.decMask, mcb=args.mcb)
-            loss, lsm = smoothed_loss(lc, lv, ls, batch["answer"], mil, with_milnce=with_mil)
+            lc, lv, ls, mil, mil_rel = run_model(model, batch, args)
+            loss, lsm = smoothed_loss(lc, lv, ls, batch["answer"], mil, with_milnce=with_mil,
+                                      mil_nce_rel=mil_rel)
             meter.update(float(loss), batch["answer"].shape[0])
             valid = batch["answer"] != 0
             correct += ((lsm.argmax(-1) == batch["answer"]) & valid).sum()
@@ -105,26 +114,35 @@ def main(gpu_rank, args):
     if reducer:
         model.attach_reducer(reducer)
     loss_meter, mil_meter = AverageMeter(), AverageMeter()
+    result = {}
 
     def batches(seed0):
         for i in range(args.steps_per_epoch):
-            yield synthetic_batch(args.batch_size, Nv=args.num_regions, Lq=args.q_len,
-                                  Ns=args.num_nodes_sg, topN=args.topN,
-                                  num_classes=args.num_classes, seed=seed0 + i, device=dev)
+            if args.only_obj:
+                yield synthetic_batch(args.batch_size, Nv=args.num_regions, Lq=args.q_len,
+                                      Ns=args.num_nodes_sg, topN=args.topN,
+                                      num_classes=args.num_classes, seed=seed0 + i, device=dev)
+            else:  # super-node batches with the relation tensors (relation loader)
+                yield synthetic_relation_batch(args.batch_size, Nv=args.num_regions,
+                                               Lq=args.q_len, topN=args.topN,
+                                               num_relations=args.num_relations,
+                                               num_classes=args.num_classes, seed=seed0 + i,
+                                               device=dev)
 
     for epoch in range(args.num_epochs):
         for i, batch in enumerate(batches(1000 * epoch + 7919 * rank)):
             if reducer:
                 reducer.begin()
-            lc, lv, ls, mil, _ = model(*model_args(batch), decMask=args.decMask, mcb=args.mcb)
+            lc, lv, ls, mil, mil_rel = run_model(model, batch, args)
             opt.zero_grad()
             loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil,
-                                    with_milnce=args.with_MILNCE_loss)
+                                    with_milnce=args.with_MILNCE_loss, mil_nce_rel=mil_rel)
             loss.backward()
             opt.step(reducer=reducer)
             if (i + 1) % args.log_steps == 0 or i + 1 == args.steps_per_epoch:
                 loss_meter.update(float(loss), batch["answer"].shape[0])
-                mil_meter.update(-float(mil), batch["answer"].shape[0])
+                mil_meter.update(-float(mil) - (float(mil_rel) if mil_rel is not None else 0.0),
+                                 batch["answer"].shape[0])
                 if rank == 0:
                     logging.info('Time %s, Epoch [%d/%d], Step [%d/%d], Loss: %.5f, MIL NCE Loss: %.5f, '
                                  'Avg Loss: %.5f', datetime.datetime.now(), epoch + 1, args.num_epochs,
@@ -139,6 +157,8 @@ def main(gpu_rank, args):
             vals = vals.unsqueeze(0)
         if rank == 0:
             acc = float(vals[:, 1].sum()) / max(float(vals[:, 2].sum()), 1.0)
+            result = {"epoch": epoch + 1, "train_loss": loss_meter.avg,
+                      "val_loss": float(vals[:, 0].mean()), "accuracy": acc}
             logging.info('Epoch [%d/%d], Val Loss: %.5f, accuracy: %.4f', epoch + 1, args.num_epochs,
                          float(vals[:, 0].mean()), acc)
             out = os.path.join(args.data_dir_azure, args.output_dir)
@@ -148,14 +168,14 @@ def main(gpu_rank, args):
                        os.path.join(out, f'model_{epoch + 1}.pth'))
     if args.world_size > 1:
         dist.destroy_process_group()
+    return result
 
 
 def cli(argv=None):
     args = build_parser().parse_args(argv)
     if "WORLD_SIZE" in os.environ:  # torchrun
         args.world_size = int(os.environ["WORLD_SIZE"])
-        main(int(os.environ.get("LOCAL_RANK", 0)), args)
-        return
+        return main(int(os.environ.get("LOCAL_RANK", 0)), args)
     if args.ngpus == -1:
         args.ngpus = torch.cuda.device_count()
     args.world_size = args.ngpus * args.num_nodes
@@ -163,7 +183,7 @@ def cli(argv=None):
     os.environ.setdefault('MASTER_PORT', '7787')
     if args.local_debug or args.world_size <= 1:
         args.world_size = 1
-        main(0, args)
+        return main(0, args)
     else:
         os.environ['WORLD_SIZE'] = str(args.world_size)
         import torch.multiprocessing as mp
