@@ -315,6 +315,41 @@ int savqa_adam(void* stream, float* p, const float* g, float* m, float* v, int64
                float lr, float beta1, float beta2, float eps, float bc1, float bc2,
                float grad_scale);
 
+/* ------------------------------------------------------------------------
+ * Batch collation. Replaces the host-side padding of
+ * collate_fn (models/data_loader_itp_bbox_super_node_onlyobj.py:341-445;
+ * dataloader/data_loader_itp_bbox_super_node.py:366-497): the host packs each
+ * field's per-sample arrays back to back with per-sample row offsets off[B+1]
+ * (n_b = off[b+1] - off[b]); one launch expands every field into its dense
+ * [B][T][row_elems] tensor:
+ *   ROWS : dst[b][t][:] = t < n_b ? src row (off[b] + t) : fill  (elem_bytes 4|8;
+ *          fill = the element's bit pattern: PAD, LOC_PAD, 0)
+ *   BOX  : int32 dst[b][t][c] = t < n_b && (!square || c < n_b)   (the masks)
+ *   FILL : dst = fill                                              (graphs, before edges)
+ * `fields` is a HOST array (copied into the kernel arguments); every pointer inside
+ * it is a device pointer. savqa_collate_edges then sets graph[b][i][j] = 1 for
+ * every (i, j) of sample b (edges int32 [E][2], already in [0, T); edge_off[B+1]).
+ * ------------------------------------------------------------------------ */
+#define SAVQA_COLLATE_MAX_FIELDS 24
+#define SAVQA_COLLATE_ROWS 0
+#define SAVQA_COLLATE_BOX 1
+#define SAVQA_COLLATE_FILL 2
+typedef struct savqa_collate_field {
+  int32_t kind;
+  int32_t elem_bytes;
+  int32_t square;
+  int32_t reserved;
+  int64_t T;
+  int64_t row_elems;
+  uint64_t fill;
+  const void* src;
+  const int64_t* off;
+  void* dst;
+} savqa_collate_field;
+int savqa_collate(void* stream, const savqa_collate_field* fields, int32_t nfields, int64_t B);
+int savqa_collate_edges(void* stream, const int32_t* edges, const int64_t* edge_off, int64_t B,
+                        int64_t E, int64_t T, int32_t* graph);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,15 @@ class GemmDesc(C.Structure):
     ]
 
 
+class CollateField(C.Structure):
+    """savqa_collate_field (include/savqa.h)."""
+    _fields_ = [
+        ("kind", c_i32), ("elem_bytes", c_i32), ("square", c_i32), ("reserved", c_i32),
+        ("T", c_i64), ("row_elems", c_i64), ("fill", C.c_uint64),
+        ("src", c_p), ("off", c_p), ("dst", c_p),
+    ]
+
+
 # name -> argtypes (restype is always int except savqa_last_error)
 _SIGS = {
     "savqa_version": [],
@@ -68,6 +77,8 @@ _SIGS = {
     "savqa_rel_loss_bwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p, c_p,
                            c_p, c_p, c_p],
     "savqa_axpby": [c_p, c_p, c_p, c_i64, c_f, c_f, c_p],
+    "savqa_collate": [c_p, C.POINTER(CollateField), c_i32, c_i64],
+    "savqa_collate_edges": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p],
     "savqa_graph_build": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p],
     "savqa_dec_init": [c_p, c_p, c_i64, c_f, c_p, c_i64, c_i64, c_u64, c_i32, c_f, c_p],
     "savqa_dec_init_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_f, c_u64, c_i32, c_f, c_p, c_p],

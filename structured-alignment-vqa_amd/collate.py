@@ -1,0 +1,288 @@
+"""Batch collation with the padding done on the device.
+
+Mirror of the reference's collate_fn
+  models/data_loader_itp_bbox_super_node_onlyobj.py:341-445      (only_obj loader)
+  dataloader/data_loader_itp_bbox_super_node.py:366-497          (relation loader)
+with the same input (a list of per-sample tuples from Dataset.__getitem__, None
+entries dropped) and the same output dict (keys, dtypes, shapes, values), split in two:
+
+  pack(data)        host side, usable as DataLoader(collate_fn=pack) in worker
+                    processes: validates the samples with numpy's own indexing rules
+                    and copies each field's per-sample arrays back to back into ONE
+                    uint8 staging tensor (+ per-sample row offsets). No padding, no
+                    dense (B,T,T) masks: the staging holds the ragged data only.
+  to_device(pk)     one H2D copy of the staging tensor, then savqa_collate (every padded
+                    field + the masks, one launch) and savqa_collate_edges (graphs).
+
+`collate_fn(data)` = to_device(pack(data)). There is no host fallback: without the
+HIP library / a device, to_device raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import CollateField, call
+
+PAD = 400000   # onlyobj:34
+LOC_PAD = -1   # onlyobj:39
+_ALIGN = 256
+ROWS, BOX, FILL = 0, 1, 2
+
+OBJ_FIELDS = ("vis_fea", "macro_nodes_idx", "macro_obj_locs", "macro_edges",
+              "micro_positive_nodes_wrd", "micro_negative_nodes_wrd")
+REL_FIELDS = ("micro_positive_relations_wrd", "micro_negative_relations_wrd",
+              "micro_positive_relations_loc", "micro_negative_relations_loc")
+TAIL_FIELDS = ("qnode_idx", "qedge", "answer", "topN")
+
+# AttModel.forward positional order (main_itp_ddp_tar_super_node.py:321-325)
+FORWARD_KEYS = ("vis_fea", "vis_fea_mask", "q_ipt", "q_ipt_mask", "q_ipt_graph",
+                "macro_node_ipt", "macro_node_mask", "macro_graph_ipt", "macro_obj_loc_ipt",
+                "micro_positive_obj_ipt", "micro_negative_obj_ipt", "micro_obj_mask",
+                "micro_positive_rel_ipt", "micro_negative_rel_ipt", "micro_positive_rel_loc",
+                "micro_negative_rel_loc")
+
+# collate_fn's output keys, in its order (onlyobj:414-444, super_node:466-496)
+OUTPUT_KEYS = ("vis_fea", "vis_fea_mask", "macro_node_ipt", "macro_graph_ipt", "macro_node_mask",
+               "macro_obj_loc_ipt", "micro_positive_obj_ipt", "micro_negative_obj_ipt",
+               "micro_obj_mask", "micro_positive_rel_ipt", "micro_negative_rel_ipt",
+               "micro_positive_rel_loc", "micro_negative_rel_loc", "q_ipt", "q_ipt_mask",
+               "q_ipt_graph", "answer")
+
+_NP = {torch.float32: np.float32, torch.int64: np.int64, torch.int32: np.int32}
+
+
+def _bits(value, dtype) -> int:
+    return int(np.array([value], dtype=_NP[dtype]).view(
+        np.uint64 if _NP[dtype] == np.int64 else np.uint32)[0])
+
+
+def _edges(edge, T: int, skip_empty: bool) -> Optional[np.ndarray]:
+    """Edge list of one sample as int32 [E][2] in [0, T), with the reference's rules:
+    np.asarray(edge).astype('int32'), macro lists: empty skipped and a flat pair promoted
+    (onlyobj:397-401); graph[row, e[:,0], e[:,1]] = 1 -> numpy index semantics (negative
+    indices wrap once, anything outside [-T, T) raises IndexError, extra columns unused)."""
+    e = np.asarray(edge).astype("int32")
+    if skip_empty:
+        if e.size == 0:
+            return None
+        if len(e.shape) == 1:
+            e = e[np.newaxis, :]
+    if e.ndim != 2 or e.shape[1] < 2:
+        raise IndexError(f"edge list of shape {e.shape}: too many indices for array")
+    e = e[:, :2].astype(np.int64)
+    if e.size and (e.min() < -T or e.max() >= T):
+        raise IndexError(f"edge index out of bounds for graph of size {T}")
+    e = np.where(e < 0, e + T, e)
+    return e.astype(np.int32)
+
+
+class PackedBatch:
+    """Ragged batch in one staging tensor + the plan that expands it on the device."""
+
+    def __init__(self, B, relations, staging, fields, edges, shapes):
+        self.B = B
+        self.relations = relations
+        self.staging = staging   # uint8 CPU tensor (pinned by pin_memory())
+        self.fields = fields     # list of dicts, see pack()
+        self.edges = edges       # list of (key, T, edge byte offset, offsets byte offset, E)
+        self.shapes = shapes     # key -> dense output shape
+
+    def field(self, key):
+        return next(f for f in self.fields if f["key"] == key)
+
+    def pin_memory(self):
+        """DataLoader(pin_memory=True) calls this in the main process."""
+        if not self.staging.is_pinned():
+            self.staging = self.staging.pin_memory()
+        return self
+
+    @property
+    def nbytes(self) -> int:
+        return int(self.staging.numel())
+
+
+class _Layout:
+    def __init__(self):
+        self.size = 0
+
+    def add(self, nbytes: int) -> int:
+        o = self.size
+        self.size += (nbytes + _ALIGN - 1) // _ALIGN * _ALIGN
+        return o
+
+
+def pack(data, relations: Optional[bool] = None) -> PackedBatch:
+    """Host half of collate_fn: validate + copy the ragged arrays into one staging buffer."""
+    data = [d for d in data if d is not None]
+    if not data:
+        raise ValueError("collate: empty batch")
+    if relations is None:
+        relations = len(data[0]) == len(OBJ_FIELDS) + len(REL_FIELDS) + len(TAIL_FIELDS)
+    names = OBJ_FIELDS + (REL_FIELDS if relations else ()) + TAIL_FIELDS
+    if any(len(d) != len(names) for d in data):
+        raise ValueError(f"collate: every sample must be a {len(names)}-tuple")
+    cols = {k: [d[i] for d in data] for i, k in enumerate(names)}
+    B = len(data)
+    topN = int(cols["topN"][0])
+
+    vis = [np.asarray(v, dtype=np.float32) for v in cols["vis_fea"]]
+    D = vis[0].shape[1]
+    if any(v.ndim != 2 or v.shape[1] != D for v in vis):
+        raise ValueError("collate: vis_fea rows must share one feature size")
+    T_v = max(v.shape[0] for v in vis)
+    nodes = [np.asarray(n).astype(np.int64).reshape(-1) for n in cols["macro_nodes_idx"]]
+    T_s = max(n.shape[0] for n in nodes)
+    qn = [np.asarray(n).astype(np.int64).reshape(-1) for n in cols["qnode_idx"]]
+    T_q = max(n.shape[0] for n in qn)
+
+    def rows_of(arrs, R, T, what):
+        out = []
+        for a in arrs:
+            a = np.asarray(a)
+            n = a.shape[0] if a.ndim else 1
+            if n > T:
+                raise ValueError(f"collate: {what} has {n} rows, more than the padded {T}")
+            out.append(np.broadcast_to(a.astype(np.int64), (n, R) if R > 1 else (n,)))
+        return out
+
+    locs = rows_of(cols["macro_obj_locs"], 1, T_v, "macro_obj_locs")
+    pos = rows_of(cols["micro_positive_nodes_wrd"], topN, T_v, "micro_positive_nodes_wrd")
+    neg = rows_of(cols["micro_negative_nodes_wrd"], topN, T_v, "micro_negative_nodes_wrd")
+    macro_edges = [_edges(e, T_s, True) for e in cols["macro_edges"]]
+    q_edges = [_edges(e, T_q, False) for e in cols["qedge"]]
+    answer = np.stack(cols["answer"], axis=0).astype(np.int64).reshape(B, -1)
+    if answer.shape[1] != 1:
+        raise ValueError("collate: one answer per sample")
+
+    # field plan: (key, kind, torch dtype, T, row_elems, fill, per-sample arrays | count key)
+    plan = [("vis_fea", ROWS, torch.float32, T_v, D, 0.0, vis),
+            ("vis_fea_mask", BOX, torch.int32, T_v, T_v, 1, "vis_fea"),
+            ("macro_node_ipt", ROWS, torch.int64, T_s, 1, PAD, nodes),
+            ("macro_graph_ipt", FILL, torch.int32, T_s, T_s, 0, None),
+            ("macro_node_mask", BOX, torch.int32, T_s, T_s, 1, "macro_node_ipt"),
+            ("macro_obj_loc_ipt", ROWS, torch.int64, T_v, 1, LOC_PAD, locs),
+            ("micro_positive_obj_ipt", ROWS, torch.int64, T_v, topN, PAD, pos),
+            ("micro_negative_obj_ipt", ROWS, torch.int64, T_v, topN, PAD, neg),
+            ("micro_obj_mask", BOX, torch.int32, T_v, topN, 0, "macro_obj_loc_ipt")]
+    if relations:  # super_node:422-439 (a sample without positives keeps only padding)
+        prw = [np.asarray(a).astype(np.int64).reshape(-1)
+               for a in cols["micro_positive_relations_wrd"]]
+        T_r = max(a.shape[0] for a in prw)
+        keep = [a.shape[0] != 0 for a in prw]
+        nrw = rows_of(cols["micro_negative_relations_wrd"], 1, T_r, "micro_negative_relations_wrd")
+        prl = rows_of(cols["micro_positive_relations_loc"], 5, T_r, "micro_positive_relations_loc")
+        nrl = rows_of(cols["micro_negative_relations_loc"], 4, T_r, "micro_negative_relations_loc")
+
+        def kept(arrs, R):
+            return [a if k else np.zeros((0, R) if R > 1 else (0,), np.int64)
+                    for a, k in zip(arrs, keep)]
+        plan += [("micro_positive_rel_ipt", ROWS, torch.int64, T_r, 1, PAD, prw),
+                 ("micro_negative_rel_ipt", ROWS, torch.int64, T_r, 1, PAD, kept(nrw, 1)),
+                 ("micro_positive_rel_loc", ROWS, torch.int64, T_r, 5, LOC_PAD, kept(prl, 5)),
+                 ("micro_negative_rel_loc", ROWS, torch.int64, T_r, 4, LOC_PAD, kept(nrl, 4))]
+    plan += [("q_ipt", ROWS, torch.int64, T_q, 1, PAD, qn),
+             ("q_ipt_mask", BOX, torch.int32, T_q, T_q, 1, "q_ipt"),
+             ("q_ipt_graph", FILL, torch.int32, T_q, T_q, 0, None),
+             ("answer", ROWS, torch.int64, 1, 1, 0, list(answer))]
+
+    lay = _Layout()
+    fields, offsets_of, writes = [], {}, []
+    for key, kind, dt, T, R, fill, srcs in plan:
+        f = dict(key=key, kind=kind, dtype=dt, T=T, row_elems=R,
+                 square=int(kind == BOX and key != "micro_obj_mask"),
+                 fill=_bits(fill, dt) if kind != BOX else 0, src=None, off=None)
+        if kind == ROWS:
+            counts = np.array([a.shape[0] if np.ndim(a) else 1 for a in srcs], np.int64)
+            off = np.zeros(B + 1, np.int64)
+            np.cumsum(counts, out=off[1:])
+            item = np.dtype(_NP[dt]).itemsize
+            f["off"] = lay.add(8 * (B + 1))
+            f["src"] = lay.add(int(off[-1]) * R * item)
+            writes.append((f["off"], off, None))
+            writes.append((f["src"], srcs, _NP[dt]))
+            offsets_of[key] = f["off"]
+        elif kind == BOX:
+            f["off"] = offsets_of[srcs]
+        fields.append(f)
+    edges = []
+    for key, T, elist in (("macro_graph_ipt", T_s, macro_edges), ("q_ipt_graph", T_q, q_edges)):
+        counts = np.array([0 if e is None else e.shape[0] for e in elist], np.int64)
+        off = np.zeros(B + 1, np.int64)
+        np.cumsum(counts, out=off[1:])
+        E = int(off[-1])
+        o_off = lay.add(8 * (B + 1))
+        o_e = lay.add(8 * E)
+        writes.append((o_off, off, None))
+        writes.append((o_e, [e for e in elist if e is not None], np.int32))
+        edges.append((key, T, o_e, o_off, E))
+
+    staging = torch.empty(max(lay.size, _ALIGN), dtype=torch.uint8)
+    buf = staging.numpy()
+    for o, arr, dt in writes:
+        if dt is None:  # offsets
+            buf[o:o + arr.nbytes] = arr.view(np.uint8)
+            continue
+        pos_b = o
+        for a in arr:
+            a = np.ascontiguousarray(a, dtype=dt)
+            nb = a.nbytes
+            buf[pos_b:pos_b + nb] = a.reshape(-1).view(np.uint8)
+            pos_b += nb
+    shapes = {f["key"]: ((B, f["T"], f["row_elems"]) if f["row_elems"] > 1 or f["kind"] != ROWS
+                         else (B, f["T"])) for f in fields}
+    shapes["answer"] = (B,)
+    return PackedBatch(B, relations, staging, fields, edges, shapes)
+
+
+def to_device(pk: PackedBatch, device=None, staging_dev: Optional[torch.Tensor] = None
+              ) -> Dict[str, torch.Tensor]:
+    """Device half of collate_fn: one H2D copy + two launches on the current stream.
+    staging_dev: the staging bytes already in HBM (skips the copy; benchmarks)."""
+    device = torch.device(device) if device is not None else \
+        torch.device("cuda", torch.cuda.current_device())
+    if device.type != "cuda":
+        raise _lib.SavqaError("collate.to_device needs a HIP device (no host fallback)")
+    _lib.load()  # raises when the library is missing
+    if staging_dev is not None:
+        dev = staging_dev
+    else:
+        dev = torch.empty(pk.staging.numel(), dtype=torch.uint8, device=device)
+        dev.copy_(pk.staging, non_blocking=pk.staging.is_pinned())
+    base = dev.data_ptr()
+    out = {}
+    arr = (CollateField * len(pk.fields))()
+    for i, f in enumerate(pk.fields):
+        t = torch.empty(pk.shapes[f["key"]], dtype=f["dtype"], device=device)
+        out[f["key"]] = t
+        c = arr[i]
+        c.kind, c.square, c.reserved = f["kind"], f["square"], 0
+        c.elem_bytes = torch.tensor([], dtype=f["dtype"]).element_size()
+        c.T, c.row_elems, c.fill = f["T"], f["row_elems"], f["fill"]
+        c.src = base + f["src"] if f["src"] is not None else None
+        c.off = base + f["off"] if f["off"] is not None else None
+        c.dst = t.data_ptr()
+    stream = torch.cuda.current_stream(device).cuda_stream
+    with torch.cuda.device(device):
+        call("savqa_collate", stream, arr, len(pk.fields), pk.B)
+        for key, T, o_e, o_off, E in pk.edges:
+            call("savqa_collate_edges", stream, base + o_e, base + o_off, pk.B, E, T,
+                 out[key].data_ptr())
+    return {k: out[k] for k in OUTPUT_KEYS if k in out}  # the reference's key order
+
+
+def collate_fn(data, device=None) -> Dict[str, torch.Tensor]:
+    """The reference collate_fn with its output already in HBM."""
+    return to_device(pack(data), device)
+
+
+def forward_inputs(batch: Dict[str, torch.Tensor]) -> List[torch.Tensor]:
+    """Positional inputs of AttModel.forward (main:321-325); the relation tensors are
+    empty (B, 0) for the only_obj loader (main:290-308)."""
+    B = batch["vis_fea"].shape[0]
+    empty = torch.empty((B, 0), device=batch["vis_fea"].device)
+    return [batch[k] if k in batch else empty for k in FORWARD_KEYS]

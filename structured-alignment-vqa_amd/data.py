@@ -105,3 +105,51 @@ def synthetic_relation_batch(B: int, Nv: int = 36, Lq: int = 14, topN: int = 5,
     batch["micro_positive_rel_loc"] = torch.from_numpy(pos_loc).to(dev)
     batch["micro_negative_rel_loc"] = torch.from_numpy(neg_loc).to(dev)
     return batch
+
+
+def synthetic_samples(B: int, relations: bool = False, Nv=(10, 36), Lq=(5, 14), topN: int = 5,
+                      fea_dim: int = 2048, n_attr: int = 4, extra_nodes=(0, 23),
+                      num_relations: int = 311, num_classes: int = 914, seed: int = 1234):
+    """Per-sample tuples shaped like the loaders' Dataset.__getitem__ (onlyobj:330-332;
+    super_node:353-357) for the device collate (collate.pack): ragged region counts in
+    [Nv[0], Nv[1]], question lengths in [Lq[0], Lq[1]]. only_obj: Nv object nodes +
+    n_attr attribute nodes + U(extra_nodes) relation nodes with Bernoulli(0.05) edges.
+    relations: the super-node layout of synthetic_relation_batch (one relation node per
+    ordered object pair, topN^2 positive and negative entries per pair)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(B):
+        nv = int(rng.integers(Nv[0], Nv[1] + 1))
+        lq = int(rng.integers(Lq[0], Lq[1] + 1))
+        vis = np.maximum(rng.standard_normal((nv, fea_dim), dtype=np.float32), 0)
+        q = rng.integers(0, PAD, lq)
+        qedge = np.argwhere(rng.random((lq, lq)) < 0.2)
+        if len(qedge) == 0:
+            qedge = np.zeros((1, 2), np.int64)
+        pos = rng.integers(0, PAD, (nv, topN))
+        neg = rng.integers(0, PAD, (nv, topN))
+        ans = np.int64(rng.integers(1, num_classes))
+        if not relations:
+            ns = nv + n_attr + int(rng.integers(extra_nodes[0], extra_nodes[1] + 1))
+            nodes = rng.integers(0, PAD, ns)
+            edges = np.argwhere(rng.random((ns, ns)) < 0.05)
+            out.append((vis, nodes, np.arange(nv), edges, pos, neg, q, qedge, ans, topN))
+            continue
+        pairs = np.array([(i, j) for i in range(nv) for j in range(nv) if i != j], np.int64)
+        ns = nv + n_attr + len(pairs)
+        nodes = rng.integers(0, PAD, ns)
+        attr = nv + rng.integers(0, n_attr, nv)
+        rel = nv + n_attr + np.arange(len(pairs))
+        edges = np.concatenate([np.stack([np.arange(nv), attr], 1), np.stack([attr, np.arange(nv)], 1),
+                                np.stack([pairs[:, 0], rel], 1), np.stack([rel, pairs[:, 1]], 1)])
+        K = topN * topN
+        L = len(pairs) * K
+        pi, pj, ploc = (np.repeat(pairs[:, 0], K), np.repeat(pairs[:, 1], K), np.repeat(rel, K))
+        cat = rng.integers(0, num_relations, L)
+        ncat = (cat + rng.integers(1, max(num_relations, 2), L)) % max(num_relations, 1)
+        prl = np.stack([pi, pj, cat, ploc, np.arange(L)], 1)
+        nrl = np.stack([pi, pj, ncat, ploc], 1)
+        out.append((vis, nodes, np.arange(nv), edges, pos, neg, rng.integers(0, PAD, L),
+                    rng.integers(0, PAD, L), prl, nrl, q, qedge, ans, topN))
+    return out

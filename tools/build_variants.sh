@@ -7,7 +7,7 @@ cd "$(dirname "$0")/../structured-alignment-vqa_amd/csrc"
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   out=build/var_$name; mkdir -p $out
-  for f in capi.cpp gemm.hip gemm_bf16.hip ln.hip attn.hip attn_flash.hip misc.hip dropout.hip rel.hip; do
+  for f in capi.cpp gemm.hip gemm_bf16.hip ln.hip attn.hip attn_flash.hip misc.hip dropout.hip rel.hip collate.hip; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $flags -c $f -o $out/$f.o &
   done
   wait

@@ -282,6 +282,28 @@ def block_cases(modules_mod):
     print("wrote blocks.npz")
 
 
+COLLATE_CASES = {"onlyobj": dict(B=9, relations=False, fea_dim=16, topN=5, tag="col"),
+                 "super_node": dict(B=10, relations=True, fea_dim=16, topN=3, tag="colrel")}
+
+
+def collate_cases():
+    """Reference collate_fn outputs (onlyobj:341-445, super_node:366-497) on the
+    oracle/collate.py sample recipe -> tests/golden/collate.npz."""
+    from oracle import collate as ocol
+    sys.path.insert(0, os.path.join(os.path.dirname(REF), "dataloader"))
+    import data_loader_itp_bbox_super_node_onlyobj as onlyobj_mod  # noqa: E402  (reference)
+    import data_loader_itp_bbox_super_node as super_mod  # noqa: E402  (reference)
+    out = {}
+    for name, kw in COLLATE_CASES.items():
+        data = ocol.make_samples(**kw)
+        fn = super_mod.collate_fn if kw["relations"] else onlyobj_mod.collate_fn
+        res = fn(data)
+        for k, v in res.items():
+            out[f"{name}:{k}"] = v.numpy()
+    np.savez_compressed(os.path.join(OUT, "collate.npz"), **out)
+    print("wrote collate.npz")
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference absent; nothing to do")
@@ -297,6 +319,8 @@ def main():
         full_model_cases(modules_mod, att_mod)
     if "rel" in which:
         relation_cases(att_mod)
+    if "collate" in which:
+        collate_cases()
 
 
 if __name__ == "__main__":
