@@ -61,24 +61,35 @@ def _bits(value, dtype) -> int:
         np.uint64 if _NP[dtype] == np.int64 else np.uint32)[0])
 
 
-def _edges(edge, T: int, skip_empty: bool) -> Optional[np.ndarray]:
-    """Edge list of one sample as int32 [E][2] in [0, T), with the reference's rules:
-    np.asarray(edge).astype('int32'), macro lists: empty skipped and a flat pair promoted
-    (onlyobj:397-401); graph[row, e[:,0], e[:,1]] = 1 -> numpy index semantics (negative
-    indices wrap once, anything outside [-T, T) raises IndexError, extra columns unused)."""
-    e = np.asarray(edge).astype("int32")
-    if skip_empty:
-        if e.size == 0:
-            return None
-        if len(e.shape) == 1:
-            e = e[np.newaxis, :]
-    if e.ndim != 2 or e.shape[1] < 2:
-        raise IndexError(f"edge list of shape {e.shape}: too many indices for array")
-    e = e[:, :2].astype(np.int64)
+def _edges(edge_lists, T: int, skip_empty: bool):
+    """Edge lists of all samples as one int32 [E][2] array in [0, T) + per-sample counts,
+    with the reference's rules: np.asarray(edge).astype('int32'); macro lists: empty
+    skipped and a flat pair promoted (onlyobj:397-401); graph[row, e[:,0], e[:,1]] = 1 ->
+    numpy index semantics (negative indices wrap once, anything outside [-T, T) raises
+    IndexError, extra columns unused). T is the batch's padded size, shared by all rows."""
+    parts, counts = [], []
+    for edge in edge_lists:
+        e = np.asarray(edge)
+        if e.dtype.kind not in "iu" or e.dtype.itemsize > 4:
+            e = e.astype("int32")
+        if skip_empty:
+            if e.size == 0:
+                counts.append(0)
+                continue
+            if e.ndim == 1:
+                e = e[np.newaxis, :]
+        if e.ndim != 2 or e.shape[1] < 2:
+            raise IndexError(f"edge list of shape {e.shape}: too many indices for array")
+        parts.append(e[:, :2])
+        counts.append(e.shape[0])
+    if not parts:
+        return np.zeros((0, 2), np.int32), counts
+    e = np.concatenate(parts).astype(np.int32, copy=False)
     if e.size and (e.min() < -T or e.max() >= T):
         raise IndexError(f"edge index out of bounds for graph of size {T}")
-    e = np.where(e < 0, e + T, e)
-    return e.astype(np.int32)
+    if e.size and e.min() < 0:
+        e = np.where(e < 0, e + T, e).astype(np.int32)
+    return e, counts
 
 
 class PackedBatch:
@@ -116,8 +127,11 @@ class _Layout:
         return o
 
 
-def pack(data, relations: Optional[bool] = None) -> PackedBatch:
-    """Host half of collate_fn: validate + copy the ragged arrays into one staging buffer."""
+def pack(data, relations: Optional[bool] = None,
+         staging: Optional[torch.Tensor] = None) -> PackedBatch:
+    """Host half of collate_fn: validate + copy the ragged arrays into one staging buffer.
+    staging: an optional reusable (e.g. pinned) uint8 buffer, used when large enough
+    (the caller must not refill it while a copy out of it is in flight; StagingRing)."""
     data = [d for d in data if d is not None]
     if not data:
         raise ValueError("collate: empty batch")
@@ -135,26 +149,29 @@ def pack(data, relations: Optional[bool] = None) -> PackedBatch:
     if any(v.ndim != 2 or v.shape[1] != D for v in vis):
         raise ValueError("collate: vis_fea rows must share one feature size")
     T_v = max(v.shape[0] for v in vis)
-    nodes = [np.asarray(n).astype(np.int64).reshape(-1) for n in cols["macro_nodes_idx"]]
+    nodes = [np.asarray(n, dtype=np.int64).reshape(-1) for n in cols["macro_nodes_idx"]]
     T_s = max(n.shape[0] for n in nodes)
-    qn = [np.asarray(n).astype(np.int64).reshape(-1) for n in cols["qnode_idx"]]
+    qn = [np.asarray(n, dtype=np.int64).reshape(-1) for n in cols["qnode_idx"]]
     T_q = max(n.shape[0] for n in qn)
 
     def rows_of(arrs, R, T, what):
         out = []
+        shape_ok = (lambda a: a.ndim == 2 and a.shape[1] == R) if R > 1 else \
+            (lambda a: a.ndim == 1)
         for a in arrs:
-            a = np.asarray(a)
+            a = np.asarray(a, dtype=np.int64)
             n = a.shape[0] if a.ndim else 1
             if n > T:
                 raise ValueError(f"collate: {what} has {n} rows, more than the padded {T}")
-            out.append(np.broadcast_to(a.astype(np.int64), (n, R) if R > 1 else (n,)))
+            # numpy assignment semantics: the sample broadcasts into its (n, R) slot
+            out.append(a if shape_ok(a) else np.broadcast_to(a, (n, R) if R > 1 else (n,)))
         return out
 
     locs = rows_of(cols["macro_obj_locs"], 1, T_v, "macro_obj_locs")
     pos = rows_of(cols["micro_positive_nodes_wrd"], topN, T_v, "micro_positive_nodes_wrd")
     neg = rows_of(cols["micro_negative_nodes_wrd"], topN, T_v, "micro_negative_nodes_wrd")
-    macro_edges = [_edges(e, T_s, True) for e in cols["macro_edges"]]
-    q_edges = [_edges(e, T_q, False) for e in cols["qedge"]]
+    macro_edges = _edges(cols["macro_edges"], T_s, True)
+    q_edges = _edges(cols["qedge"], T_q, False)
     answer = np.stack(cols["answer"], axis=0).astype(np.int64).reshape(B, -1)
     if answer.shape[1] != 1:
         raise ValueError("collate: one answer per sample")
@@ -210,29 +227,32 @@ def pack(data, relations: Optional[bool] = None) -> PackedBatch:
             f["off"] = offsets_of[srcs]
         fields.append(f)
     edges = []
-    for key, T, elist in (("macro_graph_ipt", T_s, macro_edges), ("q_ipt_graph", T_q, q_edges)):
-        counts = np.array([0 if e is None else e.shape[0] for e in elist], np.int64)
+    for key, T, (e_all, counts) in (("macro_graph_ipt", T_s, macro_edges),
+                                    ("q_ipt_graph", T_q, q_edges)):
         off = np.zeros(B + 1, np.int64)
-        np.cumsum(counts, out=off[1:])
+        np.cumsum(np.asarray(counts, np.int64), out=off[1:])
         E = int(off[-1])
         o_off = lay.add(8 * (B + 1))
         o_e = lay.add(8 * E)
         writes.append((o_off, off, None))
-        writes.append((o_e, [e for e in elist if e is not None], np.int32))
+        writes.append((o_e, [e_all], np.int32))
         edges.append((key, T, o_e, o_off, E))
 
-    staging = torch.empty(max(lay.size, _ALIGN), dtype=torch.uint8)
+    need = max(lay.size, _ALIGN)
+    if staging is None or staging.numel() < need:
+        staging = torch.empty(need, dtype=torch.uint8)
+    else:
+        staging = staging[:need]
     buf = staging.numpy()
     for o, arr, dt in writes:
         if dt is None:  # offsets
             buf[o:o + arr.nbytes] = arr.view(np.uint8)
             continue
-        pos_b = o
-        for a in arr:
-            a = np.ascontiguousarray(a, dtype=dt)
-            nb = a.nbytes
-            buf[pos_b:pos_b + nb] = a.reshape(-1).view(np.uint8)
-            pos_b += nb
+        parts = [np.asarray(a).reshape(-1) for a in arr]
+        n = sum(p.shape[0] for p in parts)
+        if n:  # one C-level copy of every sample's rows into the section
+            np.concatenate(parts, out=buf[o:o + n * np.dtype(dt).itemsize].view(dt),
+                           casting="same_kind")
     shapes = {f["key"]: ((B, f["T"], f["row_elems"]) if f["row_elems"] > 1 or f["kind"] != ROWS
                          else (B, f["T"])) for f in fields}
     shapes["answer"] = (B,)
@@ -273,6 +293,32 @@ def to_device(pk: PackedBatch, device=None, staging_dev: Optional[torch.Tensor] 
             call("savqa_collate_edges", stream, base + o_e, base + o_off, pk.B, E, T,
                  out[key].data_ptr())
     return {k: out[k] for k in OUTPUT_KEYS if k in out}  # the reference's key order
+
+
+class StagingRing:
+    """Reusable pinned staging buffers for in-process collation: buffer i is refilled
+    only after the H2D copy that last read it has completed (event per buffer), so the
+    host never pays fresh-page faults or pinning per batch."""
+
+    def __init__(self, depth: int = 2):
+        self.bufs = [None] * depth
+        self.events = [None] * depth
+        self.i = 0
+
+    def collate(self, data, relations: Optional[bool] = None, device=None):
+        k = self.i
+        self.i = (self.i + 1) % len(self.bufs)
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        pk = pack(data, relations, staging=self.bufs[k])
+        if self.bufs[k] is None or pk.staging.data_ptr() != self.bufs[k].data_ptr():
+            pk.pin_memory()
+            self.bufs[k] = pk.staging
+        res = to_device(pk, device)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+        return res
 
 
 def collate_fn(data, device=None) -> Dict[str, torch.Tensor]:

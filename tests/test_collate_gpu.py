@@ -73,6 +73,20 @@ def test_device_collate_super_node_batch():
     _check(res, ocol.collate_super_node(data))
 
 
+def test_staging_ring_reuses_pinned_buffers():
+    _need_gpu()
+    from savqa_amd.collate import StagingRing
+    ring = StagingRing(2)
+    batches = [ocol.make_samples(6, relations=r, fea_dim=32, topN=3, tag=f"ring{i}")
+               for i, r in enumerate([False, False, True, False])]
+    outs = [ring.collate(b) for b in batches]  # buffers 0,1 refilled after their copies
+    torch.cuda.synchronize()
+    assert all(b is not None and b.is_pinned() for b in ring.bufs)
+    for b, res in zip(batches, outs):
+        ref = (ocol.collate_super_node if len(b[0]) == 14 else ocol.collate_onlyobj)(b)
+        _check(res, ref)
+
+
 def test_device_collate_feeds_the_model():
     """collate -> AttModel.forward == forward on the host-collated batch (bit-exact)."""
     _need_gpu()
