@@ -19,7 +19,6 @@ HIP library / a device, to_device raises.
 """
 from __future__ import annotations
 
-import ctypes as C
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -259,40 +258,56 @@ def pack(data, relations: Optional[bool] = None,
     return PackedBatch(B, relations, staging, fields, edges, shapes)
 
 
+class DeviceBatch:
+    """Dense outputs of one packed batch + the launch arguments that fill them
+    (built once; launch() may be repeated, e.g. to time the kernels)."""
+
+    def __init__(self, pk: PackedBatch, device, staging_dev: torch.Tensor):
+        self.pk = pk
+        self.device = device
+        self.staging_dev = staging_dev  # keeps the packed bytes alive until the launch
+        base = staging_dev.data_ptr()
+        self.out = {}
+        self.args = (CollateField * len(pk.fields))()
+        for i, f in enumerate(pk.fields):
+            t = torch.empty(pk.shapes[f["key"]], dtype=f["dtype"], device=device)
+            self.out[f["key"]] = t
+            c = self.args[i]
+            c.kind, c.square, c.reserved = f["kind"], f["square"], 0
+            c.elem_bytes = t.element_size()
+            c.T, c.row_elems, c.fill = f["T"], f["row_elems"], f["fill"]
+            c.src = base + f["src"] if f["src"] is not None else None
+            c.off = base + f["off"] if f["off"] is not None else None
+            c.dst = t.data_ptr()
+        self.edges = [(base + o_e, base + o_off, E, T, self.out[key].data_ptr())
+                      for key, T, o_e, o_off, E in pk.edges]
+
+    def launch(self, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        with torch.cuda.device(self.device):
+            call("savqa_collate", s, self.args, len(self.pk.fields), self.pk.B)
+            for e, eo, E, T, g in self.edges:
+                call("savqa_collate_edges", s, e, eo, self.pk.B, E, T, g)
+
+    def result(self) -> Dict[str, torch.Tensor]:
+        return {k: self.out[k] for k in OUTPUT_KEYS if k in self.out}  # reference key order
+
+
 def to_device(pk: PackedBatch, device=None, staging_dev: Optional[torch.Tensor] = None
               ) -> Dict[str, torch.Tensor]:
     """Device half of collate_fn: one H2D copy + two launches on the current stream.
-    staging_dev: the staging bytes already in HBM (skips the copy; benchmarks)."""
+    staging_dev: the staging bytes already in HBM (skips the copy)."""
     device = torch.device(device) if device is not None else \
         torch.device("cuda", torch.cuda.current_device())
     if device.type != "cuda":
         raise _lib.SavqaError("collate.to_device needs a HIP device (no host fallback)")
     _lib.load()  # raises when the library is missing
-    if staging_dev is not None:
-        dev = staging_dev
-    else:
-        dev = torch.empty(pk.staging.numel(), dtype=torch.uint8, device=device)
-        dev.copy_(pk.staging, non_blocking=pk.staging.is_pinned())
-    base = dev.data_ptr()
-    out = {}
-    arr = (CollateField * len(pk.fields))()
-    for i, f in enumerate(pk.fields):
-        t = torch.empty(pk.shapes[f["key"]], dtype=f["dtype"], device=device)
-        out[f["key"]] = t
-        c = arr[i]
-        c.kind, c.square, c.reserved = f["kind"], f["square"], 0
-        c.elem_bytes = torch.tensor([], dtype=f["dtype"]).element_size()
-        c.T, c.row_elems, c.fill = f["T"], f["row_elems"], f["fill"]
-        c.src = base + f["src"] if f["src"] is not None else None
-        c.off = base + f["off"] if f["off"] is not None else None
-        c.dst = t.data_ptr()
-    stream = torch.cuda.current_stream(device).cuda_stream
-    with torch.cuda.device(device):
-        call("savqa_collate", stream, arr, len(pk.fields), pk.B)
-        for key, T, o_e, o_off, E in pk.edges:
-            call("savqa_collate_edges", stream, base + o_e, base + o_off, pk.B, E, T,
-                 out[key].data_ptr())
-    return {k: out[k] for k in OUTPUT_KEYS if k in out}  # the reference's key order
+    if staging_dev is None:
+        staging_dev = torch.empty(pk.staging.numel(), dtype=torch.uint8, device=device)
+        staging_dev.copy_(pk.staging, non_blocking=pk.staging.is_pinned())
+    db = DeviceBatch(pk, device, staging_dev)
+    db.launch()
+    return db.result()
 
 
 class StagingRing:

@@ -9,7 +9,9 @@
 //   savqa_collate        one launch for every padded field of the batch: each workgroup
 //                        writes a 4 KB chunk of one sample of one field (valid rows copied
 //                        from the packed source, the rest filled; masks computed from the
-//                        per-sample lengths), 16-B vector moves where both sides align;
+//                        per-sample lengths); every store is a 16-B vector on the output's
+//                        16-B grid (a sample's unaligned head/tail words aside), loads are
+//                        16-B vectors where the packed source lines up too;
 //   savqa_collate_edges  one thread per edge: graph[b][i][j] = 1 (after the zero fill).
 // Pure HBM streaming: bytes written = the dense batch, bytes read = the packed batch.
 #include "common.h"
@@ -17,7 +19,8 @@
 namespace savqa {
 
 constexpr int kColNT = 256;                 // threads per workgroup
-constexpr int kColWords = kColNT * 4;       // 32-bit words per chunk (4 KB)
+constexpr int kColIter = 4;                 // 16-B groups per thread
+constexpr int kColWords = kColNT * 4 * kColIter;  // 32-bit words per chunk (16 KB)
 
 struct CollateArgs {
   savqa_collate_field f[SAVQA_COLLATE_MAX_FIELDS];
@@ -31,56 +34,78 @@ __device__ __forceinline__ uint32_t fill_word(const savqa_collate_field& f, int6
   return (f.elem_bytes == 8 && (w & 1)) ? (uint32_t)(f.fill >> 32) : (uint32_t)f.fill;
 }
 
-__global__ __launch_bounds__(kColNT) void collate_kernel(CollateArgs a) {
-  const int64_t bid = blockIdx.x;
-  int fi = 0;
-  while (fi + 1 < a.nfields && bid >= a.first[fi + 1]) ++fi;
-  const savqa_collate_field& f = a.f[fi];
-  const int64_t local = bid - a.first[fi];
-  const int64_t b = local / a.chunks[fi];
-  const int64_t chunk = local % a.chunks[fi];
-  const int64_t wps = f.T * f.row_elems * f.elem_bytes / 4;  // words per sample
-  uint32_t* dst = reinterpret_cast<uint32_t*>(f.dst) + b * wps;
-  const int64_t w0 = chunk * kColWords + 4 * (int64_t)threadIdx.x;
-  if (w0 >= wps) return;
+// one 16-B group (words w0 .. w0+3 of sample b's dense output) of field f
+__device__ __forceinline__ void collate_group(const savqa_collate_field& f, int64_t b,
+                                              uint32_t* __restrict__ dst, int64_t wps,
+                                              int64_t w0) {
+  using u4 = uint32_t __attribute__((ext_vector_type(4)));
+  const bool full = w0 >= 0 && w0 + 4 <= wps;  // whole aligned group inside the sample
+  uint32_t v[4];
   if (f.kind == SAVQA_COLLATE_BOX) {
-    const int64_t n = f.off[b + 1] - f.off[b];
-    const int64_t C = f.row_elems;
+    // int32 mask value of word w = (t, c): t < n && (!square || c < n); one 32-bit
+    // division per group (T * row_elems < 2^31 checked on the host)
+    const int n = (int)(f.off[b + 1] - f.off[b]);
+    const int C = (int)f.row_elems;
+    const int ws = (int)(w0 < 0 ? 0 : w0);
+    int t = ws / C, c = ws - t * C;
+    const int qs = (int)(ws - w0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q >= qs) {
+        v[q] = (t < n && (!f.square || c < n)) ? 1u : 0u;
+        if (++c == C) { c = 0; ++t; }
+      }
+    }
+  } else {
+    int64_t valid = 0;  // words of this sample that come from the source
+    const uint32_t* src = nullptr;
+    if (f.kind == SAVQA_COLLATE_ROWS) {
+      const int64_t r0 = f.off[b];
+      const int64_t epw = f.row_elems * f.elem_bytes / 4;  // words per row
+      valid = min((f.off[b + 1] - r0) * epw, wps);
+      src = reinterpret_cast<const uint32_t*>(f.src) + r0 * epw;
+    }
+    if (full && w0 + 4 <= valid && ((reinterpret_cast<uintptr_t>(src + w0) & 15) == 0)) {
+      const u4 x = *reinterpret_cast<const u4*>(src + w0);
+      v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t w = w0 + q;
+        if (w >= 0 && w < wps) v[q] = (w < valid) ? src[w] : fill_word(f, w);
+      }
+    }
+  }
+  if (full) {
+    *reinterpret_cast<u4*>(dst + w0) = u4{v[0], v[1], v[2], v[3]};
+  } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int64_t w = w0 + q;
-      if (w >= wps) break;
-      const int64_t t = w / C, c = w - t * C;
-      dst[w] = (t < n && (!f.square || c < n)) ? 1u : 0u;
+      if (w >= 0 && w < wps) dst[w] = v[q];
     }
-    return;
   }
-  int64_t valid = 0;  // words of this sample that come from the source
-  const uint32_t* src = nullptr;
-  if (f.kind == SAVQA_COLLATE_ROWS) {
-    const int64_t r0 = f.off[b];
-    const int64_t epw = f.row_elems * f.elem_bytes / 4;  // words per row
-    valid = min((f.off[b + 1] - r0) * epw, wps);
-    src = reinterpret_cast<const uint32_t*>(f.src) + r0 * epw;
-  }
-  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
-  if (vec && w0 + 4 <= wps) {
-    using u4 = uint32_t __attribute__((ext_vector_type(4)));
-    u4 v;
-    if (w0 + 4 <= valid) {
-      v = *reinterpret_cast<const u4*>(src + w0);
-    } else {
+}
+
+__global__ __launch_bounds__(kColNT) void collate_kernel(CollateArgs a) {
+  const uint32_t bid = blockIdx.x;
+  int fi = 0;
+  while (fi + 1 < a.nfields && bid >= (uint32_t)a.first[fi + 1]) ++fi;
+  const savqa_collate_field& f = a.f[fi];
+  const uint32_t local = bid - (uint32_t)a.first[fi];
+  const uint32_t cps = (uint32_t)a.chunks[fi];
+  const int64_t b = local / cps;
+  const int64_t chunk = local - (uint32_t)b * cps;
+  const int64_t wps = f.T * f.row_elems * f.elem_bytes / 4;  // words per sample
+  uint32_t* dst = reinterpret_cast<uint32_t*>(f.dst) + b * wps;
+  // 4-word groups are laid on the 16-B grid of dst: the sample's first `head` words (its
+  // base is only 4-B aligned in general) form a partial group -1 (host adds one group)
+  const int head = (int)(((16u - (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u) >> 2);
+  const int64_t base = chunk * kColWords + head - (head ? 4 : 0);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = (w0 + q < valid) ? src[w0 + q] : fill_word(f, w0 + q);
-    }
-    *reinterpret_cast<u4*>(dst + w0) = v;
-    return;
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t w = w0 + q;
-    if (w >= wps) break;
-    dst[w] = (w < valid) ? src[w] : fill_word(f, w);
+  for (int k = 0; k < kColIter; ++k) {  // group k*256 + tid: each store wave-contiguous
+    const int64_t w0 = base + 4 * (int64_t)(k * kColNT + threadIdx.x);
+    if (w0 < wps) collate_group(f, b, dst, wps, w0);
   }
 }
 
@@ -124,9 +149,11 @@ extern "C" int savqa_collate(void* stream, const savqa_collate_field* fields, in
       return fail(SAVQA_EINVAL, "savqa_collate: bad field");
     if (f.kind == SAVQA_COLLATE_BOX && f.square && f.row_elems != f.T)
       return fail(SAVQA_EINVAL, "savqa_collate: square mask needs row_elems == T");
-    a.f[i] = f;
     const int64_t words = f.T * f.row_elems * f.elem_bytes / 4;
-    a.chunks[i] = words > 0 ? (words + kColWords - 1) / kColWords : 1;
+    if (words >= ((int64_t)1 << 31)) return fail(SAVQA_EUNSUP, "savqa_collate: sample too large");
+    a.f[i] = f;
+    // + one group: a sample's 16-B grid may start up to 3 words in (see the kernel)
+    a.chunks[i] = (words + 4 + kColWords - 1) / kColWords;
     a.first[i] = total;
     total += B * a.chunks[i];
   }
