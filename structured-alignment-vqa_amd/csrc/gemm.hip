@@ -35,6 +35,9 @@
 #ifndef SAVQA_GEMM_BK
 #define SAVQA_GEMM_BK 16  // k-tile; 16 beats 32 on the K=512 step shapes (shorter prologue)
 #endif
+#ifndef SAVQA_GEMM_BK_DW
+#define SAVQA_GEMM_BK_DW 16  // k-tile of the dW layouts (A = dY^T, K = B*T rows); 32 measured
+#endif                       // no better (tools/gemm_bench.py, cfg-2 dW shapes)
 
 namespace savqa {
 
@@ -173,10 +176,86 @@ struct Operand {
   }
 };
 
+// COL source (m contiguous: dY^T and X of a dW GEMM) stored ROW-wise ([m][BK+4]) so the
+// MFMA operands come from one ds_read_b128 per 8 k like the forward's, instead of four
+// ds_read_b32. Each thread owns one 4(k) x 4(m) block per k-tile: four float4 loads along
+// m (one per k row, wave-contiguous), a register transpose, four float4 stores along k.
+// Needs BMX * BK == 16 * GEMM_NT (BK = 32 at 128-wide tiles).
+template <int BMX, int BK>
+struct OperandT {
+  static constexpr int LD = BK + 4;
+  static constexpr int SIZE = BMX * LD;
+  static constexpr int PER = BMX / 4;  // m-quads per k row (colsum: column group = tid % PER)
+  static constexpr int ITERS = 1;      // colsum partial f4s per thread
+  static_assert(BMX * BK == 16 * GEMM_NT, "one 4x4 block per thread");
+  f4 r[4];
+  const float* rp;
+
+  __device__ __forceinline__ void setup_fast(const float* __restrict__ base, int64_t ld,
+                                             const int64_t* __restrict__ rows, int64_t m0,
+                                             int tid) {
+    (void)rows;  // the fast path never gathers k rows
+    rp = base + (int64_t)(4 * (tid / PER)) * ld + m0 + 4 * (tid % PER);
+  }
+  __device__ __forceinline__ void load_fast(int64_t ld, int64_t k0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = *reinterpret_cast<const f4*>(rp + (k0 + j) * ld);
+  }
+  __device__ __forceinline__ void load_slow(const float* __restrict__ base, int64_t ld,
+                                            const int64_t* __restrict__ rows, int64_t mlim,
+                                            int64_t m0, int64_t k0, int64_t kend, int tid) {
+    const int64_t col = m0 + 4 * (tid % PER);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t row = k0 + 4 * (tid / PER) + j;
+      const bool rok = row < kend;
+      const int64_t rc = rok ? row : 0;
+      const int64_t rr = rows ? rows[rc] : rc;
+      const float* p = base + rr * ld;
+      float e[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = rok && (col + q < mlim);
+        const float val = p[ok ? col + q : 0];
+        e[q] = ok ? val : 0.f;
+      }
+      r[j] = f4{e[0], e[1], e[2], e[3]};
+    }
+  }
+  __device__ __forceinline__ void accum(f4 (&cs)[ITERS]) const {
+    cs[0] += (r[0] + r[1]) + (r[2] + r[3]);
+  }
+  __device__ __forceinline__ void store(float* __restrict__ s, int tid) const {
+    const int m = 4 * (tid % PER), k = 4 * (tid / PER);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<f4*>(&s[(m + i) * LD + k]) = f4{r[0][i], r[1][i], r[2][i], r[3][i]};
+  }
+  template <class MI>
+  static __device__ __forceinline__ void fetch(const float* __restrict__ s, int wbase, int f,
+                                               int c, int lane, float (&v)[4]) {
+    Operand<BMX, BK, true>::template fetch<MI>(s, wbase, f, c, lane, v);
+  }
+};
+
+// dW layouts (a_trans) can stage both m-contiguous operands transposed (needs
+// SAVQA_GEMM_BK_DW=32). Off: measured 3-9% slower on the cfg-2 dW shapes than the
+// [k][m] staging with four ds_read_b32 (108.9 vs 117.0 TF at 6144x512x18688), so LDS
+// operand reads are not what bounds the dW kernel.
+#ifndef SAVQA_GEMM_DW_T
+#define SAVQA_GEMM_DW_T 0
+#endif
+template <int BMX, int BK, bool ROW, bool TR>
+struct OpSel { using T = Operand<BMX, BK, ROW>; };
+template <int BMX, int BK>
+struct OpSel<BMX, BK, false, true> { using T = OperandT<BMX, BK>; };
+
 template <int BM, int BN, int BK, bool AT, bool BT>
 struct GemmCfg {
-  using OA = Operand<BM, BK, !AT>;
-  using OB = Operand<BN, BK, BT>;
+  static constexpr bool TR = AT && SAVQA_GEMM_DW_T && BM * BK == 16 * GEMM_NT &&
+                             BN * BK == 16 * GEMM_NT;
+  using OA = typename OpSel<BM, BK, !AT, TR>::T;
+  using OB = typename OpSel<BN, BK, BT, TR>::T;
   using MI = GemmMi;
   using Acc = typename MI::Acc;
   static constexpr int WM = BM / 2, WN = BN / 2;
@@ -810,7 +889,8 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.colsum_a && !d.a_trans) return fail(SAVQA_EINVAL, "savqa_gemm: colsum_a needs a_trans=1");
   if (d.prec != 0 && d.prec != 1 && d.prec != 3)
     return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32), 1 (bf16) or 3 (3xbf16)");
-  const int BK = d.prec ? 32 : SAVQA_GEMM_BK;  // gemm_bf16_kernel k-tile: 32
+  // gemm_bf16_kernel k-tile: 32; the stream-K kernel always runs SAVQA_GEMM_BK
+  const int BK = d.prec ? 32 : (d.a_trans && !sk_enabled() ? SAVQA_GEMM_BK_DW : SAVQA_GEMM_BK);
   const int slots = slots_per_launch();
   const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
   int split = d.split_k > 1 ? d.split_k : 1;
@@ -901,10 +981,11 @@ static void launch_gemm(const savqa_gemm_desc& d, const GemmPlan& p, hipStream_t
 template <int BM, int BN, int BK>
 static void dispatch_layout(const savqa_gemm_desc& d, const GemmPlan& p, hipStream_t s, int avec,
                             int bvec) {
+  constexpr int BKW = SAVQA_GEMM_BK_DW;
   if (!d.a_trans && d.b_trans) launch_gemm<BM, BN, BK, false, true>(d, p, s, avec, bvec);
   else if (!d.a_trans && !d.b_trans) launch_gemm<BM, BN, BK, false, false>(d, p, s, avec, bvec);
-  else if (d.a_trans && !d.b_trans) launch_gemm<BM, BN, BK, true, false>(d, p, s, avec, bvec);
-  else launch_gemm<BM, BN, BK, true, true>(d, p, s, avec, bvec);
+  else if (d.a_trans && !d.b_trans) launch_gemm<BM, BN, BKW, true, false>(d, p, s, avec, bvec);
+  else launch_gemm<BM, BN, BKW, true, true>(d, p, s, avec, bvec);
 }
 
 extern "C" int savqa_gemm_plan(const savqa_gemm_desc* dp, int32_t* out) {

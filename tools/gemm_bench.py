@@ -57,8 +57,9 @@ def main():
             A = torch.randn(k, m, device=dev)
             X = torch.randn(k, n, device=dev)
             C = torch.zeros(m, n, device=dev)
+            sk = int(os.environ.get("SAVQA_BENCH_SPLIT", "-1"))  # forced split-K (A/B)
             f = lambda: ops.gemm(A, X, C, m, n, k, lda=m, ldb=n, ldc=n, a_trans=True, atomic=True,
-                                 split_k=-1, prec=prec)
+                                 split_k=sk, prec=prec)
             g = lambda: torch.mm(A.t(), X, out=C)
         t1 = timeit(f)
         if prec:  # yardstick: torch's bf16 GEMM on bf16 copies
