@@ -88,18 +88,22 @@ struct Operand {
   const float* rp[ITERS];  // FAST path: per-float4 source pointers, resolved once per block
 
   // ROW: stored row = m (tile row), contiguous col = k.  COL: stored row = k, col = m.
+  // mlim: rows (ROW) / columns (COL) of the operand. Edge tiles clamp: a ROW operand's
+  // rows past mlim re-read row mlim-1, a COL operand's float4 groups past mlim re-read the
+  // last group (mlim % 4 == 0); those LDS rows / columns only reach output rows / columns
+  // the epilogue never stores.
   __device__ __forceinline__ void setup_fast(const float* __restrict__ base, int64_t ld,
                                              const int64_t* __restrict__ rows, int64_t m0,
-                                             int tid) {
+                                             int64_t mlim, int tid) {
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
       const int idx = tid + it * GEMM_NT;
       if constexpr (ROW) {
-        const int64_t m = m0 + idx / PER;
+        const int64_t m = min(m0 + idx / PER, mlim - 1);
         const int64_t rr = rows ? rows[m] : m;
         rp[it] = base + rr * ld + (idx % PER) * 4;
       } else {
-        rp[it] = base + (int64_t)(idx / PER) * ld + m0 + (idx % PER) * 4;
+        rp[it] = base + (int64_t)(idx / PER) * ld + min(m0 + (idx % PER) * 4, mlim - 4);
       }
     }
   }
@@ -193,9 +197,9 @@ struct OperandT {
 
   __device__ __forceinline__ void setup_fast(const float* __restrict__ base, int64_t ld,
                                              const int64_t* __restrict__ rows, int64_t m0,
-                                             int tid) {
+                                             int64_t mlim, int tid) {
     (void)rows;  // the fast path never gathers k rows
-    rp = base + (int64_t)(4 * (tid / PER)) * ld + m0 + 4 * (tid % PER);
+    rp = base + (int64_t)(4 * (tid / PER)) * ld + min(m0 + 4 * (tid % PER), mlim - 4);
   }
   __device__ __forceinline__ void load_fast(int64_t ld, int64_t k0) {
 #pragma unroll
@@ -318,7 +322,22 @@ __host__ __device__ constexpr bool gemm_t14() {
   return SAVQA_GEMM_T14 == 2 || (SAVQA_GEMM_T14 == 1 && !AT);
 }
 
-template <int BM, int BN, int BK, bool AT, bool BT, bool FAST>
+// k-loop load mode of a block (block-uniform): 0 = guarded loads everywhere (k-row
+// gathers, unaligned operands, odd edge widths), 1 = branch-free loads on every k-tile,
+// 2 = branch-free except a guarded last k-tile (K not a multiple of BK, e.g. the 300-d
+// GloVe projections).
+template <int BM, int BN, int BK, bool AT, bool BT>
+__device__ __forceinline__ int gemm_mode(const savqa_gemm_desc& d, int64_t m0, int64_t n0,
+                                         int64_t kbeg, int64_t kend, int avec, int bvec) {
+  const bool a_kgather = AT && d.a_rows;
+  const bool b_kgather = !BT && d.b_rows;
+  if (!avec || !bvec || a_kgather || b_kgather) return 0;
+  if (m0 + BM > d.M && AT && (d.M & 3)) return 0;   // COL edge needs whole float4 groups
+  if (n0 + BN > d.N && !BT && (d.N & 3)) return 0;
+  return ((kend - kbeg) % BK == 0) ? 1 : 2;
+}
+
+template <int BM, int BN, int BK, bool AT, bool BT, int MODE>
 __device__ __forceinline__ void gemm_mainloop(
     const savqa_gemm_desc& d, float* smem, int64_t m0, int64_t n0, int64_t kbeg, int64_t kend,
     int ntiles,
@@ -333,19 +352,20 @@ __device__ __forceinline__ void gemm_mainloop(
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  if constexpr (FAST) {
-    la.setup_fast(d.A, d.lda, d.a_rows, m0, tid);
-    lb.setup_fast(d.B, d.ldb, d.b_rows, n0, tid);
+  if constexpr (MODE != 0) {
+    la.setup_fast(d.A, d.lda, d.a_rows, m0, d.M, tid);
+    lb.setup_fast(d.B, d.ldb, d.b_rows, n0, d.N, tid);
   }
-#define SAVQA_GEMM_LOAD(k0)                                         \
-  do {                                                              \
-    if constexpr (FAST) {                                           \
-      la.load_fast(d.lda, (k0));                                    \
-      lb.load_fast(d.ldb, (k0));                                    \
-    } else {                                                        \
-      la.load_slow(d.A, d.lda, d.a_rows, d.M, m0, (k0), kend, tid); \
-      lb.load_slow(d.B, d.ldb, d.b_rows, d.N, n0, (k0), kend, tid); \
-    }                                                               \
+#define SAVQA_GEMM_LOAD(k0)                                          \
+  do {                                                               \
+    const int64_t k0_ = (k0);                                        \
+    if (MODE == 1 || (MODE == 2 && k0_ + BK <= kend)) {              \
+      la.load_fast(d.lda, k0_);                                      \
+      lb.load_fast(d.ldb, k0_);                                      \
+    } else {                                                         \
+      la.load_slow(d.A, d.lda, d.a_rows, d.M, m0, k0_, kend, tid);   \
+      lb.load_slow(d.B, d.ldb, d.b_rows, d.N, n0, k0_, kend, tid);   \
+    }                                                                \
   } while (0)
   SAVQA_GEMM_LOAD(kbeg);
   if (do_cs) la.accum(cs);  // colsum_a: the staged A tile summed over its k rows
@@ -455,11 +475,7 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 #pragma unroll
       for (int r = 0; r < MI::NACC; ++r) acc[i][j][r] = 0.f;
 
-  // block-uniform choice of the branch-free main loop
-  const bool a_kgather = AT && d.a_rows;
-  const bool b_kgather = !BT && d.b_rows;
-  const bool fast = (m0 + BM <= d.M) && (n0 + BN <= d.N) && ((kend - kbeg) % BK == 0) && avec &&
-                    bvec && !a_kgather && !b_kgather;
+  const int mode = gemm_mode<BM, BN, BK, AT, BT>(d, m0, n0, kbeg, kend, avec, bvec);
   const int ntiles = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
   // colsum_a (a_trans only): column tile 0 also sums its A tiles over k (bias gradient)
   const bool do_cs = AT && d.colsum_a != nullptr && tn == 0;
@@ -467,10 +483,12 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 #pragma unroll
   for (int it = 0; it < G::OA::ITERS; ++it) cs[it] = f4{0.f, 0.f, 0.f, 0.f};
   if (ntiles > 0) {
-    if (fast)
-      gemm_mainloop<BM, BN, BK, AT, BT, true>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+    if (mode == 1)
+      gemm_mainloop<BM, BN, BK, AT, BT, 1>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+    else if (mode == 2)
+      gemm_mainloop<BM, BN, BK, AT, BT, 2>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     else
-      gemm_mainloop<BM, BN, BK, AT, BT, false>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      gemm_mainloop<BM, BN, BK, AT, BT, 0>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
   }
   if constexpr (AT) {
     if (do_cs) {  // block-uniform; smem is free after the main loop's last barrier
@@ -540,8 +558,6 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
   int64_t it = sk_begin(w, sk);
   const int64_t it_end = sk_begin(w + 1, sk);
   const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
-  const bool a_kgather = AT && d.a_rows;
-  const bool b_kgather = !BT && d.b_rows;
   for (int r = 0;; ++r) {
     // rounds r < R: the whole tile r*G + w; then this workgroup's stream-K range
     int64_t tile, t0;
@@ -569,18 +585,19 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < MI::NACC; ++r) acc[i][j][r] = 0.f;
-    const bool fast = (m0 + BM <= d.M) && (n0 + BN <= d.N) && ((kend - kbeg) % BK == 0) && avec &&
-                      bvec && !a_kgather && !b_kgather;
+    const int mode = gemm_mode<BM, BN, BK, AT, BT>(d, m0, n0, kbeg, kend, avec, bvec);
     const int ntiles = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
     const bool do_cs = AT && d.colsum_a != nullptr && tn == 0;
     f4 cs[G::OA::ITERS];
 #pragma unroll
     for (int q = 0; q < G::OA::ITERS; ++q) cs[q] = f4{0.f, 0.f, 0.f, 0.f};
     if (ntiles > 0) {
-      if (fast)
-        gemm_mainloop<BM, BN, BK, AT, BT, true>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      if (mode == 1)
+        gemm_mainloop<BM, BN, BK, AT, BT, 1>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      else if (mode == 2)
+        gemm_mainloop<BM, BN, BK, AT, BT, 2>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
       else
-        gemm_mainloop<BM, BN, BK, AT, BT, false>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+        gemm_mainloop<BM, BN, BK, AT, BT, 0>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     }
     if constexpr (AT) {
       if (do_cs) {  // this segment's share of the bias gradient (atomics: segments add up)

@@ -40,8 +40,18 @@ class GemmProbe:
     """Optional per-launch timing of savqa_gemm with HIP events on the launch stream
     (bench.py's roofline measurement). Off unless a probe is installed."""
 
-    def __init__(self):
+    def __init__(self, detail: bool = False):
         self.records = []  # (variant, flops, start_event, end_event)
+        self.detail = detail  # key launches by shape + fused options too (breakdowns)
+
+    @staticmethod
+    def shape_key(d):
+        lay = ("T" if d.a_trans else "N") + ("T" if d.b_trans else "N")
+        opts = "".join(c for c, on in (("g", d.a_rows or d.b_rows), ("s", d.c_rows),
+                                        ("b", d.bias), ("p", d.rowvec), ("r", d.resid),
+                                        ("m", d.mask), ("R", d.relu), ("a", d.atomic),
+                                        ("c", d.colsum_a)) if on)
+        return f"{lay} {d.M}x{d.N}x{d.K} {opts}"
 
     @staticmethod
     def variant(d):
@@ -131,8 +141,10 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
     e0.record()
     call("savqa_gemm", _stream(), C.byref(d))
     e1.record()
-    _probe.records.append((GemmProbe.variant(d),
-                           2.0 * M * N * K, e0, e1))
+    key = GemmProbe.variant(d)
+    if _probe.detail:
+        key += " | " + GemmProbe.shape_key(d)
+    _probe.records.append((key, 2.0 * M * N * K, e0, e1))
 
 
 def linear(X: Tensor, W: Tensor, b: Optional[Tensor], out: Tensor, *, relu=False,
