@@ -10,8 +10,9 @@ same per-epoch eval with accuracy counted on non-zero answers (main:42-142) and 
 Differences (hot path only): the model is savqa_amd.AttModel (HIP kernels), the
 gradient all-reduce is savqa_amd.ddp.GradReducer (RCCL, live gradients only, streamed
 out of the backward) instead of DistributedDataParallel(find_unused_parameters=True),
-Adam is the fused savqa_amd.optim.Adam, and the GQA tar data (absent offline) is
-replaced by savqa_amd.data.synthetic_batch unless a loader is plugged in.
+Adam is the fused savqa_amd.optim.Adam, and the GQA tar data (when present) is
+read by savqa_amd.gqa (same dataset class and items) with the padding done on the
+device (savqa_amd.collate); without the files, savqa_amd.data's synthetic batches.
 """
 from __future__ import annotations
 
@@ -24,6 +25,7 @@ import torch
 import torch.distributed as dist
 
 from .AttModel_x3 import AttModel
+from .collate import forward_inputs, pack, to_device
 from .data import model_args, model_args_rel, synthetic_batch, synthetic_relation_batch
 from .ddp import GradReducer
 from .loss import smoothed_loss
@@ -57,7 +59,24 @@ def build_parser():
     p.add_argument('--model_v', type=int, default=3)
     p.add_argument('--ngpus', type=int, default=-1)
     p.add_argument('--num_nodes', type=int, default=1)
-    # synthetic-data shape (the GQA loader is out of scope)
+    # GQA files under data_dir_azure (main:437-465 defaults); read by savqa_amd.gqa
+    p.add_argument('--fea_tar_fn_train', default='gt_bua_npz.tar')
+    p.add_argument('--q_tar_fn_train', default='train.tar')
+    p.add_argument('--g_tar_fn_train', default='gt_bua_npz.tar')
+    p.add_argument('--fea_tar_fn_val', default='gt_bua_npz.tar')
+    p.add_argument('--q_tar_fn_val', default='val.tar')
+    p.add_argument('--g_tar_fn_val', default='gt_bua_npz.tar')
+    p.add_argument('--gt_relation_fn', default='GT_relations_dict_compsite.json')
+    p.add_argument('--obj_vocab_fn', type=str, default='objects_vocab.txt')
+    p.add_argument('--attr_vocab_fn', type=str, default='attributes_vocab.txt')
+    p.add_argument('--bbox_bin_num', type=int, default=64)
+    p.add_argument('--enc_vocab_fn', type=str, default='preprocessed/de.vocab.composite2.tsv')
+    p.add_argument('--ans_vocab_fn', type=str, default='preprocessed/en.vocab.tsv')
+    p.add_argument('--min_cnt', type=int, default=10)
+    p.add_argument('--num_workers', type=int, default=4)
+    p.add_argument('--synthetic', action='store_true',
+                   help='synthetic batches even when GQA files are present')
+    # synthetic-data shape (used when the GQA files are absent)
     p.add_argument('--steps_per_epoch', type=int, default=10)
     p.add_argument('--num_regions', type=int, default=36)
     p.add_argument('--num_nodes_sg', type=int, default=59)
@@ -68,7 +87,10 @@ def build_parser():
 def run_model(model, batch, args):
     """main:318-329: forward + the MIL-NCE terms the loss subtracts (relation term only
     when only_obj is off)."""
-    inputs = model_args(batch) if args.only_obj else model_args_rel(batch)
+    if "vis_fea_mask" in batch:  # collate_fn keys (GQA reader -> device collate)
+        inputs = forward_inputs(batch)
+    else:
+        inputs = model_args(batch) if args.only_obj else model_args_rel(batch)
     lc, lv, ls, mil, mil_rel = model(*inputs, decMask=args.decMask, mcb=args.mcb)
     return lc, lv, ls, mil, (None if args.only_obj else mil_rel)
 
@@ -90,6 +112,29 @@ def evaluate(model, batches, with_mil, rank, args):
             cnt += valid.sum()
     model.train()
     return meter.avg, float(correct), float(cnt)
+
+
+def gqa_loaders(args, rank):
+    """main:180-249 with the savqa reader: bg_class from the object vocabulary, one
+    DistributedSampler'd DataLoader per split whose collate_fn packs the ragged items
+    (savqa_amd.collate.pack) for one H2D copy + the device-side padding."""
+    import torch.utils.data as tud
+    from .gqa import GQADataset_super_node
+    if not args.only_obj:
+        raise NotImplementedError("GQA reader: only the only_obj loader (onlyobj:41-334) is "
+                                  "implemented; use --synthetic for the relation branch")
+    with open(os.path.join(args.data_dir_azure, args.obj_vocab_fn)) as fid:
+        args.bg_class = len(fid.readlines()) + 1
+    out = {}
+    for split in ("train", "val"):
+        ds = GQADataset_super_node(split, args, getattr(args, f"fea_tar_fn_{split}"),
+                                   getattr(args, f"q_tar_fn_{split}"),
+                                   getattr(args, f"g_tar_fn_{split}"), args.topN, args.with_loc)
+        sampler = tud.distributed.DistributedSampler(ds, num_replicas=args.world_size, rank=rank)
+        out[split] = tud.DataLoader(ds, batch_size=args.batch_size, num_workers=args.num_workers,
+                                    drop_last=True, collate_fn=pack, sampler=sampler,
+                                    pin_memory=True)
+    return out
 
 
 def main(gpu_rank, args):
@@ -116,7 +161,16 @@ def main(gpu_rank, args):
     loss_meter, mil_meter = AverageMeter(), AverageMeter()
     result = {}
 
-    def batches(seed0):
+    gqa = (not args.synthetic) and os.path.exists(
+        os.path.join(args.data_dir_azure, args.q_tar_fn_train))
+    if gqa:
+        loaders = gqa_loaders(args, rank)
+
+    def batches(seed0, split="train"):
+        if gqa:  # main:219-249: GQA reader in DataLoader workers, padding on the device
+            for pk in loaders[split]:
+                yield to_device(pk, dev)
+            return
         for i in range(args.steps_per_epoch):
             if args.only_obj:
                 yield synthetic_batch(args.batch_size, Nv=args.num_regions, Lq=args.q_len,
@@ -147,7 +201,10 @@ def main(gpu_rank, args):
                     logging.info('Time %s, Epoch [%d/%d], Step [%d/%d], Loss: %.5f, MIL NCE Loss: %.5f, '
                                  'Avg Loss: %.5f', datetime.datetime.now(), epoch + 1, args.num_epochs,
                                  i + 1, args.steps_per_epoch, float(loss), -float(mil), loss_meter.avg)
-        val_loss, corr, cnt = evaluate(model, batches(10 ** 6 + rank), args.with_MILNCE_loss, rank, args)
+        if gqa and hasattr(loaders["train"].sampler, "set_epoch"):
+            loaders["train"].sampler.set_epoch(epoch + 1)
+        val_loss, corr, cnt = evaluate(model, batches(10 ** 6 + rank, "val"),
+                                       args.with_MILNCE_loss, rank, args)
         vals = torch.tensor([val_loss, corr, cnt], device=dev)
         if args.world_size > 1:
             gathered = [torch.zeros(3, device=dev) for _ in range(args.world_size)]

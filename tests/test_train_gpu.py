@@ -70,3 +70,23 @@ def test_train_epoch_eval_and_checkpoint_roundtrip(tmp_path, only_obj):
     if not only_obj:
         assert torch.is_tensor(o1[4]) and torch.isfinite(o1[4]).all()
         assert torch.equal(o1[4], o2[4])
+
+
+def test_train_on_gqa_files(tmp_path):
+    """main's data path end to end: GQA files (oracle/gqa_fixture.py, 2048-d features)
+    -> savqa_amd.gqa reader in DataLoader workers -> collate.pack -> device padding ->
+    train + eval + checkpoint."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from oracle import gqa_fixture as fx
+    from savqa_amd import train
+    fx.write_dataset(str(tmp_path / "gqa"), n_questions=16, fea_dim=2048)
+    argv = [a for a in _ARGS]
+    i = argv.index("--topN")
+    argv[i + 1] = "5"
+    argv += ["--maxlen", "60", "--only_obj", "--with_loc", "--data_dir_azure",
+             str(tmp_path / "gqa"), "--output_dir", "out", "--num_workers", "2"]
+    res = train.cli(argv)
+    assert res["epoch"] == 1
+    assert res["train_loss"] == res["train_loss"] and res["val_loss"] == res["val_loss"]
+    assert (tmp_path / "gqa" / "out" / "model_1.pth").exists()

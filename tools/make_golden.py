@@ -304,6 +304,37 @@ def collate_cases():
     print("wrote collate.npz")
 
 
+READER_CASES = {"loc_top5": dict(with_loc=True, pred_rel=False, topN=5),
+                "noloc_pred_top3": dict(with_loc=False, pred_rel=True, topN=3)}
+
+
+def reader_cases():
+    """Reference GQADataset_super_node (onlyobj:41-334) items on the synthetic GQA files of
+    oracle/gqa_fixture.py, python `random` seeded per item -> tests/golden/gqa_reader.npz."""
+    import random
+    import tempfile
+    from oracle import gqa_fixture as fx
+    import data_loader_itp_bbox_super_node_onlyobj as onlyobj_mod  # noqa: E402  (reference)
+    out = {}
+    with tempfile.TemporaryDirectory() as root:
+        fx.write_dataset(root)
+        for name, kw in READER_CASES.items():
+            ds = onlyobj_mod.GQADataset_super_node(
+                "train", fx.Opt(root, pred_rel=kw["pred_rel"]), "gt_bua_npz.tar", "train.tar",
+                "gt_bua_npz.tar", kw["topN"], with_loc=kw["with_loc"])
+            out[f"{name}:len"] = np.int64(len(ds))
+            for i in range(len(ds)):
+                random.seed(1000 + i)
+                item = ds[i]
+                out[f"{name}:{i}:none"] = np.bool_(item is None)
+                if item is None:
+                    continue
+                for f, v in zip(fx.ITEM_FIELDS, item):
+                    out[f"{name}:{i}:{f}"] = np.asarray(v)
+    np.savez_compressed(os.path.join(OUT, "gqa_reader.npz"), **out)
+    print("wrote gqa_reader.npz", len(out))
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference absent; nothing to do")
@@ -321,6 +352,8 @@ def main():
         relation_cases(att_mod)
     if "collate" in which:
         collate_cases()
+    if "reader" in which:
+        reader_cases()
 
 
 if __name__ == "__main__":
