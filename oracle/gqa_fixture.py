@@ -33,6 +33,11 @@ ATTRS = ["red", "blue", "green", "small", "large", "wooden", "white", "black"]
 RELS = {"man,dog": "to the left of", "dog,man": "to the right of", "cup,table": "on top of",
         "table,cup": "at the bottom of", "woman,car": "near", "tree,sky": "below",
         "man,shirt": "wearing", "cat,ball": "to the left of", "stop,car": "in front of"}
+# more categories, so that negative relation sampling (up to topN^2 per pair, super_node
+# :238-240) has a large enough pool
+for _k, (_a, _b) in enumerate(zip(OBJECTS[::2], OBJECTS[1::2] + OBJECTS[:1])):
+    RELS[_a.replace(" ", "") + "," + _b.replace(" ", "")] = f"extra relation {_k}"
+    RELS[_b.replace(" ", "") + "," + _a.replace(" ", "")] = f"extra inverse {_k}"
 QWORDS = ["what", "color", "is", "the", "left", "of", "man", "dog", "who", "wearing"]
 
 
@@ -151,3 +156,9 @@ ITEM_FIELDS = ("vis_fea", "macro_nodes_idx", "macro_obj_locs", "macro_edges",
 SYNONYMS = {"alarm clock": "clock", "in front of": "front", "on top of": "top",
             "stop sign": "stop", "tennis court": "field", "to the left of": "left",
             "to the right of": "right", "tv": "television"}
+
+# fields of one relation-loader item (super_node:353-357)
+ITEM_FIELDS_REL = ITEM_FIELDS[:6] + ("micro_positive_relations_wrd",
+                                     "micro_negative_relations_wrd",
+                                     "micro_positive_relations_loc",
+                                     "micro_negative_relations_loc") + ITEM_FIELDS[6:]

@@ -309,9 +309,34 @@ class AttModel(nn.Module):
         if not self.only_obj:  # relation branch inputs (micro_negative_rel ids are unused, :391)
             tensors = tensors + (i64(micro_positive_rel), i64(micro_positive_rel_loc),
                                  i64(micro_negative_rel_loc))
+            self._check_relation_locs(tensors[-2], tensors[-1], vis_fea.shape[1],
+                                      macro_ipt.shape[1], tensors[-3].shape[1])
         anchor = self._arena_anchor()
         lc, lv, ls, mil, mil_rel = _AttModelFn.apply(self, bool(decMask), drop, anchor, *tensors)
         return lc, lv, ls, mil, (mil_rel if not self.only_obj else 0)
+
+    def _check_relation_locs(self, pos, neg, n_obj, n_macro, n_rel):
+        """The reference indexes rels_bilinear / new_macro_ipt with these columns
+        (AttModel_x3.py:401-437) and fails with IndexError on a bad one; the kernels would
+        read outside their buffers instead, so the listed rows are bounds-checked here
+        (one device reduction + one host read per relation-mode step)."""
+        nrel = self.MIL_NCE.num_relations
+        bad = []
+        for loc, w in ((pos, 5), (neg, 4)):
+            if loc.numel() == 0:
+                continue
+            if loc.dim() != 3 or loc.shape[2] < w:
+                raise IndexError(f"relation locations need shape (B, L, >={w}), got {tuple(loc.shape)}")
+            v = loc[..., 3] >= 0
+            b = (loc[..., 0] < 0) | (loc[..., 0] >= n_obj) | (loc[..., 1] < 0) | \
+                (loc[..., 1] >= n_obj) | (loc[..., 2] < 0) | (loc[..., 2] >= nrel) | \
+                (loc[..., 3] >= n_macro)
+            if w == 5:
+                b = b | (loc[..., 4] < 0) | (loc[..., 4] >= n_rel)
+            bad.append((v & b).any())
+        if bad and bool(torch.stack(bad).any()):
+            raise IndexError("relation location out of range (objects / categories "
+                             f"< {nrel} / macro nodes / positive words)")
 
     def _arena_anchor(self):
         # any parameter that requires grad links the autograd node into the graph

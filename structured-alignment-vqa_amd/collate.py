@@ -159,6 +159,9 @@ def pack(data, relations: Optional[bool] = None,
             (lambda a: a.ndim == 1)
         for a in arrs:
             a = np.asarray(a, dtype=np.int64)
+            if a.size == 0:  # nothing to place (e.g. a single-object image's relations)
+                out.append(np.zeros((0, R) if R > 1 else (0,), np.int64))
+                continue
             n = a.shape[0] if a.ndim else 1
             if n > T:
                 raise ValueError(f"collate: {what} has {n} rows, more than the padded {T}")
@@ -190,17 +193,19 @@ def pack(data, relations: Optional[bool] = None,
                for a in cols["micro_positive_relations_wrd"]]
         T_r = max(a.shape[0] for a in prw)
         keep = [a.shape[0] != 0 for a in prw]
-        nrw = rows_of(cols["micro_negative_relations_wrd"], 1, T_r, "micro_negative_relations_wrd")
-        prl = rows_of(cols["micro_positive_relations_loc"], 5, T_r, "micro_positive_relations_loc")
-        nrl = rows_of(cols["micro_negative_relations_loc"], 4, T_r, "micro_negative_relations_loc")
 
-        def kept(arrs, R):
-            return [a if k else np.zeros((0, R) if R > 1 else (0,), np.int64)
-                    for a, k in zip(arrs, keep)]
+        def only_kept(name):  # samples without positives are never read (super_node:434)
+            return [a if k else () for a, k in zip(cols[name], keep)]
+        nrw = rows_of(only_kept("micro_negative_relations_wrd"), 1, T_r,
+                      "micro_negative_relations_wrd")
+        prl = rows_of(only_kept("micro_positive_relations_loc"), 5, T_r,
+                      "micro_positive_relations_loc")
+        nrl = rows_of(only_kept("micro_negative_relations_loc"), 4, T_r,
+                      "micro_negative_relations_loc")
         plan += [("micro_positive_rel_ipt", ROWS, torch.int64, T_r, 1, PAD, prw),
-                 ("micro_negative_rel_ipt", ROWS, torch.int64, T_r, 1, PAD, kept(nrw, 1)),
-                 ("micro_positive_rel_loc", ROWS, torch.int64, T_r, 5, LOC_PAD, kept(prl, 5)),
-                 ("micro_negative_rel_loc", ROWS, torch.int64, T_r, 4, LOC_PAD, kept(nrl, 4))]
+                 ("micro_negative_rel_ipt", ROWS, torch.int64, T_r, 1, PAD, nrw),
+                 ("micro_positive_rel_loc", ROWS, torch.int64, T_r, 5, LOC_PAD, prl),
+                 ("micro_negative_rel_loc", ROWS, torch.int64, T_r, 4, LOC_PAD, nrl)]
     plan += [("q_ipt", ROWS, torch.int64, T_q, 1, PAD, qn),
              ("q_ipt_mask", BOX, torch.int32, T_q, T_q, 1, "q_ipt"),
              ("q_ipt_graph", FILL, torch.int32, T_q, T_q, 0, None),

@@ -43,6 +43,11 @@ __global__ __launch_bounds__(256) void rel_entries_fwd_kernel(RelSlots s, const 
     if (lane == 0) val[slot] = 0.f;
     return;
   }
+  // bounds (the host checks them too): a bad row scores NaN instead of reading outside
+  if (lr[0] < 0 || lr[0] >= Nv || lr[1] < 0 || lr[1] >= Nv || lr[2] < 0 || (lr[2] + 1) * H > ldv) {
+    if (lane == 0) val[slot] = __builtin_nanf("");
+    return;
+  }
   const int b = slot / s.L;
   const float* xi = obj + ((int64_t)b * Nv + lr[0]) * H;
   const float* vr = V + ((int64_t)b * Nv + lr[1]) * ldv + lr[2] * (int64_t)H;
@@ -64,7 +69,9 @@ __global__ __launch_bounds__(256) void rel_entries_bwd_kernel(RelSlots s, const 
   const int slot = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (slot >= s.B * s.L) return;
   const int64_t* lr = s.loc + (int64_t)slot * s.W;
-  if (lr[3] < 0) return;
+  if (lr[3] < 0 || lr[0] < 0 || lr[0] >= Nv || lr[1] < 0 || lr[1] >= Nv || lr[2] < 0 ||
+      (lr[2] + 1) * H > ldv)
+    return;
   const float g = dval[slot];
   if (g == 0.f) return;
   const int b = slot / s.L;

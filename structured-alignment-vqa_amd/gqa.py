@@ -1,5 +1,6 @@
-"""GQA real-data reader: the only_obj super-node dataset of
-models/data_loader_itp_bbox_super_node_onlyobj.py:41-334, same constructor, same
+"""GQA real-data reader (rank 1's relation loader): the only_obj
+super-node dataset of models/data_loader_itp_bbox_super_node_onlyobj.py:41-334 and the
+relation loader of dataloader/data_loader_itp_bbox_super_node.py:41-357, same constructor, same
 per-item tuple, same failure behaviour (an item that cannot be built is None and is
 dropped by the collate), same use of python's `random` for the negative words -- so
 seeded runs reproduce the reference's items exactly (tests/test_gqa_reader_cpu.py).
@@ -98,7 +99,10 @@ class GQADataset_super_node(tud.Dataset):
         self.bg_class = opt.bg_class
         with open(os.path.join(root, opt.gt_relation_fn)) as f:
             self.gt_relations = json.load(f)
-        self.num_relations = len(set(self.gt_relations.values()))
+        # category order = python's set order of the names, as in the reference (it follows
+        # PYTHONHASHSEED; pin that variable for reproducible relation indices)
+        self.gt_relation_clean = list(set(self.gt_relations.values()))
+        self.num_relations = len(self.gt_relation_clean)
         with open(self.gt_graph_fn) as f:
             self.gt_graph = json.load(f)
         with open(os.path.join(root, opt.obj_vocab_fn)) as f:
@@ -202,40 +206,163 @@ class GQADataset_super_node(tud.Dataset):
     def _word_id(self, w):
         return self.enc_w2id.get(self.word_converter.get(w, w), UNK)
 
+    def _question(self, index):
+        qinfo = json.loads(self._q.read(self.q_list[index]))
+        answer = np.asarray(self.ans_w2id.get(qinfo["answer"], 0)).astype("int32")
+        return qinfo["node_list"], qinfo["edge_pair"], answer, qinfo["image_id"]
+
+    def _image(self, image_id):
+        """Features, binned boxes and the detector info of one image (onlyobj:253-285)."""
+        gt_graph = self.gt_graph[image_id]
+        vis_fea = np.load(io.BytesIO(self._fea.read(self.fea_dict[image_id])))["x"]
+        # the graph archive carries a pickled `info` dict, as written by the GQA
+        # preprocessing; it is the user's data file, read like the reference does
+        data = np.load(io.BytesIO(self._g.read(self.g_dict[image_id])), allow_pickle=True)
+        bbox = data["bbox"]
+        if len(bbox.shape) == 1:
+            bbox = np.reshape(bbox, (1, bbox.size))
+        bbox[:, 0] /= data["image_w"]
+        bbox[:, 2] /= data["image_w"]
+        bbox[:, 1] /= data["image_h"]
+        bbox[:, 3] /= data["image_h"]
+        bbox = np.floor(bbox * self.opt.bbox_bin_num).astype("int32")
+        return gt_graph, vis_fea, bbox, data["info"].tolist()
+
+    def _too_long(self, n_macro, n_q):
+        if n_macro + n_q >= self.len_threshold:
+            if self.split in ("val", "test"):
+                print("len", n_macro + n_q)
+            return True
+        return False
+
     def __getitem__(self, index):
         """onlyobj:243-334. Returns the collate tuple or None."""
-        q_mem = self.q_list[index]
-        qinfo = json.loads(self._q.read(q_mem))
-        qnode, qedge = qinfo["node_list"], qinfo["edge_pair"]
-        answer = np.asarray(self.ans_w2id.get(qinfo["answer"], 0)).astype("int32")
-        image_id = qinfo["image_id"]
+        qnode, qedge, answer, image_id = self._question(index)
         try:
-            gt_graph = self.gt_graph[image_id]
-            vis_fea = np.load(io.BytesIO(self._fea.read(self.fea_dict[image_id])))["x"]
-            # the graph archive carries a pickled `info` dict, as written by the GQA
-            # preprocessing; it is the user's data file, read like the reference does
-            data = np.load(io.BytesIO(self._g.read(self.g_dict[image_id])), allow_pickle=True)
-            bbox = data["bbox"]
-            if len(bbox.shape) == 1:
-                bbox = np.reshape(bbox, (1, bbox.size))
-            bbox[:, 0] /= data["image_w"]
-            bbox[:, 2] /= data["image_w"]
-            bbox[:, 1] /= data["image_h"]
-            bbox[:, 3] /= data["image_h"]
-            bbox = np.floor(bbox * self.opt.bbox_bin_num).astype("int32")
+            gt_graph, vis_fea, bbox, info = self._image(image_id)
             macro_nodes, macro_edges, obj_locs, pos_nodes, neg_nodes = self.convert_graph(
-                data["info"].tolist(), self.opt.bg_class, bbox, gt_graph)
+                info, self.opt.bg_class, bbox, gt_graph)
             macro_idx = [PAD if n == PAD else self._word_id(n) for n in macro_nodes]
             q_idx = [self.enc_w2id.get(w, UNK) for w in qnode]
-            if len(macro_idx) + len(q_idx) >= self.len_threshold:
-                if self.split in ("val", "test"):
-                    print("len", len(macro_idx) + len(q_idx))
+            if self._too_long(len(macro_idx), len(q_idx)):
                 return None
             pos_w = [[self._word_id(w) for w in ws] for ws in pos_nodes]
             neg_w = [[self._word_id(w) for w in ws] for ws in neg_nodes]
             return (vis_fea, np.asarray(macro_idx).astype("int64"),
                     np.asarray(obj_locs).astype("int64"), macro_edges,
                     np.asarray(pos_w).astype("int64"), np.asarray(neg_w).astype("int64"),
+                    np.asarray(q_idx).astype("int64"), qedge, answer, self.topN)
+        except Exception:  # the reference's bare except: an unreadable item is None
+            return None
+
+
+class GQADataset_super_node_rel(GQADataset_super_node):
+    """The relation loader (dataloader/data_loader_itp_bbox_super_node.py:41-357): same
+    files and constructor; every ordered object pair gets an empty relation node, and the
+    item carries the positive / negative relation words and their locations
+    [obj_i, obj_j, category, macro_rel_loc(, micro_rel_loc)] for the MIL-NCE relation
+    branch (14-field tuple, collate_fn :366-497)."""
+
+    def convert_graph(self, data_info, bg_class, bbox, gt_graph):
+        """super_node:123-249."""
+        micro_pos, micro_neg, empty, attrs = [], [], [], []
+        for obj_idxs, obj, attr_idx in zip(data_info["objects_id"], gt_graph["objects"],
+                                           data_info["attrs_id"]):
+            gt_name = gt_graph["objects"][obj]["name"].strip().replace(" ", "")
+            nodes_obj = [gt_name]
+            for oi in obj_idxs:  # (no detection-correctness flag in this loader)
+                if len(nodes_obj) < self.topN:
+                    if oi < len(self.vg_classes) and self._vg_nospace[oi] != gt_name:
+                        nodes_obj.append(self._vg_nospace[oi])
+                else:
+                    break
+            empty.append(PAD)
+            attrs.append(self.vg_attrs[attr_idx].replace(" ", ""))
+            micro_pos.append(nodes_obj)
+            population = [c for c in self._vg_nospace if c not in nodes_obj]
+            micro_neg.append(random.sample(population, self.topN))
+
+        n_obj = len(empty)
+        macro_node, macro_rel, obj_loc, idx_obj = [], [], [], []
+        attr_pos, corner_pos, rel_loc = {}, {}, {}
+
+        def node_at(table, name):
+            if name in table:
+                return table[name]
+            table[name] = len(macro_node)
+            macro_node.append(name)
+            return table[name]
+
+        for i in range(n_obj):
+            p_obj = len(macro_node)
+            macro_node.append(empty[i])
+            obj_loc.append(p_obj)
+            p_attr = node_at(attr_pos, attrs[i])
+            macro_rel += [[p_obj, p_attr], [p_attr, p_obj]]
+            idx_obj.append(p_obj)
+            if self.with_loc:
+                for cx, cy in ((0, 1), (2, 3)):
+                    p = node_at(corner_pos, "x" + str(bbox[i][cx].item()) + "y" + str(bbox[i][cy]))
+                    macro_rel += [[p_obj, p], [p, p_obj]]
+        for i in range(n_obj):  # one empty relation node per ordered pair (:190-201)
+            for j in range(n_obj):
+                if i != j:
+                    rel_loc[(i, j)] = len(macro_node)
+                    macro_node.append("__empty__")
+                    macro_rel += [[idx_obj[i], rel_loc[(i, j)]], [rel_loc[(i, j)], idx_obj[j]]]
+
+        n_cat = len(self.gt_relation_clean)
+        cat_of = {name: k for k, name in reversed(list(enumerate(self.gt_relation_clean)))}
+        pos_words, neg_words, pos_loc, neg_loc = [], [], [], []
+        micro_pos_ctr = 0
+        for i in range(n_obj):  # every (word_i, word_j) of every ordered pair (:203-247)
+            for j in range(n_obj):
+                if i == j:
+                    continue
+                pair_words, pair_idx = [], []
+                for wi in micro_pos[i]:
+                    for wj in micro_pos[j]:
+                        key = wi + "," + wj
+                        if key in self.gt_relations:
+                            name = self.gt_relations[key]
+                            r_idx = cat_of[name]
+                            pair_words.append(name.replace(" ", ""))
+                        else:
+                            r_idx = self.num_relations  # the PAD category
+                            pair_words.append(PAD)
+                        pos_loc.append([i, j, r_idx, rel_loc[(i, j)], micro_pos_ctr])
+                        pair_idx.append(r_idx)
+                        micro_pos_ctr += 1
+                pos_words += pair_words
+                neg_pool = [k for k in range(n_cat) if k not in pair_idx]
+                for r_idx in random.sample(neg_pool, len(pair_words)):
+                    neg_loc.append([i, j, r_idx, rel_loc[(i, j)]])
+                    neg_words.append(self.gt_relation_clean[r_idx] if r_idx != n_cat else PAD)
+        return (macro_node, macro_rel, obj_loc, micro_pos, micro_neg, pos_words, neg_words,
+                pos_loc, neg_loc)
+
+    def __getitem__(self, index):
+        """super_node:250-357. Returns the 14-field collate tuple or None."""
+        qnode, qedge, answer, image_id = self._question(index)
+        try:
+            gt_graph, vis_fea, bbox, info = self._image(image_id)
+            (macro_nodes, macro_edges, obj_locs, pos_nodes, neg_nodes, pos_rel, neg_rel,
+             pos_rel_loc, neg_rel_loc) = self.convert_graph(info, self.opt.bg_class, bbox,
+                                                            gt_graph)
+            macro_idx = [PAD if n == PAD else self._word_id(n) for n in macro_nodes]
+            q_idx = [self.enc_w2id.get(w, UNK) for w in qnode]
+            if self._too_long(len(macro_idx), len(q_idx)):
+                return None
+            pos_w = [[self._word_id(w) for w in ws] for ws in pos_nodes]
+            neg_w = [[self._word_id(w) for w in ws] for ws in neg_nodes]
+            pos_rw = [self._word_id(w) for w in pos_rel]  # PAD words look up as UNK (:340)
+            neg_rw = [self._word_id(w) for w in neg_rel]
+            return (vis_fea, np.asarray(macro_idx).astype("int64"),
+                    np.asarray(obj_locs).astype("int64"), macro_edges,
+                    np.asarray(pos_w).astype("int64"), np.asarray(neg_w).astype("int64"),
+                    np.asarray(pos_rw).astype("int64"), np.asarray(neg_rw).astype("int64"),
+                    np.asarray(pos_rel_loc).astype("int64"),
+                    np.asarray(neg_rel_loc).astype("int64"),
                     np.asarray(q_idx).astype("int64"), qedge, answer, self.topN)
         except Exception:  # the reference's bare except: an unreadable item is None
             return None

@@ -119,15 +119,13 @@ def gqa_loaders(args, rank):
     DistributedSampler'd DataLoader per split whose collate_fn packs the ragged items
     (savqa_amd.collate.pack) for one H2D copy + the device-side padding."""
     import torch.utils.data as tud
-    from .gqa import GQADataset_super_node
-    if not args.only_obj:
-        raise NotImplementedError("GQA reader: only the only_obj loader (onlyobj:41-334) is "
-                                  "implemented; use --synthetic for the relation branch")
+    from .gqa import GQADataset_super_node, GQADataset_super_node_rel
+    cls = GQADataset_super_node if args.only_obj else GQADataset_super_node_rel  # main:207-211
     with open(os.path.join(args.data_dir_azure, args.obj_vocab_fn)) as fid:
         args.bg_class = len(fid.readlines()) + 1
     out = {}
     for split in ("train", "val"):
-        ds = GQADataset_super_node(split, args, getattr(args, f"fea_tar_fn_{split}"),
+        ds = cls(split, args, getattr(args, f"fea_tar_fn_{split}"),
                                    getattr(args, f"q_tar_fn_{split}"),
                                    getattr(args, f"g_tar_fn_{split}"), args.topN, args.with_loc)
         sampler = tud.distributed.DistributedSampler(ds, num_replicas=args.world_size, rank=rank)
@@ -148,6 +146,12 @@ def main(gpu_rank, args):
         logging.basicConfig(level=logging.INFO, format='%(asctime)s %(levelname)-8s %(message)s')
     if args.model_v != 3:
         raise NotImplementedError("only model_v=3 is on the savqa hot path")
+    gqa = (not args.synthetic) and os.path.exists(
+        os.path.join(args.data_dir_azure, args.q_tar_fn_train))
+    if gqa:
+        loaders = gqa_loaders(args, rank)
+        if not args.only_obj:  # main:194-196: the categories + 'no relation'
+            args.num_relations = loaders["train"].dataset.num_relations + 1
     model = AttModel(None, args.hidden_size, args.hidden_size_mil, args.num_classes, args.maxlen_q,
                      args.maxlen, args.maxlen_v, args.num_blocks, args.num_heads, args.dropout_rate,
                      args.dropout_rate_mcb, args.num_relations, args.only_obj, device=dev,
@@ -160,11 +164,6 @@ def main(gpu_rank, args):
         model.attach_reducer(reducer)
     loss_meter, mil_meter = AverageMeter(), AverageMeter()
     result = {}
-
-    gqa = (not args.synthetic) and os.path.exists(
-        os.path.join(args.data_dir_azure, args.q_tar_fn_train))
-    if gqa:
-        loaders = gqa_loaders(args, rank)
 
     def batches(seed0, split="train"):
         if gqa:  # main:219-249: GQA reader in DataLoader workers, padding on the device

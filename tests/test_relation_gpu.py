@@ -70,3 +70,23 @@ def test_relation_branch_against_reference_golden():
     assert rel(params["MIL_NCE.R"].grad[used, :4].cpu().numpy(), g["R_grad_used"]) < 1e-3
     opt.step()
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("col,value", [(2, 4), (0, 99), (3, 10 ** 6), (4, 10 ** 6)])
+def test_relation_locations_out_of_range_raise(col, value):
+    """A relation row the reference would fail to index (IndexError) raises before any
+    kernel reads outside its buffers."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from savqa_amd.AttModel_x3 import AttModel
+    from savqa_amd.data import model_args_rel, synthetic_relation_batch
+    from savqa_amd.utils import init_params_
+    m = AttModel(None, 256, 64, 12, 16, 80, 10, 2, 4, 0.0, 0.0, 4, False, device="cuda",
+                 init=False)
+    init_params_(m, seed=2)
+    b = synthetic_relation_batch(2, Nv=4, Lq=5, topN=2, num_relations=4, num_classes=12,
+                                 seed=3, device="cuda")
+    m(*model_args_rel(b), decMask=True, mcb=False)  # in range: runs
+    b["micro_positive_rel_loc"][1, 3, col] = value
+    with pytest.raises(IndexError):
+        m(*model_args_rel(b), decMask=True, mcb=False)

@@ -72,7 +72,8 @@ def test_train_epoch_eval_and_checkpoint_roundtrip(tmp_path, only_obj):
         assert torch.equal(o1[4], o2[4])
 
 
-def test_train_on_gqa_files(tmp_path):
+@pytest.mark.parametrize("only_obj", [True, False], ids=["only_obj", "relations"])
+def test_train_on_gqa_files(tmp_path, only_obj):
     """main's data path end to end: GQA files (oracle/gqa_fixture.py, 2048-d features)
     -> savqa_amd.gqa reader in DataLoader workers -> collate.pack -> device padding ->
     train + eval + checkpoint."""
@@ -83,9 +84,9 @@ def test_train_on_gqa_files(tmp_path):
     fx.write_dataset(str(tmp_path / "gqa"), n_questions=16, fea_dim=2048)
     argv = [a for a in _ARGS]
     i = argv.index("--topN")
-    argv[i + 1] = "5"
-    argv += ["--maxlen", "60", "--only_obj", "--with_loc", "--data_dir_azure",
-             str(tmp_path / "gqa"), "--output_dir", "out", "--num_workers", "2"]
+    argv[i + 1] = "5" if only_obj else "2"  # relation loader: topN^2 words per object pair
+    argv += ["--maxlen", "80", "--with_loc", "--data_dir_azure", str(tmp_path / "gqa"),
+             "--output_dir", "out", "--num_workers", "2"] + (["--only_obj"] if only_obj else [])
     res = train.cli(argv)
     assert res["epoch"] == 1
     assert res["train_loss"] == res["train_loss"] and res["val_loss"] == res["val_loss"]

@@ -305,7 +305,9 @@ def collate_cases():
 
 
 READER_CASES = {"loc_top5": dict(with_loc=True, pred_rel=False, topN=5),
-                "noloc_pred_top3": dict(with_loc=False, pred_rel=True, topN=3)}
+                "noloc_pred_top3": dict(with_loc=False, pred_rel=True, topN=3),
+                "rel_loc_top3": dict(with_loc=True, pred_rel=False, topN=3, rel=True),
+                "rel_noloc_top2": dict(with_loc=False, pred_rel=False, topN=2, rel=True)}
 
 
 def reader_cases():
@@ -315,11 +317,17 @@ def reader_cases():
     import tempfile
     from oracle import gqa_fixture as fx
     import data_loader_itp_bbox_super_node_onlyobj as onlyobj_mod  # noqa: E402  (reference)
-    out = {}
+    sys.path.insert(0, os.path.join(os.path.dirname(REF), "dataloader"))
+    import data_loader_itp_bbox_super_node as super_mod  # noqa: E402  (reference)
+    # the relation loader's category order is python's set order (PYTHONHASHSEED)
+    assert os.environ.get("PYTHONHASHSEED") == "0", "run with PYTHONHASHSEED=0"
+    out = {"hashseed": np.int64(0)}
     with tempfile.TemporaryDirectory() as root:
         fx.write_dataset(root)
         for name, kw in READER_CASES.items():
-            ds = onlyobj_mod.GQADataset_super_node(
+            mod = super_mod if kw.get("rel") else onlyobj_mod
+            fields = fx.ITEM_FIELDS_REL if kw.get("rel") else fx.ITEM_FIELDS
+            ds = mod.GQADataset_super_node(
                 "train", fx.Opt(root, pred_rel=kw["pred_rel"]), "gt_bua_npz.tar", "train.tar",
                 "gt_bua_npz.tar", kw["topN"], with_loc=kw["with_loc"])
             out[f"{name}:len"] = np.int64(len(ds))
@@ -329,7 +337,7 @@ def reader_cases():
                 out[f"{name}:{i}:none"] = np.bool_(item is None)
                 if item is None:
                     continue
-                for f, v in zip(fx.ITEM_FIELDS, item):
+                for f, v in zip(fields, item):
                     out[f"{name}:{i}:{f}"] = np.asarray(v)
     np.savez_compressed(os.path.join(OUT, "gqa_reader.npz"), **out)
     print("wrote gqa_reader.npz", len(out))
