@@ -691,7 +691,14 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 // 8 short MFMA chains instead of 32 workgroups of one long one. Operands go straight from
 // global memory (L2) into MFMA registers: lane half q of an 8-k group takes k = 8g+4q+s,
 // s = 0..3 -- one b128 load on a k-contiguous operand, 4 coalesced scalars otherwise.
-constexpr int SK_WAVES = 8;
+#ifndef SAVQA_SK_WAVES
+#define SAVQA_SK_WAVES 8
+#endif
+#ifndef SAVQA_SK_DEPTH
+#define SAVQA_SK_DEPTH 2  // 4 and 8 measured no faster (tools/ab_skinny.sh)
+#endif
+constexpr int SK_WAVES = SAVQA_SK_WAVES;
+constexpr int SK_DEPTH = SAVQA_SK_DEPTH;
 
 template <bool KCONTIG>
 __device__ __forceinline__ void sk_load4(const float* __restrict__ P, int64_t ld,
@@ -744,8 +751,7 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(savqa_gemm_d
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   float cs = 0.f;  // colsum_a partial (AT): sum over this wave's k of A(m0 + i, k), half q
-  // software pipeline: the loads of group pair p+1 are in flight while pair p's MFMAs run
-  float a[2][2][4], b[2][2][4];
+  float a[SK_DEPTH][2][4], b[SK_DEPTH][2][4];
   auto load_pair = [&](int64_t gg, float (&aa)[2][4], float (&bb)[2][4]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -763,14 +769,21 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(savqa_gemm_d
       for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(aa[u][s], bb[u][s], acc, 0, 0, 0);
     }
   };
+  // SK_DEPTH group pairs in flight: the k range of a wave is short (K/8), so global-load
+  // latency, not the MFMAs, bounds these launches; a ring of register buffers with
+  // compile-time slots keeps SK_DEPTH loads outstanding while the oldest is consumed
   const int npair = (int)((g1 - g0 + 1) / 2);
-  if (npair > 0) load_pair(g0, a[0], b[0]);
-  for (int pi = 0; pi < npair; pi += 2) {  // buffers alternate with compile-time indices
-    if (pi + 1 < npair) load_pair(g0 + 2 * (pi + 1), a[1], b[1]);
-    mma_pair(a[0], b[0]);
-    if (pi + 1 >= npair) break;
-    if (pi + 2 < npair) load_pair(g0 + 2 * (pi + 2), a[0], b[0]);
-    mma_pair(a[1], b[1]);
+#pragma unroll
+  for (int q2 = 0; q2 < SK_DEPTH; ++q2)
+    if (q2 < npair) load_pair(g0 + 2 * q2, a[q2], b[q2]);
+  for (int pi = 0; pi < npair; pi += SK_DEPTH) {
+#pragma unroll
+    for (int q2 = 0; q2 < SK_DEPTH; ++q2) {
+      if (pi + q2 < npair) {
+        mma_pair(a[q2], b[q2]);
+        if (pi + q2 + SK_DEPTH < npair) load_pair(g0 + 2 * (pi + q2 + SK_DEPTH), a[q2], b[q2]);
+      }
+    }
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[w][(r & 3) + 8 * (r >> 2) + 4 * q][i] = acc[r];
