@@ -68,6 +68,11 @@ struct Mi16 {
   static __device__ __forceinline__ int row(int r, int lane) { return 4 * (lane >> 4) + r; }
   static __device__ __forceinline__ int col(int lane) { return lane & 15; }
 };
+// epilogue operand prefetch: 0 = none (one load per element, after the previous store),
+// 1 = mask bits + residual per 32-row fragment, 2 = the tile's mask bits up front
+#ifndef SAVQA_EPI_PRE
+#define SAVQA_EPI_PRE 1
+#endif
 #ifndef SAVQA_GEMM_MI
 #define SAVQA_GEMM_MI 32
 #endif
@@ -498,6 +503,12 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 
   // ---------------------------------------------------------------- epilogue
   const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
+  // Operands of the epilogue are fetched before a fragment's first store: vmcnt also
+  // counts stores, so a load issued after a store waits for it, and one load per element
+  // (bias, ReLU-backward mask, residual) serialised a memory round trip per element.
+  //   bias: FN values per lane and the mask bits (rows indexed by m) for the whole tile,
+  //   the residual per 32-row fragment (a whole tile's would spill).
+#if SAVQA_EPI_PRE == 0
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -514,6 +525,94 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
     }
   }
 }
+#else
+  const bool mask_pre = d.mask && !d.mask_arows;
+  const bool res_pre = first_split && d.resid != nullptr;
+  float bv[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int64_t n = min(n0 + wn * WN + j * MI::FR + MI::col(lane), (int64_t)d.N - 1);
+    bv[j] = (first_split && d.bias) ? d.bias[n] : 0.f;
+  }
+  uint32_t keep[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {  // mask bits of the whole tile before its first store
+    keep[i] = 0xffffffffu;
+    if (SAVQA_EPI_PRE == 2 && mask_pre) {
+      float mv[MI::NACC][FN];
+#pragma unroll
+      for (int r = 0; r < MI::NACC; ++r) {
+        const int64_t m = min(m0 + wm * WM + i * MI::FR + MI::row(r, lane), (int64_t)d.M - 1);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int64_t n = min(n0 + wn * WN + j * MI::FR + MI::col(lane), (int64_t)d.N - 1);
+          mv[r][j] = d.mask[m * d.ldmask + n];
+        }
+      }
+      keep[i] = 0;
+#pragma unroll
+      for (int r = 0; r < MI::NACC; ++r)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) keep[i] |= (mv[r][j] > 0.f ? 1u : 0u) << (r * FN + j);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    if (SAVQA_EPI_PRE == 1 && mask_pre) {  // this fragment's mask bits
+      float mv[MI::NACC][FN];
+#pragma unroll
+      for (int r = 0; r < MI::NACC; ++r) {
+        const int64_t m = min(m0 + wm * WM + i * MI::FR + MI::row(r, lane), (int64_t)d.M - 1);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int64_t n = min(n0 + wn * WN + j * MI::FR + MI::col(lane), (int64_t)d.N - 1);
+          mv[r][j] = d.mask[m * d.ldmask + n];
+        }
+      }
+      keep[i] = 0;
+#pragma unroll
+      for (int r = 0; r < MI::NACC; ++r)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) keep[i] |= (mv[r][j] > 0.f ? 1u : 0u) << (r * FN + j);
+    }
+    float rv[MI::NACC][FN];  // this fragment's residual values (32 registers)
+#pragma unroll
+    for (int r = 0; r < MI::NACC; ++r) {
+      const int64_t m = min(m0 + wm * WM + i * MI::FR + MI::row(r, lane), (int64_t)d.M - 1);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int64_t n = min(n0 + wn * WN + j * MI::FR + MI::col(lane), (int64_t)d.N - 1);
+        rv[r][j] = res_pre ? d.resid[m * d.ldr + n] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < MI::NACC; ++r) {
+      const int64_t m = m0 + wm * WM + i * MI::FR + MI::row(r, lane);
+      if (m >= d.M) continue;
+      const EpiRow er = epi_row(d, m, ident);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int64_t n = n0 + wn * WN + j * MI::FR + MI::col(lane);
+        if (n >= d.N) continue;
+        // savqa_gemm epilogue (include/savqa.h), operands prefetched above
+        float v = acc[i][j][r] * d.alpha + bv[j];
+        if (first_split && d.rowvec) v += d.rowvec[er.pr * d.ldrv + n];
+        if (d.relu) v = fmaxf(v, 0.f);
+        v *= er.rs;
+        if (d.mask && (mask_pre ? !((keep[i] >> (r * FN + j)) & 1u)
+                                : !(d.mask[er.mr * d.ldmask + n] > 0.f)))
+          v = 0.f;
+        v += rv[r][j];
+        float* cp = er.crow + n;
+        if (atomic) atomicAdd(cp, v);
+        else if (d.beta != 0.f) *cp = v + d.beta * *cp;
+        else *cp = v;
+      }
+    }
+  }
+}
+
+#endif
 
 // ---------------------------------------------------------------------------------------
 // Stream-K launch of the same 128x128 tile machinery (opt-in, see sk_enabled()).

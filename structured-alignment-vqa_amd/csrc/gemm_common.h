@@ -44,8 +44,10 @@ __device__ __forceinline__ EpiRow epi_row(const savqa_gemm_desc& d, int64_t m, b
   return e;
 }
 
-__device__ __forceinline__ void epi_store(const savqa_gemm_desc& d, const EpiRow& e, int64_t m,
-                                          int64_t n, float acc, bool first_split, bool atomic) {
+// keep: < 0 = read the mask from memory, 0 / 1 = the caller's prefetched mask bit
+__device__ __forceinline__ void epi_store_t(const savqa_gemm_desc& d, const EpiRow& e, int64_t m,
+                                            int64_t n, float acc, bool first_split, bool atomic,
+                                            int keep) {
   float v = acc * d.alpha;
   if (first_split) {
     if (d.bias) v += d.bias[n];
@@ -53,7 +55,7 @@ __device__ __forceinline__ void epi_store(const savqa_gemm_desc& d, const EpiRow
   }
   if (d.relu) v = fmaxf(v, 0.f);
   v *= e.rs;
-  if (d.mask && !(d.mask[e.mr * d.ldmask + n] > 0.f)) v = 0.f;
+  if (keep == 0 || (keep < 0 && d.mask && !(d.mask[e.mr * d.ldmask + n] > 0.f))) v = 0.f;
   if (first_split && d.resid) v += d.resid[m * d.ldr + n];
   float* cp = e.crow + n;
   if (atomic) {
@@ -63,6 +65,11 @@ __device__ __forceinline__ void epi_store(const savqa_gemm_desc& d, const EpiRow
   } else {
     *cp = v;
   }
+}
+
+__device__ __forceinline__ void epi_store(const savqa_gemm_desc& d, const EpiRow& e, int64_t m,
+                                          int64_t n, float acc, bool first_split, bool atomic) {
+  epi_store_t(d, e, m, n, acc, first_split, atomic, -1);
 }
 
 }  // namespace savqa
