@@ -122,6 +122,28 @@ struct Operand {
     }
   }
 
+  // k-row gathers of a COL operand (an embedding table read through the token ids of
+  // a dW GEMM): setup_kg drops the row term of the pointers, load_fast_kg adds the
+  // gathered row of each k per tile
+  __device__ __forceinline__ void setup_kg(int64_t ld, int tid) {
+    if constexpr (!ROW) {
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) rp[it] -= (int64_t)((tid + it * GEMM_NT) / PER) * ld;
+    }
+  }
+  __device__ __forceinline__ void load_fast_kg(int64_t ld, const int64_t* __restrict__ rows,
+                                               int64_t k0, int tid) {
+    if constexpr (ROW) {
+      load_fast(ld, k0);
+    } else {
+      int64_t rr[ITERS];
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) rr[it] = rows[k0 + (tid + it * GEMM_NT) / PER];
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) r[it] = *reinterpret_cast<const f4*>(rp[it] + rr[it] * ld);
+    }
+  }
+
   // guarded path: clamped addresses, out-of-range elements selected to 0 (branch-free)
   __device__ __forceinline__ void load_slow(const float* __restrict__ base, int64_t ld,
                                             const int64_t* __restrict__ rows, int64_t mlim,
@@ -209,6 +231,15 @@ struct OperandT {
   __device__ __forceinline__ void load_fast(int64_t ld, int64_t k0) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) r[j] = *reinterpret_cast<const f4*>(rp + (k0 + j) * ld);
+  }
+  __device__ __forceinline__ void setup_kg(int64_t ld, int tid) {
+    rp -= (int64_t)(4 * (tid / PER)) * ld;
+  }
+  __device__ __forceinline__ void load_fast_kg(int64_t ld, const int64_t* __restrict__ rows,
+                                               int64_t k0, int tid) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      r[j] = *reinterpret_cast<const f4*>(rp + rows[k0 + 4 * (tid / PER) + j] * ld);
   }
   __device__ __forceinline__ void load_slow(const float* __restrict__ base, int64_t ld,
                                             const int64_t* __restrict__ rows, int64_t mlim,
@@ -327,18 +358,19 @@ __host__ __device__ constexpr bool gemm_t14() {
   return SAVQA_GEMM_T14 == 2 || (SAVQA_GEMM_T14 == 1 && !AT);
 }
 
-// k-loop load mode of a block (block-uniform): 0 = guarded loads everywhere (k-row
-// gathers, unaligned operands, odd edge widths), 1 = branch-free loads on every k-tile,
-// 2 = branch-free except a guarded last k-tile (K not a multiple of BK, e.g. the 300-d
-// GloVe projections).
+// k-loop load mode of a block (block-uniform): 0 = guarded loads everywhere (unaligned
+// operands, odd edge widths), 1 = branch-free loads on every k-tile, 2 = branch-free
+// except a guarded last k-tile (K not a multiple of BK, e.g. the 300-d GloVe
+// projections), 3 = as 2 with k-row gathers (the GloVe-table dW: rows by token id).
 template <int BM, int BN, int BK, bool AT, bool BT>
 __device__ __forceinline__ int gemm_mode(const savqa_gemm_desc& d, int64_t m0, int64_t n0,
                                          int64_t kbeg, int64_t kend, int avec, int bvec) {
   const bool a_kgather = AT && d.a_rows;
   const bool b_kgather = !BT && d.b_rows;
-  if (!avec || !bvec || a_kgather || b_kgather) return 0;
+  if (!avec || !bvec) return 0;
   if (m0 + BM > d.M && AT && (d.M & 3)) return 0;   // COL edge needs whole float4 groups
   if (n0 + BN > d.N && !BT && (d.N & 3)) return 0;
+  if (a_kgather || b_kgather) return 3;
   return ((kend - kbeg) % BK == 0) ? 1 : 2;
 }
 
@@ -357,9 +389,12 @@ __device__ __forceinline__ void gemm_mainloop(
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  const bool agk = AT && d.a_rows, bgk = !BT && d.b_rows;  // MODE 3: k-row gathers
   if constexpr (MODE != 0) {
-    la.setup_fast(d.A, d.lda, d.a_rows, m0, d.M, tid);
-    lb.setup_fast(d.B, d.ldb, d.b_rows, n0, d.N, tid);
+    la.setup_fast(d.A, d.lda, AT ? nullptr : d.a_rows, m0, d.M, tid);
+    lb.setup_fast(d.B, d.ldb, BT ? d.b_rows : nullptr, n0, d.N, tid);
+    if (MODE == 3 && agk) la.setup_kg(d.lda, tid);
+    if (MODE == 3 && bgk) lb.setup_kg(d.ldb, tid);
   }
 #define SAVQA_GEMM_LOAD(k0)                                          \
   do {                                                               \
@@ -367,6 +402,11 @@ __device__ __forceinline__ void gemm_mainloop(
     if (MODE == 1 || (MODE == 2 && k0_ + BK <= kend)) {              \
       la.load_fast(d.lda, k0_);                                      \
       lb.load_fast(d.ldb, k0_);                                      \
+    } else if (MODE == 3 && k0_ + BK <= kend) {                      \
+      if (agk) la.load_fast_kg(d.lda, d.a_rows, k0_, tid);           \
+      else la.load_fast(d.lda, k0_);                                 \
+      if (bgk) lb.load_fast_kg(d.ldb, d.b_rows, k0_, tid);           \
+      else lb.load_fast(d.ldb, k0_);                                 \
     } else {                                                         \
       la.load_slow(d.A, d.lda, d.a_rows, d.M, m0, k0_, kend, tid);   \
       lb.load_slow(d.B, d.ldb, d.b_rows, d.N, n0, k0_, kend, tid);   \
@@ -492,6 +532,8 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
       gemm_mainloop<BM, BN, BK, AT, BT, 1>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     else if (mode == 2)
       gemm_mainloop<BM, BN, BK, AT, BT, 2>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+    else if (mode == 3)
+      gemm_mainloop<BM, BN, BK, AT, BT, 3>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     else
       gemm_mainloop<BM, BN, BK, AT, BT, 0>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
   }
@@ -695,6 +737,8 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
         gemm_mainloop<BM, BN, BK, AT, BT, 1>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
       else if (mode == 2)
         gemm_mainloop<BM, BN, BK, AT, BT, 2>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      else if (mode == 3)
+        gemm_mainloop<BM, BN, BK, AT, BT, 3>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
       else
         gemm_mainloop<BM, BN, BK, AT, BT, 0>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     }

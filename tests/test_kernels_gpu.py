@@ -414,3 +414,25 @@ def test_gemm_bf16_paths(prec, tol, lay, M, N, K):
     assert err < tol, err
     if prec == 3:  # 3xbf16 is not plain bf16: at least 100x closer to fp64
         assert err < 1e-4
+
+
+@pytest.mark.parametrize("gather", ["b", "a", "ab"])
+@pytest.mark.parametrize("N", [300, 256])
+def test_gemm_k_row_gathers(gather, N):
+    """dW-layout GEMMs whose k rows are gathered through token ids (the GloVe-table
+    gradient of the micro-object projections: K = B*Nv*topN rows, N = 300): branch-free
+    gathered loads on full k-tiles, a guarded last k-tile, clamped edge columns."""
+    O = ops()
+    M, K, V = 1024, 4612, 700
+    gen = torch.Generator().manual_seed(41)
+    ia = torch.randint(0, V, (K,), generator=gen).to(dev)
+    ib = torch.randint(0, V, (K,), generator=gen).to(dev)
+    A = g(V if "a" in gather else K, M, seed=42)  # A(m, k) = A[ra(k)][m]
+    B = g(V if "b" in gather else K, N, seed=43)  # B(k, n) = B[rb(k)][n]
+    out = torch.zeros(M, N, device=dev)
+    O.gemm(A, B, out, M, N, K, lda=M, ldb=N, ldc=N, a_trans=True, atomic=True, split_k=-1,
+           a_rows=ia if "a" in gather else None, b_rows=ib if "b" in gather else None)
+    Ag = A[ia] if "a" in gather else A
+    Bg = B[ib] if "b" in gather else B
+    ref = Ag.double().t() @ Bg.double()
+    assert rel(out, ref) < 1e-5
