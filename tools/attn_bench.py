@@ -1,50 +1,53 @@
-"""Time the graph-attention kernels on the step shapes (B=256, H=8, dk=64).
-
-SAVQA_ATTN_PATH=rows|mfma selects the kernel family (read once per process).
-"""
+#!/usr/bin/env python
+"""Graph-attention core in isolation at the cfg-2 step shapes (QKV interleaved as the
+engine lays it out: one [B*T, 3*d] buffer), HIP-event timed; bytes = Q,K,V + graph +
+flags read and O (fwd) / dQ,dK,dV (bwd) written, per launch."""
 import os
 import sys
 
-import torch
-
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import savqa_amd.ops as O  # noqa: E402
+import torch  # noqa: E402
 
-dev = torch.device("cuda")
-B, H, D = 256, 8, 512
-for Tq, Tk in [(73, 73), (1, 73), (50, 50), (1, 50)]:
-    g = torch.Generator(device=dev).manual_seed(0)
-    q = torch.rand(B * Tq, D, device=dev, generator=g) - 0.3
-    kv = torch.rand(B * Tk, 2 * D, device=dev, generator=g) - 0.3
-    G = (torch.rand(B, Tq, Tk, device=dev, generator=g) < 0.4).float()
-    kf = torch.ones(B, Tk, device=dev)
-    qf = torch.ones(B, Tq, device=dev)
-    o = torch.empty(B * Tq, D, device=dev)
-    dO = torch.randn(B * Tq, D, device=dev, generator=g)
-    dq = torch.empty_like(q)
-    dkv = torch.empty_like(kv)
-    K, V = kv[:, :D], kv[:, D:]
+from savqa_amd import ops  # noqa: E402
 
-    def fwd():
-        O.gattn_fwd(q, D, K, 2 * D, V, 2 * D, G, kf, qf, B, Tq, Tk, H, o, D)
+dev = "cuda"
 
-    def bwd():
-        O.gattn_bwd(q, D, K, 2 * D, V, 2 * D, G, kf, qf, B, Tq, Tk, H, dO, D, dq, D, dkv, 2 * D,
-                    dkv[:, D:], 2 * D)
-    res = []
-    for fn in (fwd, bwd):
-        for _ in range(3):
-            fn()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        n = 20
-        e0.record()
-        for _ in range(n):
-            fn()
-        e1.record()
-        torch.cuda.synchronize()
-        res.append(e0.elapsed_time(e1) / n * 1e3)
-    fl = 2 * B * H * Tq * Tk * 64
-    print(f"{os.environ.get('SAVQA_ATTN_PATH', 'default'):7s} Tq={Tq:3d} Tk={Tk:3d}  fwd {res[0]:8.1f} us "
-          f"({2 * fl / res[0] / 1e6:6.1f} TF)  bwd {res[1]:8.1f} us ({5 * fl / res[1] / 1e6:6.1f} TF)",
-          flush=True)
+
+def timeit(fn, iters=20):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def main():
+    H, dk = 8, 64
+    d = H * dk
+    for B, T in ((256, 73), (256, 50)):
+        qkv = torch.randn(B * T, 3 * d, device=dev).relu_()
+        G = (torch.rand(B, T, T, device=dev) < 0.3).float()
+        flag = torch.ones(B * T, device=dev)
+        o = torch.empty(B * T, d, device=dev)
+        dout = torch.randn(B * T, d, device=dev)
+        dqkv = torch.zeros(B * T, 3 * d, device=dev)
+        f = lambda: ops.gattn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag,
+                                  flag, B, T, T, H, o, d)
+        g = lambda: ops.gattn_bwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag,
+                                  flag, B, T, T, H, dout, d, dqkv, 3 * d, dqkv[:, d:], 3 * d,
+                                  dqkv[:, 2 * d:], 3 * d)
+        tf, tb = timeit(f), timeit(g)
+        fb = B * T * 3 * d * 4 + B * T * T * 4 + B * T * d * 4
+        bb = B * T * 4 * d * 4 + B * T * T * 4 + B * T * 3 * d * 4
+        ffl = B * H * 4 * T * T * dk
+        bfl = B * H * 10 * T * T * dk
+        print(f"B={B} T={T}: fwd {tf*1e6:7.1f} us {fb/tf/1e9:6.0f} GB/s {ffl/tf/1e12:5.1f} TF | "
+              f"bwd {tb*1e6:7.1f} us {bb/tb/1e9:6.0f} GB/s {bfl/tb/1e12:5.1f} TF", flush=True)
+
+
+if __name__ == "__main__":
+    main()
