@@ -73,6 +73,9 @@ struct Mi16 {
 #ifndef SAVQA_EPI_PRE
 #define SAVQA_EPI_PRE 1
 #endif
+#ifndef SAVQA_GEMM_ROWPAIR
+#define SAVQA_GEMM_ROWPAIR 1  // conflict-free ROW-tile stores (Operand::row_of)
+#endif
 #ifndef SAVQA_GEMM_MI
 #define SAVQA_GEMM_MI 32
 #endif
@@ -92,6 +95,16 @@ struct Operand {
   f4 r[ITERS];
   const float* rp[ITERS];  // FAST path: per-float4 source pointers, resolved once per block
 
+  // Stored row of staging slot q. ds_write_b128 serves 8 contiguous lanes per LDS cycle
+  // with banks (a/4) mod 32: at BK = 16 a ROW tile row is 80 B, so two consecutive rows
+  // share a 16-B slot (2-way conflict on every store); pairing rows r and r+4 in one
+  // lane group makes their slots disjoint. (The ds_read_b128 fetch stays conflict-free.)
+  static __device__ __forceinline__ int row_of(int q) {
+    if constexpr (SAVQA_GEMM_ROWPAIR && ROW && PER == 4)
+      return (q & ~7) | ((q & 7) >> 1) | ((q & 1) << 2);
+    else return q;
+  }
+
   // ROW: stored row = m (tile row), contiguous col = k.  COL: stored row = k, col = m.
   // mlim: rows (ROW) / columns (COL) of the operand. Edge tiles clamp: a ROW operand's
   // rows past mlim re-read row mlim-1, a COL operand's float4 groups past mlim re-read the
@@ -104,7 +117,7 @@ struct Operand {
     for (int it = 0; it < ITERS; ++it) {
       const int idx = tid + it * GEMM_NT;
       if constexpr (ROW) {
-        const int64_t m = min(m0 + idx / PER, mlim - 1);
+        const int64_t m = min(m0 + row_of(idx / PER), mlim - 1);
         const int64_t rr = rows ? rows[m] : m;
         rp[it] = base + rr * ld + (idx % PER) * 4;
       } else {
@@ -153,7 +166,7 @@ struct Operand {
       const int idx = tid + it * GEMM_NT;
       int64_t row, col, rlim, clim;
       if constexpr (ROW) {
-        row = m0 + idx / PER;
+        row = m0 + row_of(idx / PER);
         col = k0 + (idx % PER) * 4;
         rlim = mlim;
         clim = kend;
@@ -187,7 +200,7 @@ struct Operand {
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
       const int idx = tid + it * GEMM_NT;
-      *reinterpret_cast<f4*>(&s[(idx / PER) * LD + (idx % PER) * 4]) = r[it];
+      *reinterpret_cast<f4*>(&s[row_of(idx / PER) * LD + (idx % PER) * 4]) = r[it];
     }
   }
 
