@@ -73,6 +73,12 @@ struct Mi16 {
 #ifndef SAVQA_EPI_PRE
 #define SAVQA_EPI_PRE 1
 #endif
+#ifndef SAVQA_GEMM_DW_TILE
+#define SAVQA_GEMM_DW_TILE 128
+#endif
+#ifndef SAVQA_GEMM_BK_DW64
+#define SAVQA_GEMM_BK_DW64 32
+#endif
 #ifndef SAVQA_GEMM_ROWPAIR
 #define SAVQA_GEMM_ROWPAIR 1  // conflict-free ROW-tile stores (Operand::row_of)
 #endif
@@ -1075,8 +1081,13 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.colsum_a && !d.a_trans) return fail(SAVQA_EINVAL, "savqa_gemm: colsum_a needs a_trans=1");
   if (d.prec != 0 && d.prec != 1 && d.prec != 3)
     return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32), 1 (bf16) or 3 (3xbf16)");
+  // 64x64-tile dW launches (SAVQA_GEMM_DW_TILE=64, A/B option): 4x the tiles, so less
+  // split-K; k-tile SAVQA_GEMM_BK_DW64
+  const bool dw64 = SAVQA_GEMM_DW_TILE == 64 && d.a_trans && d.prec == 0 && !sk_enabled();
   // gemm_bf16_kernel k-tile: 32; the stream-K kernel always runs SAVQA_GEMM_BK
-  const int BK = d.prec ? 32 : (d.a_trans && !sk_enabled() ? SAVQA_GEMM_BK_DW : SAVQA_GEMM_BK);
+  const int BK = d.prec ? 32
+                        : (dw64 ? SAVQA_GEMM_BK_DW64
+                                : (d.a_trans && !sk_enabled() ? SAVQA_GEMM_BK_DW : SAVQA_GEMM_BK));
   const int slots = slots_per_launch();
   const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
   int split = d.split_k > 1 ? d.split_k : 1;
@@ -1109,6 +1120,12 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
     return 0;
   }
   p.tile = 128;
+  if (dw64) {
+    p.tile = 64;
+    const int64_t tiles64 = ((d.M + 63) / 64) * ((d.N + 63) / 64);
+    split = d.split_k > 1 ? d.split_k : 1;
+    if (d.split_k < 0) split = auto_split(tiles64, d.K, BK, slots);
+  }
   const int tm = (int)((d.M + p.tile - 1) / p.tile);
   const int tn = (int)((d.N + p.tile - 1) / p.tile);
   const int T = tm * tn;
@@ -1231,6 +1248,9 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
     else hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, true, true>), g, b, 0, s, d, sk, avec, bvec);
   } else if (p.tile == 128 && d.prec != 0) {
     savqa_launch_gemm_bf16(d, p.gg, p.grid_x, p.nsplit, s, avec, bvec);
+  } else if (p.tile == 64) {  // dW only (a_trans)
+    if (!d.b_trans) launch_gemm<64, 64, SAVQA_GEMM_BK_DW64, true, false>(d, p, s, avec, bvec);
+    else launch_gemm<64, 64, SAVQA_GEMM_BK_DW64, true, true>(d, p, s, avec, bvec);
   } else if (p.tile == 128) {
     dispatch_layout<128, 128, SAVQA_GEMM_BK>(d, p, s, avec, bvec);
   } else {
