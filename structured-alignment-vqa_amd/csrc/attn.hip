@@ -23,6 +23,10 @@
 // for the column sums dV = P^T dO and dK = dS^T Q.
 #include "attn_common.h"
 
+#ifndef SAVQA_ATT_ALIAS
+#define SAVQA_ATT_ALIAS 1
+#endif
+
 namespace savqa {
 
 // Stage K_h, V_h rows [0,Tk) of sample b into LDS (row stride ATT_KLD).
@@ -421,9 +425,18 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgs a) {
   const int i0 = w * 16;
   constexpr int TK = NJT * 16;
   constexpr int WLD = 20;                   // per-wave P^T image [TK][16 + 4]
+#if SAVQA_ATT_ALIAS
+  // V first, then K; the per-wave P^T images reuse K's space once S is computed (one
+  // block barrier), so the block needs V + max(K, P) instead of V + K + P (T=73: 54 KB,
+  // 3 workgroups per CU instead of 2)
+  float* Vs = sm;                           // [TK][ATT_KLD]
+  float* Ks = Vs + TK * ATT_KLD;            // [TK][ATT_KLD]
+  float* Pw = Ks + w * TK * WLD;
+#else
   float* Ks = sm;                           // [TK][ATT_KLD]
   float* Vs = Ks + TK * ATT_KLD;            // [TK][ATT_KLD]
   float* Pw = Vs + TK * ATT_KLD + w * TK * WLD;
+#endif
   stage_kv_tiles<TK>(a, b, h, Ks, Vs);
   f4v qa[4];
   {
@@ -440,6 +453,9 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgs a) {
   __syncthreads();  // K/V staged
   f4v s[NJT];
   strip_dots_lds<NJT>(qa, Ks, col, g, s);
+#if SAVQA_ATT_ALIAS
+  __syncthreads();  // every wave is done with K before the P images overwrite it
+#endif
 
   f4v pv[NJT];
 #pragma unroll
@@ -896,7 +912,12 @@ extern "C" int savqa_gattn_fwd(void* stream, const float* q, int64_t ldq, const 
     }
   } else if (path == 1) {
     const int njt = (int)((Tk + 15) / 16), nw = (int)((Tq + 15) / 16);
+#if SAVQA_ATT_ALIAS
+    const size_t lds = sizeof(float) * ((size_t)njt * 16 * ATT_KLD +
+                                        std::max((size_t)njt * 16 * ATT_KLD, (size_t)nw * njt * 16 * 20));
+#else
     const size_t lds = sizeof(float) * ((size_t)2 * njt * 16 * ATT_KLD + (size_t)nw * njt * 16 * 20);
+#endif
     switch (njt) {
 #define SAVQA_FWD_CASE(N)                                                                  \
   case N:                                                                                  \
