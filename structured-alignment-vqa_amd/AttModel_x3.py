@@ -207,6 +207,8 @@ class _AttModelFn(torch.autograd.Function):
         B = ctx.saved[1].B
         Cc = model.num_classes
         red = model.__dict__.get("_reducer")
+        if red is not None:
+            red.prepare_rows()           # on the backward's main stream
         model._engine.backward(ctx.saved, z(dlc, (B, Cc)), z(dlv, (B, Cc)), z(dls, (B, Cc)),
                                z(dmil, ()), on_range=red.reduce_range if red else None,
                                dmil_rel=z(dmil_rel, ()) if ctx.rel else None)
@@ -264,8 +266,14 @@ class AttModel(nn.Module):
                                                         num_heads, gemm_precision))
 
     def attach_reducer(self, reducer):
-        """Stream the data-parallel gradient all-reduce out of the backward (ddp.GradReducer)."""
+        """Stream the data-parallel gradient all-reduce out of the backward (ddp.GradReducer).
+        The two stacks' syb_emb tables only get question-token rows (AttModel_x3.py:96-99,
+        :216-219), so they are exchanged by rows (ddp.GradReducer.add_sparse_table)."""
         object.__setattr__(self, "_reducer", reducer)
+        if reducer is not None and getattr(reducer, "world", 1) > 1:
+            for pre in ("att_vis_grid", "att_syb"):
+                o, shp = self._arena.offsets[f"{pre}.syb_emb.weight"]
+                reducer.add_sparse_table(o, o + shp.numel(), shp[1])
 
     # parameters live in the arena: moving the module moves the arena
     def _apply(self, fn, recurse=True):
@@ -312,6 +320,9 @@ class AttModel(nn.Module):
             self._check_relation_locs(tensors[-2], tensors[-1], vis_fea.shape[1],
                                       macro_ipt.shape[1], tensors[-3].shape[1])
         anchor = self._arena_anchor()
+        red = self.__dict__.get("_reducer")
+        if red is not None and anchor is not None:
+            red.set_rows(tensors[2])     # q_ipt: the stack tables' touched rows
         lc, lv, ls, mil, mil_rel = _AttModelFn.apply(self, bool(decMask), drop, anchor, *tensors)
         return lc, lv, ls, mil, (mil_rel if not self.only_obj else 0)
 

@@ -70,6 +70,66 @@ def test_grad_reducer_gloo_world2():
         assert spans[2] == (3000, 5621)   # full bucket issued during the layer loop
 
 
+def _sparse_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from savqa_amd.ddp import GradReducer
+    width, rows = 7, 50
+    t0, t1 = 1000, 1000 + width * rows            # a row table inside the arena
+    n = t1 + 777
+    gen = torch.Generator().manual_seed(rank)
+    ids = torch.randint(0, rows, (3, 6), generator=gen)  # duplicates within and across ranks
+    ids[0, 0] = rows - 1                           # last row touched by every rank
+    g = torch.randn(n, generator=gen)
+    table = torch.zeros(rows, width)
+    table.index_add_(0, ids.reshape(-1), torch.randn(ids.numel(), width, generator=gen))
+    g[t0:t1] = table.reshape(-1)                   # untouched rows are zero, as in the model
+    dense = g.clone()
+    dist.all_reduce(dense)
+    arena = types.SimpleNamespace(grad=g.clone())
+    red = GradReducer(arena, bucket_mb=0.001)      # 262 floats per bucket: the table spans several
+    red.add_sparse_table(t0, t1, width)
+    red.begin()
+    red.set_rows(ids)
+    red.reduce_range(0, 600, True)
+    red.prepare_rows()
+    red.reduce_range(600, 1100)                    # declarations split the table ...
+    red.reduce_range(1100, t1 + 100)               # ... and complete it
+    red.reduce_range(t1 + 100, n, True)
+    works, scale = red.drain()
+    assert red.rows_exchanged == 1
+    spans = sorted((lo, hi) for _, lo, hi in works)
+    for w, _, _ in works:
+        w.wait()
+    q.put((rank, float((arena.grad - dense).abs().max()), spans, scale))
+    dist.destroy_process_group()
+
+
+def test_sparse_table_rows_exchange_equals_dense_gloo_world2():
+    """Row-sparse exchange of a table range (GradReducer.add_sparse_table / set_rows):
+    after wait() the arena equals the dense all-reduce, and the spans still tile [0, n)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sparse_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, spans, scale in res:
+        assert err < 1e-6
+        assert scale == 0.5
+        assert (1000, 1350) in spans
+        pos = 0
+        for lo, hi in spans:
+            assert lo == pos and hi > lo
+            pos = hi
+        assert pos == 1350 + 777
+
+
 def test_adam_grad_scale_matches_mean_of_grads():
     """Adam(grad_scale=1/world) on summed grads == Adam on the mean (oracle restatement)."""
     from oracle import savqa_oracle as O
