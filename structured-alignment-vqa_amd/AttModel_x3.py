@@ -270,6 +270,7 @@ class AttModel(nn.Module):
         The two stacks' syb_emb tables only get question-token rows (AttModel_x3.py:96-99,
         :216-219), so they are exchanged by rows (ddp.GradReducer.add_sparse_table)."""
         object.__setattr__(self, "_reducer", reducer)
+        self._engine.multi_rank = reducer is not None and getattr(reducer, "world", 1) > 1
         if reducer is not None and getattr(reducer, "world", 1) > 1:
             for pre in ("att_vis_grid", "att_syb"):
                 o, shp = self._arena.offsets[f"{pre}.syb_emb.weight"]

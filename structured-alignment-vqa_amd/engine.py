@@ -23,6 +23,7 @@ gradients are exactly zero in the reference too.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -566,12 +567,44 @@ class ModelEngine:
             self._gbound = g
 
     concurrent = True  # False: run both stacks on the caller's stream (serial profiling)
+    # backward schedule of the two stacks: "concurrent" = both from the start;
+    # "syb_first" = the visual stack waits for the semantic stack and then overlaps the
+    # MIL-NCE backward + the MIL-NCE table all-reduce
+    bwd_order = os.environ.get("SAVQA_BWD_ORDER", "auto")
+    multi_rank = False  # set by AttModel.attach_reducer when gradients are all-reduced
+
+    def vis_gate(self):
+        """Name of the semantic-stack gradient marker after which the visual stack's
+        backward may start (None: both stacks from the start, "end": after the whole
+        semantic stack). "auto": concurrent on one rank; with an all-reduce, gated so
+        the MIL-NCE phase finishes first."""
+        o = self.bwd_order
+        if o == "auto":
+            o = self.AUTO_GATE if self.multi_rank else "concurrent"
+        if o == "concurrent":
+            return None
+        if o == "syb_first":
+            return "end"
+        if o.startswith("enc"):      # encN: after the semantic stack's encoder layer N
+            n = int(o[3:])
+            return f"enc_feed_forward_{n - 1}.normalization.gamma"
+        if o == "dec":               # after the semantic stack's decoder layers
+            return f"enc_feed_forward_{len(self.syb.enc) - 1}.normalization.gamma"
+        raise ValueError(f"SAVQA_BWD_ORDER: unknown schedule {o!r}")
+
+    # measured at cfg 2 (tools/tail_probe.py, profiles/r01_bwd_schedule.jsonl): the gate after
+    # encoder layer 4 costs +1.3 ms of backward and leaves a 5.8 ms window for the
+    # MIL-NCE all-reduce (~3 ms of 500 MB at N=8); "dec" +0.85 ms / 2.6 ms window,
+    # "syb_first" +2.8 ms / 12.8 ms
+    AUTO_GATE = "enc4"
 
     def _streams(self, dev):
         if not self.concurrent:
             cur = torch.cuda.current_stream(dev)
             return cur, cur
         if getattr(self, "_side", None) is None or self._side[0].device != dev:
+            # (a higher priority for the semantic stack's stream was measured: no effect on
+            # when either stack finishes (tools/tail_probe.py); the vis_gate schedule is what works)
             self._side = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
         return self._side
 
@@ -671,16 +704,37 @@ class ModelEngine:
         dmil.record_stream(s_syb)
         if dmil_rel is not None:
             dmil_rel.record_stream(s_syb)
-        with torch.cuda.stream(s_vis):
-            mk = Marker("att_vis_grid", b_heads)
-            stack_backward(self.vis, self.gvis, sv, df_vis, H, d, want_node_grad=False, mark=mk)
-            mk.upto(b_vis, flush=True)
+        def vis_phase():
+            with torch.cuda.stream(s_vis):
+                mk = Marker("att_vis_grid", b_heads)
+                stack_backward(self.vis, self.gvis, sv, df_vis, H, d, want_node_grad=False,
+                               mark=mk)
+                mk.upto(b_vis, flush=True)
+
+        gate = self.vis_gate() if s_vis is not s_syb else None
+        if gate is None:
+            vis_phase()
+        ev = torch.cuda.Event() if gate is not None else None
+
+        class SybMarker(Marker):
+            def __call__(self, name):
+                super().__call__(name)
+                if ev is not None and name == gate:
+                    ev.record(s_syb)
         with torch.cuda.stream(s_syb):
-            mk = Marker("att_syb", b_vis)
+            mk = SybMarker("att_syb", b_vis)
             dnode = stack_backward(self.syb, self.gsyb, ss, df_syb, H, d, want_node_grad=True,
                                    mark=mk)
             mk.upto(b_syb, flush=True)
+            if gate == "end":
+                ev.record(s_syb)
             mil_backward(self.mil, self.gmil, ms, dnode, dmil, dmil_rel=dmil_rel)
             mk.upto(self.arena.n_live, flush=True)
+        if gate is not None:
+            # the visual stack starts once the semantic stack has passed the gate and
+            # overlaps the MIL-NCE backward and its table's all-reduce; it is issued
+            # after the MIL-NCE buckets, so RCCL's in-order stream runs those first
+            s_vis.wait_event(ev)
+            vis_phase()
         main.wait_stream(s_vis)
         main.wait_stream(s_syb)

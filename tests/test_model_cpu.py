@@ -71,3 +71,29 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert lib.savqa_version() == 1
+
+
+def test_backward_schedule_gates_name_real_markers(meta_model):
+    """Every SAVQA_BWD_ORDER gate names a semantic-stack gradient marker that the backward
+    actually emits (an unmatched name would leave the event unrecorded and the gate a
+    silent no-op); "auto" is concurrent on one rank and gated with an all-reduce."""
+    eng = meta_model._engine
+    offs = meta_model._arena.offsets
+    saved = eng.bwd_order, eng.multi_rank
+    try:
+        for o in ["dec"] + [f"enc{n}" for n in range(1, 6)]:
+            eng.bwd_order = o
+            assert f"att_syb.{eng.vis_gate()}" in offs, o
+        eng.bwd_order = "syb_first"
+        assert eng.vis_gate() == "end"
+        eng.bwd_order = "concurrent"
+        assert eng.vis_gate() is None
+        eng.bwd_order, eng.multi_rank = "auto", False
+        assert eng.vis_gate() is None
+        eng.multi_rank = True
+        assert f"att_syb.{eng.vis_gate()}" in offs
+        eng.bwd_order = "bogus"
+        with pytest.raises(ValueError):
+            eng.vis_gate()
+    finally:
+        eng.bwd_order, eng.multi_rank = saved
