@@ -27,6 +27,7 @@
 #include "gemm_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 
@@ -977,6 +978,86 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(savqa_gemm_d
   }
 }
 
+// 16x16-tile variant (v_mfma_f32_16x16x4_f32) for the skinny shapes with too few 32x32
+// tiles to fill the chip (a 256x512 output is 128 32x32 tiles for 256 CUs, 512 16x16
+// ones): same K split over the waves and LDS fold. Lane (i, q) = (lane % 16, lane / 16)
+// takes k = 16g + 4q + s in MFMA step s of 16-k group g: one b128 load on a k-contiguous
+// operand, 4 coalesced scalars otherwise; accumulator row 4q + r, column i.
+#ifndef SAVQA_SK16
+#define SAVQA_SK16 1
+#endif
+#ifndef SAVQA_SK16_DEPTH
+#define SAVQA_SK16_DEPTH 4
+#endif
+constexpr int SK16_DEPTH = SAVQA_SK16_DEPTH;
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny16_kernel(savqa_gemm_desc d,
+                                                                     int tiles_n, int avec,
+                                                                     int bvec) {
+  __shared__ float red[SK_WAVES][16][17];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t = blockIdx.x;
+  const int64_t m0 = (int64_t)(t / tiles_n) * 16, n0 = (int64_t)(t % tiles_n) * 16;
+  const int64_t ngrp = (d.K + 15) / 16;
+  const int64_t g0 = ngrp * w / SK_WAVES, g1 = ngrp * (w + 1) / SK_WAVES;
+  const int i = lane & 15, q = lane >> 4;
+  const int64_t am = m0 + i, bn = n0 + i;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  float cs = 0.f;
+  float a[SK16_DEPTH][4], b[SK16_DEPTH][4];
+  auto load = [&](int64_t gg, float (&aa)[4], float (&bb)[4]) {
+    const int64_t k = gg * 16 + 4 * q;
+    sk_load4<!AT>(d.A, d.lda, d.a_rows, am, d.M, k, d.K, avec, aa);
+    sk_load4<BT>(d.B, d.ldb, d.b_rows, bn, d.N, k, d.K, bvec, bb);
+  };
+  auto mma = [&](const float (&aa)[4], const float (&bb)[4]) {
+    cs += (aa[0] + aa[1]) + (aa[2] + aa[3]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[s], bb[s], acc, 0, 0, 0);
+  };
+  const int ng = (int)(g1 - g0);
+#pragma unroll
+  for (int q2 = 0; q2 < SK16_DEPTH; ++q2)
+    if (q2 < ng) load(g0 + q2, a[q2], b[q2]);
+  for (int pi = 0; pi < ng; pi += SK16_DEPTH) {
+#pragma unroll
+    for (int q2 = 0; q2 < SK16_DEPTH; ++q2) {
+      if (pi + q2 < ng) {
+        mma(a[q2], b[q2]);
+        if (pi + q2 + SK16_DEPTH < ng) load(g0 + pi + q2 + SK16_DEPTH, a[q2], b[q2]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[w][4 * q + r][i] = acc[r];
+  __syncthreads();
+  const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
+  for (int e = threadIdx.x; e < 16 * 16; e += 64 * SK_WAVES) {
+    const int r = e >> 4, c = e & 15;
+    const int64_t m = m0 + r, n = n0 + c;
+    if (m >= d.M || n >= d.N) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < SK_WAVES; ++ww) v += red[ww][r][c];
+    const EpiRow er = epi_row(d, m, ident);
+    epi_store(d, er, m, n, v, true, d.atomic != 0);
+  }
+  if constexpr (AT) {
+    if (d.colsum_a && n0 == 0) {
+      __syncthreads();
+      float* flat = &red[0][0][0];
+      flat[threadIdx.x] = cs;  // 64 * SK_WAVES partials: ((wave, q), i)
+      __syncthreads();
+      if (threadIdx.x < 16 && m0 + threadIdx.x < d.M) {
+        float sum = 0.f;
+        for (int j = 0; j < 4 * SK_WAVES; ++j) sum += flat[j * 16 + threadIdx.x];
+        atomicAdd(&d.colsum_a[m0 + threadIdx.x], sum);
+      }
+    }
+  }
+}
+
 static int slots_per_launch() {
   // 2 workgroups per CU (launch bounds / LDS); the CU count of the current device
   static int cached[64] = {0};
@@ -1071,6 +1152,18 @@ using namespace savqa;
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// skinny shapes with fewer 32x32 tiles than this run on 16x16 tiles (SAVQA_SK16=0: never;
+// measured: 256x512 outputs (128 tiles) 1.25-1.55x faster at K=2048, 256x914 (232) slower;
+// env SAVQA_SK16_MAX overrides the threshold for A/B runs)
+static int64_t sk16_max() {
+  static int64_t v = -1;
+  if (v < 0) {
+    const char* e = getenv("SAVQA_SK16_MAX");
+    v = e ? atoll(e) : (SAVQA_SK16 ? 192 : 0);
+  }
+  return v;
+}
+
 static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.M < 0 || d.N < 0 || d.K < 0) return fail(SAVQA_EINVAL, "savqa_gemm: negative dims");
   if (d.M >= (1LL << 31) || d.N >= (1LL << 31)) return fail(SAVQA_EUNSUP, "savqa_gemm: M/N >= 2^31");
@@ -1094,13 +1187,15 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   int split = d.split_k > 1 ? d.split_k : 1;
   if (d.split_k < 0) split = auto_split(tiles128, d.K, BK, slots);
   // 128x128 tiles once there is enough parallelism (split-K counts), else the skinny
-  // kernel (32x32 tiles, K split over the 4 waves of a workgroup; no split-K launch)
+  // kernel (32x32 tiles, K split over the 8 waves of a workgroup; no split-K launch),
+  // 16x16 tiles while 32x32 ones would leave CUs idle (< sk16_max() tiles)
   if (tiles128 * split < 160) {
-    p.tile = 32;
+    const int64_t tiles32 = ((d.M + 31) / 32) * ((d.N + 31) / 32);
+    p.tile = tiles32 < sk16_max() ? 16 : 32;
     p.split = 1;
     p.nsplit = 1;
-    p.gg.tiles_n = (int)((d.N + 31) / 32);
-    p.grid_x = (int)((d.M + 31) / 32) * p.gg.tiles_n;
+    p.gg.tiles_n = (int)((d.N + p.tile - 1) / p.tile);
+    p.grid_x = (int)((d.M + p.tile - 1) / p.tile) * p.gg.tiles_n;
     p.zero_row0 = -1;
     p.gg.tail_f = 1;
     p.sk = false;
@@ -1254,6 +1349,13 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
     else launch_gemm<64, 64, SAVQA_GEMM_BK_DW64, true, true>(d, p, s, avec, bvec);
   } else if (p.tile == 128) {
     dispatch_layout<128, 128, SAVQA_GEMM_BK>(d, p, s, avec, bvec);
+  } else if (p.tile == 16) {
+    const dim3 g(p.grid_x), b(64 * SK_WAVES);
+    const int tn = p.gg.tiles_n;
+    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, true>), g, b, 0, s, d, tn, avec, bvec);
+    else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, false>), g, b, 0, s, d, tn, avec, bvec);
+    else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<true, false>), g, b, 0, s, d, tn, avec, bvec);
+    else hipLaunchKernelGGL((gemm_skinny16_kernel<true, true>), g, b, 0, s, d, tn, avec, bvec);
   } else {
     const dim3 g(p.grid_x), b(64 * SK_WAVES);
     const int tn = p.gg.tiles_n;

@@ -60,6 +60,8 @@ class GemmProbe:
         lay = f"{str(bool(d.a_trans)).lower()},{str(bool(d.b_trans)).lower()}"
         if plan[0] == 32:
             return f"gemm_skinny_kernel<{lay}>"
+        if plan[0] == 16:
+            return f"gemm_skinny16_kernel<{lay}>"
         if d.prec:
             return f"gemm_bf16_kernel<{lay},{d.prec}>"
         return f"gemm_f32_kernel<{plan[0]},{plan[0]},{lay}>"
