@@ -166,10 +166,13 @@ def linear_dx(dY: Tensor, W: Tensor, dX: Tensor, *, rows: int, a_rows=None, mask
               beta=0.0, lddy=None, lddx=None):
     """dX = dY W  (mask: ReLU-backward gate of the producer of X; c_rows: scatter-add)."""
     N, K = W.shape  # dY has N cols, dX has K cols
+    # a pure scatter-add (the GloVe-table gradient: few output tiles, K = 2048) may split K
+    # across workgroups: every slice adds its partial with the same atomics
+    split = -1 if (atomic and mask is None and resid is None and beta == 0.0) else 1
     gemm(dY, W, dX, rows, K, N, lda=lddy if lddy is not None else N, ldb=K,
          ldc=lddx if lddx is not None else K, a_rows=a_rows, mask=mask, ldmask=ldmask,
          mask_arows=mask_arows, resid=resid, ldr=ldr if ldr is not None else K, c_rows=c_rows,
-         atomic=atomic, beta=beta)
+         atomic=atomic, beta=beta, split_k=split)
 
 
 def linear_dw(dY: Tensor, X: Tensor, dW: Tensor, db: Optional[Tensor], *, rows: int,
