@@ -991,16 +991,16 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(savqa_gemm_d
 #endif
 constexpr int SK16_DEPTH = SAVQA_SK16_DEPTH;
 
-template <bool AT, bool BT>
-__global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny16_kernel(savqa_gemm_desc d,
+template <bool AT, bool BT, int NW>
+__global__ __launch_bounds__(64 * NW) void gemm_skinny16_kernel(savqa_gemm_desc d,
                                                                      int tiles_n, int avec,
                                                                      int bvec) {
-  __shared__ float red[SK_WAVES][16][17];
+  __shared__ float red[NW][16][17];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int t = blockIdx.x;
   const int64_t m0 = (int64_t)(t / tiles_n) * 16, n0 = (int64_t)(t % tiles_n) * 16;
   const int64_t ngrp = (d.K + 15) / 16;
-  const int64_t g0 = ngrp * w / SK_WAVES, g1 = ngrp * (w + 1) / SK_WAVES;
+  const int64_t g0 = ngrp * w / NW, g1 = ngrp * (w + 1) / NW;
   const int i = lane & 15, q = lane >> 4;
   const int64_t am = m0 + i, bn = n0 + i;
   f4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -1033,13 +1033,13 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny16_kernel(savqa_gemm
   for (int r = 0; r < 4; ++r) red[w][4 * q + r][i] = acc[r];
   __syncthreads();
   const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
-  for (int e = threadIdx.x; e < 16 * 16; e += 64 * SK_WAVES) {
+  for (int e = threadIdx.x; e < 16 * 16; e += 64 * NW) {
     const int r = e >> 4, c = e & 15;
     const int64_t m = m0 + r, n = n0 + c;
     if (m >= d.M || n >= d.N) continue;
     float v = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < SK_WAVES; ++ww) v += red[ww][r][c];
+    for (int ww = 0; ww < NW; ++ww) v += red[ww][r][c];
     const EpiRow er = epi_row(d, m, ident);
     epi_store(d, er, m, n, v, true, d.atomic != 0);
   }
@@ -1047,11 +1047,11 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny16_kernel(savqa_gemm
     if (d.colsum_a && n0 == 0) {
       __syncthreads();
       float* flat = &red[0][0][0];
-      flat[threadIdx.x] = cs;  // 64 * SK_WAVES partials: ((wave, q), i)
+      flat[threadIdx.x] = cs;  // 64 * NW partials: ((wave, q), i)
       __syncthreads();
       if (threadIdx.x < 16 && m0 + threadIdx.x < d.M) {
         float sum = 0.f;
-        for (int j = 0; j < 4 * SK_WAVES; ++j) sum += flat[j * 16 + threadIdx.x];
+        for (int j = 0; j < 4 * NW; ++j) sum += flat[j * 16 + threadIdx.x];
         atomicAdd(&d.colsum_a[m0 + threadIdx.x], sum);
       }
     }
@@ -1155,6 +1155,20 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // skinny shapes with fewer 32x32 tiles than this run on 16x16 tiles (SAVQA_SK16=0: never;
 // measured: 256x512 outputs (128 tiles) 1.25-1.55x faster at K=2048, 256x914 (232) slower;
 // env SAVQA_SK16_MAX overrides the threshold for A/B runs)
+// short-K skinny GEMMs (the decoder / head dW at K = B = 256) on 16x16 tiles with 2 waves
+// per workgroup (A/B option, env SAVQA_SK16_KSMALL = K limit; default 0 = off): measured
+// in-step 1.5-1.6x SLOWER than the 8-wave 32x32 kernel on all five dW shapes (the
+// m-contiguous dY^T loads coalesce into 64 B instead of 128 B and 2 waves hide less
+// latency; tools/gpu_sk16k.sh)
+static int64_t sk16_ksmall() {
+  static int64_t v = -1;
+  if (v < 0) {
+    const char* e = getenv("SAVQA_SK16_KSMALL");
+    v = e ? atoll(e) : 0;
+  }
+  return v;
+}
+
 static int64_t sk16_max() {
   static int64_t v = -1;
   if (v < 0) {
@@ -1191,7 +1205,7 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   // 16x16 tiles while 32x32 ones would leave CUs idle (< sk16_max() tiles)
   if (tiles128 * split < 160) {
     const int64_t tiles32 = ((d.M + 31) / 32) * ((d.N + 31) / 32);
-    p.tile = tiles32 < sk16_max() ? 16 : 32;
+    p.tile = (tiles32 < sk16_max() || (d.K <= sk16_ksmall() && tiles32 <= 1024)) ? 16 : 32;
     p.split = 1;
     p.nsplit = 1;
     p.gg.tiles_n = (int)((d.N + p.tile - 1) / p.tile);
@@ -1350,12 +1364,21 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   } else if (p.tile == 128) {
     dispatch_layout<128, 128, SAVQA_GEMM_BK>(d, p, s, avec, bvec);
   } else if (p.tile == 16) {
-    const dim3 g(p.grid_x), b(64 * SK_WAVES);
     const int tn = p.gg.tiles_n;
-    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, true>), g, b, 0, s, d, tn, avec, bvec);
-    else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, false>), g, b, 0, s, d, tn, avec, bvec);
-    else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<true, false>), g, b, 0, s, d, tn, avec, bvec);
-    else hipLaunchKernelGGL((gemm_skinny16_kernel<true, true>), g, b, 0, s, d, tn, avec, bvec);
+    const dim3 g(p.grid_x);
+    if (d.K <= sk16_ksmall()) {
+      const dim3 b(64 * 2);
+      if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, true, 2>), g, b, 0, s, d, tn, avec, bvec);
+      else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, false, 2>), g, b, 0, s, d, tn, avec, bvec);
+      else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<true, false, 2>), g, b, 0, s, d, tn, avec, bvec);
+      else hipLaunchKernelGGL((gemm_skinny16_kernel<true, true, 2>), g, b, 0, s, d, tn, avec, bvec);
+    } else {
+      const dim3 b(64 * SK_WAVES);
+      if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+      else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+      else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<true, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+      else hipLaunchKernelGGL((gemm_skinny16_kernel<true, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+    }
   } else {
     const dim3 g(p.grid_x), b(64 * SK_WAVES);
     const int tn = p.gg.tiles_n;
