@@ -413,6 +413,11 @@ __global__ void scatter_rows_kernel(const float* __restrict__ g, const int64_t* 
 // m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2; p -= (lr/bc1) m / (sqrt(v)/sqrt(bc2) + eps).
 // Streaming, 28 B/param: each thread moves 2 float4 of p, g, m, v per iteration with
 // non-temporal loads/stores (11 GB per step at the cfg-2 arena never fits in cache).
+// grid cap of the grid-stride Adam launch (A/B knob; tools/adam_bench.py over 457M params,
+// interleaved runs: 8192 blocks 2.17-2.37 ms, 32768 2.05-2.32 ms, i.e. ~4% within noise)
+#ifndef SAVQA_ADAM_BLOCKS
+#define SAVQA_ADAM_BLOCKS 32768
+#endif
 typedef float adam_f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void adam4(adam_f4& pp, adam_f4 gg, adam_f4& mm, adam_f4& vv, float b1,
                                       float b2, float eps, float step_size, float sbc2, float gs) {
@@ -595,7 +600,7 @@ extern "C" int savqa_adam(void* stream, float* p, const float* g, float* m, floa
   const float step_size = lr / bc1;
   const float sbc2 = sqrtf(bc2);
   int64_t blocks = (n / 4 + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > SAVQA_ADAM_BLOCKS) blocks = SAVQA_ADAM_BLOCKS;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr,
                      beta1, beta2, eps, step_size, sbc2, grad_scale);
