@@ -77,32 +77,35 @@ def _sparse_worker(rank, world, port, q):
     from savqa_amd.ddp import GradReducer
     width, rows = 7, 50
     t0, t1 = 1000, 1000 + width * rows            # a row table inside the arena
-    n = t1 + 777
+    u0, u1 = t1 + 13, t1 + 13 + width * rows       # a second one (same ids), 13 floats later
+    n = u1 + 777
     gen = torch.Generator().manual_seed(rank)
     ids = torch.randint(0, rows, (3, 6), generator=gen)  # duplicates within and across ranks
     ids[0, 0] = rows - 1                           # last row touched by every rank
     g = torch.randn(n, generator=gen)
-    table = torch.zeros(rows, width)
-    table.index_add_(0, ids.reshape(-1), torch.randn(ids.numel(), width, generator=gen))
-    g[t0:t1] = table.reshape(-1)                   # untouched rows are zero, as in the model
+    for a0, a1 in ((t0, t1), (u0, u1)):
+        table = torch.zeros(rows, width)
+        table.index_add_(0, ids.reshape(-1), torch.randn(ids.numel(), width, generator=gen))
+        g[a0:a1] = table.reshape(-1)               # untouched rows are zero, as in the model
     dense = g.clone()
     dist.all_reduce(dense)
     arena = types.SimpleNamespace(grad=g.clone())
     red = GradReducer(arena, bucket_mb=0.001)      # 262 floats per bucket: the table spans several
+    red.add_sparse_table(u0, u1, width)            # registration order does not matter
     red.add_sparse_table(t0, t1, width)
     red.begin()
     red.set_rows(ids)
     red.reduce_range(0, 600, True)
     red.prepare_rows()
     red.reduce_range(600, 1100)                    # declarations split the table ...
-    red.reduce_range(1100, t1 + 100)               # ... and complete it
-    red.reduce_range(t1 + 100, n, True)
+    red.reduce_range(1100, u1 + 5)                 # ... and complete both
+    red.reduce_range(u1 + 5, n, True)
     works, scale = red.drain()
-    assert red.rows_exchanged == 1
+    assert red.rows_exchanged == 2
     spans = sorted((lo, hi) for _, lo, hi in works)
     for w, _, _ in works:
         w.wait()
-    q.put((rank, float((arena.grad - dense).abs().max()), spans, scale))
+    q.put((rank, float((arena.grad - dense).abs().max()), spans, scale, n, (u0, u1)))
     dist.destroy_process_group()
 
 
@@ -119,15 +122,15 @@ def test_sparse_table_rows_exchange_equals_dense_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, err, spans, scale in res:
+    for rank, err, spans, scale, n, tab2 in res:
         assert err < 1e-6
         assert scale == 0.5
-        assert (1000, 1350) in spans
+        assert (1000, 1350) in spans and tab2 in spans
         pos = 0
         for lo, hi in spans:
             assert lo == pos and hi > lo
             pos = hi
-        assert pos == 1350 + 777
+        assert pos == n
 
 
 def test_adam_grad_scale_matches_mean_of_grads():
