@@ -897,16 +897,16 @@ __device__ __forceinline__ void sk_load4(const float* __restrict__ P, int64_t ld
   }
 }
 
-template <bool AT, bool BT>
-__global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(savqa_gemm_desc d, int tiles_n,
+template <bool AT, bool BT, int NW>
+__global__ __launch_bounds__(64 * NW) void gemm_skinny_kernel(savqa_gemm_desc d, int tiles_n,
                                                                    int avec, int bvec) {
-  __shared__ float red[SK_WAVES][32][33];
+  __shared__ float red[NW][32][33];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int t = blockIdx.x;
   const int64_t m0 = (int64_t)(t / tiles_n) * 32, n0 = (int64_t)(t % tiles_n) * 32;
   // this wave's k range, in whole 8-k groups
   const int64_t ngrp = (d.K + 7) / 8;
-  const int64_t g0 = ngrp * w / SK_WAVES, g1 = ngrp * (w + 1) / SK_WAVES;
+  const int64_t g0 = ngrp * w / NW, g1 = ngrp * (w + 1) / NW;
   const int i = lane & 31, q = lane >> 5;
   const int64_t am = m0 + i, bn = n0 + i;
   const int64_t* arows = d.a_rows;  // !AT: gather on m; AT: gather on k
@@ -953,13 +953,13 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(savqa_gemm_d
   for (int r = 0; r < 16; ++r) red[w][(r & 3) + 8 * (r >> 2) + 4 * q][i] = acc[r];
   __syncthreads();
   const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
-  for (int e = threadIdx.x; e < 32 * 32; e += 64 * SK_WAVES) {
+  for (int e = threadIdx.x; e < 32 * 32; e += 64 * NW) {
     const int r = e >> 5, c = e & 31;
     const int64_t m = m0 + r, n = n0 + c;
     if (m >= d.M || n >= d.N) continue;
     float v = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < SK_WAVES; ++ww) v += red[ww][r][c];
+    for (int ww = 0; ww < NW; ++ww) v += red[ww][r][c];
     const EpiRow er = epi_row(d, m, ident);
     epi_store(d, er, m, n, v, true, d.atomic != 0);
   }
@@ -967,11 +967,11 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(savqa_gemm_d
     if (d.colsum_a && n0 == 0) {
       __syncthreads();
       float* flat = &red[0][0][0];
-      flat[threadIdx.x] = cs;  // 64 * SK_WAVES partials: (wave, half q, i)
+      flat[threadIdx.x] = cs;  // 64 * NW partials: (wave, half q, i)
       __syncthreads();
       if (threadIdx.x < 32 && m0 + threadIdx.x < d.M) {
         float sum = 0.f;
-        for (int j = 0; j < 2 * SK_WAVES; ++j) sum += flat[j * 32 + threadIdx.x];
+        for (int j = 0; j < 2 * NW; ++j) sum += flat[j * 32 + threadIdx.x];
         atomicAdd(&d.colsum_a[m0 + threadIdx.x], sum);
       }
     }
@@ -1164,6 +1164,19 @@ static int64_t sk16_ksmall() {
   static int64_t v = -1;
   if (v < 0) {
     const char* e = getenv("SAVQA_SK16_KSMALL");
+    v = e ? atoll(e) : 0;
+  }
+  return v;
+}
+
+// 32x32 skinny launches with K <= this use 4 waves per workgroup instead of 8 (env
+// SAVQA_SK32_KSMALL; A/B knob, default off: measured in-step on the K = 256 dW shapes
+// 1.0-1.6x slower -- the short k chains are latency-bound, fewer waves hide less;
+// tools/gpu_sk32k.sh)
+static int64_t sk32_ksmall() {
+  static int64_t v = -1;
+  if (v < 0) {
+    const char* e = getenv("SAVQA_SK32_KSMALL");
     v = e ? atoll(e) : 0;
   }
   return v;
@@ -1379,13 +1392,20 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
       else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<true, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
       else hipLaunchKernelGGL((gemm_skinny16_kernel<true, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
     }
+  } else if (d.K <= sk32_ksmall()) {
+    const dim3 g(p.grid_x), b(64 * 4);
+    const int tn = p.gg.tiles_n;
+    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, true, 4>), g, b, 0, s, d, tn, avec, bvec);
+    else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, false, 4>), g, b, 0, s, d, tn, avec, bvec);
+    else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<true, false, 4>), g, b, 0, s, d, tn, avec, bvec);
+    else hipLaunchKernelGGL((gemm_skinny_kernel<true, true, 4>), g, b, 0, s, d, tn, avec, bvec);
   } else {
     const dim3 g(p.grid_x), b(64 * SK_WAVES);
     const int tn = p.gg.tiles_n;
-    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, true>), g, b, 0, s, d, tn, avec, bvec);
-    else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, false>), g, b, 0, s, d, tn, avec, bvec);
-    else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<true, false>), g, b, 0, s, d, tn, avec, bvec);
-    else hipLaunchKernelGGL((gemm_skinny_kernel<true, true>), g, b, 0, s, d, tn, avec, bvec);
+    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+    else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+    else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<true, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+    else hipLaunchKernelGGL((gemm_skinny_kernel<true, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
   }
   return check_launch("savqa_gemm");
 }
