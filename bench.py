@@ -42,55 +42,94 @@ def train_flops_per_sample(Tv=50, Ts=73, Lq=14, Nv=36, Ns=59, d=512, L=6, C=914,
     return 3.0 * (stack(Tv) + stack(Ts) + heads + mil)
 
 
-def cpu_baseline(seconds=15.0, B=4, rate=0.5):
-    """Time the CPU oracle (oracle/savqa_oracle.py, the parity checker) on the host:
-    fwd + loss + bwd + Adam at the cfg-1 shape (B=4). Bounded sample."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds=24.0, rate=0.5):
+    """Time the CPU oracle (oracle/savqa_oracle.py, the parity checker) on the host, per
+    SURVEY.md 8(d): forward+loss AND the full train step (fwd+loss+bwd+Adam), at the cfg-1
+    shape B=4 and at the reference's per-GPU batch B=32, with every host thread the job
+    may use (OMP_NUM_THREADS, else the affinity mask). Bounded: ~seconds/4 per leg. The
+    headline `value` is the train step at B=32."""
     from oracle import hashfill
     from oracle import savqa_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
     torch.set_num_threads(threads)
-    gen = torch.Generator().manual_seed(0)
     Nv, Lq, Ns, K = 36, 14, 59, 5
-    inp = {
-        "vis_fea": torch.randn(B, Nv, 2048, generator=gen).clamp_min(0),
-        "vis_mask": torch.ones(B, Nv, Nv, dtype=torch.int32),
-        "q_ipt": torch.randint(0, 400000, (B, Lq), generator=gen),
-        "q_mask": torch.ones(B, Lq, Lq, dtype=torch.int32),
-        "q_graph": (torch.rand(B, Lq, Lq, generator=gen) < 0.2).int(),
-        "macro_ipt": torch.randint(0, 400000, (B, Ns), generator=gen),
-        "macro_mask": torch.ones(B, Ns, Ns, dtype=torch.int32),
-        "macro_graph": (torch.rand(B, Ns, Ns, generator=gen) < 0.05).int(),
-        "macro_obj_loc": torch.arange(Nv).repeat(B, 1),
-        "micro_positive_obj": torch.randint(0, 400000, (B, Nv, K), generator=gen),
-        "micro_negative_obj": torch.randint(0, 400000, (B, Nv, K), generator=gen),
-        "micro_obj_mask": torch.ones(B, Nv, K, dtype=torch.int32),
-    }
-    answer = torch.randint(1, 914, (B,), generator=gen)
     P = hashfill.HashParams(requires_grad=True)
     state = {}
 
-    def step(i):
+    def inputs(B):
+        gen = torch.Generator().manual_seed(B)
+        inp = {
+            "vis_fea": torch.randn(B, Nv, 2048, generator=gen).clamp_min(0),
+            "vis_mask": torch.ones(B, Nv, Nv, dtype=torch.int32),
+            "q_ipt": torch.randint(0, 400000, (B, Lq), generator=gen),
+            "q_mask": torch.ones(B, Lq, Lq, dtype=torch.int32),
+            "q_graph": (torch.rand(B, Lq, Lq, generator=gen) < 0.2).int(),
+            "macro_ipt": torch.randint(0, 400000, (B, Ns), generator=gen),
+            "macro_mask": torch.ones(B, Ns, Ns, dtype=torch.int32),
+            "macro_graph": (torch.rand(B, Ns, Ns, generator=gen) < 0.05).int(),
+            "macro_obj_loc": torch.arange(Nv).repeat(B, 1),
+            "micro_positive_obj": torch.randint(0, 400000, (B, Nv, K), generator=gen),
+            "micro_negative_obj": torch.randint(0, 400000, (B, Nv, K), generator=gen),
+            "micro_obj_mask": torch.ones(B, Nv, K, dtype=torch.int32),
+        }
+        return inp, torch.randint(1, 914, (B,), generator=gen)
+
+    nstep = [0]
+
+    def fwd_loss(inp, answer):
+        with torch.no_grad():
+            lc, lv, ls, mil, _ = O.attmodel_forward(P, inp)
+            O.train_loss(lc, lv, ls, answer, mil)
+
+    def train_step(inp, answer):
+        nstep[0] += 1
         for p in P.values():
             p.grad = None
-        drop = (1000 + i, rate) if rate > 0 else None
+        drop = (1000 + nstep[0], rate) if rate > 0 else None
         lc, lv, ls, mil, _ = O.attmodel_forward(P, inp, drop=drop)
         loss, _ = O.train_loss(lc, lv, ls, answer, mil)
         loss.backward()
         with torch.no_grad():
-            O.adam_step(P, {k: v.grad for k, v in P.items() if v.grad is not None}, state, i + 1)
+            O.adam_step(P, {k: v.grad for k, v in P.items() if v.grad is not None}, state,
+                        nstep[0])
 
-    step(0)  # materialise the lazily hash-filled parameters (setup, untimed)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        step(n + 1)
-        n += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(B * n / dt, 3), "unit": "QA-samples/s", "cores": threads,
+    legs = {}
+    for name, fn in (("train_step", train_step), ("fwd_loss", fwd_loss)):
+        for B in (4, 32):
+            inp, answer = inputs(B)
+            fn(inp, answer)  # warm (the first call materialises the hash-filled params)
+            n, t0 = 0, time.perf_counter()
+            while True:
+                fn(inp, answer)
+                n += 1
+                if time.perf_counter() - t0 >= seconds / 4:
+                    break
+            dt = time.perf_counter() - t0
+            legs[f"{name}_b{B}"] = {"samples_per_s": round(B * n / dt, 3), "iters": n,
+                                    "seconds": round(dt, 2)}
+    head = legs["train_step_b32"]
+    return {"value": head["samples_per_s"], "unit": "QA-samples/s", "cores": threads,
             "kind": "port",
-            "sample": f"oracle/savqa_oracle.py train step (fwd+loss+bwd+Adam), cfg-1 shape "
-                      f"B={B}, dropout {rate}, {n} steps in {dt:.1f}s, torch CPU {threads} threads"}
+            "host_cpus": os.cpu_count(), "affinity_cpus": avail, "cpu_model": _cpu_model(),
+            "legs": legs,
+            "sample": f"oracle/savqa_oracle.py on torch CPU ({threads} threads): train step "
+                      f"(fwd+loss+bwd+Adam, dropout {rate}) and fwd+loss at the cfg-1 shape, "
+                      f"B=4 and B=32 (value = train step, B=32), ~{seconds / 4:.0f}s per leg"}
 
 
 WORKLOADS = {
@@ -143,7 +182,7 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.5,
                     help="dropout_rate (reference training default 0.5, main:466)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=24.0)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--serial", action="store_true",
                     help="run both stacks on one stream (per-kernel profiling)")

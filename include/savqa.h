@@ -51,8 +51,6 @@ const char* savqa_last_error(void);
  * Non-atomic launches with a linear epilogue (relu=0, beta=0, C not aliasing resid) may
  * split the last partial wave of tiles over K internally (zero-fill + atomics): results
  * then differ from a single-pass launch only in fp32 summation order.
- * SAVQA_GEMM_SK=1 selects a stream-K launch instead (tiles cut between workgroups are
- * combined in-launch in a fixed order; 64 MB library-owned workspace per stream).
  * prec (128x128-tile launches; the skinny kernel stays fp32): 1 = operands rounded to
  * bf16 while they are staged in LDS, v_mfma_f32_32x32x16_bf16, fp32 accumulate and
  * epilogue (BASELINE cfg 3's bf16 training); 3 = each operand split into bf16 hi + lo
@@ -80,8 +78,8 @@ typedef struct savqa_gemm_desc {
 
 int savqa_gemm(void* stream, const savqa_gemm_desc* d);
 
-/* The launch plan savqa_gemm would use for *d (no launch): out[0] = tile (32: skinny kernel, 128),
- * out[1] = split-K factor (-1: stream-K launch), out[2] = tail split factor (0: none),
+/* The launch plan savqa_gemm would use for *d (no launch): out[0] = tile (16 / 32: skinny
+ * kernels, 128), out[1] = split-K factor, out[2] = tail split factor (0: none),
  * out[3] = workgroups. */
 int savqa_gemm_plan(const savqa_gemm_desc* d, int32_t* out);
 
@@ -102,12 +100,16 @@ int savqa_ln_fwd(void* stream, const float* x, const float* xscale, const float*
                  float* z_out, float* y, float* mean, float* rden, float* stdv, float* flag);
 
 /* Backward of the above: dz = dLN/dz (+ dz_add), dgamma += ..., dbeta += ...
- * (column sums land in a library-owned 128 KB per-stream slot workspace first -- see
- * ln.hip -- and a second tiny kernel on the same stream folds them into dgamma/dbeta) */
+ * Column sums land in the caller's slot workspace `ws` first (ws_bytes >=
+ * savqa_ln_bwd_workspace_bytes(cols), 16-B aligned, ZERO-FILLED before its first use);
+ * a second tiny kernel on the same stream folds them into dgamma/dbeta and re-zeroes
+ * the slots, so one workspace serves every later call on the same stream (calls on
+ * concurrently running streams need one workspace each). */
+int64_t savqa_ln_bwd_workspace_bytes(int64_t cols);
 int savqa_ln_bwd(void* stream, const float* dy, const float* z, const float* mean,
                  const float* rden, const float* stdv, const float* gamma,
                  int64_t rows, int64_t cols, const float* dz_add, float* dz,
-                 float* dgamma, float* dbeta);
+                 float* dgamma, float* dbeta, float* ws, int64_t ws_bytes);
 
 /* flag[r] = sign(|sum_c X[r*ldx+c]|)  (modules.py:257 key mask / :289 query mask) */
 int savqa_rowflag(void* stream, const float* X, int64_t rows, int64_t cols, int64_t ldx, float* flag);

@@ -10,7 +10,8 @@ reference's state_dict keys, the algorithm of
                                           label_smoothing)
   /root/reference/models/AttModel_x3.py  (AttModel_vis_grid, AttModel_syb, MIL_NCE
                                           only_obj branch, AttModel heads)
-  /root/reference/models/main_itp_ddp_tar_super_node.py:335-366 (loss, Adam step)
+  /root/reference/models/main_itp_ddp_tar_super_node.py:335-366 (loss, Adam step),
+                                          :42-142, :380-404 (eval metrics + gather)
 Each function cites the reference lines it follows. Backward is torch autograd
 over these ops.
 
@@ -334,6 +335,38 @@ def train_loss(logits_concat, logits_vis, logits_syb, answer, mil_nce_obj,
     if with_milnce:
         loss = loss + (-mil_nce_obj - mil_nce_rel)
     return loss, lsm
+
+
+def eval_batch(logits_concat, logits_vis, logits_syb, answer, mil_nce_obj, mil_nce_rel=0,
+               with_milnce=False, epsilon=0.1):
+    """One batch of eval(), main_itp_ddp_tar_super_node.py:103-133: the label-smoothed loss
+    (+ the MIL-NCE loss if --with_MILNCE_loss, :129-131), cnt_correct over NON-ZERO answers
+    (:125-126, torch.max = first maximal index), cnt += batch_size (:127: every sample).
+    Returns (loss, correct, batch_size, mil_nce_loss) as Python numbers."""
+    loss, lsm = train_loss(logits_concat, logits_vis, logits_syb, answer, mil_nce_obj,
+                           with_milnce=with_milnce, epsilon=epsilon, mil_nce_rel=mil_nce_rel)
+    _, pred = torch.max(lsm, dim=1)
+    nz = torch.nonzero(answer)
+    correct = int((pred[nz] == answer[nz]).long().sum())
+    mil_loss = -mil_nce_obj - mil_nce_rel
+    return float(loss), correct, int(answer.shape[0]), float(mil_loss)
+
+
+def eval_epoch(batch_stats):
+    """eval()'s return value (main:42-142): (loss_meter.avg, cnt_correct, cnt) over the
+    batches' eval_batch() results (AverageMeter weighted by batch size, misc.py:46-63)."""
+    tot = sum(b for _, _, b, _ in batch_stats)
+    avg = sum(l * b for l, _, b, _ in batch_stats) / tot if tot else 0.0
+    return avg, sum(c for _, c, _, _ in batch_stats), tot
+
+
+def gather_epoch_metrics(per_rank):
+    """main:383-404: the 3-float (loss, cnt_correct, cnt) vectors of every rank are
+    all-gathered; loss = mean over ranks, counts summed; accuracy = correct / cnt."""
+    loss = sum(v[0] for v in per_rank) / len(per_rank)
+    corr = sum(v[1] for v in per_rank)
+    cnt = sum(v[2] for v in per_rank)
+    return loss, corr, cnt, (corr / cnt if cnt else 0.0)
 
 
 def adam_step(params, grads, state, step, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8):

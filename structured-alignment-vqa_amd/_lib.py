@@ -56,7 +56,9 @@ _SIGS = {
     "savqa_gemm_plan": [C.POINTER(GemmDesc), c_p],
     "savqa_colsum_acc": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
     "savqa_ln_fwd": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p],
-    "savqa_ln_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p],
+    "savqa_ln_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p,
+                     c_i64],
+    "savqa_ln_bwd_workspace_bytes": [c_i64],
     "savqa_rowflag": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
     "savqa_gattn_fwd": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
                         c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p],
@@ -101,6 +103,8 @@ _SIGS = {
     "savqa_adam": [c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_f, c_f],
 }
 
+_I64_RET = {"savqa_ln_bwd_workspace_bytes"}
+
 _lib = None
 
 
@@ -123,7 +127,7 @@ def load(path: str = None):
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = C.c_int
+        fn.restype = C.c_int64 if name in _I64_RET else C.c_int
     lib.savqa_last_error.argtypes = []
     lib.savqa_last_error.restype = C.c_char_p
     _lib = lib

@@ -593,11 +593,7 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
   //   groups [8,12): dQ = dS K                        (nw query tiles each, k = key).
   // Each wave takes a CONTIGUOUS run of tiles, so consecutive tiles share the group's
   // B column block (dO / Q / K[:, dt]), loaded once into registers per group.
-#ifdef SAVQA_ATTN_SKIP_P2  // timing experiment only: phase 1 alone
-  const int nitems = 0;
-#else
   const int nitems = 8 * NJT + 4 * nw;
-#endif
   const int it0 = nitems * w / nw, it1 = nitems * (w + 1) / nw;
   int cur = -1;
   float bcol[8][4];  // B rows k = 16 kc + 4g + t of column dt*16 + col (kc < 8)

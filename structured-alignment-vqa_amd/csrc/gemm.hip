@@ -1,5 +1,4 @@
-// fp32 GEMM on gfx950 matrix cores (v_mfma_f32_16x16x4_f32 by default, 32x32x2 as a build
-// option: exact f32, 64 FLOP/clk/SIMD either way).
+// fp32 GEMM on gfx950 matrix cores (v_mfma_f32_16x16x4_f32: exact f32, 64 FLOP/clk/SIMD).
 //
 // Replaces every nn.Linear of the SA-VQA model_v=3 path and the two backward GEMMs of
 // each (dX = dY W, dW = dY^T X). One kernel template covers the operand layouts:
@@ -10,7 +9,7 @@
 // ReLU, row scale, ReLU-backward mask, beta-accumulate, atomic scatter to indexed rows
 // (embedding-table gradient) -- see include/savqa.h for the exact formula.
 //
-// Tiling: 256 threads = 4 waves (2x2), block tile BMxBN (128x128 or 64x64), BK 16/32.
+// Tiling: 256 threads = 4 waves (2x2), block tile 128x128, BK 16.
 // Each operand tile keeps its global orientation in LDS, so every global->LDS move is a
 // float4 load + one ds_write_b128 (no transposition):
 //   ROW operand (k contiguous: X, W of the forward, dY of dX) -> LDS [m][BK+4]; the
@@ -27,39 +26,18 @@
 #include "gemm_common.h"
 
 #include <algorithm>
-#include <cstdlib>
-#include <map>
-#include <mutex>
-
-#ifndef SAVQA_GEMM_OCC
-#define SAVQA_GEMM_OCC 2  // workgroups (= waves per SIMD) per CU
-#endif
-#ifndef SAVQA_GEMM_BK
-#define SAVQA_GEMM_BK 16  // k-tile; 16 beats 32 on the K=512 step shapes (shorter prologue)
-#endif
-#ifndef SAVQA_GEMM_BK_DW
-#define SAVQA_GEMM_BK_DW 16  // k-tile of the dW layouts (A = dY^T, K = B*T rows); 32 measured
-#endif                       // no better (tools/gemm_bench.py, cfg-2 dW shapes)
 
 namespace savqa {
 
-// MFMA shape of the 128x128 path (fp32 in, fp32 accumulate; same 64 FLOP/clk/SIMD):
-//   Mi32: v_mfma_f32_32x32x2_f32, 32-row fragments, 16 accumulator VGPRs per fragment;
-//   Mi16: v_mfma_f32_16x16x4_f32, 16-row fragments, 4 accumulator VGPRs per fragment
-//         (per FLOP it moves 40% fewer accumulator registers through the matrix core).
-// A fragment's operand lane (i, q) feeds k = KCH*c + 4q + j in MFMA step j (b128 trick).
-struct Mi32 {
-  static constexpr int FR = 32, KCH = 8, NACC = 16;
-  using Acc = f32x16;
-  static __device__ __forceinline__ Acc mma(float a, float b, Acc c) {
-    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-  }
-  static __device__ __forceinline__ int lane_i(int lane) { return lane & 31; }
-  static __device__ __forceinline__ int lane_q(int lane) { return lane >> 5; }
-  static __device__ __forceinline__ int row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
-  static __device__ __forceinline__ int col(int lane) { return lane & 31; }
-};
-struct Mi16 {
+constexpr int GEMM_OCC = 2;   // workgroups (= waves per SIMD) per CU
+constexpr int GEMM_BK = 16;   // k-tile; 16 beats 32 on the K=512 step shapes (shorter prologue)
+constexpr int GEMM_BK_DW = 16;  // k-tile of the dW layouts (A = dY^T, K = B*T rows); 32 no better
+
+// MFMA of the 128x128 path: v_mfma_f32_16x16x4_f32 (fp32 in, fp32 accumulate, 64
+// FLOP/clk/SIMD), 16-row fragments, 4 accumulator VGPRs each. A fragment's operand lane
+// (i, q) feeds k = 16c + 4q + j in MFMA step j of k-chunk c (the b128 trick).
+// (v_mfma_f32_32x32x2_f32 measured 5-10% slower on every cfg-2 shape: DESIGN.md 6.)
+struct GemmMi {
   static constexpr int FR = 16, KCH = 16, NACC = 4;
   using Acc = f4;
   static __device__ __forceinline__ Acc mma(float a, float b, Acc c) {
@@ -70,28 +48,6 @@ struct Mi16 {
   static __device__ __forceinline__ int row(int r, int lane) { return 4 * (lane >> 4) + r; }
   static __device__ __forceinline__ int col(int lane) { return lane & 15; }
 };
-// epilogue operand prefetch: 0 = none (one load per element, after the previous store),
-// 1 = mask bits + residual per 32-row fragment, 2 = the tile's mask bits up front
-#ifndef SAVQA_EPI_PRE
-#define SAVQA_EPI_PRE 1
-#endif
-#ifndef SAVQA_GEMM_DW_TILE
-#define SAVQA_GEMM_DW_TILE 128
-#endif
-#ifndef SAVQA_GEMM_BK_DW64
-#define SAVQA_GEMM_BK_DW64 32
-#endif
-#ifndef SAVQA_GEMM_ROWPAIR
-#define SAVQA_GEMM_ROWPAIR 1  // conflict-free ROW-tile stores (Operand::row_of)
-#endif
-#ifndef SAVQA_GEMM_MI
-#define SAVQA_GEMM_MI 16  // 16x16x4: 5-10% faster than 32x32x2 on every cfg-2 shape (A/B)
-#endif
-#if SAVQA_GEMM_MI == 16
-using GemmMi = Mi16;
-#else
-using GemmMi = Mi32;
-#endif
 
 template <int BMX, int BK, bool ROW>
 struct Operand {
@@ -108,7 +64,7 @@ struct Operand {
   // share a 16-B slot (2-way conflict on every store); pairing rows r and r+4 in one
   // lane group makes their slots disjoint. (The ds_read_b128 fetch stays conflict-free.)
   static __device__ __forceinline__ int row_of(int q) {
-    if constexpr (SAVQA_GEMM_ROWPAIR && ROW && PER == 4)
+    if constexpr (ROW && PER == 4)
       return (q & ~7) | ((q & 7) >> 1) | ((q & 1) << 2);
     else return q;
   }
@@ -228,95 +184,10 @@ struct Operand {
   }
 };
 
-// COL source (m contiguous: dY^T and X of a dW GEMM) stored ROW-wise ([m][BK+4]) so the
-// MFMA operands come from one ds_read_b128 per 8 k like the forward's, instead of four
-// ds_read_b32. Each thread owns one 4(k) x 4(m) block per k-tile: four float4 loads along
-// m (one per k row, wave-contiguous), a register transpose, four float4 stores along k.
-// Needs BMX * BK == 16 * GEMM_NT (BK = 32 at 128-wide tiles).
-template <int BMX, int BK>
-struct OperandT {
-  static constexpr int LD = BK + 4;
-  static constexpr int SIZE = BMX * LD;
-  static constexpr int PER = BMX / 4;  // m-quads per k row (colsum: column group = tid % PER)
-  static constexpr int ITERS = 1;      // colsum partial f4s per thread
-  static_assert(BMX * BK == 16 * GEMM_NT, "one 4x4 block per thread");
-  f4 r[4];
-  const float* rp;
-
-  __device__ __forceinline__ void setup_fast(const float* __restrict__ base, int64_t ld,
-                                             const int64_t* __restrict__ rows, int64_t m0,
-                                             int64_t mlim, int tid) {
-    (void)rows;  // the fast path never gathers k rows
-    rp = base + (int64_t)(4 * (tid / PER)) * ld + min(m0 + 4 * (tid % PER), mlim - 4);
-  }
-  __device__ __forceinline__ void load_fast(int64_t ld, int64_t k0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = *reinterpret_cast<const f4*>(rp + (k0 + j) * ld);
-  }
-  __device__ __forceinline__ void setup_kg(int64_t ld, int tid) {
-    rp -= (int64_t)(4 * (tid / PER)) * ld;
-  }
-  __device__ __forceinline__ void load_fast_kg(int64_t ld, const int64_t* __restrict__ rows,
-                                               int64_t k0, int tid) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      r[j] = *reinterpret_cast<const f4*>(rp + rows[k0 + 4 * (tid / PER) + j] * ld);
-  }
-  __device__ __forceinline__ void load_slow(const float* __restrict__ base, int64_t ld,
-                                            const int64_t* __restrict__ rows, int64_t mlim,
-                                            int64_t m0, int64_t k0, int64_t kend, int tid) {
-    const int64_t col = m0 + 4 * (tid % PER);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t row = k0 + 4 * (tid / PER) + j;
-      const bool rok = row < kend;
-      const int64_t rc = rok ? row : 0;
-      const int64_t rr = rows ? rows[rc] : rc;
-      const float* p = base + rr * ld;
-      float e[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool ok = rok && (col + q < mlim);
-        const float val = p[ok ? col + q : 0];
-        e[q] = ok ? val : 0.f;
-      }
-      r[j] = f4{e[0], e[1], e[2], e[3]};
-    }
-  }
-  __device__ __forceinline__ void accum(f4 (&cs)[ITERS]) const {
-    cs[0] += (r[0] + r[1]) + (r[2] + r[3]);
-  }
-  __device__ __forceinline__ void store(float* __restrict__ s, int tid) const {
-    const int m = 4 * (tid % PER), k = 4 * (tid / PER);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<f4*>(&s[(m + i) * LD + k]) = f4{r[0][i], r[1][i], r[2][i], r[3][i]};
-  }
-  template <class MI>
-  static __device__ __forceinline__ void fetch(const float* __restrict__ s, int wbase, int f,
-                                               int c, int lane, float (&v)[4]) {
-    Operand<BMX, BK, true>::template fetch<MI>(s, wbase, f, c, lane, v);
-  }
-};
-
-// dW layouts (a_trans) can stage both m-contiguous operands transposed (needs
-// SAVQA_GEMM_BK_DW=32). Off: measured 3-9% slower on the cfg-2 dW shapes than the
-// [k][m] staging with four ds_read_b32 (108.9 vs 117.0 TF at 6144x512x18688), so LDS
-// operand reads are not what bounds the dW kernel.
-#ifndef SAVQA_GEMM_DW_T
-#define SAVQA_GEMM_DW_T 0
-#endif
-template <int BMX, int BK, bool ROW, bool TR>
-struct OpSel { using T = Operand<BMX, BK, ROW>; };
-template <int BMX, int BK>
-struct OpSel<BMX, BK, false, true> { using T = OperandT<BMX, BK>; };
-
 template <int BM, int BN, int BK, bool AT, bool BT>
 struct GemmCfg {
-  static constexpr bool TR = AT && SAVQA_GEMM_DW_T && BM * BK == 16 * GEMM_NT &&
-                             BN * BK == 16 * GEMM_NT;
-  using OA = typename OpSel<BM, BK, !AT, TR>::T;
-  using OB = typename OpSel<BN, BK, BT, TR>::T;
+  using OA = Operand<BM, BK, !AT>;
+  using OB = Operand<BN, BK, BT>;
   using MI = GemmMi;
   using Acc = typename MI::Acc;
   static constexpr int WM = BM / 2, WN = BN / 2;
@@ -345,12 +216,6 @@ __device__ __forceinline__ void gemm_compute_tile(
 #pragma unroll
       for (int j = 0; j < G::FN; ++j) G::OB::template fetch<MI>(Bs, wn * G::WN, j, c + 1, lane, b[cur ^ 1][j]);
     }
-#ifdef SAVQA_GEMM_SGB
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-#ifdef SAVQA_GEMM_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -358,26 +223,14 @@ __device__ __forceinline__ void gemm_compute_tile(
 #pragma unroll
         for (int j = 0; j < G::FN; ++j)
           acc[i][j] = MI::mma(a[cur][i][s], b[cur][j][s], acc[i][j]);
-#ifdef SAVQA_GEMM_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
-#ifdef SAVQA_GEMM_SGB
-    __builtin_amdgcn_sched_barrier(0);
-#endif
   }
 }
 
 // k-loop order. Measured (tools/gemm_bench.py, cfg-2 shapes): storing the staged tile
 // right after the barrier (T14) is +1-4% on the k-contiguous-A layouts (forward, dX) and
 // -1..-4% on dW (A = dY^T, m-contiguous), so dW keeps the store-after-compute order.
-// SAVQA_GEMM_T14=0/2 forces the old / new order everywhere (A/B builds).
-#ifndef SAVQA_GEMM_T14
-#define SAVQA_GEMM_T14 1
-#endif
 template <bool AT>
-__host__ __device__ constexpr bool gemm_t14() {
-  return SAVQA_GEMM_T14 == 2 || (SAVQA_GEMM_T14 == 1 && !AT);
-}
+__host__ __device__ constexpr bool gemm_t14() { return !AT; }
 
 // k-loop load mode of a block (block-uniform): 0 = guarded loads everywhere (unaligned
 // operands, odd edge widths), 1 = branch-free loads on every k-tile, 2 = branch-free
@@ -499,7 +352,7 @@ __device__ __forceinline__ void cs_fold(const f4 (&cs)[ITERS], float* smem, int6
 }
 
 template <int BM, int BN, int BK, bool AT, bool BT>
-__global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_waves_per_eu(SAVQA_GEMM_OCC, SAVQA_GEMM_OCC))) void gemm_f32_kernel(savqa_gemm_desc d, GemmGrid gg,
+__global__ __launch_bounds__(GEMM_NT, GEMM_OCC) __attribute__((amdgpu_waves_per_eu(GEMM_OCC, GEMM_OCC))) void gemm_f32_kernel(savqa_gemm_desc d, GemmGrid gg,
                                                              int avec, int bvec) {
   using G = GemmCfg<BM, BN, BK, AT, BT>;
   constexpr int FM = G::FM, FN = G::FN, WM = G::WM, WN = G::WN;
@@ -571,24 +424,6 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
   // (bias, ReLU-backward mask, residual) serialised a memory round trip per element.
   //   bias: FN values per lane and the mask bits (rows indexed by m) for the whole tile,
   //   the residual per 32-row fragment (a whole tile's would spill).
-#if SAVQA_EPI_PRE == 0
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-#pragma unroll
-    for (int r = 0; r < MI::NACC; ++r) {
-      const int64_t m = m0 + wm * WM + i * MI::FR + MI::row(r, lane);
-      if (m >= d.M) continue;
-      const EpiRow er = epi_row(d, m, ident);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int64_t n = n0 + wn * WN + j * MI::FR + MI::col(lane);
-        if (n >= d.N) continue;
-        epi_store(d, er, m, n, acc[i][j][r], first_split, atomic);
-      }
-    }
-  }
-}
-#else
   const bool mask_pre = d.mask && !d.mask_arows;
   const bool res_pre = first_split && d.resid != nullptr;
   float bv[FN];
@@ -599,29 +434,9 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
   }
   uint32_t keep[FM];
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {  // mask bits of the whole tile before its first store
-    keep[i] = 0xffffffffu;
-    if (SAVQA_EPI_PRE == 2 && mask_pre) {
-      float mv[MI::NACC][FN];
-#pragma unroll
-      for (int r = 0; r < MI::NACC; ++r) {
-        const int64_t m = min(m0 + wm * WM + i * MI::FR + MI::row(r, lane), (int64_t)d.M - 1);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int64_t n = min(n0 + wn * WN + j * MI::FR + MI::col(lane), (int64_t)d.N - 1);
-          mv[r][j] = d.mask[m * d.ldmask + n];
-        }
-      }
-      keep[i] = 0;
-#pragma unroll
-      for (int r = 0; r < MI::NACC; ++r)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) keep[i] |= (mv[r][j] > 0.f ? 1u : 0u) << (r * FN + j);
-    }
-  }
-#pragma unroll
   for (int i = 0; i < FM; ++i) {
-    if (SAVQA_EPI_PRE == 1 && mask_pre) {  // this fragment's mask bits
+    keep[i] = 0xffffffffu;
+    if (mask_pre) {  // this fragment's mask bits (a whole tile's up front spilled)
       float mv[MI::NACC][FN];
 #pragma unroll
       for (int r = 0; r < MI::NACC; ++r) {
@@ -675,179 +490,6 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
   }
 }
 
-#endif
-
-// ---------------------------------------------------------------------------------------
-// Stream-K launch of the same 128x128 tile machinery (opt-in, see sk_enabled()).
-// The T x nch (tile, k-tile) iteration space is cut into G equal contiguous ranges, one per
-// workgroup (G = 2 per CU): no wave-quantisation tail, whatever T is. A workgroup walks its
-// range tile segment by tile segment; a segment covering a whole tile runs the normal
-// epilogue. A tile cut between workgroups is combined in-launch (cdna_hip_programming.md,
-// "In-launch split-K reduction"): each contributor stores its fp32 accumulator slab
-// (plain dwordx4) -> vmcnt(0) -> barrier -> lane 0 agent-scope release -> vmcnt(0) ->
-// relaxed agent fetch_add on the tile's ticket; the contributor drawing the last ticket
-// acquires (agent scope), sums every contributor's slab in workgroup order (deterministic
-// whichever arrives last), runs the full epilogue (any epilogue: ReLU included) and
-// resets the ticket. A workgroup has at most two cut segments (its first and its last),
-// so slabs are [G][2][BM*BN] floats, owned per stream by the library.
-struct SkGrid {
-  int tiles_n, nch, G;
-  int R;       // data-parallel rounds first: workgroup w owns whole tiles r*G + w, r < R
-  int64_t I0;  // = R * G * nch: start of the stream-K iteration range
-  int64_t I;   // stream-K iterations: (T - R*G) * nch
-  float* slabs;
-  int* cnt;    // per-tile tickets (zero between launches)
-};
-
-__device__ __forceinline__ int64_t sk_begin(int64_t w, const SkGrid& s) { return s.I0 + w * s.I / s.G; }
-__device__ __forceinline__ int64_t sk_owner(int64_t x, const SkGrid& s) {  // workgroup holding iteration x
-  return ((x - s.I0 + 1) * s.G - 1) / s.I;
-}
-
-template <int BM, int BN, int BK, bool AT, bool BT>
-__global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_waves_per_eu(SAVQA_GEMM_OCC, SAVQA_GEMM_OCC))) void gemm_sk_kernel(savqa_gemm_desc d, SkGrid sk,
-                                                             int avec, int bvec) {
-  using G = GemmCfg<BM, BN, BK, AT, BT>;
-  constexpr int FM = G::FM, FN = G::FN, WM = G::WM, WN = G::WN;
-  using MI = typename G::MI;
-  constexpr int NACC4 = FM * FN * MI::NACC / 4;  // float4 groups of accumulators per thread
-  __shared__ __attribute__((aligned(16))) float smem[2 * (G::OA::SIZE + G::OB::SIZE)];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int64_t w = xcd_remap(blockIdx.x, sk.G);  // neighbouring tiles share an XCD's L2
-  int64_t it = sk_begin(w, sk);
-  const int64_t it_end = sk_begin(w + 1, sk);
-  const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
-  for (int r = 0;; ++r) {
-    // rounds r < R: the whole tile r*G + w; then this workgroup's stream-K range
-    int64_t tile, t0;
-    int kc0, kc1;
-    if (r < sk.R) {
-      tile = (int64_t)r * sk.G + w;
-      t0 = tile * sk.nch;
-      kc0 = 0;
-      kc1 = sk.nch;
-    } else {
-      if (it >= it_end) break;
-      tile = it / sk.nch;
-      t0 = tile * sk.nch;
-      kc0 = (int)(it - t0);
-      kc1 = (int)min((int64_t)sk.nch, it_end - t0);
-    }
-    const int tn = (int)(tile % sk.tiles_n);
-    const int tm = (int)(tile / sk.tiles_n);
-    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-    const int64_t kbeg = (int64_t)kc0 * BK, kend = min(d.K, (int64_t)kc1 * BK);
-    typename G::Acc acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < MI::NACC; ++r) acc[i][j][r] = 0.f;
-    const int mode = gemm_mode<BM, BN, BK, AT, BT>(d, m0, n0, kbeg, kend, avec, bvec);
-    const int ntiles = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
-    const bool do_cs = AT && d.colsum_a != nullptr && tn == 0;
-    f4 cs[G::OA::ITERS];
-#pragma unroll
-    for (int q = 0; q < G::OA::ITERS; ++q) cs[q] = f4{0.f, 0.f, 0.f, 0.f};
-    if (ntiles > 0) {
-      if (mode == 1)
-        gemm_mainloop<BM, BN, BK, AT, BT, 1>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
-      else if (mode == 2)
-        gemm_mainloop<BM, BN, BK, AT, BT, 2>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
-      else if (mode == 3)
-        gemm_mainloop<BM, BN, BK, AT, BT, 3>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
-      else
-        gemm_mainloop<BM, BN, BK, AT, BT, 0>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
-    }
-    if constexpr (AT) {
-      if (do_cs) {  // this segment's share of the bias gradient (atomics: segments add up)
-        cs_fold<G::OA::PER, G::OA::ITERS, BM>(cs, smem, m0, d);
-        __syncthreads();
-      }
-    }
-    bool epi = true;
-    if (!(kc0 == 0 && kc1 == sk.nch)) {
-      // ---- cut tile: publish this segment's slab, the last arriver combines
-      f4* slab = reinterpret_cast<f4*>(sk.slabs + (w * 2 + (kc0 != 0 ? 0 : 1)) * (int64_t)(BM * BN));
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int q = 0; q < MI::NACC / 4; ++q) {
-            const f4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-            slab[((i * FN + j) * (MI::NACC / 4) + q) * GEMM_NT + tid] = v;
-          }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const int64_t w0 = sk_owner(t0, sk), w1 = sk_owner(t0 + sk.nch - 1, sk);
-      int* flag = reinterpret_cast<int*>(smem);
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int ticket = __hip_atomic_fetch_add(&sk.cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = ticket == (int)(w1 - w0) ? 1 : 0;
-      }
-      __syncthreads();
-      epi = *flag != 0;
-      __syncthreads();  // the flag word is read before smem is reused
-      if (epi) {
-        if (tid == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int r = 0; r < MI::NACC; ++r) acc[i][j][r] = 0.f;
-        for (int64_t wc = w0; wc <= w1; ++wc) {  // fixed order: deterministic sum
-          const int slot = sk_begin(wc, sk) > t0 ? 0 : 1;
-          const f4* sl = reinterpret_cast<const f4*>(sk.slabs + (wc * 2 + slot) * (int64_t)(BM * BN));
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-#pragma unroll
-              for (int q = 0; q < MI::NACC / 4; ++q) {
-                const f4 v = sl[((i * FN + j) * (MI::NACC / 4) + q) * GEMM_NT + tid];
-                acc[i][j][4 * q] += v[0];
-                acc[i][j][4 * q + 1] += v[1];
-                acc[i][j][4 * q + 2] += v[2];
-                acc[i][j][4 * q + 3] += v[3];
-              }
-        }
-        if (tid == 0) sk.cnt[tile] = 0;  // ready for the next launch on this stream
-      }
-    }
-    if (epi) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-#pragma unroll
-        for (int r = 0; r < MI::NACC; ++r) {
-          const int64_t m = m0 + wm * WM + i * MI::FR + MI::row(r, lane);
-          if (m >= d.M) continue;
-          const EpiRow er = epi_row(d, m, ident);
-#pragma unroll
-          for (int j = 0; j < FN; ++j) {
-            const int64_t n = n0 + wn * WN + j * MI::FR + MI::col(lane);
-            if (n >= d.N) continue;
-            epi_store(d, er, m, n, acc[i][j][r], true, d.atomic != 0);
-          }
-        }
-      }
-    }
-    if (r >= sk.R) it = t0 + kc1;
-  }
-  (void)NACC4;
-}
-
 // ---------------------------------------------------------------------------------------
 // Small-M / small-N GEMMs (the decoder and head Linears at M = B = 256 rows, their dW at
 // K = 256): one 32x32 output tile per 512-thread workgroup, the 8 waves split K eight ways
@@ -855,14 +497,8 @@ __global__ __launch_bounds__(GEMM_NT, SAVQA_GEMM_OCC) __attribute__((amdgpu_wave
 // 8 short MFMA chains instead of 32 workgroups of one long one. Operands go straight from
 // global memory (L2) into MFMA registers: lane half q of an 8-k group takes k = 8g+4q+s,
 // s = 0..3 -- one b128 load on a k-contiguous operand, 4 coalesced scalars otherwise.
-#ifndef SAVQA_SK_WAVES
-#define SAVQA_SK_WAVES 8
-#endif
-#ifndef SAVQA_SK_DEPTH
-#define SAVQA_SK_DEPTH 2  // 4 and 8 measured no faster (tools/ab_skinny.sh)
-#endif
-constexpr int SK_WAVES = SAVQA_SK_WAVES;
-constexpr int SK_DEPTH = SAVQA_SK_DEPTH;
+constexpr int SK_WAVES = 8;
+constexpr int SK_DEPTH = 2;  // 4 and 8 measured no faster
 
 template <bool KCONTIG>
 __device__ __forceinline__ void sk_load4(const float* __restrict__ P, int64_t ld,
@@ -983,13 +619,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_skinny_kernel(savqa_gemm_desc d,
 // ones): same K split over the waves and LDS fold. Lane (i, q) = (lane % 16, lane / 16)
 // takes k = 16g + 4q + s in MFMA step s of 16-k group g: one b128 load on a k-contiguous
 // operand, 4 coalesced scalars otherwise; accumulator row 4q + r, column i.
-#ifndef SAVQA_SK16
-#define SAVQA_SK16 1
-#endif
-#ifndef SAVQA_SK16_DEPTH
-#define SAVQA_SK16_DEPTH 4
-#endif
-constexpr int SK16_DEPTH = SAVQA_SK16_DEPTH;
+constexpr int SK16_DEPTH = 4;
 
 template <bool AT, bool BT, int NW>
 __global__ __launch_bounds__(64 * NW) void gemm_skinny16_kernel(savqa_gemm_desc d,
@@ -1067,7 +697,7 @@ static int slots_per_launch() {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
-    cached[dev] = SAVQA_GEMM_OCC * cus;
+    cached[dev] = GEMM_OCC * cus;
   }
   return cached[dev];
 }
@@ -1091,60 +721,7 @@ struct GemmPlan {
   GemmGrid gg;
   int grid_x, nsplit;
   int64_t zero_row0;  // >= 0: rows [zero_row0, M) of C are zero-filled before the launch
-  bool sk;            // stream-K launch (gemm_sk_kernel): G = grid_x workgroups
-  int64_t sk_iters, sk_tiles;
 };
-
-// Stream-K launch of the 128x128 path: opt-in (SAVQA_GEMM_SK=1). Measured on the step
-// shapes it loses 2-8% to the data-parallel launch (split-K / tail split) even where it
-// removes a 10-20% wave-quantisation tail: the persistent walk gives up the dynamic
-// block dispatch that staggers tiles, and in the training step the other HIP stream's
-// kernels already fill the data-parallel tail.
-static bool sk_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("SAVQA_GEMM_SK");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-// Per-(device, stream) stream-K workspace: accumulator slabs [G][2][128*128] fp32 and
-// per-tile tickets (zeroed once; each combining workgroup resets its ticket).
-struct SkWorkspace {
-  float* slabs = nullptr;
-  int* cnt = nullptr;
-  int64_t slab_floats = 0, ncnt = 0;
-};
-
-static int sk_workspace(hipStream_t s, int64_t slab_floats, int64_t ncnt, SkWorkspace& out) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, SkWorkspace> pool;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return fail(SAVQA_EUNSUP, "savqa_gemm: hipGetDevice");
-  std::lock_guard<std::mutex> lk(mu);
-  SkWorkspace& w = pool[{dev, s}];
-  if (w.slab_floats < slab_floats || w.ncnt < ncnt) {
-    if (w.slabs || w.cnt) (void)hipStreamSynchronize(s);  // previous launches may still read them
-    if (w.slab_floats < slab_floats) {
-      if (w.slabs) (void)hipFree(w.slabs);
-      w.slabs = nullptr;
-      if (hipMalloc(&w.slabs, slab_floats * sizeof(float)) != hipSuccess)
-        return fail(SAVQA_EUNSUP, "savqa_gemm: stream-K slab allocation failed");
-      w.slab_floats = slab_floats;
-    }
-    if (w.ncnt < ncnt) {
-      if (w.cnt) (void)hipFree(w.cnt);
-      w.cnt = nullptr;
-      const int64_t n = std::max<int64_t>(ncnt, 4096);
-      if (hipMalloc(&w.cnt, n * sizeof(int)) != hipSuccess ||
-          hipMemsetAsync(w.cnt, 0, n * sizeof(int), s) != hipSuccess)
-        return fail(SAVQA_EUNSUP, "savqa_gemm: stream-K ticket allocation failed");
-      w.ncnt = n;
-    }
-  }
-  out = w;
-  return 0;
-}
 
 }  // namespace savqa
 
@@ -1152,44 +729,10 @@ using namespace savqa;
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// skinny shapes with fewer 32x32 tiles than this run on 16x16 tiles (SAVQA_SK16=0: never;
-// measured: 256x512 outputs (128 tiles) 1.25-1.55x faster at K=2048, 256x914 (232) slower;
-// env SAVQA_SK16_MAX overrides the threshold for A/B runs)
-// short-K skinny GEMMs (the decoder / head dW at K = B = 256) on 16x16 tiles with 2 waves
-// per workgroup (A/B option, env SAVQA_SK16_KSMALL = K limit; default 0 = off): measured
-// in-step 1.5-1.6x SLOWER than the 8-wave 32x32 kernel on all five dW shapes (the
-// m-contiguous dY^T loads coalesce into 64 B instead of 128 B and 2 waves hide less
-// latency; tools/gpu_sk16k.sh)
-static int64_t sk16_ksmall() {
-  static int64_t v = -1;
-  if (v < 0) {
-    const char* e = getenv("SAVQA_SK16_KSMALL");
-    v = e ? atoll(e) : 0;
-  }
-  return v;
-}
-
-// 32x32 skinny launches with K <= this use 4 waves per workgroup instead of 8 (env
-// SAVQA_SK32_KSMALL; A/B knob, default off: measured in-step on the K = 256 dW shapes
-// 1.0-1.6x slower -- the short k chains are latency-bound, fewer waves hide less;
-// tools/gpu_sk32k.sh)
-static int64_t sk32_ksmall() {
-  static int64_t v = -1;
-  if (v < 0) {
-    const char* e = getenv("SAVQA_SK32_KSMALL");
-    v = e ? atoll(e) : 0;
-  }
-  return v;
-}
-
-static int64_t sk16_max() {
-  static int64_t v = -1;
-  if (v < 0) {
-    const char* e = getenv("SAVQA_SK16_MAX");
-    v = e ? atoll(e) : (SAVQA_SK16 ? 192 : 0);
-  }
-  return v;
-}
+// skinny shapes with fewer 32x32 tiles than this run on 16x16 tiles (measured: 256x512
+// outputs (128 tiles) 1.25-1.55x faster at K=2048, 256x914 (232) slower; thresholds 192 /
+// 257 / 1100 A/B'd in-step, 192 best)
+constexpr int64_t SK16_MAX_TILES = 192;
 
 static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.M < 0 || d.N < 0 || d.K < 0) return fail(SAVQA_EINVAL, "savqa_gemm: negative dims");
@@ -1202,53 +745,27 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.colsum_a && !d.a_trans) return fail(SAVQA_EINVAL, "savqa_gemm: colsum_a needs a_trans=1");
   if (d.prec != 0 && d.prec != 1 && d.prec != 3)
     return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32), 1 (bf16) or 3 (3xbf16)");
-  // 64x64-tile dW launches (SAVQA_GEMM_DW_TILE=64, A/B option): 4x the tiles, so less
-  // split-K; k-tile SAVQA_GEMM_BK_DW64
-  const bool dw64 = SAVQA_GEMM_DW_TILE == 64 && d.a_trans && d.prec == 0 && !sk_enabled();
-  // gemm_bf16_kernel k-tile: 32; the stream-K kernel always runs SAVQA_GEMM_BK
-  const int BK = d.prec ? 32
-                        : (dw64 ? SAVQA_GEMM_BK_DW64
-                                : (d.a_trans && !sk_enabled() ? SAVQA_GEMM_BK_DW : SAVQA_GEMM_BK));
+  // gemm_bf16_kernel k-tile: 32
+  const int BK = d.prec ? 32 : (d.a_trans ? GEMM_BK_DW : GEMM_BK);
   const int slots = slots_per_launch();
   const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
   int split = d.split_k > 1 ? d.split_k : 1;
   if (d.split_k < 0) split = auto_split(tiles128, d.K, BK, slots);
   // 128x128 tiles once there is enough parallelism (split-K counts), else the skinny
   // kernel (32x32 tiles, K split over the 8 waves of a workgroup; no split-K launch),
-  // 16x16 tiles while 32x32 ones would leave CUs idle (< sk16_max() tiles)
+  // 16x16 tiles while 32x32 ones would leave CUs idle (< SK16_MAX_TILES tiles)
   if (tiles128 * split < 160) {
     const int64_t tiles32 = ((d.M + 31) / 32) * ((d.N + 31) / 32);
-    p.tile = (tiles32 < sk16_max() || (d.K <= sk16_ksmall() && tiles32 <= 1024)) ? 16 : 32;
+    p.tile = tiles32 < SK16_MAX_TILES ? 16 : 32;
     p.split = 1;
     p.nsplit = 1;
     p.gg.tiles_n = (int)((d.N + p.tile - 1) / p.tile);
     p.grid_x = (int)((d.M + p.tile - 1) / p.tile) * p.gg.tiles_n;
     p.zero_row0 = -1;
     p.gg.tail_f = 1;
-    p.sk = false;
-    return 0;
-  }
-  p.sk = false;
-  if (sk_enabled() && d.prec == 0) {
-    p.tile = 128;
-    p.split = 1;
-    p.nsplit = 1;
-    p.gg.tiles_n = (int)((d.N + 127) / 128);
-    p.sk_tiles = tiles128;
-    p.sk_iters = tiles128 * ((d.K + BK - 1) / BK);
-    p.grid_x = (int)std::min<int64_t>(slots, std::max<int64_t>(p.sk_iters, 1));
-    p.zero_row0 = -1;
-    p.gg.tail_f = 1;
-    p.sk = true;
     return 0;
   }
   p.tile = 128;
-  if (dw64) {
-    p.tile = 64;
-    const int64_t tiles64 = ((d.M + 63) / 64) * ((d.N + 63) / 64);
-    split = d.split_k > 1 ? d.split_k : 1;
-    if (d.split_k < 0) split = auto_split(tiles64, d.K, BK, slots);
-  }
   const int tm = (int)((d.M + p.tile - 1) / p.tile);
   const int tn = (int)((d.N + p.tile - 1) / p.tile);
   const int T = tm * tn;
@@ -1307,7 +824,7 @@ static void launch_gemm(const savqa_gemm_desc& d, const GemmPlan& p, hipStream_t
 template <int BM, int BN, int BK>
 static void dispatch_layout(const savqa_gemm_desc& d, const GemmPlan& p, hipStream_t s, int avec,
                             int bvec) {
-  constexpr int BKW = SAVQA_GEMM_BK_DW;
+  constexpr int BKW = GEMM_BK_DW;
   if (!d.a_trans && d.b_trans) launch_gemm<BM, BN, BK, false, true>(d, p, s, avec, bvec);
   else if (!d.a_trans && !d.b_trans) launch_gemm<BM, BN, BK, false, false>(d, p, s, avec, bvec);
   else if (d.a_trans && !d.b_trans) launch_gemm<BM, BN, BKW, true, false>(d, p, s, avec, bvec);
@@ -1320,7 +837,7 @@ extern "C" int savqa_gemm_plan(const savqa_gemm_desc* dp, int32_t* out) {
   GemmPlan p{};
   if (int rc = plan_gemm(d, p)) return rc;
   out[0] = p.tile;
-  out[1] = p.sk ? -1 : p.split;
+  out[1] = p.split;
   out[2] = p.gg.tail_f > 1 ? p.gg.tail_f : 0;
   out[3] = p.grid_x * p.nsplit;
   return 0;
@@ -1340,65 +857,17 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
       hipMemset2DAsync(d.C + p.zero_row0 * d.ldc, d.ldc * sizeof(float), 0, d.N * sizeof(float),
                        d.M - p.zero_row0, s) != hipSuccess)
     return fail(SAVQA_EUNSUP, "savqa_gemm: tail zero-fill failed");
-  if (p.sk) {
-    if (d.K == 0) {  // empty reduction: the epilogue alone (bias, residual, ...) via the
-      GemmPlan q = p;  // data-parallel kernel
-      q.sk = false;
-      q.gg.kchunk = 0;
-      q.gg.full = (int)p.sk_tiles;
-      q.gg.tail_t0 = (int)p.sk_tiles;
-      q.grid_x = (int)p.sk_tiles;
-      dispatch_layout<128, 128, SAVQA_GEMM_BK>(d, q, s, avec, bvec);
-      return check_launch("savqa_gemm");
-    }
-    SkWorkspace ws;
-    if (int rc = sk_workspace(s, (int64_t)p.grid_x * 2 * 128 * 128, p.sk_tiles, ws)) return rc;
-    SkGrid sk;
-    sk.tiles_n = p.gg.tiles_n;
-    sk.nch = (int)((d.K + SAVQA_GEMM_BK - 1) / SAVQA_GEMM_BK);
-    sk.G = p.grid_x;
-    // whole-tile rounds while at least two rounds' worth remain; stream-K over the rest
-    sk.R = (int)std::max<int64_t>(0, p.sk_tiles / p.grid_x - 1);
-    sk.I0 = (int64_t)sk.R * p.grid_x * sk.nch;
-    sk.I = p.sk_iters - sk.I0;
-    sk.slabs = ws.slabs;
-    sk.cnt = ws.cnt;
-    const dim3 g(p.grid_x), b(GEMM_NT);
-    constexpr int BK = SAVQA_GEMM_BK;
-    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, false, true>), g, b, 0, s, d, sk, avec, bvec);
-    else if (!d.a_trans) hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, false, false>), g, b, 0, s, d, sk, avec, bvec);
-    else if (!d.b_trans) hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, true, false>), g, b, 0, s, d, sk, avec, bvec);
-    else hipLaunchKernelGGL((gemm_sk_kernel<128, 128, BK, true, true>), g, b, 0, s, d, sk, avec, bvec);
-  } else if (p.tile == 128 && d.prec != 0) {
+  if (p.tile == 128 && d.prec != 0) {
     savqa_launch_gemm_bf16(d, p.gg, p.grid_x, p.nsplit, s, avec, bvec);
-  } else if (p.tile == 64) {  // dW only (a_trans)
-    if (!d.b_trans) launch_gemm<64, 64, SAVQA_GEMM_BK_DW64, true, false>(d, p, s, avec, bvec);
-    else launch_gemm<64, 64, SAVQA_GEMM_BK_DW64, true, true>(d, p, s, avec, bvec);
   } else if (p.tile == 128) {
-    dispatch_layout<128, 128, SAVQA_GEMM_BK>(d, p, s, avec, bvec);
+    dispatch_layout<128, 128, GEMM_BK>(d, p, s, avec, bvec);
   } else if (p.tile == 16) {
     const int tn = p.gg.tiles_n;
-    const dim3 g(p.grid_x);
-    if (d.K <= sk16_ksmall()) {
-      const dim3 b(64 * 2);
-      if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, true, 2>), g, b, 0, s, d, tn, avec, bvec);
-      else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, false, 2>), g, b, 0, s, d, tn, avec, bvec);
-      else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<true, false, 2>), g, b, 0, s, d, tn, avec, bvec);
-      else hipLaunchKernelGGL((gemm_skinny16_kernel<true, true, 2>), g, b, 0, s, d, tn, avec, bvec);
-    } else {
-      const dim3 b(64 * SK_WAVES);
-      if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
-      else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
-      else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<true, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
-      else hipLaunchKernelGGL((gemm_skinny16_kernel<true, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
-    }
-  } else if (d.K <= sk32_ksmall()) {
-    const dim3 g(p.grid_x), b(64 * 4);
-    const int tn = p.gg.tiles_n;
-    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, true, 4>), g, b, 0, s, d, tn, avec, bvec);
-    else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, false, 4>), g, b, 0, s, d, tn, avec, bvec);
-    else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<true, false, 4>), g, b, 0, s, d, tn, avec, bvec);
-    else hipLaunchKernelGGL((gemm_skinny_kernel<true, true, 4>), g, b, 0, s, d, tn, avec, bvec);
+    const dim3 g(p.grid_x), b(64 * SK_WAVES);
+    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+    else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+    else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<true, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+    else hipLaunchKernelGGL((gemm_skinny16_kernel<true, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
   } else {
     const dim3 g(p.grid_x), b(64 * SK_WAVES);
     const int tn = p.gg.tiles_n;

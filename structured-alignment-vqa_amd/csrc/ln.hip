@@ -8,8 +8,6 @@
 // query mask (modules.py:257, :289), so that mask never re-reads the activations.
 #include "common.h"
 
-#include <map>
-#include <mutex>
 
 namespace savqa {
 
@@ -89,7 +87,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 // Backward. 512-thread workgroups (8 waves), two per CU: each wave walks rows with a
 // grid stride, keeping its dgamma/dbeta partial sums in registers; the 8 waves fold
 // them through per-wave LDS rows and the workgroup adds once per column into one of
-// LN_SLOTS partial copies (a library workspace: 512 adders on ONE address serialise in L2
+// LN_SLOTS partial copies (the caller's workspace: 512 adders on ONE address serialise in L2
 // and cost ~35 us per launch; 32 per address run at the chip's atomic rate), which
 // ln_bwd_reduce_kernel then folds into dgamma/dbeta (and re-zeroes). NV (float4 per
 // lane = cols/256) is a template parameter, and the row loop is software-pipelined two
@@ -237,26 +235,6 @@ __global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(float* __restrict__ 
   }
 }
 
-// per-(device, stream) zeroed slot workspace [LN_SLOTS][2][1024] (each stream's launches
-// are ordered, so one workspace per stream is race-free)
-static float* ln_workspace(hipStream_t s) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, float*> pool;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  float*& w = pool[{dev, s}];
-  if (!w) {
-    const size_t bytes = sizeof(float) * LN_SLOTS * 2 * 256 * LN_MAXV;
-    if (hipMalloc(&w, bytes) != hipSuccess) {
-      w = nullptr;
-      return nullptr;
-    }
-    if (hipMemsetAsync(w, 0, bytes, s) != hipSuccess) return nullptr;
-  }
-  return w;
-}
-
 __global__ __launch_bounds__(256) void rowflag_kernel(const float* __restrict__ X, int64_t rows,
                                                       int64_t cols, int64_t ldx,
                                                       float* __restrict__ flag) {
@@ -286,19 +264,23 @@ extern "C" int savqa_ln_fwd(void* stream, const float* x, const float* xscale, c
   return check_launch("savqa_ln_fwd");
 }
 
+extern "C" int64_t savqa_ln_bwd_workspace_bytes(int64_t cols) {
+  return (int64_t)sizeof(float) * LN_SLOTS * 2 * cols;
+}
+
 extern "C" int savqa_ln_bwd(void* stream, const float* dy, const float* z, const float* mean,
                             const float* rden, const float* stdv, const float* gamma,
                             int64_t rows, int64_t cols, const float* dz_add, float* dz,
-                            float* dgamma, float* dbeta) {
+                            float* dgamma, float* dbeta, float* ws, int64_t ws_bytes) {
   if (rows <= 0) return 0;
   if (cols % 256 != 0 || cols > 256 * LN_MAXV)
     return fail(SAVQA_EUNSUP, "savqa_ln_bwd: cols must be a multiple of 256 and <= 1024");
+  if (!ws || ws_bytes < savqa_ln_bwd_workspace_bytes(cols) || ((uintptr_t)ws & 15))
+    return fail(SAVQA_EINVAL, "savqa_ln_bwd: workspace missing, too small or not 16-B aligned");
   int64_t blocks = (rows + LN_BWD_WAVES - 1) / LN_BWD_WAVES;
   if (blocks > 512) blocks = 512;
   const dim3 g((unsigned)blocks), b(64 * LN_BWD_WAVES);
   hipStream_t st = as_stream(stream);
-  float* ws = ln_workspace(st);
-  if (!ws) return fail(SAVQA_EUNSUP, "savqa_ln_bwd: workspace allocation failed");
   switch (cols / 256) {
 #define SAVQA_LNB(NV)                                                                        \
   case NV:                                                                                   \

@@ -61,6 +61,14 @@ class GradReducer:
         self.arena = arena
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # host-side metadata exchange (the per-rank id counts of set_rows): a gloo group on
+        # CPU tensors, so agreeing on a size never synchronises a GPU stream. Created here,
+        # where every rank constructs its reducer (new_group is collective).
+        self.meta = None
+        if self.world > 1:
+            self.meta = group if dist.get_backend(group) == "gloo" else dist.new_group(
+                ranks=None if group is None else dist.get_process_group_ranks(group),
+                backend="gloo")
         self.bucket = max(1, int(bucket_mb * (1 << 20) // 4))
         self.works: List = []
         self.pending = {}
@@ -84,15 +92,30 @@ class GradReducer:
         self.rows_exchanged = 0
 
     def set_rows(self, ids: torch.Tensor):
-        """This step's touched rows of the sparse tables (any integer tensor; the same
-        numel on every rank, as DistributedSampler guarantees): all-gathered now, async,
-        while the forward runs."""
+        """This step's touched rows of the sparse tables (any integer tensor): all-gathered
+        now, async, while the forward runs. Ranks may hold different numbers of ids (the
+        collate pads questions to each batch's own longest one, so q_ipt is ragged across
+        ranks): the counts are agreed on the host first (gloo, no GPU synchronisation) and
+        every rank pads its ids to the largest count with a duplicate of one of its own ids
+        (duplicates are exchanged once). Several calls before the backward (e.g. several
+        forwards) accumulate: the union of their rows is exchanged."""
         if self.world <= 1 or not self.sparse:
             return
         ids = ids.reshape(-1).to(torch.int64).contiguous()
+        n = ids.numel()
+        cnt = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world)]
+        dist.all_gather(cnt, torch.tensor([n], dtype=torch.int64), group=self.meta)
+        cap = max(int(c) for c in cnt)
+        if cap == 0:
+            return
+        if n < cap:
+            fill = ids[:1] if n > 0 else torch.zeros(1, dtype=torch.int64, device=ids.device)
+            ids = torch.cat([ids, fill.expand(cap - n)])
         outs = [torch.empty_like(ids) for _ in range(self.world)]
         w = dist.all_gather(outs, ids, group=self.group, async_op=True)
-        self._ids = (w, outs)
+        if self._ids is None or self._rows is not None:
+            self._ids = []
+        self._ids.append((w, outs))
         self._rows = None
 
     def prepare_rows(self):
@@ -100,8 +123,10 @@ class GradReducer:
         backward, when the all-gather has long landed)."""
         if self._ids is None or self._rows is not None:
             return
-        w, outs = self._ids
-        w.wait()
+        outs = []
+        for w, o in self._ids:
+            w.wait()
+            outs.extend(o)
         ids, _ = torch.sort(torch.cat(outs))
         first = torch.ones_like(ids, dtype=torch.bool)
         first[1:] = ids[1:] != ids[:-1]

@@ -198,12 +198,29 @@ def ln_fwd(x: Tensor, gamma: Tensor, beta: Tensor, y: Tensor, mean: Tensor, rden
          float(eps), _p(z_out), _p(y), _p(mean), _p(rden), _p(std), _p(flag))
 
 
+_ln_ws = {}
+
+
+def ln_workspace(cols: int, dev) -> Tensor:
+    """The caller-owned, zero-filled slot workspace of savqa_ln_bwd for the current stream
+    (the library re-zeroes it after every call, so one per (device, stream) is reused;
+    the two stacks' streams run LN backwards concurrently and get one each)."""
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), _stream())
+    nbytes = int(_lib.load().savqa_ln_bwd_workspace_bytes(int(cols)))
+    ws = _ln_ws.get(key)
+    if ws is None or ws.numel() * 4 < nbytes:
+        ws = torch.zeros((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+        _ln_ws[key] = ws
+    return ws
+
+
 def ln_bwd(dy: Tensor, z: Tensor, mean: Tensor, rden: Tensor, std: Tensor, gamma: Tensor,
            dz: Tensor, dgamma: Tensor, dbeta: Tensor, *, dz_add=None):
     cols = gamma.numel()
     rows = z.numel() // cols
+    ws = ln_workspace(cols, z.device)
     call("savqa_ln_bwd", _stream(), _p(dy), _p(z), _p(mean), _p(rden), _p(std), _p(gamma), rows,
-         cols, _p(dz_add), _p(dz), _p(dgamma), _p(dbeta))
+         cols, _p(dz_add), _p(dz), _p(dgamma), _p(dbeta), _p(ws), ws.numel() * 4)
 
 
 def rowflag(X: Tensor, rows: int, cols: int, ldx: int, flag: Tensor):

@@ -46,21 +46,33 @@ class Adam(torch.optim.Optimizer):
         scale = self.grad_scale
         if reducer is not None and reducer.world > 1:
             works, scale = reducer.drain()
-            covered = sorted((lo, hi) for _, lo, hi in works)
-            pos = 0
-            for lo, hi in covered:
-                pos = hi if lo == pos else -1
-            if pos == a.n_live:
-                ranges = works
-            else:  # declarations did not tile the live range: wait for all, one launch
-                for w, _, _ in works:
-                    w.wait()
+            ranges = works + self._coverage_gaps(reducer, works, a.n_live)
         for w, lo, hi in ranges:
             if w is not None:
                 w.wait()   # this stream waits for this bucket's all-reduce only
             ops.adam(a.flat[lo:hi], g[lo:hi], self.m[lo:hi], self.v[lo:hi], hi - lo, grp["lr"], b1,
                      b2, grp["eps"], bc1, bc2, scale)
         return loss
+
+    @staticmethod
+    def _coverage_gaps(reducer, works, n_live):
+        """All-reduce (densely) every live span the backward never declared final, so no
+        rank applies a local-only gradient; overlapping declarations are a bug."""
+        gaps, pos = [], 0
+        for lo, hi in sorted((lo, hi) for _, lo, hi in works):
+            if lo < pos:
+                raise RuntimeError(f"gradient ranges declared twice: [{lo}, {hi}) overlaps "
+                                   f"[.., {pos})")
+            if lo > pos:
+                gaps.append((pos, lo))
+            pos = hi
+        if pos < n_live:
+            gaps.append((pos, n_live))
+        for lo, hi in gaps:
+            reducer._dense(lo, hi)
+        extra = reducer.works
+        reducer.works = []
+        return extra
 
     def zero_grad(self, set_to_none: bool = False):
         # keep the arena views attached; zero the live gradient range in one memset

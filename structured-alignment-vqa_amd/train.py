@@ -3,8 +3,9 @@
 Same CLI flags (argparse main:430-500), same process model (one process per GPU:
 `mp.spawn(main, nprocs=ngpus)` main:517, or torchrun env vars), same step
 (forward → zero_grad → label-smoothed loss (+ -MIL-NCE) → backward → Adam, main:268-378),
-same per-epoch eval with accuracy counted on non-zero answers (main:42-142) and the
-3-float all_gather of metrics (main:383-400), same checkpoint naming with the DDP
+same per-epoch eval of the validation AND training splits (main:42-142, :380-382: argmax
+hits counted on non-zero answers, divided by every sample) and the 3-float all_gather of
+both metric sets (main:383-404), same checkpoint naming with the DDP
 `module.` key prefix (main:425-428).
 
 Differences (hot path only): the model is savqa_amd.AttModel (HIP kernels), the
@@ -96,22 +97,40 @@ def run_model(model, batch, args):
 
 
 def evaluate(model, batches, with_mil, rank, args):
-    """main:42-142: loss meter + accuracy over non-zero answers."""
+    """eval(), main:42-142: (loss_meter.avg, cnt_correct, cnt). The loss is the
+    label-smoothed loss (+ the MIL-NCE loss with --with_MILNCE_loss, :129-131), averaged
+    over samples; cnt_correct counts argmax hits among NON-ZERO answers (:125-126) while
+    cnt counts every sample (:127 `cnt += batch_size`), as the reference does."""
     model.eval()
     meter = AverageMeter()
-    cnt = torch.zeros((), device=torch.cuda.current_device())
-    correct = torch.zeros_like(cnt)
+    correct = torch.zeros((), dtype=torch.int64, device=torch.cuda.current_device())
+    cnt = 0
     with torch.no_grad():
         for batch in batches:
             lc, lv, ls, mil, mil_rel = run_model(model, batch, args)
             loss, lsm = smoothed_loss(lc, lv, ls, batch["answer"], mil, with_milnce=with_mil,
                                       mil_nce_rel=mil_rel)
-            meter.update(float(loss), batch["answer"].shape[0])
+            B = batch["answer"].shape[0]
+            meter.update(float(loss), B)
             valid = batch["answer"] != 0
             correct += ((lsm.argmax(-1) == batch["answer"]) & valid).sum()
-            cnt += valid.sum()
+            cnt += B
     model.train()
     return meter.avg, float(correct), float(cnt)
+
+
+def gather_metrics(vals, world_size, dev):
+    """main:383-404: all_gather of every rank's (loss, cnt_correct, cnt); returns (loss
+    averaged over ranks, summed correct, summed cnt, accuracy)."""
+    t = torch.tensor(vals, dtype=torch.float32, device=dev)
+    if world_size > 1:
+        gathered = [torch.zeros(3, dtype=torch.float32, device=dev) for _ in range(world_size)]
+        dist.all_gather(gathered, t)
+        t = torch.stack(gathered)
+    else:
+        t = t.unsqueeze(0)
+    loss, corr, cnt = float(t[:, 0].mean()), float(t[:, 1].sum()), float(t[:, 2].sum())
+    return loss, corr, cnt, (corr / cnt if cnt else 0.0)
 
 
 def gqa_loaders(args, rank):
@@ -202,21 +221,21 @@ def main(gpu_rank, args):
                                  i + 1, args.steps_per_epoch, float(loss), -float(mil), loss_meter.avg)
         if gqa and hasattr(loaders["train"].sampler, "set_epoch"):
             loaders["train"].sampler.set_epoch(epoch + 1)
-        val_loss, corr, cnt = evaluate(model, batches(10 ** 6 + rank, "val"),
-                                       args.with_MILNCE_loss, rank, args)
-        vals = torch.tensor([val_loss, corr, cnt], device=dev)
-        if args.world_size > 1:
-            gathered = [torch.zeros(3, device=dev) for _ in range(args.world_size)]
-            dist.all_gather(gathered, vals)
-            vals = torch.stack(gathered)
-        else:
-            vals = vals.unsqueeze(0)
+        # main:380-382: eval on the validation split, then on the training split
+        val = evaluate(model, batches(10 ** 6 + rank, "val"), args.with_MILNCE_loss, rank, args)
+        trn = evaluate(model, batches(1000 * epoch + 7919 * rank), args.with_MILNCE_loss, rank,
+                       args)
+        val_loss, corr, cnt, acc = gather_metrics(val, args.world_size, dev)
+        train_loss, corr_t, cnt_t, acc_t = gather_metrics(trn, args.world_size, dev)
         if rank == 0:
-            acc = float(vals[:, 1].sum()) / max(float(vals[:, 2].sum()), 1.0)
-            result = {"epoch": epoch + 1, "train_loss": loss_meter.avg,
-                      "val_loss": float(vals[:, 0].mean()), "accuracy": acc}
-            logging.info('Epoch [%d/%d], Val Loss: %.5f, accuracy: %.4f', epoch + 1, args.num_epochs,
-                         float(vals[:, 0].mean()), acc)
+            result = {"epoch": epoch + 1, "train_loss": loss_meter.avg, "val_loss": val_loss,
+                      "accuracy": acc, "correct": corr, "cnt": cnt,
+                      "train_eval_loss": train_loss, "train_accuracy": acc_t,
+                      "train_correct": corr_t, "train_cnt": cnt_t}
+            logging.info('Epoch [%d/%d], Val Loss: %.5f, accuracy: %d/%d = %.4f', epoch + 1,
+                         args.num_epochs, val_loss, corr, cnt, acc)
+            logging.info('Epoch [%d/%d], Train Loss: %.5f, accuracy: %d/%d = %.4f', epoch + 1,
+                         args.num_epochs, train_loss, corr_t, cnt_t, acc_t)
             out = os.path.join(args.data_dir_azure, args.output_dir)
             os.makedirs(out, exist_ok=True)
             sd = model.state_dict()

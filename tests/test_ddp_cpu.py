@@ -133,6 +133,67 @@ def test_sparse_table_rows_exchange_equals_dense_gloo_world2():
         assert pos == n
 
 
+def _ragged_worker(rank, world, port, q):
+    """Ranks with different question lengths (the collate pads to each batch's own longest
+    question), two forwards before one backward, and declarations that leave a gap."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from savqa_amd.ddp import GradReducer
+    from savqa_amd.optim import Adam
+    width, rows = 5, 40
+    t0, t1 = 300, 300 + width * rows
+    n = t1 + 400
+    gen = torch.Generator().manual_seed(10 + rank)
+    ids_a = torch.randint(0, rows, (3, 4 + 5 * rank), generator=gen)   # Lq 4 vs 9
+    ids_b = torch.randint(0, rows, (2, 7 - 3 * rank), generator=gen)   # Lq 7 vs 4
+    g = torch.randn(n, generator=gen)
+    table = torch.zeros(rows, width)
+    for ids in (ids_a, ids_b):
+        table.index_add_(0, ids.reshape(-1), torch.randn(ids.numel(), width, generator=gen))
+    g[t0:t1] = table.reshape(-1)
+    dense = g.clone()
+    dist.all_reduce(dense)
+    arena = types.SimpleNamespace(grad=g.clone())
+    red = GradReducer(arena, bucket_mb=0.001)
+    red.add_sparse_table(t0, t1, width)
+    red.begin()
+    red.set_rows(ids_a)
+    red.set_rows(ids_b)                 # second forward: its rows join the union
+    red.reduce_range(0, 100, True)
+    red.reduce_range(250, n, True)      # [100, 250) never declared
+    works, scale = red.drain()
+    works = works + Adam._coverage_gaps(red, works, n)
+    for w, _, _ in works:
+        w.wait()
+    q.put((rank, float((arena.grad - dense).abs().max()),
+           sorted((lo, hi) for _, lo, hi in works)))
+    dist.destroy_process_group()
+
+
+def test_ragged_rows_accumulated_forwards_and_coverage_gap_gloo_world2():
+    """ragged q_ipt across ranks must not desynchronise the id all-gather; rows of
+    every forward since begin() are exchanged; an undeclared span is all-reduced densely
+    before Adam instead of being updated with the local gradient."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ragged_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, spans in res:
+        assert err < 1e-6, (rank, err)
+        assert (100, 250) in spans
+        pos = 0
+        for lo, hi in spans:
+            assert lo == pos
+            pos = hi
+
+
 def test_adam_grad_scale_matches_mean_of_grads():
     """Adam(grad_scale=1/world) on summed grads == Adam on the mean (oracle restatement)."""
     from oracle import savqa_oracle as O
@@ -144,3 +205,34 @@ def test_adam_grad_scale_matches_mean_of_grads():
     P2 = {"w": p0.clone()}
     O.adam_step(P2, {"w": (g1 + g2) * 0.5}, {}, 1)
     assert torch.allclose(P["w"], P2["w"])
+
+
+def _metrics_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from savqa_amd.train import gather_metrics
+    vals = [(0.5 + rank, 3.0 + rank, 8.0), (2.0, 1.0 + 2 * rank, 4.0 + rank)]
+    q.put((rank, [gather_metrics(v, world, torch.device("cpu")) for v in vals], vals))
+    dist.destroy_process_group()
+
+
+def test_epoch_metric_gather_matches_reference_gloo_world2():
+    """main:383-404 (3-float all_gather, loss mean over ranks, counts summed) for both the
+    validation and the train-split metrics, against the oracle's restatement."""
+    from oracle import savqa_oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_metrics_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k in range(2):
+        ref = O.gather_epoch_metrics([res[r][2][k] for r in range(2)])
+        for rank in range(2):
+            got = res[rank][1][k]
+            assert all(abs(a - b) < 1e-6 for a, b in zip(got, ref)), (got, ref)

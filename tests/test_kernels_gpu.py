@@ -353,32 +353,6 @@ def test_adam_matches_oracle():
     assert rel(p, P["x"]) < 1e-6
 
 
-def test_gemm_stream_k_path():
-    """The opt-in stream-K launch (SAVQA_GEMM_SK=1, read once per process): cut tiles are
-    combined in-launch before a non-linear epilogue; run in a child process."""
-    import os
-    import subprocess
-    import sys
-    code = (
-        "import sys, torch; sys.path.insert(0, '.'); import savqa_amd.ops as O\n"
-        "g = torch.Generator().manual_seed(5)\n"
-        "for (M, N, K, at) in [(16600, 512, 2048, False), (2000, 1536, 18688, True), (4000, 2048, 300, False)]:\n"
-        "    A = (torch.randn(K, M, generator=g) if at else torch.randn(M, K, generator=g)).cuda()\n"
-        "    W = torch.randn(N, K, generator=g).cuda(); b = torch.randn(N, generator=g).cuda()\n"
-        "    C = torch.empty(M, N, device='cuda')\n"
-        "    Ar = A.t() if at else A\n"
-        "    O.gemm(A, W, C, M, N, K, lda=M if at else K, ldb=K, ldc=N, a_trans=at, b_trans=True, bias=b, relu=True)\n"
-        "    ref = torch.relu(Ar.double() @ W.double().t() + b.double())\n"
-        "    e = float((C.double() - ref).abs().max() / ref.abs().max())\n"
-        "    assert e < 1e-5, (M, N, K, e)\n"
-        "print('ok')\n")
-    env = dict(os.environ, SAVQA_GEMM_SK="1")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
-                       text=True, timeout=300)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
-
-
 @pytest.mark.parametrize("prec,tol", [(1, 2e-2), (3, 1e-4)])
 @pytest.mark.parametrize("lay", ["NT", "NN", "TN"])
 @pytest.mark.parametrize("M,N,K", [(2048, 2048, 512), (4100, 1280, 520), (2100, 1536, 96)])

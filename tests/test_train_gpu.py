@@ -91,3 +91,47 @@ def test_train_on_gqa_files(tmp_path, only_obj):
     assert res["epoch"] == 1
     assert res["train_loss"] == res["train_loss"] and res["val_loss"] == res["val_loss"]
     assert (tmp_path / "gqa" / "out" / "model_1.pth").exists()
+
+
+def test_evaluate_matches_reference_eval():
+    """train.evaluate (eval(), main:42-142) against the oracle's restatement of main:103-133
+    evaluated on the REFERENCE's own logits (tests/golden/full_b4.npz): the accuracy
+    numerator counts argmax hits among non-zero answers only, the denominator counts every
+    sample (main:127 `cnt += batch_size`), the loss meter is sample-weighted."""
+    import os
+    import types
+    import numpy as np
+    from oracle import hashfill
+    from oracle import savqa_oracle as O
+    from savqa_amd.AttModel_x3 import AttModel
+    from savqa_amd.data import MODEL_INPUTS
+    from savqa_amd.train import evaluate
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "full_b4.npz"))
+    m = AttModel(None, 512, 1024, 914, 40, 450, 49, 6, 8, 0.0, 0.0, 4, True, device="cuda",
+                 init=False)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            p.copy_(torch.from_numpy(hashfill.param_value(n, tuple(p.shape))))
+    lc, lv, ls = (torch.from_numpy(g[k]).double() for k in
+                  ("logits_concat", "logits_vis", "logits_syb"))
+    lsm = (torch.log_softmax(lc, -1) + torch.log_softmax(lv, -1) + torch.log_softmax(ls, -1)) / 3
+    top = lsm.argmax(-1)
+    # batch 1: three answers the reference predicts, one zero answer (counted in cnt only);
+    # batch 2: the golden answers (mostly wrong on random weights)
+    a1 = top.clone()
+    a1[3] = 0
+    a2 = torch.from_numpy(g["answer"])
+    base = {k: torch.from_numpy(g[k]).cuda() for k in MODEL_INPUTS}
+    batches = [dict(base, answer=a1.cuda()), dict(base, answer=a2.cuda())]
+    args = types.SimpleNamespace(only_obj=True, decMask=bool(g["decMask"]), mcb=False)
+    for with_mil in (False, True):
+        loss, corr, cnt = evaluate(m, batches, with_mil, 0, args)
+        mil = torch.tensor(float(g["mil_nce_obj"]), dtype=torch.float64)
+        ref = O.eval_epoch([O.eval_batch(lc, lv, ls, a, mil, with_milnce=with_mil)
+                            for a in (a1, a2)])
+        assert cnt == ref[2] == 8
+        assert corr == ref[1], (corr, ref)
+        assert ref[1] >= 3
+        assert abs(loss - ref[0]) < 1e-4 * abs(ref[0]), (loss, ref)
