@@ -83,6 +83,67 @@ int savqa_gemm(void* stream, const savqa_gemm_desc* d);
  * out[3] = workgroups. */
 int savqa_gemm_plan(const savqa_gemm_desc* d, int32_t* out);
 
+/* ------------------------------------------------------------------------
+ * Low-precision-operand GEMM (BASELINE cfg 3 bf16 training, cfg 5 fp8 region features):
+ * the same operator as savqa_gemm, with bf16-RESIDENT operands (or fp8-e4m3 ones with
+ * per-32-k block scales) read straight from HBM, fp32 accumulation, and an fp32 and/or
+ * bf16 output.
+ *   A(m,k) = a_trans ? A[k*lda + m] : A[ra(m)*lda + k]     ra(i) = a_rows ? a_rows[i] : i
+ *   B(k,n) = b_trans ? B[n*ldb + k] : B[k*ldb + n]
+ *   a_type / b_type: SAVQA_DT_BF16 or SAVQA_DT_FP8 (OCP e4m3fn). fp8 needs both operands
+ *   fp8, a_trans = 0, b_trans = 1, K % 128 == 0, and e8m0 block scales a_scale[m][k/32]
+ *   (row stride lds_a bytes) / b_scale[n][k/32]: value = e4m3 * 2^(scale - 127)
+ *   (v_mfma_scale_f32_16x16x128_f8f6f4). bf16 needs K % 64 == 0, 16-B aligned operands
+ *   with ld % 8 == 0, and M % 8 == 0 (a_trans) / N % 8 == 0 (b_trans = 0).
+ *   v = acc*alpha + bias[n] + rowvec[(m % rowvec_period)*ldrv + n]  (bias/rowvec/resid:
+ *       first K slice only) ; v = relu ? max(v,0) : v ;
+ *   v = (mask && !(mask[mr*ldmask+n] > 0)) ? 0 : v   mr = mask_arows ? a_rows[m] : m
+ *       (mask_type SAVQA_DT_BF16 or SAVQA_DT_F32) ; v += resid[m*ldr + n]
+ *   crow(m) = (m / c_group)*c_stride + m % c_group + c_offset  (c_group <= 0: identity)
+ *   C[crow*ldc + n] = v  (atomic: +=)      Cb[crow*ldcb + n] = bf16(v)  (not with atomic)
+ * split_k > 1 / < 0 (auto) requires atomic = 1 and C. savqa_gemm_lp_supported() says
+ * whether a descriptor meets these constraints (no launch).
+ * ------------------------------------------------------------------------ */
+#define SAVQA_DT_F32 0
+#define SAVQA_DT_BF16 1
+#define SAVQA_DT_FP8 2
+typedef struct savqa_gemm_lp_desc {
+    int64_t M, N, K;
+    const void* A; int64_t lda; int32_t a_trans; int32_t a_type;
+    const int64_t* a_rows;
+    const uint8_t* a_scale; int64_t lds_a;
+    const void* B; int64_t ldb; int32_t b_trans; int32_t b_type;
+    const uint8_t* b_scale; int64_t lds_b;
+    float* C; int64_t ldc;
+    void* Cb; int64_t ldcb;
+    int64_t c_group, c_stride, c_offset;
+    const float* bias;
+    const float* rowvec; int64_t ldrv; int64_t rowvec_period;
+    const float* resid; int64_t ldr;
+    const void* mask; int64_t ldmask; int32_t mask_arows; int32_t mask_type;
+    float alpha;
+    int32_t relu, atomic, split_k;
+} savqa_gemm_lp_desc;
+
+int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* d);
+int savqa_gemm_lp_supported(const savqa_gemm_lp_desc* d);
+
+/* Conversions feeding the low-precision operands:
+ *   savqa_cast_bf16: out[r*ldo + c] = bf16(in[r*ldi + c])  (fp32 -> bf16, round to nearest even)
+ *   savqa_quant_fp8: per row r and 32-column block b: s = e8m0 scale making max|x| <= 448,
+ *     q[r*ldq + c] = e4m3fn(x / 2^(s-127)) (round to nearest even), scale[r*lds + b] = s;
+ *     cols % 32 == 0
+ *   savqa_dequant_fp8_bf16: out = bf16(q * 2^(s-127))  (the backward's bf16 copy) */
+int savqa_cast_bf16(void* stream, const float* in, int64_t rows, int64_t cols, int64_t ldi,
+                    void* out, int64_t ldo);
+int savqa_quant_fp8(void* stream, const float* in, int64_t rows, int64_t cols, int64_t ldi,
+                    void* q, int64_t ldq, uint8_t* scale, int64_t lds);
+int savqa_dequant_fp8_bf16(void* stream, const void* q, int64_t rows, int64_t cols, int64_t ldq,
+                           const uint8_t* scale, int64_t lds, void* out, int64_t ldo);
+/* out[c] += sum_r X[r*ldx + c] over a bf16 X (bias gradients of the low-precision GEMMs) */
+int savqa_colsum_bf16(void* stream, const void* X, int64_t rows, int64_t cols, int64_t ldx,
+                      float* out);
+
 /* out[c] += sum_r X[r*ldx + c]  (bias gradients of every Linear above) */
 int savqa_colsum_acc(void* stream, const float* X, int64_t rows, int64_t cols, int64_t ldx, float* out);
 

@@ -40,6 +40,27 @@ class GemmDesc(C.Structure):
     ]
 
 
+class GemmLpDesc(C.Structure):
+    """savqa_gemm_lp_desc (include/savqa.h)."""
+    _fields_ = [
+        ("M", c_i64), ("N", c_i64), ("K", c_i64),
+        ("A", c_p), ("lda", c_i64), ("a_trans", c_i32), ("a_type", c_i32),
+        ("a_rows", c_p),
+        ("a_scale", c_p), ("lds_a", c_i64),
+        ("B", c_p), ("ldb", c_i64), ("b_trans", c_i32), ("b_type", c_i32),
+        ("b_scale", c_p), ("lds_b", c_i64),
+        ("C", c_p), ("ldc", c_i64),
+        ("Cb", c_p), ("ldcb", c_i64),
+        ("c_group", c_i64), ("c_stride", c_i64), ("c_offset", c_i64),
+        ("bias", c_p),
+        ("rowvec", c_p), ("ldrv", c_i64), ("rowvec_period", c_i64),
+        ("resid", c_p), ("ldr", c_i64),
+        ("mask", c_p), ("ldmask", c_i64), ("mask_arows", c_i32), ("mask_type", c_i32),
+        ("alpha", c_f),
+        ("relu", c_i32), ("atomic", c_i32), ("split_k", c_i32),
+    ]
+
+
 class CollateField(C.Structure):
     """savqa_collate_field (include/savqa.h)."""
     _fields_ = [
@@ -55,6 +76,12 @@ _SIGS = {
     "savqa_gemm": [c_p, C.POINTER(GemmDesc)],
     "savqa_gemm_plan": [C.POINTER(GemmDesc), c_p],
     "savqa_colsum_acc": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
+    "savqa_gemm_lp": [c_p, C.POINTER(GemmLpDesc)],
+    "savqa_gemm_lp_supported": [C.POINTER(GemmLpDesc)],
+    "savqa_cast_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64],
+    "savqa_quant_fp8": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64],
+    "savqa_dequant_fp8_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64],
+    "savqa_colsum_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
     "savqa_ln_fwd": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p],
     "savqa_ln_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p,
                      c_i64],

@@ -149,6 +149,76 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
     _probe.records.append((key, 2.0 * M * N * K, e0, e1))
 
 
+# ------------------------------------------------------------------------------ low precision
+DT = {torch.float32: 0, torch.bfloat16: 1, torch.float8_e4m3fn: 2}
+
+
+def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int, a_trans=False,
+            b_trans=False, a_rows=None, a_scale=None, lds_a=0, b_scale=None, lds_b=0, C=None,
+            ldc=0, Cb=None, ldcb=0, c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None,
+            ldrv=0, rowvec_period=0, resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False,
+            alpha=1.0, relu=False, atomic=False, split_k=1):
+    """savqa_gemm_lp_desc for bf16 / fp8 operands (include/savqa.h)."""
+    d = _lib.GemmLpDesc()
+    d.M, d.N, d.K = int(M), int(N), int(K)
+    d.A, d.lda, d.a_trans, d.a_type = _p(A), int(lda), int(bool(a_trans)), DT[A.dtype]
+    d.a_rows, d.a_scale, d.lds_a = _p(a_rows), _p(a_scale), int(lds_a)
+    d.B, d.ldb, d.b_trans, d.b_type = _p(B), int(ldb), int(bool(b_trans)), DT[B.dtype]
+    d.b_scale, d.lds_b = _p(b_scale), int(lds_b)
+    d.C, d.ldc, d.Cb, d.ldcb = _p(C), int(ldc), _p(Cb), int(ldcb)
+    d.c_group, d.c_stride, d.c_offset = int(c_group), int(c_stride), int(c_offset)
+    d.bias, d.rowvec, d.ldrv, d.rowvec_period = _p(bias), _p(rowvec), int(ldrv), int(rowvec_period)
+    d.resid, d.ldr = _p(resid), int(ldr)
+    d.mask, d.ldmask, d.mask_arows = _p(mask), int(ldmask), int(bool(mask_arows))
+    d.mask_type = DT[mask.dtype] if mask is not None else 0
+    d.alpha = float(alpha)
+    d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
+    return d
+
+
+def lp_supported(d) -> bool:
+    return bool(_lib.load().savqa_gemm_lp_supported(C.byref(d)))
+
+
+def gemm_lp(*args, **kw):
+    """Low-precision-operand MFMA GEMM (savqa_gemm_lp): same arguments as lp_desc."""
+    d = lp_desc(*args, **kw)
+    if _probe is None:
+        call("savqa_gemm_lp", _stream(), C.byref(d))
+        return
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    call("savqa_gemm_lp", _stream(), C.byref(d))
+    e1.record()
+    fp8 = d.a_type == 2
+    key = (f"gemm_lp_kernel<{str(bool(d.a_trans)).lower()},{str(bool(d.b_trans)).lower()},"
+           f"{str(fp8).lower()}>")
+    if _probe.detail:
+        key += f" | {'T' if d.a_trans else 'N'}{'T' if d.b_trans else 'N'} {d.M}x{d.N}x{d.K}"
+    _probe.records.append((key, 2.0 * d.M * d.N * d.K, e0, e1))
+
+
+def cast_bf16(x: Tensor, rows: int, cols: int, ldi: int, out: Tensor, ldo: int):
+    call("savqa_cast_bf16", _stream(), _p(x), int(rows), int(cols), int(ldi), _p(out), int(ldo))
+
+
+def quant_fp8(x: Tensor, rows: int, cols: int, ldi: int, q: Tensor, ldq: int, scale: Tensor,
+              lds: int):
+    call("savqa_quant_fp8", _stream(), _p(x), int(rows), int(cols), int(ldi), _p(q), int(ldq),
+         _p(scale), int(lds))
+
+
+def dequant_fp8_bf16(q: Tensor, rows: int, cols: int, ldq: int, scale: Tensor, lds: int,
+                     out: Tensor, ldo: int):
+    call("savqa_dequant_fp8_bf16", _stream(), _p(q), int(rows), int(cols), int(ldq), _p(scale),
+         int(lds), _p(out), int(ldo))
+
+
+def colsum_bf16(X: Tensor, rows: int, cols: int, ldx: int, out: Tensor):
+    call("savqa_colsum_bf16", _stream(), _p(X), int(rows), int(cols), int(ldx), _p(out))
+
+
 def linear(X: Tensor, W: Tensor, b: Optional[Tensor], out: Tensor, *, relu=False,
            rows: Optional[int] = None, a_rows=None, rowvec=None, rowvec_period=0, resid=None,
            c_group=0, c_stride=0, c_offset=0, ldx=None, ldo=None, rowscale=None):

@@ -1,0 +1,168 @@
+"""Low-precision-operand GEMM (savqa_gemm_lp: bf16-resident operands on
+v_mfma_f32_16x16x32_bf16, fp8-e4m3 + e8m0 block scales on v_mfma_scale_f32_16x16x128_f8f6f4)
+and the conversions that feed it, through the C ABI.
+
+Reference: fp64 torch on the SAME rounded operands (bf16 values / dequantised fp8 values),
+so what is checked is the kernel's indexing, transposed LDS reads, swizzles, scales and
+epilogue; products of bf16 or fp8 values are exact in fp32 and only the fp32 summation
+order differs (bar 2e-5 of sum|a*b| scale).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from savqa_amd import ops as O
+    return O
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
+
+
+def bf(shape, seed, scale=1.0):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device=dev) * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("lay", ["NT", "NN", "TN", "TT"])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 136, 640), (37376 // 8, 1536, 512),
+                                   (512, 2048, 1024), (8, 8, 128)])
+def test_bf16_layouts_bias_relu(lay, M, N, K):
+    O = ops()
+    at, bt = lay[0] == "T", lay[1] == "T"
+    A = bf((K, M) if at else (M, K), 1)
+    B = bf((N, K) if bt else (K, N), 2)
+    bias = torch.randn(N, device=dev)
+    C = torch.empty(M, N, device=dev)
+    Cb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    O.gemm_lp(A, B, M, N, K, lda=M if at else K, ldb=K if bt else N, a_trans=at, b_trans=bt,
+              C=C, ldc=N, Cb=Cb, ldcb=N, bias=bias, relu=True)
+    Ar = (A.t() if at else A).double()
+    Br = (B.t() if bt else B).double()
+    ref = torch.relu(Ar @ Br + bias.double())
+    assert rel(C, ref) < 2e-5
+    assert torch.equal(Cb.cpu(), C.to(torch.bfloat16).cpu())
+
+
+def test_bf16_dw_split_k_atomic_and_colsum():
+    """dW += dY^T X (TN) at the encoder shape with the auto split-K (atomic accumulation
+    into an existing gradient) and the bf16 bias-gradient column sums."""
+    O = ops()
+    M, N, K = 512, 1536, 18688          # dW [1536 x 512] over B*T = 18688 rows
+    dY = bf((K, N), 3)
+    X = bf((K, M), 4)
+    W0 = torch.randn(N, M, device=dev)
+    dW = W0.clone()
+    O.gemm_lp(dY, X, N, M, K, lda=N, ldb=M, a_trans=True, b_trans=False, C=dW, ldc=M,
+              atomic=True, split_k=-1)
+    ref = W0.double() + dY.double().t() @ X.double()
+    assert rel(dW - W0, ref - W0.double()) < 2e-5
+    cs = torch.ones(N, device=dev)
+    O.colsum_bf16(dY, K, N, N, cs)
+    assert rel(cs - 1, dY.double().sum(0)) < 1e-5
+
+
+def test_bf16_epilogues_rows_mask_resid_rowvec():
+    """Row gathers of A (a_rows), the ReLU-backward mask read through them (mask_arows, bf16
+    mask), residual, periodic position rows, and the c_group row map of the concat buffer."""
+    O = ops()
+    M, N, K, T, G = 300, 264, 192, 50, 14
+    src = bf((700, K), 5)
+    rows = torch.randperm(700, device=dev)[:M].contiguous()
+    W = bf((N, K), 6)
+    mask = bf((700, N), 7)
+    resid = torch.randn(M, N, device=dev)
+    rowvec = torch.randn(T, N, device=dev)
+    C = torch.full((M // G * T + T, N), 7.0, device=dev)
+    O.gemm_lp(src, W, M, N, K, lda=K, ldb=K, b_trans=True, a_rows=rows, C=C, ldc=N,
+              c_group=G, c_stride=T, c_offset=3, rowvec=rowvec, ldrv=N, rowvec_period=T,
+              resid=resid, ldr=N, mask=mask, ldmask=N, mask_arows=True, alpha=0.5)
+    m = torch.arange(M, device=dev)
+    v = 0.5 * (src[rows].double() @ W.double().t()) + rowvec.double()[m % T]
+    v = torch.where(mask[rows].double() > 0, v, torch.zeros_like(v)) + resid.double()
+    crow = (m // G) * T + m % G + 3
+    assert rel(C[crow], v) < 2e-5
+    untouched = torch.ones(C.shape[0], dtype=torch.bool, device=dev)
+    untouched[crow] = False
+    assert (C[untouched] == 7.0).all()
+
+
+def test_gemm_lp_rejects_unsupported():
+    O = ops()
+    A = bf((100, 60), 8)
+    W = bf((64, 60), 9)
+    C = torch.empty(100, 64, device=dev)
+    d = O.lp_desc(A, W, 100, 64, 60, lda=60, ldb=60, b_trans=True, C=C, ldc=64)
+    assert not O.lp_supported(d)          # K % 64 != 0
+    from savqa_amd._lib import SavqaError
+    with pytest.raises(SavqaError):
+        O.gemm_lp(A, W, 100, 64, 60, lda=60, ldb=60, b_trans=True, C=C, ldc=64)
+
+
+def _dequant(q, s):
+    v = q.view(torch.float8_e4m3fn).cpu().double()
+    sc = torch.pow(2.0, s.cpu().double() - 127)
+    return v * sc.repeat_interleave(32, dim=1)
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e-3, 300.0])
+def test_quant_fp8_matches_torch_e4m3fn(scale):
+    """savqa_quant_fp8: per-32 block e8m0 scale (smallest power of two with max|x|/2^e <=
+    448) and round-to-nearest-even e4m3fn codes identical to torch's float8_e4m3fn cast."""
+    O = ops()
+    R, Cc = 77, 256
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.randn(R, Cc, generator=g, device=dev) * scale
+    x[3, :32] = 0.0
+    x[5, 7] = 448.0 * 2 ** 3 * 1.03    # forces a rounding near the top of a block
+    q = torch.empty(R, Cc, dtype=torch.uint8, device=dev)
+    s = torch.empty(R, Cc // 32, dtype=torch.uint8, device=dev)
+    O.quant_fp8(x, R, Cc, Cc, q, Cc, s, Cc // 32)
+    xc = x.cpu().double().reshape(R, Cc // 32, 32)
+    mx = xc.abs().amax(-1)
+    e = torch.where(mx > 0, torch.ceil(torch.log2(mx / 448.0)), torch.zeros_like(mx))
+    assert torch.equal(s.cpu().long(), (e + 127).long())
+    ref = (xc / torch.pow(2.0, e).unsqueeze(-1)).float().reshape(R, Cc).to(torch.float8_e4m3fn)
+    got = q.cpu().view(torch.float8_e4m3fn)
+    assert torch.equal(got.view(torch.uint8), ref.view(torch.uint8))
+    back = torch.empty(R, Cc, dtype=torch.bfloat16, device=dev)
+    O.dequant_fp8_bf16(q, R, Cc, Cc, s, Cc // 32, back, Cc)
+    assert torch.equal(back.cpu(), _dequant(q, s).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (1800, 512, 2048), (700, 1024, 2048),
+                                   (33, 40, 256)])
+def test_fp8_scaled_mfma_gemm(M, N, K):
+    """fp8 x fp8 with block scales (cfg 5's region-feature GEMMs): against fp64 on the
+    dequantised operands; rows of very different magnitude exercise the per-block scales."""
+    O = ops()
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    X = torch.randn(M, K, generator=g, device=dev).clamp_min(0)
+    X *= torch.pow(2.0, torch.randint(-6, 7, (M, 1), generator=g, device=dev).float())
+    W = torch.randn(N, K, generator=g, device=dev) / K ** 0.5
+    qx = torch.empty(M, K, dtype=torch.uint8, device=dev)
+    sx = torch.empty(M, K // 32, dtype=torch.uint8, device=dev)
+    qw = torch.empty(N, K, dtype=torch.uint8, device=dev)
+    sw = torch.empty(N, K // 32, dtype=torch.uint8, device=dev)
+    O.quant_fp8(X, M, K, K, qx, K, sx, K // 32)
+    O.quant_fp8(W, N, K, K, qw, K, sw, K // 32)
+    bias = torch.randn(N, device=dev)
+    C = torch.empty(M, N, device=dev)
+    O.gemm_lp(qx.view(torch.float8_e4m3fn), qw.view(torch.float8_e4m3fn), M, N, K, lda=K,
+              ldb=K, b_trans=True, a_scale=sx, lds_a=K // 32, b_scale=sw, lds_b=K // 32, C=C,
+              ldc=N, bias=bias)
+    ref = _dequant(qx, sx) @ _dequant(qw, sw).t() + bias.cpu().double()
+    row_scale = (_dequant(qx, sx).abs() @ _dequant(qw, sw).abs().t()).amax(1, keepdim=True)
+    err = ((C.cpu().double() - ref).abs() / row_scale.clamp_min(1e-30)).max()
+    # the scaled MFMA sums its 128 products with less than fp32 internal precision
+    # (measured 2.1e-5 of sum|a*b| at K=128): bar 1e-4
+    assert float(err) < 1e-4
+    # and the quantisation itself stays within e4m3's half-ulp (2^-4 relative) per element
+    assert rel(_dequant(qx, sx), X.cpu()) < 2 ** -4
