@@ -123,6 +123,7 @@ typedef struct savqa_gemm_lp_desc {
     const void* mask; int64_t ldmask; int32_t mask_arows; int32_t mask_type;
     float alpha;
     int32_t relu, atomic, split_k;
+    int32_t tile_hint;  /* 0 = library's choice; 1..5 force a kernel variant (gemm_lp.hip) */
 } savqa_gemm_lp_desc;
 
 int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* d);

@@ -58,6 +58,7 @@ class GemmLpDesc(C.Structure):
         ("mask", c_p), ("ldmask", c_i64), ("mask_arows", c_i32), ("mask_type", c_i32),
         ("alpha", c_f),
         ("relu", c_i32), ("atomic", c_i32), ("split_k", c_i32),
+        ("tile_hint", c_i32),
     ]
 
 

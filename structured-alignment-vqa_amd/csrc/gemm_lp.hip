@@ -57,6 +57,7 @@ struct LpArgs {
   int tiles_n, ntiles_k;  // k-tiles per split slice
   int64_t kchunk;         // elements of k per split slice
   int nblk;               // tiles (grid.x)
+  int dbg;                // diagnostics: 1 = skip the MFMAs, 2 = skip the k-loop DMAs
 };
 
 // Per-lane LDS-DMA sources of one operand, resolved once per workgroup.
@@ -136,6 +137,153 @@ __device__ __forceinline__ i32x8 frag_fp8(const char* img, int base, int lane) {
 }
 
 __device__ __forceinline__ float bf2f(__bf16 v) { return (float)v; }
+
+// Epilogue of one wave's TM x 64 output tile (savqa_gemm_lp formula), staged through the
+// wave's own 16 KB of LDS in passes of 64 rows so that the global traffic is whole rows:
+// the swapped-MFMA accumulators (lane: 4 consecutive columns of one row) are written as
+// f4s into a [64][64] fp32 image (16-B chunk c of row r at c ^ (r & 15): conflict-free
+// for both the writes and the read-back), then read back row-major -- 16 lanes cover one
+// row's 256 B, so every epilogue operand load and every store is a 16-B access in full
+// lines; atomic outputs read one float per lane so a wave instruction adds 256 contiguous
+// bytes (the full-rate shape of global float atomics). The caller has barriered the
+// workgroup after its last k-tile read.
+template <int FM, int FN>
+__device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&acc)[FM][FN],
+                                            char* reg, int64_t row0, int64_t col0,
+                                            bool first_split, int lane) {
+  static_assert(FN == 4, "wave tiles are 64 columns wide");
+  const int g = lane >> 4;
+  const bool ident = d.c_group <= 0;
+  const bool vec_c = (d.ldc & 3) == 0 && (((uintptr_t)d.C) & 15) == 0;
+  const bool vec_cb = (d.ldcb & 3) == 0 && (((uintptr_t)d.Cb) & 7) == 0;
+#pragma unroll
+  for (int pass = 0; pass < FM / 4; ++pass) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int lr = 16 * i + (lane & 15);
+        *reinterpret_cast<f4*>(reg + lr * 256 + (((4 * j + g) ^ (lr & 15)) * 16)) = acc[4 * pass + i][j];
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is complete
+    __builtin_amdgcn_wave_barrier();
+    if (d.atomic) {
+      // one float per lane: row q, column lane (256 contiguous bytes per atomic instruction)
+      const int64_t n = col0 + lane;
+      const float bv = (first_split && d.bias && n < d.N) ? d.bias[n] : 0.f;
+      for (int q = 0; q < 64; ++q) {
+        const int64_t m = row0 + 64 * pass + q;
+        if (m >= d.M) break;
+        float v = *reinterpret_cast<const float*>(reg + q * 256 + ((((lane >> 2) ^ (q & 15)) * 16)) +
+                                                  (lane & 3) * 4);
+        if (n >= d.N) continue;
+        v = v * d.alpha + bv;
+        if (first_split && d.rowvec) v += d.rowvec[(m % d.rowvec_period) * d.ldrv + n];
+        if (d.relu) v = fmaxf(v, 0.f);
+        if (d.mask) {
+          const int64_t mr = d.mask_arows ? d.a_rows[m] : m;
+          const float mv = d.mask_type == SAVQA_DT_BF16
+                               ? bf2f(static_cast<const __bf16*>(d.mask)[mr * d.ldmask + n])
+                               : static_cast<const float*>(d.mask)[mr * d.ldmask + n];
+          if (!(mv > 0.f)) v = 0.f;
+        }
+        if (first_split && d.resid) v += d.resid[m * d.ldr + n];
+        int64_t cr = m;
+        if (!ident) {
+          const uint32_t mu = (uint32_t)m, cg = (uint32_t)d.c_group;
+          cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
+        }
+        atomicAdd(d.C + cr * d.ldc + n, v);
+      }
+    } else {
+      // 16 lanes per row, 4 rows per instruction, 16 instructions per pass
+      const int c = lane & 15;
+      const int64_t n = col0 + 4 * c;
+      const bool full = n + 4 <= d.N;
+      f4 bv = {0.f, 0.f, 0.f, 0.f};
+      if (first_split && d.bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = n + r < d.N ? d.bias[n + r] : 0.f;
+      }
+#pragma unroll 4
+      for (int q = 0; q < 16; ++q) {
+        const int lr = 4 * q + (lane >> 4);
+        const int64_t m = row0 + 64 * pass + lr;
+        if (m >= d.M || n >= d.N) continue;
+        f4 v = *reinterpret_cast<const f4*>(reg + lr * 256 + ((c ^ (lr & 15)) * 16));
+        v = v * d.alpha + bv;
+        if (first_split && d.rowvec) {
+          const float* rp = d.rowvec + (m % d.rowvec_period) * d.ldrv + n;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += n + r < d.N ? rp[r] : 0.f;
+        }
+        if (d.relu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (d.mask) {
+          const int64_t mr = d.mask_arows ? d.a_rows[m] : m;
+          f4 mv;
+          if (d.mask_type == SAVQA_DT_BF16) {
+            const __bf16* mp = static_cast<const __bf16*>(d.mask) + mr * d.ldmask + n;
+            if (full && (d.ldmask & 3) == 0 && (((uintptr_t)d.mask) & 7) == 0) {
+              mv = __builtin_convertvector(*reinterpret_cast<const bf16x4*>(mp), f4);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) mv[r] = n + r < d.N ? bf2f(mp[r]) : 0.f;
+            }
+          } else {
+            const float* mp = static_cast<const float*>(d.mask) + mr * d.ldmask + n;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mv[r] = n + r < d.N ? mp[r] : 0.f;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (!(mv[r] > 0.f)) v[r] = 0.f;
+        }
+        if (first_split && d.resid) {
+          const float* rp = d.resid + m * d.ldr + n;
+          if (full && (d.ldr & 3) == 0 && (((uintptr_t)d.resid) & 15) == 0) {
+            v += *reinterpret_cast<const f4*>(rp);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += n + r < d.N ? rp[r] : 0.f;
+          }
+        }
+        int64_t cr = m;
+        if (!ident) {
+          const uint32_t mu = (uint32_t)m, cg = (uint32_t)d.c_group;
+          cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
+        }
+        if (d.C) {
+          float* cp = d.C + cr * d.ldc + n;
+          if (full && vec_c) {
+            *reinterpret_cast<f4*>(cp) = v;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < d.N) cp[r] = v[r];
+          }
+        }
+        if (d.Cb) {
+          __bf16* cp = static_cast<__bf16*>(d.Cb) + cr * d.ldcb + n;
+          const bf16x4 h = __builtin_convertvector(v, bf16x4);
+          if (full && vec_cb) {
+            *reinterpret_cast<bf16x4*>(cp) = h;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < d.N) cp[r] = h[r];
+          }
+        }
+      }
+    }
+    if (pass + 1 < FM / 4) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
 
 template <bool AT, bool BT, bool FP8>
 __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
@@ -234,87 +382,171 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   }
 
   // ---------------------------------------------------------------- epilogue
-  // acc[i][j][r] = C(m = m0 + 64wm + 16i + (lane & 15), n = n0 + 64wn + 16j + 4g + r)
-  const bool ident = d.c_group <= 0;
-  const bool vec_c = d.C && (d.ldc & 3) == 0 && (((uintptr_t)d.C) & 15) == 0;
-  float bv[4][4];
+  __syncthreads();  // every wave's last k-tile reads are done: LDS is free
+  lp_epilogue<4, 4>(d, acc, smem + wave * 16384, m0 + wm * 64, n0 + wn * 64, first_split, lane);
+}
+
+// ---------------------------------------------------------------------------------------
+// Large-tile bf16 variants, one 512-thread workgroup (8 waves) per CU:
+//   BM x BN = 256 x 256 (waves 2 x 4, 128 x 64 each) or 256 x 128 (waves 4 x 2, 64 x 64),
+//   k-tile BK = 32 or 64 bf16 (64-B / 128-B operand rows), an NS-slot LDS-DMA ring
+//   (NS = 2: k-tile t+1 in flight while t is computed; NS = 3: t+1 and t+2), counted
+//   `s_waitcnt vmcnt` + raw s_barrier once per k-tile, so with NS = 3 a k-tile's DMAs stay
+//   in flight across the barrier (cdna_hip_programming.md "Pipelining across barriers").
+//   The slot refilled at iteration t was last read in iteration t-1, before the barrier
+//   that ended it.
+//   R image: [rows][2*BK B], 16-B chunk c of row r at c ^ swz(r): r & 7 for 128-B rows,
+//     (r ^ (r >> 1)) & 3 for 64-B rows (both conflict-free for the fragment reads);
+//   T image: [BK k rows][cols] bf16, byte b of row r at b ^ 32 h(r) (as above).
+template <int BK>
+__device__ __forceinline__ int rswz2(int r) {
+  return BK == 64 ? (r & 7) : ((r ^ (r >> 1)) & 3);
+}
+
+// LDS-DMA sources of one operand tile of R rows (R image) / R columns (T image).
+template <bool T, int R, int BK>
+struct Lp2Stage {
+  static constexpr int INS = R * BK * 2 / 1024 / 8;  // glds per wave per k-tile
+  const char* p[INS];
+  int64_t step;
+
+  __device__ __forceinline__ void setup(const __bf16* base, int64_t ld,
+                                        const int64_t* __restrict__ rows, int64_t r0, int64_t lim,
+                                        int64_t kbeg, int wave, int lane) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t n = min(n0 + wn * 64 + 16 * j + 4 * g + r, d.N - 1);
-      bv[j][r] = (first_split && d.bias) ? d.bias[n] : 0.f;
+    for (int u = 0; u < INS; ++u) {
+      const int ins = INS * wave + u;
+      if constexpr (!T) {
+        constexpr int CPR = BK * 2 / 16, RPI = 64 / CPR;  // chunks per row, rows per instruction
+        const int r = RPI * ins + lane / CPR;
+        const int lc = (lane % CPR) ^ rswz2<BK>(r);
+        int64_t m = r0 + r;
+        m = m < lim ? m : lim - 1;
+        const int64_t rr = rows ? rows[m] : m;
+        p[u] = reinterpret_cast<const char*>(base + rr * ld + kbeg + lc * 8);
+      } else {
+        constexpr int CPR = 2 * R / 16, RPI = 64 / CPR;
+        const int r = RPI * ins + lane / CPR;
+        const int lc = (lane % CPR) ^ (2 * th(r));
+        int64_t c = r0 + lc * 8;
+        c = c + 8 <= lim ? c : lim - 8;
+        p[u] = reinterpret_cast<const char*>(base + (kbeg + r) * ld + c);
+      }
     }
+    step = T ? (int64_t)BK * ld * 2 : BK * 2;
+  }
+
+  __device__ __forceinline__ void issue(char* img, int wave, int64_t t) const {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t m = m0 + wm * 64 + 16 * i + (lane & 15);
-    const int64_t mc = m < d.M ? m : d.M - 1;
-    // this row's epilogue operands, loaded before its first store (vmcnt counts stores)
-    float rv[4][4], mk[4][4], pv[4][4];
-    const int64_t mr = d.mask_arows ? d.a_rows[mc] : mc;
-    const int64_t pr = d.rowvec ? (mc % d.rowvec_period) : 0;
+    for (int u = 0; u < INS; ++u)
+      glds16(p[u] + t * step, (lds_void*)(img + (INS * wave + u) * 1024));
+  }
+};
+
+// fragment: 16 rows (R image) / 16 columns (T image) x k 32kk + 8g .. +7
+template <bool T, int R, int BK>
+__device__ __forceinline__ bf16x8 frag2(const char* img, int base, int kk, int lane) {
+  const int g = lane >> 4;
+  if constexpr (!T) {
+    const int r = base + (lane & 15);
+    return *reinterpret_cast<const bf16x8*>(img + r * (2 * BK) + ((4 * kk + g) ^ rswz2<BK>(r)) * 16);
+  } else {
+    const int q = (lane & 15) >> 2, p = lane & 3;
+    const int r1 = 32 * kk + 8 * g + q, r2 = r1 + 4;
+    const int cb = (base + 4 * p) * 2;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (__attribute__((address_space(3))) bf16x4*)(img + r1 * (2 * R) + (cb ^ (32 * th(r1)))));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (__attribute__((address_space(3))) bf16x4*)(img + r2 * (2 * R) + (cb ^ (32 * th(r2)))));
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WM, int BK, int NS, bool AT, bool BT>
+__global__ __launch_bounds__(512, 1) void gemm_lp2_kernel(LpArgs args) {
+  constexpr int WN = 8 / WM;
+  constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int IMG_A = BM * BK * 2, IMG_B = BN * BK * 2;
+  constexpr int STAGE = IMG_A + IMG_B;
+  static_assert(NS * STAGE <= 160 * 1024, "LDS");
+  const savqa_gemm_lp_desc& d = args.d;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int t = xcd_remap(blockIdx.x, args.nblk);
+  const int tn = t % args.tiles_n, tm = t / args.tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)blockIdx.y * args.kchunk;
+  const int64_t kend = min(d.K, kbeg + args.kchunk);
+  const int nt = (int)((kend - kbeg) / BK);
+  const bool first_split = blockIdx.y == 0;
+
+  Lp2Stage<AT, BM, BK> sa;
+  Lp2Stage<!BT, BN, BK> sb;
+  sa.setup(static_cast<const __bf16*>(d.A), d.lda, AT ? nullptr : d.a_rows, m0, d.M, kbeg, wave, lane);
+  sb.setup(static_cast<const __bf16*>(d.B), d.ldb, nullptr, n0, d.N, kbeg, wave, lane);
+  constexpr int PER_TILE = Lp2Stage<AT, BM, BK>::INS + Lp2Stage<!BT, BN, BK>::INS;
+
+  f4 acc[FM][FN];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t n = min(n0 + wn * 64 + 16 * j + 4 * g + r, d.N - 1);
-        rv[j][r] = (first_split && d.resid) ? d.resid[mc * d.ldr + n] : 0.f;
-        pv[j][r] = (first_split && d.rowvec) ? d.rowvec[pr * d.ldrv + n] : 0.f;
-        if (d.mask)
-          mk[j][r] = d.mask_type == SAVQA_DT_BF16
-                         ? bf2f(static_cast<const __bf16*>(d.mask)[mr * d.ldmask + n])
-                         : static_cast<const float*>(d.mask)[mr * d.ldmask + n];
-        else
-          mk[j][r] = 1.f;
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) {
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+      if (s < nt) {
+        sa.issue(smem + s * STAGE, wave, s);
+        sb.issue(smem + s * STAGE + IMG_A, wave, s);
       }
-    if (m >= d.M) continue;
-    int64_t cr;
-    if (ident) {
-      cr = m;
-    } else {
-      const uint32_t mu = (uint32_t)m, cg = (uint32_t)d.c_group;
-      cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t nb = n0 + wn * 64 + 16 * j + 4 * g;
-      if (nb >= d.N) continue;
-      f4 v;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float x = acc[i][j][r] * d.alpha + bv[j][r] + pv[j][r];
-        if (d.relu) x = fmaxf(x, 0.f);
-        if (!(mk[j][r] > 0.f)) x = 0.f;
-        v[r] = x + rv[j][r];
+    if (NS == 3 && nt > 1) wait_vm<PER_TILE>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    int cur = 0;
+    for (int kt = 0; kt < nt; ++kt) {
+      const char* ia = smem + cur * STAGE;
+      const char* ib = ia + IMG_A;
+      const int nxt = kt + NS - 1;
+      if (nxt < nt && args.dbg != 2) {  // into slot nxt % NS, last read in iteration kt-1
+        const int sl = cur == 0 ? NS - 1 : cur - 1;
+        sa.issue(smem + sl * STAGE, wave, nxt);
+        sb.issue(smem + sl * STAGE + IMG_A, wave, nxt);
       }
-      const bool full = nb + 4 <= d.N;
-      if (d.C) {
-        float* cp = d.C + cr * d.ldc + nb;
-        if (d.atomic) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (nb + r < d.N) atomicAdd(cp + r, v[r]);
-        } else if (full && vec_c) {
-          *reinterpret_cast<f4*>(cp) = v;
-        } else {
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        if (args.dbg == 1) break;
+        bf16x8 a[FM], b[FN];
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (nb + r < d.N) cp[r] = v[r];
-        }
+        for (int i = 0; i < FM; ++i) a[i] = frag2<AT, BM, BK>(ia, wm * TM + 16 * i, kk, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b[j] = frag2<!BT, BN, BK>(ib, wn * TN + 16 * j, kk, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
       }
-      if (d.Cb) {
-        __bf16* cp = static_cast<__bf16*>(d.Cb) + cr * d.ldcb + nb;
-        const bf16x4 h = __builtin_convertvector(v, bf16x4);
-        if (full && (d.ldcb & 3) == 0 && (((uintptr_t)d.Cb) & 7) == 0) {
-          *reinterpret_cast<bf16x4*>(cp) = h;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (nb + r < d.N) cp[r] = h[r];
-        }
+      if (kt + 1 < nt) {  // k-tile kt+1 landed; with NS = 3 the DMAs of kt+2 stay in flight
+        if (NS == 3 && kt + 2 < nt) wait_vm<PER_TILE>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
       }
+      cur = cur == NS - 1 ? 0 : cur + 1;
     }
   }
+
+  // ---------------------------------------------------------------- epilogue
+  static_assert(NS * STAGE >= 8 * 16384, "epilogue images need 16 KB per wave");
+  __syncthreads();  // every wave's last k-tile reads are done: LDS is free
+  lp_epilogue<FM, FN>(d, acc, smem + wave * 16384, m0 + wm * TM, n0 + wn * TN, first_split, lane);
 }
 
 static int lp_slots() {
@@ -382,12 +614,27 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   if (!lp_ok(d, &msg)) return fail(SAVQA_EUNSUP, std::string("savqa_gemm_lp: ") + msg);
   if (d.c_group <= 0) d.c_group = 0;
   const bool fp8 = d.a_type == SAVQA_DT_FP8;
+  // kernel: variants of gemm_lp2_kernel (bf16, one workgroup per CU) when there are enough
+  // tiles to fill the chip, else the 128 x 128 kernel (two per CU); d.tile_hint selects one
+  // explicitly (tests / tuning): 1 = 128x128, 3 = 256x256 BK64 NS2, 4 = 256x128 BK64 NS3
+  // (k-tile 32 with a three-slot ring measured slower: 64-B rows halve each DMA's lines)
+  // measured (tools/lp_bench.py --variants, cfg-3 shapes): the two-per-CU 128 x 128 kernel is
+  // fastest except for the very wide outputs (N = 6144 forward, M = 6144 split-K dW), where
+  // the 256 x 256 tile's halved operand traffic wins by ~10%
+  int var = 1;
+  if (!fp8) {
+    const bool split = d.split_k > 1 || d.split_k < 0;
+    const int h = d.tile_hint & 255;
+    if (h == 1 || h == 3 || h == 4) var = h;
+    else if (d.N >= 4096 || (split && d.M >= 4096 && d.N >= 256)) var = 3;
+  }
+  const int bm = var == 1 ? 128 : 256, bn = var == 3 ? 256 : 128;
   const int bk = fp8 ? 128 : 64;
-  const int64_t tiles = ((d.M + 127) / 128) * ((d.N + 127) / 128);
+  const int slots = var == 1 ? lp_slots() : lp_slots() / LP_OCC;
+  const int64_t tiles = ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn);
   const int64_t nk = d.K / bk;
   int split = d.split_k > 1 ? d.split_k : 1;
   if (d.split_k < 0) {  // minimise rounds(s) * (k-tiles per slice + per-block overhead)
-    const int slots = lp_slots();
     int64_t best_cost = INT64_MAX;
     for (int s = 1; s <= 64 && (s == 1 || nk / s >= 4); ++s) {
       const int64_t rounds = (tiles * s + slots - 1) / slots;
@@ -398,13 +645,30 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   const int64_t per = (nk + split - 1) / split;
   a.kchunk = per * bk;
   const int nsplit = nk > 0 ? (int)((nk + per - 1) / per) : 1;
-  a.tiles_n = (int)((d.N + 127) / 128);
+  a.tiles_n = (int)((d.N + bn - 1) / bn);
+  a.dbg = d.tile_hint >> 8;
   a.nblk = (int)tiles;
   a.ntiles_k = (int)per;
   if (d.K == 0) a.kchunk = 0;
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)tiles, (unsigned)nsplit), block(LP_NT);
-  if (fp8)
+  if (var != 1) {
+    const dim3 b2(512);
+#define SAVQA_LP2(BN_, WM_, BK_, NS_)                                                              \
+  do {                                                                                             \
+    if (!d.a_trans && d.b_trans)                                                                   \
+      hipLaunchKernelGGL((gemm_lp2_kernel<256, BN_, WM_, BK_, NS_, false, true>), grid, b2, 0, s, a);  \
+    else if (!d.a_trans)                                                                           \
+      hipLaunchKernelGGL((gemm_lp2_kernel<256, BN_, WM_, BK_, NS_, false, false>), grid, b2, 0, s, a); \
+    else if (!d.b_trans)                                                                           \
+      hipLaunchKernelGGL((gemm_lp2_kernel<256, BN_, WM_, BK_, NS_, true, false>), grid, b2, 0, s, a);  \
+    else                                                                                           \
+      hipLaunchKernelGGL((gemm_lp2_kernel<256, BN_, WM_, BK_, NS_, true, true>), grid, b2, 0, s, a);   \
+  } while (0)
+    if (var == 3) SAVQA_LP2(256, 2, 64, 2);
+    else SAVQA_LP2(128, 4, 64, 3);
+#undef SAVQA_LP2
+  } else if (fp8)
     hipLaunchKernelGGL((gemm_lp_kernel<false, true, true>), grid, block, 0, s, a);
   else if (!d.a_trans && d.b_trans)
     hipLaunchKernelGGL((gemm_lp_kernel<false, true, false>), grid, block, 0, s, a);

@@ -157,7 +157,7 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
             b_trans=False, a_rows=None, a_scale=None, lds_a=0, b_scale=None, lds_b=0, C=None,
             ldc=0, Cb=None, ldcb=0, c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None,
             ldrv=0, rowvec_period=0, resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False,
-            alpha=1.0, relu=False, atomic=False, split_k=1):
+            alpha=1.0, relu=False, atomic=False, split_k=1, tile_hint=0):
     """savqa_gemm_lp_desc for bf16 / fp8 operands (include/savqa.h)."""
     d = _lib.GemmLpDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
@@ -173,6 +173,7 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
     d.mask_type = DT[mask.dtype] if mask is not None else 0
     d.alpha = float(alpha)
     d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
+    d.tile_hint = int(tile_hint)
     return d
 
 

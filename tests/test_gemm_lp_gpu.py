@@ -51,6 +51,29 @@ def test_bf16_layouts_bias_relu(lay, M, N, K):
     assert torch.equal(Cb.cpu(), C.to(torch.bfloat16).cpu())
 
 
+@pytest.mark.parametrize("hint", [1, 3, 4])
+@pytest.mark.parametrize("lay,M,N,K", [("NT", 1800, 1536, 512), ("NN", 1304, 1000, 512),
+                                       ("TN", 1304, 1544, 576), ("TT", 704, 1536, 256),
+                                       ("NT", 3700, 512, 2048)])
+def test_bf16_kernel_variants(hint, lay, M, N, K):
+    """Every kernel variant (tile_hint: 128x128 two per CU; 256x256 with a two-slot and
+    256x128 with a three-slot LDS-DMA ring, one per CU), incl. M / N edge tiles."""
+    O = ops()
+    at, bt = lay[0] == "T", lay[1] == "T"
+    A = bf((K, M) if at else (M, K), 21)
+    B = bf((N, K) if bt else (K, N), 22)
+    resid = torch.randn(M, N, device=dev)
+    C = torch.empty(M, N, device=dev)
+    Cb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    O.gemm_lp(A, B, M, N, K, lda=M if at else K, ldb=K if bt else N, a_trans=at, b_trans=bt,
+              C=C, ldc=N, Cb=Cb, ldcb=N, resid=resid, ldr=N, tile_hint=hint)
+    Ar = (A.t() if at else A).double()
+    Br = (B.t() if bt else B).double()
+    ref = Ar @ Br + resid.double()
+    assert rel(C, ref) < 2e-5
+    assert torch.equal(Cb.cpu(), C.to(torch.bfloat16).cpu())
+
+
 def test_bf16_dw_split_k_atomic_and_colsum():
     """dW += dY^T X (TN) at the encoder shape with the auto split-K (atomic accumulation
     into an existing gradient) and the bf16 bias-gradient column sums."""

@@ -1,0 +1,112 @@
+#!/usr/bin/env python
+"""Micro-benchmark of savqa_gemm_lp (bf16 / fp8 operands) on the cfg-3 (B=512) and cfg-5
+(B=1024) training-step GEMM shapes, with torch.mm on bf16 (hipBLASLt) as a yardstick.
+HIP-event timed; random operands (cdna_hip_programming.md rule 25)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from savqa_amd import ops  # noqa: E402
+
+dev = "cuda"
+BF = torch.bfloat16
+
+
+def timeit(fn, iters=20):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def bf16_case(lay, m, n, k, out, hint=0):
+    if lay == "NT":
+        A, B = torch.randn(m, k, device=dev).to(BF), torch.randn(n, k, device=dev).to(BF)
+        kw = dict(lda=k, ldb=k, b_trans=True)
+        ref = lambda: torch.mm(A, B.t())
+    elif lay == "NN":
+        A, B = torch.randn(m, k, device=dev).to(BF), torch.randn(k, n, device=dev).to(BF)
+        kw = dict(lda=k, ldb=n)
+        ref = lambda: torch.mm(A, B)
+    else:
+        A, B = torch.randn(k, m, device=dev).to(BF), torch.randn(k, n, device=dev).to(BF)
+        kw = dict(lda=m, ldb=n, a_trans=True)
+        ref = lambda: torch.mm(A.t(), B)
+    if out == "bf16":
+        Cb = torch.empty(m, n, device=dev, dtype=BF)
+        f = lambda: ops.gemm_lp(A, B, m, n, k, Cb=Cb, ldcb=n, relu=True, tile_hint=hint, **kw)
+    elif out == "atomic":
+        C = torch.zeros(m, n, device=dev)
+        f = lambda: ops.gemm_lp(A, B, m, n, k, C=C, ldc=n, atomic=True, split_k=-1,
+                                tile_hint=hint, **kw)
+    else:
+        C = torch.empty(m, n, device=dev)
+        f = lambda: ops.gemm_lp(A, B, m, n, k, C=C, ldc=n, tile_hint=hint, **kw)
+    return f, ref
+
+
+def fp8_case(m, n, k):
+    X = torch.randn(m, k, device=dev).clamp_min(0)
+    W = torch.randn(n, k, device=dev) / k ** 0.5
+    qx, sx = torch.empty(m, k, dtype=torch.uint8, device=dev), torch.empty(m, k // 32, dtype=torch.uint8, device=dev)
+    qw, sw = torch.empty(n, k, dtype=torch.uint8, device=dev), torch.empty(n, k // 32, dtype=torch.uint8, device=dev)
+    ops.quant_fp8(X, m, k, k, qx, k, sx, k // 32)
+    ops.quant_fp8(W, n, k, k, qw, k, sw, k // 32)
+    C = torch.empty(m, n, device=dev)
+    f = lambda: ops.gemm_lp(qx.view(torch.float8_e4m3fn), qw.view(torch.float8_e4m3fn), m, n, k,
+                            lda=k, ldb=k, b_trans=True, a_scale=sx, lds_a=k // 32, b_scale=sw,
+                            lds_b=k // 32, C=C, ldc=n)
+    A16, W16 = X.to(BF), W.to(BF)
+    return f, lambda: torch.mm(A16, W16.t())
+
+
+def main():
+    Ms = 37376  # cfg 3 semantic stack rows: 512 x 73
+    cases = [("fwd qkv", "NT", Ms, 1536, 512, "bf16"), ("fwd ffn1", "NT", Ms, 2048, 512, "bf16"),
+             ("fwd ffn2", "NT", Ms, 512, 2048, "f32"), ("fwd kv_all", "NT", Ms, 6144, 512, "bf16"),
+             ("fwd in", "NT", Ms, 512, 2048, "f32"),
+             ("dx ffn2", "NN", Ms, 2048, 512, "bf16"), ("dx ffn1", "NN", Ms, 512, 2048, "f32"),
+             ("dx qkv", "NN", Ms, 512, 1536, "f32"), ("dx kv", "NN", Ms, 512, 6144, "f32"),
+             ("dw qkv", "TN", 1536, 512, Ms, "atomic"), ("dw ffn1", "TN", 2048, 512, Ms, "atomic"),
+             ("dw ffn2", "TN", 512, 2048, Ms, "atomic"), ("dw kv", "TN", 6144, 512, Ms, "atomic")]
+    hints = [0] + ([1, 3, 4] if "--variants" in sys.argv else [])
+    if "--dbg" in sys.argv:  # v3 as is / without MFMAs / without k-loop DMAs
+        hints = [3, 3 + 256, 3 + 512, 4, 4 + 256, 4 + 512]
+        cases = cases[1:2] + cases[6:7] + cases[10:11]
+    tot_f = 0.0
+    tot_t = {h: 0.0 for h in hints}
+    for name, lay, m, n, k, out in cases:
+        fl = 2.0 * m * n * k
+        tot_f += fl
+        fs = {h: bf16_case(lay, m, n, k, out, h) for h in hints}
+        t2 = timeit(fs[hints[0]][1])
+        ts = {h: [] for h in hints}
+        for _ in range(3):  # interleaved rounds (rule 24), min
+            for h in hints:
+                ts[h].append(timeit(fs[h][0]))
+        line = f"{name:10s} {lay} {m:6d}x{n:5d}x{k:6d} {out:6s}"
+        for h in hints:
+            t1 = min(ts[h])
+            tot_t[h] += t1
+            line += f" v{h} {t1*1e6:7.1f}us {fl/t1/1e12:6.1f}TF"
+        print(line + f" | torch bf16 {t2*1e6:7.1f}us {fl/t2/1e12:6.1f}TF", flush=True)
+    for h in hints:
+        print(f"bf16 total v{h}: {tot_f/tot_t[h]/1e12:.1f} TF over the cfg-3 encoder shapes",
+              flush=True)
+    for name, m, n, k in (("fp8 vis in", 1024 * 50, 512, 2048), ("fp8 vis_mlp", 1024 * 36, 1024, 2048)):
+        f, g = fp8_case(m, n, k)
+        fl = 2.0 * m * n * k
+        t1, t2 = timeit(f), timeit(g)
+        print(f"{name:10s} NT {m:6d}x{n:5d}x{k:6d} fp8    savqa_lp {t1*1e6:8.1f}us "
+              f"{fl/t1/1e12:7.1f} TF   torch bf16 {t2*1e6:8.1f}us {fl/t2/1e12:7.1f} TF", flush=True)
+
+
+if __name__ == "__main__":
+    main()
