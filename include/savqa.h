@@ -93,7 +93,7 @@ int savqa_gemm_plan(const savqa_gemm_desc* d, int32_t* out);
  *   a_type / b_type: SAVQA_DT_BF16 or SAVQA_DT_FP8 (OCP e4m3fn). fp8 needs both operands
  *   fp8, a_trans = 0, b_trans = 1, K % 128 == 0, and e8m0 block scales a_scale[m][k/32]
  *   (row stride lds_a bytes) / b_scale[n][k/32]: value = e4m3 * 2^(scale - 127)
- *   (v_mfma_scale_f32_16x16x128_f8f6f4). bf16 needs K % 64 == 0, 16-B aligned operands
+ *   (v_mfma_scale_f32_16x16x128_f8f6f4). bf16 needs K % 8 == 0, 16-B aligned operands
  *   with ld % 8 == 0, and M % 8 == 0 (a_trans) / N % 8 == 0 (b_trans = 0).
  *   v = acc*alpha + bias[n] + rowvec[(m % rowvec_period)*ldrv + n]  (bias/rowvec/resid:
  *       first K slice only) ; v = relu ? max(v,0) : v ;
@@ -129,16 +129,19 @@ typedef struct savqa_gemm_lp_desc {
 int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* d);
 int savqa_gemm_lp_supported(const savqa_gemm_lp_desc* d);
 
-/* Conversions feeding the low-precision operands:
- *   savqa_cast_bf16: out[r*ldo + c] = bf16(in[r*ldi + c])  (fp32 -> bf16, round to nearest even)
+/* Conversions feeding the low-precision operands (output row of input row r: ro(r) =
+ * (r / group)*stride + r % group + offset, or r when group <= 0 -- e.g. the question rows
+ * of a [B][T] concat buffer):
+ *   savqa_cast_bf16: out[ro(r)*ldo + c] = bf16(in[r*ldi + c])  (round to nearest even)
  *   savqa_quant_fp8: per row r and 32-column block b: s = e8m0 scale making max|x| <= 448,
- *     q[r*ldq + c] = e4m3fn(x / 2^(s-127)) (round to nearest even), scale[r*lds + b] = s;
- *     cols % 32 == 0
+ *     q[ro(r)*ldq + c] = e4m3fn(x / 2^(s-127)) (round to nearest even), scale[ro(r)*lds + b]
+ *     = s; cols % 32 == 0
  *   savqa_dequant_fp8_bf16: out = bf16(q * 2^(s-127))  (the backward's bf16 copy) */
 int savqa_cast_bf16(void* stream, const float* in, int64_t rows, int64_t cols, int64_t ldi,
-                    void* out, int64_t ldo);
+                    void* out, int64_t ldo, int64_t group, int64_t stride, int64_t offset);
 int savqa_quant_fp8(void* stream, const float* in, int64_t rows, int64_t cols, int64_t ldi,
-                    void* q, int64_t ldq, uint8_t* scale, int64_t lds);
+                    void* q, int64_t ldq, uint8_t* scale, int64_t lds, int64_t group,
+                    int64_t stride, int64_t offset);
 int savqa_dequant_fp8_bf16(void* stream, const void* q, int64_t rows, int64_t cols, int64_t ldq,
                            const uint8_t* scale, int64_t lds, void* out, int64_t ldo);
 /* out[c] += sum_r X[r*ldx + c] over a bf16 X (bias gradients of the low-precision GEMMs) */
@@ -159,7 +162,8 @@ int savqa_colsum_acc(void* stream, const float* X, int64_t rows, int64_t cols, i
 int savqa_ln_fwd(void* stream, const float* x, const float* xscale, const float* r,
                  int64_t rows, int64_t cols,
                  const float* gamma, const float* beta, float eps,
-                 float* z_out, float* y, float* mean, float* rden, float* stdv, float* flag);
+                 float* z_out, float* y, float* mean, float* rden, float* stdv, float* flag,
+                 void* yb /* optional bf16 copy of y (the next low-precision GEMM's operand) */);
 
 /* Backward of the above: dz = dLN/dz (+ dz_add), dgamma += ..., dbeta += ...
  * Column sums land in the caller's slot workspace `ws` first (ws_bytes >=
@@ -171,7 +175,8 @@ int64_t savqa_ln_bwd_workspace_bytes(int64_t cols);
 int savqa_ln_bwd(void* stream, const float* dy, const float* z, const float* mean,
                  const float* rden, const float* stdv, const float* gamma,
                  int64_t rows, int64_t cols, const float* dz_add, float* dz,
-                 float* dgamma, float* dbeta, float* ws, int64_t ws_bytes);
+                 float* dgamma, float* dbeta, float* ws, int64_t ws_bytes,
+                 void* dzb /* optional bf16 copy of dz */);
 
 /* flag[r] = sign(|sum_c X[r*ldx+c]|)  (modules.py:257 key mask / :289 query mask) */
 int savqa_rowflag(void* stream, const float* X, int64_t rows, int64_t cols, int64_t ldx, float* flag);
@@ -198,6 +203,21 @@ int savqa_gattn_bwd(void* stream, const float* q, int64_t ldq, const float* k, i
                     const float* qflag, int64_t B, int64_t Tq, int64_t Tk, int64_t H, int64_t dk,
                     const float* dout, int64_t lddo, float* dq, int64_t lddq, float* dk_, int64_t lddk,
                     float* dv, int64_t lddv);
+
+/* bf16-storage variants (BASELINE cfg 3 / cfg 5 bf16 attention core): K / V and dK / dV are
+ * bf16 (rows 8-B aligned, ld % 4 == 0), Q / dQ are bf16 if q_bf16 else fp32 (the decoder's
+ * single query; mixed types need T_q = 1); O, dO, G and the flags stay fp32 and the softmax /
+ * graph / L1 chain and all products run in fp32 (MFMA strip kernels for T_q > 1, the
+ * single-query kernels for T_q = 1; T_k <= 128). */
+int savqa_gattn_fwd_bf16(void* stream, int32_t q_bf16, const void* q, int64_t ldq, const void* k,
+                         int64_t ldk, const void* v, int64_t ldv, const float* G,
+                         const float* kflag, const float* qflag, int64_t B, int64_t Tq,
+                         int64_t Tk, int64_t H, int64_t dk, float* o, int64_t ldo, float* att);
+int savqa_gattn_bwd_bf16(void* stream, int32_t q_bf16, const void* q, int64_t ldq, const void* k,
+                         int64_t ldk, const void* v, int64_t ldv, const float* G,
+                         const float* kflag, const float* qflag, int64_t B, int64_t Tq,
+                         int64_t Tk, int64_t H, int64_t dk, const float* dout, int64_t lddo,
+                         void* dq, int64_t lddq, void* dk_, int64_t lddk, void* dv, int64_t lddv);
 
 /* Key-tiled variant of the same operator for long sequences (any Tq, Tk; used for
  * Tk > 128: cfg 4's 449-token stacks, super-node relation graphs up to T = 1600).

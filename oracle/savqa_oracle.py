@@ -249,7 +249,8 @@ def mil_nce_forward(P, vis_fea, macro_ipt, macro_obj_loc, pos_obj, neg_obj, obj_
     w = F.softmax(torch.matmul(Pf, v), dim=2)                                 # :372-374
     obj = torch.sum(w * Pf, dim=2)                                            # (B,Nv,H)
     valid = (macro_obj_loc >= 0).nonzero()                                    # :377-380
-    macro[valid[:, 0], macro_obj_loc[valid[:, 0], valid[:, 1]].long(), :] = obj[valid[:, 0], valid[:, 1], :]
+    macro[valid[:, 0], macro_obj_loc[valid[:, 0], valid[:, 1]].long(), :] = \
+        obj[valid[:, 0], valid[:, 1], :].to(macro.dtype)  # (dtype cast: autocast runs)
     mil_rel = 0
     if rel is not None:
         macro, mil_rel = mil_nce_relations(P, macro, obj, *rel, pre=pre, eps=eps)

@@ -186,6 +186,8 @@ class _AttModelFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, model, decMask, drop, anchor, *tensors):
         inp = dict(zip(_INPUT_NAMES + _REL_NAMES, tensors))
+        if model.__dict__.get("_vis_scale") is not None:
+            inp["vis_fea_scale"] = model._vis_scale
         (lc, lv, ls, mil, mil_rel), saved = model._engine.forward(inp, decMask, drop)
         ctx.model = model
         ctx.saved = saved
@@ -259,9 +261,11 @@ class AttModel(nn.Module):
         self.label_smoothing = label_smoothing()
         # flatten every parameter into the arena (state_dict keys unchanged)
         object.__setattr__(self, "_arena", ParamArena(self, num_blocks, device=device))
-        # gemm_precision: "fp32" (default, exact fp32 products), "bf16" (BASELINE cfg 3:
-        # bf16 MFMA products, fp32 accumulation / master weights / everything else) or
-        # "bf16x3" (three bf16 MFMAs per product, ~2^-16 relative)
+        # gemm_precision (engine.ModelEngine): "fp32" (default, exact fp32 products),
+        # "bf16x3" (three bf16 MFMAs per product, ~2^-16 relative), "bf16" (BASELINE cfg 3:
+        # bf16-resident GEMM / attention operands, fp32 accumulation, residual stream, LN,
+        # softmax, loss and master weights) or "fp8" (cfg 5: "bf16" + fp8-e4m3 region
+        # features on block-scaled fp8 MFMA; forward(..., vis_fea_scale=) for fp8 inputs)
         object.__setattr__(self, "_engine", ModelEngine(self._arena, num_blocks, hidden_size,
                                                         num_heads, gemm_precision))
 
@@ -289,7 +293,9 @@ class AttModel(nn.Module):
                 macro_ipt, macro_mask, macro_graph, macro_obj_loc,
                 micro_positive_obj, micro_negative_obj, micro_obj_mask,
                 micro_positive_rel, micro_negative_rel, micro_positive_rel_loc,
-                micro_negative_rel_loc, decMask=True, mcb=False):
+                micro_negative_rel_loc, decMask=True, mcb=False, vis_fea_scale=None):
+        """AttModel_x3.py:512-542. vis_fea may be float8_e4m3fn (fp8 mode, BASELINE cfg 5) with
+        its e8m0 block scales vis_fea_scale [B, Nv, 2048/32] (savqa_quant_fp8's layout)."""
         if mcb:
             raise NotImplementedError("mcb=True needs torch.rfft (removed in torch>=1.8); out of scope")
         drop = None
@@ -312,7 +318,13 @@ class AttModel(nn.Module):
         def i64(t):
             return t.to(device=dev, dtype=torch.int64).contiguous()
 
-        tensors = (f32(vis_fea), i32(vis_mask), i64(q_ipt), i32(q_mask), i32(q_graph), i64(macro_ipt),
+        fp8_in = vis_fea.dtype == torch.float8_e4m3fn
+        if fp8_in and self._engine.gemm_precision != "fp8":
+            raise ValueError("fp8 region features need AttModel(..., gemm_precision='fp8')")
+        vis_t = vis_fea.to(device=dev).contiguous() if fp8_in else f32(vis_fea)
+        object.__setattr__(self, "_vis_scale", vis_fea_scale.to(device=dev).contiguous()
+                           if (fp8_in and vis_fea_scale is not None) else None)
+        tensors = (vis_t, i32(vis_mask), i64(q_ipt), i32(q_mask), i32(q_graph), i64(macro_ipt),
                    i32(macro_mask), i32(macro_graph), i64(macro_obj_loc), i64(micro_positive_obj),
                    i64(micro_negative_obj), i32(micro_obj_mask))
         if not self.only_obj:  # relation branch inputs (micro_negative_rel ids are unused, :391)

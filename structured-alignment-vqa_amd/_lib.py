@@ -79,13 +79,15 @@ _SIGS = {
     "savqa_colsum_acc": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
     "savqa_gemm_lp": [c_p, C.POINTER(GemmLpDesc)],
     "savqa_gemm_lp_supported": [C.POINTER(GemmLpDesc)],
-    "savqa_cast_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64],
-    "savqa_quant_fp8": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64],
+    "savqa_cast_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64],
+    "savqa_quant_fp8": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64,
+                        c_i64],
     "savqa_dequant_fp8_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64],
     "savqa_colsum_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
-    "savqa_ln_fwd": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p],
+    "savqa_ln_fwd": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p,
+                     c_p],
     "savqa_ln_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p,
-                     c_i64],
+                     c_i64, c_p],
     "savqa_ln_bwd_workspace_bytes": [c_i64],
     "savqa_rowflag": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
     "savqa_gattn_fwd": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
@@ -93,6 +95,11 @@ _SIGS = {
     "savqa_gattn_bwd": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
                         c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64,
                         c_p, c_i64],
+    "savqa_gattn_fwd_bf16": [c_p, c_i32, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
+                             c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p],
+    "savqa_gattn_bwd_bf16": [c_p, c_i32, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
+                             c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64,
+                             c_p, c_i64],
     "savqa_gattn_fwd_flash": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
                               c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p],
     "savqa_gattn_bwd_flash": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,

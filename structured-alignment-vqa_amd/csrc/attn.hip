@@ -23,6 +23,8 @@
 // for the column sums dV = P^T dO and dK = dS^T Q.
 #include "attn_common.h"
 
+#include <type_traits>
+
 #ifndef SAVQA_ATT_ALIAS
 #define SAVQA_ATT_ALIAS 1
 #endif
@@ -347,15 +349,15 @@ __device__ __forceinline__ void strip_dots(const f4v (&x)[4], const float* y, in
 
 // Cooperative stage of K_h and V_h rows [0, TK) into LDS (zero rows past Tk): every
 // thread issues its b128 loads back to back, so the workgroup waits one latency.
-template <int TK>
-__device__ __forceinline__ void stage_kv_tiles(const AttnArgs& a, int b, int h, float* Ks, float* Vs) {
+template <int TK, class A>
+__device__ __forceinline__ void stage_kv_tiles(const A& a, int b, int h, float* Ks, float* Vs) {
   for (int idx = threadIdx.x; idx < TK * 16; idx += blockDim.x) {
     const int j = idx >> 4, c4 = (idx & 15) * 4;
     f4v kv = {0.f, 0.f, 0.f, 0.f}, vv = kv;
     if (j < a.Tk) {
       const int64_t row = (int64_t)b * a.Tk + j;
-      kv = ld4(a.k + row * a.ldk + h * ATT_DK + c4);
-      vv = ld4(a.v + row * a.ldv + h * ATT_DK + c4);
+      kv = ldx4(a.k + row * a.ldk + h * ATT_DK + c4);
+      vv = ldx4(a.v + row * a.ldv + h * ATT_DK + c4);
     }
     *reinterpret_cast<f4v*>(&Ks[j * ATT_KLD + c4]) = kv;
     *reinterpret_cast<f4v*>(&Vs[j * ATT_KLD + c4]) = vv;
@@ -404,8 +406,8 @@ __device__ __forceinline__ float strip_row_forward(const f4v (&s)[NJT], int r, c
 // graph values of this lane's 4 accumulator rows (queries i0+4g+r) x keys 16 jt + col,
 // loaded up front with clamped (branch-free) addresses so their latency overlaps the
 // MFMA strip products instead of serialising inside the row chain
-template <int NJT>
-__device__ __forceinline__ void preload_graph(const AttnArgs& a, int b, int i0, int g, int col,
+template <int NJT, class A>
+__device__ __forceinline__ void preload_graph(const A& a, int b, int i0, int g, int col,
                                               float (&gp)[4][NJT]) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -415,8 +417,8 @@ __device__ __forceinline__ void preload_graph(const AttnArgs& a, int b, int i0, 
   }
 }
 
-template <int NJT>
-__global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgs a) {
+template <int NJT, typename T>
+__global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgsT<T> a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int bh = blockIdx.x;
   const int b = bh / a.H, h = bh % a.H;
@@ -441,9 +443,9 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgs a) {
   f4v qa[4];
   {
     const int iq = min(i0 + col, a.Tq - 1);
-    const float* qr = a.q + ((int64_t)b * a.Tq + iq) * a.ldq + h * ATT_DK + 4 * g;
+    const T* qr = a.q + ((int64_t)b * a.Tq + iq) * a.ldq + h * ATT_DK + 4 * g;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) qa[c] = ld4(qr + 16 * c);
+    for (int c = 0; c < 4; ++c) qa[c] = ldx4(qr + 16 * c);
   }
   float gp[4][NJT];
   preload_graph<NJT>(a, b, i0, g, col, gp);
@@ -504,8 +506,8 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgs a) {
   }
 }
 
-template <int NJT>
-__global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
+template <int NJT, typename T>
+__global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgsT<T> a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int bh = blockIdx.x;
   const int b = bh / a.H, h = bh % a.H;
@@ -527,11 +529,11 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
   {
     f4v qa[4], oa[4];
     const int iq = min(i0 + col, a.Tq - 1);
-    const float* qr = a.q + (qb + iq) * a.ldq + hd + 4 * g;
+    const T* qr = a.q + (qb + iq) * a.ldq + hd + 4 * g;
     const float* orr = a.dout + (qb + iq) * a.lddo + hd + 4 * g;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      qa[c] = ld4(qr + 16 * c);
+      qa[c] = ldx4(qr + 16 * c);
       oa[c] = ld4(orr + 16 * c);
     }
     float gp[4][NJT];
@@ -610,7 +612,7 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
     const int dcol = hd + dt * 16 + col;
     if (grp != cur) {  // wave-uniform
       cur = grp;
-      const float* src = grp < 4 ? a.dout : (grp < 8 ? a.q : a.k);
+      const T* src = grp < 8 ? a.q : a.k;  // dO (fp32) for grp < 4
       const int64_t ld = grp < 4 ? a.lddo : (grp < 8 ? a.ldq : a.ldk);
       const int64_t base = grp < 8 ? qb : kb;
       const int lim = grp < 8 ? a.Tq : a.Tk;
@@ -619,20 +621,22 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
       for (int kc = 0; kc < 8; ++kc) {
         if (kc < nk) {
 #pragma unroll
-          for (int t = 0; t < 4; ++t)
-            bcol[kc][t] = src[(base + min(kc * 16 + 4 * g + t, lim - 1)) * ld + dcol];
+          for (int t = 0; t < 4; ++t) {
+            const int64_t off = (base + min(kc * 16 + 4 * g + t, lim - 1)) * ld + dcol;
+            bcol[kc][t] = grp < 4 ? a.dout[off] : ldx1(src + off);
+          }
         }
       }
     }
     // ReLU-mask values of this tile's 4 output rows, fetched before the MFMAs (clamped rows)
     float mk[4];
     {
-      const float* msrc = grp < 4 ? a.v : (grp < 8 ? a.k : a.q);
+      const T* msrc = grp < 4 ? a.v : (grp < 8 ? a.k : a.q);
       const int64_t mld = grp < 4 ? a.ldv : (grp < 8 ? a.ldk : a.ldq);
       const int64_t base = grp < 8 ? kb : qb;
       const int lim = grp < 8 ? a.Tk : a.Tq;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) mk[r] = msrc[(base + min(tile * 16 + 4 * g + r, lim - 1)) * mld + dcol];
+      for (int r = 0; r < 4; ++r) mk[r] = ldx1(msrc + (base + min(tile * 16 + 4 * g + r, lim - 1)) * mld + dcol);
     }
     f4v acc = {0.f, 0.f, 0.f, 0.f};
     if (grp < 8) {
@@ -649,12 +653,12 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
         }
       }
       // dV / dK rows j = 16 tile + 4g + r, ReLU mask of the saved V / K
-      float* dst = isv ? a.dv : a.dk;
+      T* dst = isv ? a.dv : a.dk;
       const int64_t dld = isv ? a.lddv : a.lddk;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = tile * 16 + 4 * g + r;
-        if (j < a.Tk) dst[(kb + j) * dld + dcol] = mk[r] > 0.f ? acc[r] : 0.f;
+        if (j < a.Tk) stx1(dst + (kb + j) * dld + dcol, mk[r] > 0.f ? acc[r] : 0.f);
       }
     } else {
 #pragma unroll
@@ -668,7 +672,7 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = tile * 16 + 4 * g + r;
-        if (i < a.Tq) a.dq[(qb + i) * a.lddq + dcol] = mk[r] > 0.f ? acc[r] : 0.f;
+        if (i < a.Tq) stx1(a.dq + (qb + i) * a.lddq + dcol, mk[r] > 0.f ? acc[r] : 0.f);
       }
     }
   }
@@ -696,8 +700,8 @@ __device__ __forceinline__ f4v xrow_sum(f4v v) {  // sum over the 4 rows, lane c
 }
 
 // s[it] (scaled, masked; -inf past Tk) and the forward chain for the single query of (b,h)
-template <int NIT>
-__device__ __forceinline__ void q1_forward(const AttnArgs& a, int b, int hd, int kk, int c,
+template <int NIT, class A>
+__device__ __forceinline__ void q1_forward(const A& a, int b, int hd, int kk, int c,
                                            const f4v q4, float (&s)[NIT], float (&aa)[NIT],
                                            float (&gg)[NIT], float (&bm)[NIT], float& nrm) {
   const int64_t kb = (int64_t)b * a.Tk;
@@ -706,7 +710,7 @@ __device__ __forceinline__ void q1_forward(const AttnArgs& a, int b, int hd, int
     float x = -INFINITY;
     if (4 * it < a.Tk) {
       const int j = 4 * it + kk;
-      const f4v k4 = ld4(a.k + (kb + min(j, a.Tk - 1)) * a.ldk + hd + 4 * c);
+      const f4v k4 = ldx4(a.k + (kb + min(j, a.Tk - 1)) * a.ldk + hd + 4 * c);
       const float d = row16_sum((q4.x * k4.x + q4.y * k4.y) + (q4.z * k4.z + q4.w * k4.w));
       if (j < a.Tk) x = a.kflag[kb + j] == 0.f ? ATT_MASKED : d * 0.125f;
     }
@@ -737,14 +741,14 @@ __device__ __forceinline__ void q1_forward(const AttnArgs& a, int b, int hd, int
   nrm = rows4_sum(nr);
 }
 
-template <int NIT>
-__global__ __launch_bounds__(256) void gattn_fwd_q1_kernel(AttnArgs a) {
+template <int NIT, typename TQ, typename TKV>
+__global__ __launch_bounds__(256) void gattn_fwd_q1_kernel(AttnArgsT<TQ, TKV> a) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int bh = blockIdx.x * 4 + w;
   if (bh >= a.B * a.H) return;  // wave-uniform
   const int b = bh / a.H, h = bh % a.H, hd = h * ATT_DK;
   const int kk = lane >> 4, c = lane & 15;
-  const f4v q4 = ld4(a.q + (int64_t)b * a.ldq + hd + 4 * c);
+  const f4v q4 = ldx4(a.q + (int64_t)b * a.ldq + hd + 4 * c);
   float s[NIT], aa[NIT], gg[NIT], bm[NIT], nrm;
   q1_forward<NIT>(a, b, hd, kk, c, q4, s, aa, gg, bm, nrm);
   const float sden = fmaxf(nrm, 1e-12f);
@@ -758,7 +762,7 @@ __global__ __launch_bounds__(256) void gattn_fwd_q1_kernel(AttnArgs a) {
       const float n = bm[it] / sden;
       if (a.att && c == 0 && j < a.Tk) a.att[((int64_t)h * a.B + b) * a.Tk + j] = n;
       const float pj = j < a.Tk ? n * qf : 0.f;
-      const f4v v4 = ld4(a.v + (kb + min(j, a.Tk - 1)) * a.ldv + hd + 4 * c);
+      const f4v v4 = ldx4(a.v + (kb + min(j, a.Tk - 1)) * a.ldv + hd + 4 * c);
       o += pj * v4;
     }
   }
@@ -770,15 +774,15 @@ __global__ __launch_bounds__(256) void gattn_fwd_q1_kernel(AttnArgs a) {
   }
 }
 
-template <int NIT>
-__global__ __launch_bounds__(256) void gattn_bwd_q1_kernel(AttnArgs a) {
+template <int NIT, typename TQ, typename TKV>
+__global__ __launch_bounds__(256) void gattn_bwd_q1_kernel(AttnArgsT<TQ, TKV> a) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int bh = blockIdx.x * 4 + w;
   if (bh >= a.B * a.H) return;
   const int b = bh / a.H, h = bh % a.H, hd = h * ATT_DK;
   const int kk = lane >> 4, c = lane & 15;
   const int64_t kb = (int64_t)b * a.Tk;
-  const f4v q4 = ld4(a.q + (int64_t)b * a.ldq + hd + 4 * c);
+  const f4v q4 = ldx4(a.q + (int64_t)b * a.ldq + hd + 4 * c);
   const f4v do4 = ld4(a.dout + (int64_t)b * a.lddo + hd + 4 * c);
   float s[NIT], aa[NIT], gg[NIT], bm[NIT], nrm;
   q1_forward<NIT>(a, b, hd, kk, c, q4, s, aa, gg, bm, nrm);
@@ -791,7 +795,7 @@ __global__ __launch_bounds__(256) void gattn_bwd_q1_kernel(AttnArgs a) {
     float x = 0.f;
     if (4 * it < a.Tk) {
       const int j = 4 * it + kk;
-      const f4v v4 = ld4(a.v + (kb + min(j, a.Tk - 1)) * a.ldv + hd + 4 * c);
+      const f4v v4 = ldx4(a.v + (kb + min(j, a.Tk - 1)) * a.ldv + hd + 4 * c);
       x = row16_sum((do4.x * v4.x + do4.y * v4.y) + (do4.z * v4.z + do4.w * v4.w)) * qf;
       if (j >= a.Tk) x = 0.f;
     }
@@ -820,25 +824,25 @@ __global__ __launch_bounds__(256) void gattn_bwd_q1_kernel(AttnArgs a) {
       ds *= 0.125f;
       const float pj = ok ? bm[it] / sden * qf : 0.f;
       const int64_t row = kb + min(j, a.Tk - 1);
-      const f4v k4 = ld4(a.k + row * a.ldk + hd + 4 * c);
-      const f4v v4 = ld4(a.v + row * a.ldv + hd + 4 * c);
+      const f4v k4 = ldx4(a.k + row * a.ldk + hd + 4 * c);
+      const f4v v4 = ldx4(a.v + row * a.ldv + hd + 4 * c);
       dq += ds * k4;
       if (ok) {
-        float* dkr = a.dk + row * a.lddk + hd + 4 * c;
-        float* dvr = a.dv + row * a.lddv + hd + 4 * c;
+        TKV* dkr = a.dk + row * a.lddk + hd + 4 * c;
+        TKV* dvr = a.dv + row * a.lddv + hd + 4 * c;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          dkr[e] = k4[e] > 0.f ? ds * q4[e] : 0.f;
-          dvr[e] = v4[e] > 0.f ? pj * do4[e] : 0.f;
+          stx1(dkr + e, k4[e] > 0.f ? ds * q4[e] : 0.f);
+          stx1(dvr + e, v4[e] > 0.f ? pj * do4[e] : 0.f);
         }
       }
     }
   }
   dq = xrow_sum(dq);
   if (kk == 0) {
-    float* dqr = a.dq + (int64_t)b * a.lddq + hd + 4 * c;
+    TQ* dqr = a.dq + (int64_t)b * a.lddq + hd + 4 * c;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) dqr[e] = q4[e] > 0.f ? dq[e] : 0.f;
+    for (int e = 0; e < 4; ++e) stx1(dqr + e, q4[e] > 0.f ? dq[e] : 0.f);
   }
 }
 
@@ -851,22 +855,24 @@ static size_t bwd_lds(int Tq, int Tk) {
 }
 constexpr size_t kMaxLds = 160 * 1024;
 
-static int validate(const AttnArgs& a, int64_t dk, const char* who) {
+template <typename TQ, typename TKV>
+static int validate(const AttnArgsT<TQ, TKV>& a, int64_t dk, const char* who) {
+  constexpr uintptr_t AQ = sizeof(TQ) * 4 - 1, AK = sizeof(TKV) * 4 - 1;  // 4-element vector loads
   if (dk != ATT_DK) return fail(SAVQA_EUNSUP, std::string(who) + ": head dim must be 64");
   if (a.Tk <= 0 || a.Tq <= 0 || a.B <= 0 || a.H <= 0) return fail(SAVQA_EINVAL, std::string(who) + ": empty");
   if (a.Tk > 128) return fail(SAVQA_EUNSUP, std::string(who) + ": Tk > 128 not supported yet");
-  const uintptr_t al = (uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v;
-  if ((al & 15) || (a.ldk & 3) || (a.ldv & 3))
-    return fail(SAVQA_EINVAL, std::string(who) + ": K/V must be 16-B aligned with ld % 4 == 0");
+  if ((((uintptr_t)a.q) & AQ) || ((((uintptr_t)a.k) | ((uintptr_t)a.v)) & AK) || (a.ldk & 3) ||
+      (a.ldv & 3) || (a.ldq & 3))
+    return fail(SAVQA_EINVAL, std::string(who) + ": Q/K/V must be vector-aligned with ld % 4 == 0");
   if (a.Tq > 128) return fail(SAVQA_EUNSUP, std::string(who) + ": Tq > 128 not supported yet");
-  if (a.ldq & 3 || ((uintptr_t)a.q & 15))
-    return fail(SAVQA_EINVAL, std::string(who) + ": Q must be 16-B aligned with ld % 4 == 0");
   return 0;
 }
 
-// Path choice: 0 = row kernels (lane per key), 1 = MFMA strip kernels, 2 = single-query
-// kernels; overridable with SAVQA_ATTN_PATH=rows|mfma|q1 for A/B timing.
-static int attn_path(const AttnArgs& a) {
+// Path choice: 0 = row kernels (lane per key; fp32 only), 1 = MFMA strip kernels, 2 = single-
+// query kernels; overridable with SAVQA_ATTN_PATH=rows|mfma|q1 for A/B timing.
+template <typename TQ, typename TKV>
+static int attn_path(const AttnArgsT<TQ, TKV>& a) {
+  constexpr bool F32 = sizeof(TQ) == 4 && sizeof(TKV) == 4;
   static const int forced = [] {
     const char* e = getenv("SAVQA_ATTN_PATH");
     if (!e) return -1;
@@ -874,13 +880,121 @@ static int attn_path(const AttnArgs& a) {
     return v == "rows" ? 0 : (v == "mfma" ? 1 : (v == "q1" ? 2 : -1));
   }();
   if (forced == 2) return a.Tq == 1 ? 2 : 1;
-  if (forced >= 0) return forced;
+  if (forced == 0 && F32) return 0;
+  if (forced == 1) return 1;
   if (a.Tq == 1) return 2;
-  // a few query rows would fill <1/2 of each MFMA tile: lane-per-key kernels
-  return a.Tq >= 8 ? 1 : 0;
+  // a few query rows would fill <1/2 of each MFMA tile: lane-per-key kernels (fp32)
+  return (a.Tq >= 8 || !F32) ? 1 : 0;
 }
 
 static int q1_nit(int Tk) { return ((Tk + 3) / 4 + 7) / 8 * 8; }
+
+template <typename TQ, typename TKV>
+static int launch_fwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const char* who) {
+  if (int rc = validate(a, dk, who)) return rc;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const int path = attn_path(a);
+  if (path != 2 && !std::is_same<TQ, TKV>::value)
+    return fail(SAVQA_EUNSUP, std::string(who) + ": fp32 Q with bf16 K/V needs T_q = 1");
+  if (path == 2) {
+    const dim3 g((unsigned)((B * H + 3) / 4));
+    switch (q1_nit(Tk)) {
+      case 8: hipLaunchKernelGGL((gattn_fwd_q1_kernel<8, TQ, TKV>), g, dim3(256), 0, s, a); break;
+      case 16: hipLaunchKernelGGL((gattn_fwd_q1_kernel<16, TQ, TKV>), g, dim3(256), 0, s, a); break;
+      case 24: hipLaunchKernelGGL((gattn_fwd_q1_kernel<24, TQ, TKV>), g, dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL((gattn_fwd_q1_kernel<32, TQ, TKV>), g, dim3(256), 0, s, a); break;
+    }
+  } else if (path == 1) {
+    if constexpr (std::is_same<TQ, TKV>::value) {
+    using T = TKV;
+    const int njt = (Tk + 15) / 16, nw = (Tq + 15) / 16;
+#if SAVQA_ATT_ALIAS
+    const size_t lds = sizeof(float) * ((size_t)njt * 16 * ATT_KLD +
+                                        std::max((size_t)njt * 16 * ATT_KLD, (size_t)nw * njt * 16 * 20));
+#else
+    const size_t lds = sizeof(float) * ((size_t)2 * njt * 16 * ATT_KLD + (size_t)nw * njt * 16 * 20);
+#endif
+    switch (njt) {
+#define SAVQA_FWD_CASE(N)                                                                      \
+  case N:                                                                                      \
+    hipLaunchKernelGGL((gattn_fwd_mfma_kernel<N, T>), dim3(B * H), dim3(64 * nw), lds, s, a);  \
+    break;
+      SAVQA_FWD_CASE(1) SAVQA_FWD_CASE(2) SAVQA_FWD_CASE(3) SAVQA_FWD_CASE(4)
+      SAVQA_FWD_CASE(5) SAVQA_FWD_CASE(6) SAVQA_FWD_CASE(7) SAVQA_FWD_CASE(8)
+#undef SAVQA_FWD_CASE
+    }
+    }
+  } else {
+    if constexpr (sizeof(TQ) == 4 && sizeof(TKV) == 4) {
+      if (Tk <= 64)
+        hipLaunchKernelGGL(gattn_fwd_kernel<1>, dim3(B * H), dim3(256), fwd_lds(Tk, 1), s, a);
+      else
+        hipLaunchKernelGGL(gattn_fwd_kernel<2>, dim3(B * H), dim3(256), fwd_lds(Tk, 2), s, a);
+    }
+  }
+  return check_launch(who);
+}
+
+template <typename TQ, typename TKV>
+static int launch_bwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const char* who) {
+  if (int rc = validate(a, dk, who)) return rc;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const int path = attn_path(a);
+  if (path != 2 && !std::is_same<TQ, TKV>::value)
+    return fail(SAVQA_EUNSUP, std::string(who) + ": fp32 Q with bf16 K/V needs T_q = 1");
+  if (path >= 1 && ((a.lddo & 3) || (((uintptr_t)a.dout) & 15)))
+    return fail(SAVQA_EINVAL, std::string(who) + ": dO must be 16-B aligned with ld % 4 == 0");
+  if (path == 2) {
+    const dim3 g((unsigned)((B * H + 3) / 4));
+    switch (q1_nit(Tk)) {
+      case 8: hipLaunchKernelGGL((gattn_bwd_q1_kernel<8, TQ, TKV>), g, dim3(256), 0, s, a); break;
+      case 16: hipLaunchKernelGGL((gattn_bwd_q1_kernel<16, TQ, TKV>), g, dim3(256), 0, s, a); break;
+      case 24: hipLaunchKernelGGL((gattn_bwd_q1_kernel<24, TQ, TKV>), g, dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL((gattn_bwd_q1_kernel<32, TQ, TKV>), g, dim3(256), 0, s, a); break;
+    }
+    return check_launch(who);
+  }
+  if (path == 1) {
+    if constexpr (std::is_same<TQ, TKV>::value) {
+    using T = TKV;
+    const int njt = (Tk + 15) / 16, nw = (Tq + 15) / 16;
+    const size_t lds = sizeof(float) * 2 * (size_t)njt * 16 * (size_t)std::max(16 * nw + 4, ATT_KLD);
+    switch (njt) {
+#define SAVQA_BWD_CASE(N)                                                                      \
+  case N:                                                                                      \
+    hipLaunchKernelGGL((gattn_bwd_mfma_kernel<N, T>), dim3(B * H), dim3(64 * nw), lds, s, a);  \
+    break;
+      SAVQA_BWD_CASE(1) SAVQA_BWD_CASE(2) SAVQA_BWD_CASE(3) SAVQA_BWD_CASE(4)
+      SAVQA_BWD_CASE(5) SAVQA_BWD_CASE(6) SAVQA_BWD_CASE(7) SAVQA_BWD_CASE(8)
+#undef SAVQA_BWD_CASE
+    }
+    }
+    return check_launch(who);
+  }
+  if constexpr (sizeof(TQ) == 4 && sizeof(TKV) == 4) {
+    const size_t lds = bwd_lds(Tq, Tk);
+    if (lds > kMaxLds) return fail(SAVQA_EUNSUP, std::string(who) + ": Tq*Tk too large for the LDS path");
+    if (Tk <= 64)
+      hipLaunchKernelGGL(gattn_bwd_kernel<1>, dim3(B * H), dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL(gattn_bwd_kernel<2>, dim3(B * H), dim3(256), lds, s, a);
+  }
+  return check_launch(who);
+}
+
+template <typename TQ, typename TKV>
+static AttnArgsT<TQ, TKV> make_args(const void* q, int64_t ldq, const void* k, int64_t ldk,
+                                    const void* v, int64_t ldv, const float* G, const float* kflag,
+                                    const float* qflag, int64_t B, int64_t Tq, int64_t Tk,
+                                    int64_t H) {
+  AttnArgsT<TQ, TKV> a{};
+  a.q = static_cast<const TQ*>(q); a.ldq = ldq;
+  a.k = static_cast<const TKV*>(k); a.ldk = ldk;
+  a.v = static_cast<const TKV*>(v); a.ldv = ldv;
+  a.G = G; a.kflag = kflag; a.qflag = qflag;
+  a.B = (int)B; a.Tq = (int)Tq; a.Tk = (int)Tk; a.H = (int)H;
+  return a;
+}
 
 }  // namespace savqa
 
@@ -891,46 +1005,9 @@ extern "C" int savqa_gattn_fwd(void* stream, const float* q, int64_t ldq, const 
                                const float* kflag, const float* qflag, int64_t B, int64_t Tq,
                                int64_t Tk, int64_t H, int64_t dk, float* o, int64_t ldo,
                                float* att) {
-  AttnArgs a{};
-  a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv; a.G = G;
-  a.kflag = kflag; a.qflag = qflag; a.B = (int)B; a.Tq = (int)Tq; a.Tk = (int)Tk; a.H = (int)H;
+  AttnArgs a = make_args<float, float>(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H);
   a.o = o; a.ldo = ldo; a.att = att;
-  if (int rc = validate(a, dk, "savqa_gattn_fwd")) return rc;
-  hipStream_t s = as_stream(stream);
-  const int path = attn_path(a);
-  if (path == 2) {
-    const dim3 g((unsigned)((B * H + 3) / 4));
-    switch (q1_nit((int)Tk)) {
-      case 8: hipLaunchKernelGGL(gattn_fwd_q1_kernel<8>, g, dim3(256), 0, s, a); break;
-      case 16: hipLaunchKernelGGL(gattn_fwd_q1_kernel<16>, g, dim3(256), 0, s, a); break;
-      case 24: hipLaunchKernelGGL(gattn_fwd_q1_kernel<24>, g, dim3(256), 0, s, a); break;
-      default: hipLaunchKernelGGL(gattn_fwd_q1_kernel<32>, g, dim3(256), 0, s, a); break;
-    }
-  } else if (path == 1) {
-    const int njt = (int)((Tk + 15) / 16), nw = (int)((Tq + 15) / 16);
-#if SAVQA_ATT_ALIAS
-    const size_t lds = sizeof(float) * ((size_t)njt * 16 * ATT_KLD +
-                                        std::max((size_t)njt * 16 * ATT_KLD, (size_t)nw * njt * 16 * 20));
-#else
-    const size_t lds = sizeof(float) * ((size_t)2 * njt * 16 * ATT_KLD + (size_t)nw * njt * 16 * 20);
-#endif
-    switch (njt) {
-#define SAVQA_FWD_CASE(N)                                                                  \
-  case N:                                                                                  \
-    hipLaunchKernelGGL(gattn_fwd_mfma_kernel<N>, dim3(B * H), dim3(64 * nw), lds, s, a);   \
-    break;
-      SAVQA_FWD_CASE(1) SAVQA_FWD_CASE(2) SAVQA_FWD_CASE(3) SAVQA_FWD_CASE(4)
-      SAVQA_FWD_CASE(5) SAVQA_FWD_CASE(6) SAVQA_FWD_CASE(7) SAVQA_FWD_CASE(8)
-#undef SAVQA_FWD_CASE
-    }
-  } else if (Tk <= 64) {
-    const size_t lds = fwd_lds((int)Tk, 1);
-    hipLaunchKernelGGL(gattn_fwd_kernel<1>, dim3(B * H), dim3(256), lds, s, a);
-  } else {
-    const size_t lds = fwd_lds((int)Tk, 2);
-    hipLaunchKernelGGL(gattn_fwd_kernel<2>, dim3(B * H), dim3(256), lds, s, a);
-  }
-  return check_launch("savqa_gattn_fwd");
+  return launch_fwd(a, dk, as_stream(stream), "savqa_gattn_fwd");
 }
 
 extern "C" int savqa_gattn_bwd(void* stream, const float* q, int64_t ldq, const float* k,
@@ -939,45 +1016,55 @@ extern "C" int savqa_gattn_bwd(void* stream, const float* q, int64_t ldq, const 
                                int64_t Tk, int64_t H, int64_t dk, const float* dout, int64_t lddo,
                                float* dq, int64_t lddq, float* dk_, int64_t lddk, float* dv,
                                int64_t lddv) {
-  AttnArgs a{};
-  a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv; a.G = G;
-  a.kflag = kflag; a.qflag = qflag; a.B = (int)B; a.Tq = (int)Tq; a.Tk = (int)Tk; a.H = (int)H;
+  AttnArgs a = make_args<float, float>(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H);
   a.dout = dout; a.lddo = lddo; a.dq = dq; a.lddq = lddq; a.dk = dk_; a.lddk = lddk;
   a.dv = dv; a.lddv = lddv;
-  if (int rc = validate(a, dk, "savqa_gattn_bwd")) return rc;
-  hipStream_t s = as_stream(stream);
-  const int path = attn_path(a);
-  if (path >= 1 && ((a.ldq & 3) || (a.lddo & 3) || (((uintptr_t)a.dout) & 15)))
-    return fail(SAVQA_EINVAL, "savqa_gattn_bwd: Q/dO must be 16-B aligned with ld % 4 == 0");
-  if (path == 2) {
-    const dim3 g((unsigned)((B * H + 3) / 4));
-    switch (q1_nit((int)Tk)) {
-      case 8: hipLaunchKernelGGL(gattn_bwd_q1_kernel<8>, g, dim3(256), 0, s, a); break;
-      case 16: hipLaunchKernelGGL(gattn_bwd_q1_kernel<16>, g, dim3(256), 0, s, a); break;
-      case 24: hipLaunchKernelGGL(gattn_bwd_q1_kernel<24>, g, dim3(256), 0, s, a); break;
-      default: hipLaunchKernelGGL(gattn_bwd_q1_kernel<32>, g, dim3(256), 0, s, a); break;
-    }
-    return check_launch("savqa_gattn_bwd");
-  }
-  if (path == 1) {
-    const int njt = (int)((Tk + 15) / 16), nw = (int)((Tq + 15) / 16);
-    const size_t lds = sizeof(float) * 2 * (size_t)njt * 16 * (size_t)std::max(16 * nw + 4, ATT_KLD);
-    switch (njt) {
-#define SAVQA_BWD_CASE(N)                                                                  \
-  case N:                                                                                  \
-    hipLaunchKernelGGL(gattn_bwd_mfma_kernel<N>, dim3(B * H), dim3(64 * nw), lds, s, a);   \
-    break;
-      SAVQA_BWD_CASE(1) SAVQA_BWD_CASE(2) SAVQA_BWD_CASE(3) SAVQA_BWD_CASE(4)
-      SAVQA_BWD_CASE(5) SAVQA_BWD_CASE(6) SAVQA_BWD_CASE(7) SAVQA_BWD_CASE(8)
-#undef SAVQA_BWD_CASE
-    }
-    return check_launch("savqa_gattn_bwd");
-  }
-  const size_t lds = bwd_lds((int)Tq, (int)Tk);
-  if (lds > kMaxLds) return fail(SAVQA_EUNSUP, "savqa_gattn_bwd: Tq*Tk too large for the LDS path");
-  if (Tk <= 64)
-    hipLaunchKernelGGL(gattn_bwd_kernel<1>, dim3(B * H), dim3(256), lds, s, a);
-  else
-    hipLaunchKernelGGL(gattn_bwd_kernel<2>, dim3(B * H), dim3(256), lds, s, a);
-  return check_launch("savqa_gattn_bwd");
+  return launch_bwd(a, dk, as_stream(stream), "savqa_gattn_bwd");
+}
+
+template <typename TQ>
+static int fwd_bf16(void* stream, const void* q, int64_t ldq, const void* k, int64_t ldk,
+                    const void* v, int64_t ldv, const float* G, const float* kflag,
+                    const float* qflag, int64_t B, int64_t Tq, int64_t Tk, int64_t H, int64_t dk,
+                    float* o, int64_t ldo, float* att) {
+  auto a = make_args<TQ, __bf16>(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H);
+  a.o = o; a.ldo = ldo; a.att = att;
+  return launch_fwd(a, dk, as_stream(stream), "savqa_gattn_fwd_bf16");
+}
+
+template <typename TQ>
+static int bwd_bf16(void* stream, const void* q, int64_t ldq, const void* k, int64_t ldk,
+                    const void* v, int64_t ldv, const float* G, const float* kflag,
+                    const float* qflag, int64_t B, int64_t Tq, int64_t Tk, int64_t H, int64_t dk,
+                    const float* dout, int64_t lddo, void* dq, int64_t lddq, void* dk_,
+                    int64_t lddk, void* dv, int64_t lddv) {
+  auto a = make_args<TQ, __bf16>(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H);
+  a.dout = dout; a.lddo = lddo;
+  a.dq = static_cast<TQ*>(dq); a.lddq = lddq;
+  a.dk = static_cast<__bf16*>(dk_); a.lddk = lddk;
+  a.dv = static_cast<__bf16*>(dv); a.lddv = lddv;
+  return launch_bwd(a, dk, as_stream(stream), "savqa_gattn_bwd_bf16");
+}
+
+extern "C" int savqa_gattn_fwd_bf16(void* stream, int32_t q_bf16, const void* q, int64_t ldq,
+                                    const void* k, int64_t ldk, const void* v, int64_t ldv,
+                                    const float* G, const float* kflag, const float* qflag,
+                                    int64_t B, int64_t Tq, int64_t Tk, int64_t H, int64_t dk,
+                                    float* o, int64_t ldo, float* att) {
+  return q_bf16 ? fwd_bf16<__bf16>(stream, q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H,
+                                   dk, o, ldo, att)
+                : fwd_bf16<float>(stream, q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H,
+                                  dk, o, ldo, att);
+}
+
+extern "C" int savqa_gattn_bwd_bf16(void* stream, int32_t q_bf16, const void* q, int64_t ldq,
+                                    const void* k, int64_t ldk, const void* v, int64_t ldv,
+                                    const float* G, const float* kflag, const float* qflag,
+                                    int64_t B, int64_t Tq, int64_t Tk, int64_t H, int64_t dk,
+                                    const float* dout, int64_t lddo, void* dq, int64_t lddq,
+                                    void* dk_, int64_t lddk, void* dv, int64_t lddv) {
+  return q_bf16 ? bwd_bf16<__bf16>(stream, q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H,
+                                   dk, dout, lddo, dq, lddq, dk_, lddk, dv, lddv)
+                : bwd_bf16<float>(stream, q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H,
+                                  dk, dout, lddo, dq, lddq, dk_, lddk, dv, lddv);
 }

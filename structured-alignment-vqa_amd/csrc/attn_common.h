@@ -10,10 +10,13 @@ constexpr int ATT_KLD = 68;  // padded K/V row (floats), 16-B aligned
 constexpr int ATT_RB = 4;    // query rows per wave per pass
 constexpr float ATT_MASKED = -4294967296.0f;  // fp32(-2**32 + 1)
 
-struct AttnArgs {
-  const float* q; int64_t ldq;
-  const float* k; int64_t ldk;
-  const float* v; int64_t ldv;
+// TQ / TKV: storage types of Q, dQ and of K, V, dK, dV (float, or __bf16 in the bf16
+// training mode); O, dO, the graph and the flags stay fp32, and every kernel computes in fp32.
+template <typename TQ, typename TKV = TQ>
+struct AttnArgsT {
+  const TQ* q; int64_t ldq;
+  const TKV* k; int64_t ldk;
+  const TKV* v; int64_t ldv;
   const float* G;
   const float* kflag;
   const float* qflag;
@@ -22,10 +25,11 @@ struct AttnArgs {
   float* att;
   // backward
   const float* dout; int64_t lddo;
-  float* dq; int64_t lddq;
-  float* dk; int64_t lddk;
-  float* dv; int64_t lddv;
+  TQ* dq; int64_t lddq;
+  TKV* dk; int64_t lddk;
+  TKV* dv; int64_t lddv;
 };
+using AttnArgs = AttnArgsT<float>;
 
 using f4v = float __attribute__((ext_vector_type(4)));
 
@@ -54,6 +58,17 @@ __device__ __forceinline__ float row16_max(float v) {
 }
 
 __device__ __forceinline__ f4v ld4(const float* p) { return *reinterpret_cast<const f4v*>(p); }
+
+// 4 consecutive values of a Q/K/V row (fp32 or bf16 storage) as fp32; one value; a store
+typedef __bf16 att_bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4v ldx4(const float* p) { return ld4(p); }
+__device__ __forceinline__ f4v ldx4(const __bf16* p) {
+  return __builtin_convertvector(*reinterpret_cast<const att_bf16x4*>(p), f4v);
+}
+__device__ __forceinline__ float ldx1(const float* p) { return *p; }
+__device__ __forceinline__ float ldx1(const __bf16* p) { return (float)*p; }
+__device__ __forceinline__ void stx1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void stx1(__bf16* p, float v) { *p = (__bf16)v; }
 
 // Same with Y staged in LDS ([TK][ATT_KLD], rows >= Tk zero): b128 reads, lanes 0-15 of a
 // read phase hit 16 disjoint bank quads (row stride 68 floats).

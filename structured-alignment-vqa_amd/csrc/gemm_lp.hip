@@ -52,6 +52,10 @@ __device__ __forceinline__ void glds16(const void* src, lds_void* dst) {
   __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
 }
 
+// 16 zero bytes: the LDS-DMA source of every operand granule past the end of K (the last,
+// partial k-tile of a K that is not a multiple of the k-tile)
+__device__ __attribute__((aligned(16))) uint4 g_lp_zero[1];
+
 struct LpArgs {
   savqa_gemm_lp_desc d;
   int tiles_n, ntiles_k;  // k-tiles per split slice
@@ -68,6 +72,7 @@ struct LpArgs {
 template <bool T, bool FP8>
 struct LpStage {
   const char* p[4];
+  int koff[4];   // k of this lane's granule within a k-tile
   int64_t step;  // bytes per k-tile
 
   __device__ __forceinline__ void setup(const void* base, int64_t ld, int esz,
@@ -84,12 +89,14 @@ struct LpStage {
         m = m < lim ? m : lim - 1;
         const int64_t rr = rows ? rows[m] : m;
         p[u] = b + (rr * ld + kbeg) * esz + lc * 16;
+        koff[u] = lc * 16 / esz;
       } else {
         const int r = 4 * ins + (lane >> 4);
         const int lc = (lane & 15) ^ (2 * th(r));
         int64_t c = r0 + lc * 8;
         c = c + 8 <= lim ? c : lim - 8;
         p[u] = b + ((kbeg + r) * ld + c) * esz;
+        koff[u] = r;
       }
     }
     step = T ? (int64_t)64 * ld * esz : LP_KB;
@@ -99,6 +106,14 @@ struct LpStage {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       glds16(p[u] + t * step, (lds_void*)(img + (4 * wave + u) * 1024));
+  }
+
+  // partial last k-tile: granules at k >= krem (within the tile) load zeros
+  __device__ __forceinline__ void issue_tail(char* img, int wave, int64_t t, int krem) const {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      glds16(koff[u] < krem ? (const void*)(p[u] + t * step) : (const void*)g_lp_zero,
+             (lds_void*)(img + (4 * wave + u) * 1024));
   }
 };
 
@@ -297,7 +312,9 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   const int64_t m0 = (int64_t)tm * LP_TILE, n0 = (int64_t)tn * LP_TILE;
   const int64_t kbeg = (int64_t)blockIdx.y * args.kchunk;
   const int64_t kend = min(d.K, kbeg + args.kchunk);
-  const int nt = (int)((kend - kbeg) / (FP8 ? 128 : 64));
+  constexpr int BKE = FP8 ? 128 : 64;  // k elements per k-tile
+  const int nt = (int)((kend - kbeg + BKE - 1) / BKE);
+  const int krem = (int)(kend - kbeg - (int64_t)(nt - 1) * BKE);  // k of the last k-tile
   const bool first_split = blockIdx.y == 0;
   const int esz = FP8 ? 1 : 2;
 
@@ -331,9 +348,17 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
     }
   };
 
+  auto stage = [&](char* img, int64_t kt) {
+    if (kt + 1 == nt && krem < BKE) {
+      sa.issue_tail(img, wave, kt, krem);
+      sb.issue_tail(img + LP_IMG, wave, kt, krem);
+    } else {
+      sa.issue(img, wave, kt);
+      sb.issue(img + LP_IMG, wave, kt);
+    }
+  };
   if (nt > 0) {
-    sa.issue(smem, wave, 0);
-    sb.issue(smem + LP_IMG, wave, 0);
+    stage(smem, 0);
     load_scales(0);
     __syncthreads();  // vmcnt(0) + barrier: stage 0 landed for every wave
     for (int kt = 0; kt < nt; ++kt) {
@@ -345,9 +370,7 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
         for (int i = 0; i < 4; ++i) { sca_c[i] = sca[i]; scb_c[i] = scb[i]; }
       }
       if (kt + 1 < nt) {  // next k-tile into the other buffer (read one barrier ago)
-        char* nx = smem + ((kt + 1) & 1) * 2 * LP_IMG;
-        sa.issue(nx, wave, kt + 1);
-        sb.issue(nx + LP_IMG, wave, kt + 1);
+        stage(smem + ((kt + 1) & 1) * 2 * LP_IMG, kt + 1);
         load_scales(kt + 1);
       }
       if constexpr (FP8) {
@@ -408,6 +431,7 @@ template <bool T, int R, int BK>
 struct Lp2Stage {
   static constexpr int INS = R * BK * 2 / 1024 / 8;  // glds per wave per k-tile
   const char* p[INS];
+  int koff[INS];  // k of this lane's granule within a k-tile
   int64_t step;
 
   __device__ __forceinline__ void setup(const __bf16* base, int64_t ld,
@@ -424,6 +448,7 @@ struct Lp2Stage {
         m = m < lim ? m : lim - 1;
         const int64_t rr = rows ? rows[m] : m;
         p[u] = reinterpret_cast<const char*>(base + rr * ld + kbeg + lc * 8);
+        koff[u] = lc * 8;
       } else {
         constexpr int CPR = 2 * R / 16, RPI = 64 / CPR;
         const int r = RPI * ins + lane / CPR;
@@ -431,6 +456,7 @@ struct Lp2Stage {
         int64_t c = r0 + lc * 8;
         c = c + 8 <= lim ? c : lim - 8;
         p[u] = reinterpret_cast<const char*>(base + (kbeg + r) * ld + c);
+        koff[u] = r;
       }
     }
     step = T ? (int64_t)BK * ld * 2 : BK * 2;
@@ -440,6 +466,13 @@ struct Lp2Stage {
 #pragma unroll
     for (int u = 0; u < INS; ++u)
       glds16(p[u] + t * step, (lds_void*)(img + (INS * wave + u) * 1024));
+  }
+
+  __device__ __forceinline__ void issue_tail(char* img, int wave, int64_t t, int krem) const {
+#pragma unroll
+    for (int u = 0; u < INS; ++u)
+      glds16(koff[u] < krem ? (const void*)(p[u] + t * step) : (const void*)g_lp_zero,
+             (lds_void*)(img + (INS * wave + u) * 1024));
   }
 };
 
@@ -485,7 +518,8 @@ __global__ __launch_bounds__(512, 1) void gemm_lp2_kernel(LpArgs args) {
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t kbeg = (int64_t)blockIdx.y * args.kchunk;
   const int64_t kend = min(d.K, kbeg + args.kchunk);
-  const int nt = (int)((kend - kbeg) / BK);
+  const int nt = (int)((kend - kbeg + BK - 1) / BK);
+  const int krem = (int)(kend - kbeg - (int64_t)(nt - 1) * BK);  // k of the last k-tile
   const bool first_split = blockIdx.y == 0;
 
   Lp2Stage<AT, BM, BK> sa;
@@ -500,13 +534,19 @@ __global__ __launch_bounds__(512, 1) void gemm_lp2_kernel(LpArgs args) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
+  auto stage = [&](char* img, int64_t kt) {
+    if (kt + 1 == nt && krem < BK) {
+      sa.issue_tail(img, wave, kt, krem);
+      sb.issue_tail(img + IMG_A, wave, kt, krem);
+    } else {
+      sa.issue(img, wave, kt);
+      sb.issue(img + IMG_A, wave, kt);
+    }
+  };
   if (nt > 0) {
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
-      if (s < nt) {
-        sa.issue(smem + s * STAGE, wave, s);
-        sb.issue(smem + s * STAGE + IMG_A, wave, s);
-      }
+      if (s < nt) stage(smem + s * STAGE, s);
     if (NS == 3 && nt > 1) wait_vm<PER_TILE>();
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
@@ -517,8 +557,7 @@ __global__ __launch_bounds__(512, 1) void gemm_lp2_kernel(LpArgs args) {
       const int nxt = kt + NS - 1;
       if (nxt < nt && args.dbg != 2) {  // into slot nxt % NS, last read in iteration kt-1
         const int sl = cur == 0 ? NS - 1 : cur - 1;
-        sa.issue(smem + sl * STAGE, wave, nxt);
-        sb.issue(smem + sl * STAGE + IMG_A, wave, nxt);
+        stage(smem + sl * STAGE, nxt);
       }
 #pragma unroll
       for (int kk = 0; kk < BK / 32; ++kk) {
@@ -587,7 +626,7 @@ static bool lp_ok(const savqa_gemm_lp_desc& d, const char** msg) {
     if (d.lda % 16 || d.ldb % 16) return no("fp8 needs ld % 16 == 0");
     if (!d.a_scale || !d.b_scale) return no("fp8 needs block scales");
   } else {
-    if (d.K % 64) return no("bf16 needs K % 64 == 0");
+    if (d.K % 8) return no("bf16 needs K % 8 == 0");
     if (d.lda % 8 || d.ldb % 8) return no("bf16 needs ld % 8 == 0");
     if (d.a_trans && d.M % 8) return no("a_trans needs M % 8 == 0");
     if (!d.b_trans && d.N % 8) return no("b_trans = 0 needs N % 8 == 0");
@@ -632,7 +671,7 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   const int bk = fp8 ? 128 : 64;
   const int slots = var == 1 ? lp_slots() : lp_slots() / LP_OCC;
   const int64_t tiles = ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn);
-  const int64_t nk = d.K / bk;
+  const int64_t nk = (d.K + bk - 1) / bk;
   int split = d.split_k > 1 ? d.split_k : 1;
   if (d.split_k < 0) {  // minimise rounds(s) * (k-tiles per slice + per-block overhead)
     int64_t best_cost = INT64_MAX;

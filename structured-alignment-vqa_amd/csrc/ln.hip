@@ -12,6 +12,7 @@
 namespace savqa {
 
 constexpr int LN_MAXV = 4;  // float4 per lane -> cols <= 1024
+typedef __bf16 ln_bf16x4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x,
                                                      const float* __restrict__ xscale,
@@ -23,7 +24,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
                                                      float* __restrict__ mean_out,
                                                      float* __restrict__ rden_out,
                                                      float* __restrict__ std_out,
-                                                     float* __restrict__ flag) {
+                                                     float* __restrict__ flag,
+                                                     __bf16* __restrict__ yb) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -71,6 +73,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
       o.z = g.z * (v[i].z - mean) / den + bt.z;
       o.w = g.w * (v[i].w - mean) / den + bt.w;
       reinterpret_cast<float4*>(y + row * cols)[c4] = o;
+      if (yb) reinterpret_cast<ln_bf16x4*>(yb + row * cols)[c4] =
+          ln_bf16x4{(__bf16)o.x, (__bf16)o.y, (__bf16)o.z, (__bf16)o.w};
       if (z_out) reinterpret_cast<float4*>(z_out + row * cols)[c4] = v[i];
       fsum += (o.x + o.y) + (o.z + o.w);
     }
@@ -127,7 +131,7 @@ template <int NV, bool ADD>
 __device__ __forceinline__ void ln_bwd_row(const LnBwdRow<NV, ADD>& b, int64_t row, int lane, int cols,
                                            float invN, const float4 (&g)[NV], float4 (&dg)[NV],
                                            float4 (&db)[NV], const float* __restrict__ dz_add,
-                                           float* __restrict__ dz) {
+                                           float* __restrict__ dz, __bf16* __restrict__ dzb) {
   float4 gg[NV], xc[NV];
   float sg = 0.f, sgx = 0.f;
   const float mean = b.mean, rden = b.rden;
@@ -158,6 +162,8 @@ __device__ __forceinline__ void ln_bwd_row(const LnBwdRow<NV, ADD>& b, int64_t r
       o.x += b.a[i].x; o.y += b.a[i].y; o.z += b.a[i].z; o.w += b.a[i].w;
     }
     reinterpret_cast<float4*>(dz + row * cols)[lane + 64 * i] = o;
+    if (dzb) reinterpret_cast<ln_bf16x4*>(dzb + row * cols)[lane + 64 * i] =
+        ln_bf16x4{(__bf16)o.x, (__bf16)o.y, (__bf16)o.z, (__bf16)o.w};
   }
 }
 
@@ -171,6 +177,7 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(const float* 
                                                      int64_t rows, int cols,
                                                      const float* __restrict__ dz_add,
                                                      float* __restrict__ dz,
+                                                     __bf16* __restrict__ dzb,
                                                      float* __restrict__ ws) {
   __shared__ float red[LN_BWD_WAVES][2][256 * NV];
   const int lane = threadIdx.x & 63;
@@ -190,11 +197,11 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(const float* 
   while (row < rows) {
     const int64_t r1 = row + stride;
     if (r1 < rows) ln_bwd_fetch<NV, ADD>(b1, r1, lane, cols, dy, z, dz_add, mean_in, rden_in, std_in);
-    ln_bwd_row<NV, ADD>(b0, row, lane, cols, invN, g, dg, db, dz_add, dz);
+    ln_bwd_row<NV, ADD>(b0, row, lane, cols, invN, g, dg, db, dz_add, dz, dzb);
     if (r1 >= rows) break;
     const int64_t r2 = r1 + stride;
     if (r2 < rows) ln_bwd_fetch<NV, ADD>(b0, r2, lane, cols, dy, z, dz_add, mean_in, rden_in, std_in);
-    ln_bwd_row<NV, ADD>(b1, r1, lane, cols, invN, g, dg, db, dz_add, dz);
+    ln_bwd_row<NV, ADD>(b1, r1, lane, cols, invN, g, dg, db, dz_add, dz, dzb);
     row = r2;
   }
   // fold the 8 waves' partials: plain per-wave LDS rows, then one thread per column
@@ -255,12 +262,13 @@ extern "C" int savqa_ln_fwd(void* stream, const float* x, const float* xscale, c
                             int64_t rows,
                             int64_t cols, const float* gamma, const float* beta, float eps,
                             float* z_out, float* y, float* mean, float* rden, float* stdv,
-                            float* flag) {
+                            float* flag, void* yb) {
   if (rows <= 0) return 0;
   if (cols % 256 != 0 || cols > 256 * LN_MAXV)
     return fail(SAVQA_EUNSUP, "savqa_ln_fwd: cols must be a multiple of 256 and <= 1024");
   hipLaunchKernelGGL(ln_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream), x, xscale,
-                     r, rows, (int)cols, gamma, beta, eps, z_out, y, mean, rden, stdv, flag);
+                     r, rows, (int)cols, gamma, beta, eps, z_out, y, mean, rden, stdv, flag,
+                     static_cast<__bf16*>(yb));
   return check_launch("savqa_ln_fwd");
 }
 
@@ -271,7 +279,7 @@ extern "C" int64_t savqa_ln_bwd_workspace_bytes(int64_t cols) {
 extern "C" int savqa_ln_bwd(void* stream, const float* dy, const float* z, const float* mean,
                             const float* rden, const float* stdv, const float* gamma,
                             int64_t rows, int64_t cols, const float* dz_add, float* dz,
-                            float* dgamma, float* dbeta, float* ws, int64_t ws_bytes) {
+                            float* dgamma, float* dbeta, float* ws, int64_t ws_bytes, void* dzb) {
   if (rows <= 0) return 0;
   if (cols % 256 != 0 || cols > 256 * LN_MAXV)
     return fail(SAVQA_EUNSUP, "savqa_ln_bwd: cols must be a multiple of 256 and <= 1024");
@@ -286,10 +294,10 @@ extern "C" int savqa_ln_bwd(void* stream, const float* dy, const float* z, const
   case NV:                                                                                   \
     if (dz_add)                                                                              \
       hipLaunchKernelGGL((ln_bwd_kernel<NV, true>), g, b, 0, st, dy, z, mean, rden, stdv,    \
-                         gamma, rows, (int)cols, dz_add, dz, ws);                            \
+                         gamma, rows, (int)cols, dz_add, dz, static_cast<__bf16*>(dzb), ws);  \
     else                                                                                     \
       hipLaunchKernelGGL((ln_bwd_kernel<NV, false>), g, b, 0, st, dy, z, mean, rden, stdv,   \
-                         gamma, rows, (int)cols, dz_add, dz, ws);                            \
+                         gamma, rows, (int)cols, dz_add, dz, static_cast<__bf16*>(dzb), ws);  \
     break;
     SAVQA_LNB(1) SAVQA_LNB(2) SAVQA_LNB(3) SAVQA_LNB(4)
 #undef SAVQA_LNB

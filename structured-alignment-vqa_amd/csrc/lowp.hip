@@ -43,19 +43,29 @@ __device__ __forceinline__ float e4m3_to_f32(uint32_t c) {
   return s ? -v : v;
 }
 
+// destination row of source row r: (r / group) * stride + r % group + offset (group <= 0:
+// r) -- writes straight into the question rows of a [B][T] concat buffer
+struct RowMap {
+  int64_t group, stride, offset;
+  __device__ __forceinline__ int64_t operator()(int64_t r) const {
+    return group > 0 ? (r / group) * stride + r % group + offset : r;
+  }
+};
+
 __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ in, int64_t rows,
                                                         int64_t cols, int64_t ldi,
                                                         __bf16* __restrict__ out, int64_t ldo,
-                                                        int vec) {
+                                                        int vec, RowMap map) {
   const int64_t per_row = vec ? cols / 4 : cols;
   const int64_t n = rows * per_row;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int64_t r = i / per_row, c = i - r * per_row;
+    const int64_t ro = map(r);
     if (vec) {
       const f4v v = *reinterpret_cast<const f4v*>(in + r * ldi + 4 * c);
-      *reinterpret_cast<bf16x4*>(out + r * ldo + 4 * c) = __builtin_convertvector(v, bf16x4);
+      *reinterpret_cast<bf16x4*>(out + ro * ldo + 4 * c) = __builtin_convertvector(v, bf16x4);
     } else {
-      out[r * ldo + c] = (__bf16)in[r * ldi + c];
+      out[ro * ldo + c] = (__bf16)in[r * ldi + c];
     }
   }
 }
@@ -64,7 +74,8 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict_
 __global__ __launch_bounds__(256) void quant_fp8_kernel(const float* __restrict__ in, int64_t rows,
                                                         int64_t cols, int64_t ldi,
                                                         uint8_t* __restrict__ q, int64_t ldq,
-                                                        uint8_t* __restrict__ scale, int64_t lds) {
+                                                        uint8_t* __restrict__ scale, int64_t lds,
+                                                        RowMap map) {
   const int64_t nb = cols / 32;
   const int64_t total = rows * nb;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -96,10 +107,11 @@ __global__ __launch_bounds__(256) void quant_fp8_kernel(const float* __restrict_
       w[k] = f32_to_e4m3(v[4 * k] * inv) | (f32_to_e4m3(v[4 * k + 1] * inv) << 8) |
              (f32_to_e4m3(v[4 * k + 2] * inv) << 16) | (f32_to_e4m3(v[4 * k + 3] * inv) << 24);
     }
-    uint4* dst = reinterpret_cast<uint4*>(q + r * ldq + b * 32);
+    const int64_t ro = map(r);
+    uint4* dst = reinterpret_cast<uint4*>(q + ro * ldq + b * 32);
     dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
     dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    scale[r * lds + b] = (uint8_t)(e + 127);
+    scale[ro * lds + b] = (uint8_t)(e + 127);
   }
 }
 
@@ -150,23 +162,26 @@ static unsigned grid_for(int64_t n) {
 using namespace savqa;
 
 extern "C" int savqa_cast_bf16(void* stream, const float* in, int64_t rows, int64_t cols, int64_t ldi,
-                               void* out, int64_t ldo) {
+                               void* out, int64_t ldo, int64_t group, int64_t stride,
+                               int64_t offset) {
   if (rows <= 0 || cols <= 0) return 0;
   const int vec = (cols % 4 == 0) && (ldi % 4 == 0) && (ldo % 4 == 0) &&
                   (((uintptr_t)in) & 15) == 0 && (((uintptr_t)out) & 7) == 0;
   const int64_t n = rows * (vec ? cols / 4 : cols);
   hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), in, rows,
-                     cols, ldi, static_cast<__bf16*>(out), ldo, vec);
+                     cols, ldi, static_cast<__bf16*>(out), ldo, vec, RowMap{group, stride, offset});
   return check_launch("savqa_cast_bf16");
 }
 
 extern "C" int savqa_quant_fp8(void* stream, const float* in, int64_t rows, int64_t cols, int64_t ldi,
-                               void* q, int64_t ldq, uint8_t* scale, int64_t lds) {
+                               void* q, int64_t ldq, uint8_t* scale, int64_t lds, int64_t group,
+                               int64_t stride, int64_t offset) {
   if (rows <= 0 || cols <= 0) return 0;
   if (cols % 32 || ldi % 4 || ldq % 16 || (((uintptr_t)in) & 15) || (((uintptr_t)q) & 15))
     return fail(SAVQA_EINVAL, "savqa_quant_fp8: cols % 32, 16-B aligned rows required");
   hipLaunchKernelGGL(quant_fp8_kernel, dim3(grid_for(rows * (cols / 32))), dim3(256), 0,
-                     as_stream(stream), in, rows, cols, ldi, static_cast<uint8_t*>(q), ldq, scale, lds);
+                     as_stream(stream), in, rows, cols, ldi, static_cast<uint8_t*>(q), ldq, scale, lds,
+                     RowMap{group, stride, offset});
   return check_launch("savqa_quant_fp8");
 }
 

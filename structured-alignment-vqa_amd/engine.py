@@ -38,6 +38,10 @@ def _empty(*shape, dev):
     return torch.empty(*shape, dtype=F32, device=dev)
 
 
+def _bf(*shape, dev):
+    return torch.empty(*shape, dtype=torch.bfloat16, device=dev)
+
+
 def _rows_index(B: int, T: int, start: int, count: int, dev) -> torch.Tensor:
     """int64 row ids b*T + start + t for t < count (gather index into a [B,T,...] buffer)."""
     return (torch.arange(B, device=dev, dtype=torch.int64).unsqueeze(1) * T
@@ -45,12 +49,19 @@ def _rows_index(B: int, T: int, start: int, count: int, dev) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------- weights
+def _views(arena, grad=False, buf=None):
+    """(view, span) accessors over the parameters, their gradients, or a shadow buffer laid
+    out like the arena (the bf16 weight copies of the low-precision modes)."""
+    if buf is not None:
+        return (lambda n: arena.view(n, buf)), (lambda a, b, shape: arena.span(a, b, shape, buf))
+    return (arena.gview, arena.gspan) if grad else (arena.view, arena.span)
+
+
 class StackWeights:
     """Views of one stack's parameters (and of its gradients) in the arena."""
 
-    def __init__(self, arena, pre: str, num_blocks: int, d: int, grad: bool = False):
-        v = arena.gview if grad else arena.view
-        sp = arena.gspan if grad else arena.span
+    def __init__(self, arena, pre: str, num_blocks: int, d: int, grad: bool = False, buf=None):
+        v, sp = _views(arena, grad, buf)
         self.E = v(f"{pre}.syb_emb.weight")
         self.Wq, self.bq = v(f"{pre}.syb_mlp.0.weight"), v(f"{pre}.syb_mlp.0.bias")
         self.Win, self.bin = v(f"{pre}.syb_mlp2.weight"), v(f"{pre}.syb_mlp2.bias")
@@ -86,16 +97,16 @@ class StackWeights:
 
 
 class MilWeights:
-    def __init__(self, arena, grad=False):
-        v = arena.gview if grad else arena.view
+    def __init__(self, arena, grad=False, buf=None):
+        v, _ = _views(arena, grad, buf)
         m = "MIL_NCE"
         live = f"{m}.R" in arena.live_names
-        self.R = v(f"{m}.R") if (live or not grad) else None  # relation branch only
+        self.R = v(f"{m}.R") if (live or (not grad and buf is None)) else None  # relations only
         self.E = v(f"{m}.syb_emb.weight")
         self.Ws, self.bs = v(f"{m}.syb_mlp.0.weight"), v(f"{m}.syb_mlp.0.bias")
         self.Wv, self.bv = v(f"{m}.vis_mlp.0.weight"), v(f"{m}.vis_mlp.0.bias")
         self.Wipt, self.bipt = v(f"{m}.ipt_mlp.0.weight"), v(f"{m}.ipt_mlp.0.bias")
-        if not grad:
+        if not grad and buf is None:
             self.Wm, self.bm = v(f"{m}.marco_mlp.0.weight"), v(f"{m}.marco_mlp.0.bias")
 
 
@@ -127,6 +138,8 @@ class StackSaved:
     out: torch.Tensor = None
     drop: Optional[tuple] = None
     sites: tuple = (-1, 4, 5)
+    lp: object = None
+    x6b: torch.Tensor = None
 
 
 # dropout sites (site ids of the library's counter-hash masks, include/savqa.h)
@@ -141,22 +154,49 @@ def _ln_stats(rows, dev):
 
 def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
                   q_ipt: torch.Tensor, node_mask, q_mask, q_graph, node_graph, decMask: bool,
-                  H: int, d: int, drop=None, sites=SYB_SITES) -> StackSaved:
+                  H: int, d: int, drop=None, sites=SYB_SITES, lp=None) -> StackSaved:
     """AttModel_vis_grid.forward (:91-156) / AttModel_syb.forward (:214-282).
 
     `cat` is the [B*T, 2048] input buffer whose node rows [0, Nn) of every sample
     are already filled by the caller; the question rows are produced here.
-    drop = (seed, p) applies the stack's nn.Dropout sites (training, p > 0)."""
+    drop = (seed, p) applies the stack's nn.Dropout sites (training, p > 0).
+    lp (StackLp, the bf16 / fp8 modes): `cat` holds bf16 (or fp8 with lp.cat_scale) rows, the
+    big GEMMs read bf16-resident operands (lp.W: the bf16 weight shadow) and every operand
+    they consume is emitted in bf16 by its producer (LN / GEMM epilogues); the residual
+    stream, LN statistics, attention output and the decoder stay fp32."""
     dev = cat.device
     T = Nn + Lq
     M = B * T
     s = StackSaved(B=B, Nn=Nn, Lq=Lq, T=T, cat=cat, drop=drop, sites=sites)
     s.q_flat = q_ipt.reshape(-1)
-    # question tokens: relu(syb_emb[q] W^T + b) straight into rows [Nn, T) of cat
-    ops.linear(W.E, W.Wq, W.bq, cat, relu=True, rows=B * Lq, a_rows=s.q_flat, c_group=Lq,
-               c_stride=T, c_offset=Nn, ldo=cat.shape[1])
+    s.lp = lp
+    if lp is None:
+        # question tokens: relu(syb_emb[q] W^T + b) straight into rows [Nn, T) of cat
+        ops.linear(W.E, W.Wq, W.bq, cat, relu=True, rows=B * Lq, a_rows=s.q_flat, c_group=Lq,
+                   c_stride=T, c_offset=Nn, ldo=cat.shape[1])
+    else:
+        # the 300-d GloVe projection stays on the fp32 kernel; its rows are then rounded into
+        # the low-precision concat buffer (bf16, or fp8 + block scales)
+        qrows = _empty(B * Lq, W.Wq.shape[0], dev=dev)
+        ops.linear(W.E, W.Wq, W.bq, qrows, relu=True, a_rows=s.q_flat)
+        Dv = cat.shape[1]
+        if lp.cat_scale is not None:
+            ops.quant_fp8(qrows, B * Lq, Dv, Dv, cat, Dv, lp.cat_scale, Dv // 32, Lq, T, Nn)
+        else:
+            ops.cast_bf16(qrows, B * Lq, Dv, Dv, cat, Dv, Lq, T, Nn)
+        del qrows
     s.x0 = _empty(M, d, dev=dev)
-    if drop is None:
+    xb = _bf(M, d, dev=dev) if lp is not None else None
+    if lp is not None:
+        Win = lp.Win8 if lp.cat_scale is not None else lp.W.Win
+        if drop is None:
+            ops.linear_lp(cat, Win, W.bin, s.x0, xb, rowvec=W.pos, rowvec_period=T,
+                          x_scale=lp.cat_scale, w_scale=lp.Win8_scale)
+        else:
+            ops.linear_lp(cat, Win, W.bin, s.x0, x_scale=lp.cat_scale, w_scale=lp.Win8_scale)
+            ops.posadd_dropout(s.x0, W.pos, B, T, d, drop, sites[0], sites[1], s.x0)
+            ops.cast_bf16(s.x0, M, d, d, xb, d)
+    elif drop is None:
         ops.linear(cat, W.Win, W.bin, s.x0, rowvec=W.pos, rowvec_period=T)
     else:
         ops.linear(cat, W.Win, W.bin, s.x0)
@@ -171,35 +211,53 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
     for i, L in enumerate(W.enc):
         G = s.gdiag if i < 2 else s.graph
         e = dict(x=x, flag=flag)
-        qkv = _empty(M, 3 * d, dev=dev)
-        ops.linear(x, L["Wqkv"], L["bqkv"], qkv, relu=True)
         o = _empty(M, d, dev=dev)
-        if ops.use_flash(T, T):  # key-tiled path: keeps the per-row statistics
-            ast = _empty(B * H * T * 4, dev=dev)
-            ops.gattn_fwd_flash(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag, flag,
-                                B, T, T, H, o, d, ast)
-            e.update(ast=ast)
-        else:
+        if lp is not None:
+            Lb = lp.W.enc[i]
+            qkv = _bf(M, 3 * d, dev=dev)
+            ops.linear_lp(xb, Lb["Wqkv"], L["bqkv"], None, qkv, relu=True)
             ops.gattn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag, flag, B,
                           T, T, H, o, d)
+        else:
+            qkv = _empty(M, 3 * d, dev=dev)
+            ops.linear(x, L["Wqkv"], L["bqkv"], qkv, relu=True)
+            if ops.use_flash(T, T):  # key-tiled path: keeps the per-row statistics
+                ast = _empty(B * H * T * 4, dev=dev)
+                ops.gattn_fwd_flash(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag,
+                                    flag, B, T, T, H, o, d, ast)
+                e.update(ast=ast)
+            else:
+                ops.gattn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag, flag,
+                              B, T, T, H, o, d)
         z1, y1 = _empty(M, d, dev=dev), _empty(M, d, dev=dev)
+        y1b = _bf(M, d, dev=dev) if lp is not None else None
         st1 = _ln_stats(M, dev)
-        ops.ln_fwd(o, L["g1"], L["b1"], y1, *st1, r=x, z_out=z1)
-        h = _empty(M, 4 * d, dev=dev)
-        ops.linear(y1, L["W1"], L["c1"], h, relu=True)
+        ops.ln_fwd(o, L["g1"], L["b1"], y1, *st1, r=x, z_out=z1, yb=y1b)
         z2 = _empty(M, d, dev=dev)
-        ops.linear(h, L["W2"], L["c2"], z2, resid=y1)
+        if lp is not None:
+            h = _bf(M, 4 * d, dev=dev)
+            ops.linear_lp(y1b, Lb["W1"], L["c1"], None, h, relu=True)
+            ops.linear_lp(h, Lb["W2"], L["c2"], z2, resid=y1)
+        else:
+            h = _empty(M, 4 * d, dev=dev)
+            ops.linear(y1, L["W1"], L["c1"], h, relu=True)
+            ops.linear(h, L["W2"], L["c2"], z2, resid=y1)
         xn = _empty(M, d, dev=dev)
+        xnb = _bf(M, d, dev=dev) if lp is not None else None
         st2 = _ln_stats(M, dev)
         fn = _empty(M, dev=dev)
-        ops.ln_fwd(z2, L["g2"], L["b2"], xn, *st2, flag=fn)
-        e.update(qkv=qkv, z1=z1, st1=st1, y1=y1, h=h, z2=z2, st2=st2)
+        ops.ln_fwd(z2, L["g2"], L["b2"], xn, *st2, flag=fn, yb=xnb)
+        e.update(qkv=qkv, z1=z1, st1=st1, y1=y1, y1b=y1b, h=h, z2=z2, st2=st2, xb=xb)
         s.enc.append(e)
-        x, flag = xn, fn
-    s.x6, s.f6 = x, flag
+        x, flag, xb = xn, fn, xnb
+    s.x6, s.f6, s.x6b = x, flag, xb
     nb = len(W.dec)
-    s.kv = _empty(M, 2 * nb * d, dev=dev)
-    ops.linear(x, W.Wkv, W.bkv, s.kv, relu=True)
+    if lp is not None:
+        s.kv = _bf(M, 2 * nb * d, dev=dev)
+        ops.linear_lp(xb, lp.W.Wkv, W.bkv, None, s.kv, relu=True)
+    else:
+        s.kv = _empty(M, 2 * nb * d, dev=dev)
+        ops.linear(x, W.Wkv, W.bkv, s.kv, relu=True)
     dec = _empty(B, d, dev=dev)
     ops.dec_init(W.dec_emb, 2, math.sqrt(d), W.dec_pos, B, d, dec, drop=drop, site=sites[2])
     fdec = _empty(B, dev=dev)
@@ -216,7 +274,7 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
         ops.linear(d1, L["Wqc"], L["bqc"], qc, relu=True)
         oc = _empty(B, d, dev=dev)
         kvi = s.kv[:, 2 * i * d:]
-        if ops.use_flash(1, T):
+        if lp is None and ops.use_flash(1, T):
             ast = _empty(B * H * 4, dev=dev)
             ops.gattn_fwd_flash(qc, d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6, f1, B,
                                 1, T, H, oc, d, ast)
@@ -248,7 +306,8 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
     """Backward of stack_forward; accumulates parameter grads into G (arena views).
 
     Returns d(pre-activation of the node rows of cat) [B*Nn, 2048] when want_node_grad
-    (the syb stack feeds it to the MIL-NCE backward), else None.
+    (the syb stack feeds it to the MIL-NCE backward), else None; in the low-precision modes
+    a (fp32, bf16) pair.
     mark(name) declares every arena gradient before parameter `name` final (the arena is
     in backward-completion order), so the all-reduce streams out layer by layer."""
     mark = mark or (lambda name: None)
@@ -256,8 +315,9 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
     B, T, Nn, Lq = s.B, s.T, s.Nn, s.Lq
     M = B * T
     nb = len(W.dec)
+    lp = s.lp
     ddec = dout
-    dkv = _empty(M, 2 * nb * d, dev=dev)
+    dkv = (_bf if lp is not None else _empty)(M, 2 * nb * d, dev=dev)
     for i in reversed(range(nb)):
         L, Lg, e = W.dec[i], G.dec[i], s.dec[i]
         # feed-forward
@@ -298,27 +358,42 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
     ops.dec_init_bwd(ddec, B, d, 2, math.sqrt(d), G.dec_emb, G.dec_pos, drop=s.drop,
                      site=s.sites[2])
     # all decoder K/V projections at once
-    ops.linear_dw(dkv, s.x6, G.Wkv, G.bkv, rows=M)
     dx = _empty(M, d, dev=dev)
-    ops.linear_dx(dkv, W.Wkv, dx, rows=M)
+    if lp is not None:
+        ops.linear_dw_lp(dkv, s.x6b, G.Wkv, G.bkv, rows=M)
+        ops.linear_dx_lp(dkv, lp.W.Wkv, dx, rows=M)
+    else:
+        ops.linear_dw(dkv, s.x6, G.Wkv, G.bkv, rows=M)
+        ops.linear_dx(dkv, W.Wkv, dx, rows=M)
     del dkv
     mark(f"enc_feed_forward_{len(W.enc) - 1}.normalization.gamma")
     for i in reversed(range(len(W.enc))):
         L, Lg, e = W.enc[i], G.enc[i], s.enc[i]
         Gm = s.gdiag if i < 2 else s.graph
         dz2 = _empty(M, d, dev=dev)
-        ops.ln_bwd(dx, e["z2"], *e["st2"], L["g2"], dz2, Lg["g2"], Lg["b2"])
-        ops.linear_dw(dz2, e["h"], Lg["W2"], Lg["c2"], rows=M)
-        dh = _empty(M, 4 * d, dev=dev)
-        ops.linear_dx(dz2, L["W2"], dh, rows=M, mask=e["h"], ldmask=4 * d)
-        ops.linear_dw(dh, e["y1"], Lg["W1"], Lg["c1"], rows=M)
         dy1 = _empty(M, d, dev=dev)
-        ops.linear_dx(dh, L["W1"], dy1, rows=M, resid=dz2)
+        if lp is not None:
+            Lb = lp.W.enc[i]
+            dz2b = _bf(M, d, dev=dev)
+            ops.ln_bwd(dx, e["z2"], *e["st2"], L["g2"], dz2, Lg["g2"], Lg["b2"], dzb=dz2b)
+            ops.linear_dw_lp(dz2b, e["h"], Lg["W2"], Lg["c2"], rows=M, dy32=dz2)
+            dh = _bf(M, 4 * d, dev=dev)
+            ops.linear_dx_lp(dz2b, Lb["W2"], None, dh, rows=M, mask=e["h"], ldmask=4 * d)
+            del dz2b
+            ops.linear_dw_lp(dh, e["y1b"], Lg["W1"], Lg["c1"], rows=M)
+            ops.linear_dx_lp(dh, Lb["W1"], dy1, rows=M, resid=dz2)
+        else:
+            ops.ln_bwd(dx, e["z2"], *e["st2"], L["g2"], dz2, Lg["g2"], Lg["b2"])
+            ops.linear_dw(dz2, e["h"], Lg["W2"], Lg["c2"], rows=M)
+            dh = _empty(M, 4 * d, dev=dev)
+            ops.linear_dx(dz2, L["W2"], dh, rows=M, mask=e["h"], ldmask=4 * d)
+            ops.linear_dw(dh, e["y1"], Lg["W1"], Lg["c1"], rows=M)
+            ops.linear_dx(dh, L["W1"], dy1, rows=M, resid=dz2)
         del dh
         dz1 = _empty(M, d, dev=dev)
         ops.ln_bwd(dy1, e["z1"], *e["st1"], L["g1"], dz1, Lg["g1"], Lg["b1"])
-        dqkv = _empty(M, 3 * d, dev=dev)
         qkv = e["qkv"]
+        dqkv = (_bf if lp is not None else _empty)(M, 3 * d, dev=dev)
         if "ast" in e:
             ops.gattn_bwd_flash(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, Gm, e["flag"],
                                 e["flag"], B, T, T, H, dz1, d, e["ast"], dqkv, 3 * d,
@@ -327,9 +402,13 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
             ops.gattn_bwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, Gm, e["flag"],
                           e["flag"], B, T, T, H, dz1, d, dqkv, 3 * d, dqkv[:, d:], 3 * d,
                           dqkv[:, 2 * d:], 3 * d)
-        ops.linear_dw(dqkv, e["x"], Lg["Wqkv"], Lg["bqkv"], rows=M)
         dxn = _empty(M, d, dev=dev)
-        ops.linear_dx(dqkv, L["Wqkv"], dxn, rows=M, resid=dz1)
+        if lp is not None:
+            ops.linear_dw_lp(dqkv, e["xb"], Lg["Wqkv"], Lg["bqkv"], rows=M)
+            ops.linear_dx_lp(dqkv, Lb["Wqkv"], dxn, rows=M, resid=dz1)
+        else:
+            ops.linear_dw(dqkv, e["x"], Lg["Wqkv"], Lg["bqkv"], rows=M)
+            ops.linear_dx(dqkv, L["Wqkv"], dxn, rows=M, resid=dz1)
         dx = dxn
         if i > 0:
             mark(f"enc_feed_forward_{i - 1}.normalization.gamma")
@@ -338,18 +417,36 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         ops.period_sum_acc(dx, B, T, d, d, G.pos)
     else:  # dx <- enc_dropout'(dx); dpos += sum_b pos_dropout'(dx)
         ops.posadd_dropout_bwd(dx, B, T, d, s.drop, s.sites[0], s.sites[1], dx, G.pos)
-    ops.linear_dw(dx, s.cat, G.Win, G.bin, rows=M)
     qrows = _rows_index(B, T, Nn, Lq, dev)
-    dq = _empty(B * Lq, W.Win.shape[1], dev=dev)
-    ops.linear_dx(dx, W.Win, dq, rows=B * Lq, a_rows=qrows, mask=s.cat, ldmask=s.cat.shape[1],
-                  mask_arows=True)
+    nrows = _rows_index(B, T, 0, Nn, dev)
+    D2 = W.Win.shape[1]
+    if lp is not None:
+        dxb = _bf(M, d, dev=dev)
+        ops.cast_bf16(dx, M, d, d, dxb, d)
+        catb = s.cat
+        if lp.cat_scale is not None:  # fp8 concat buffer: a bf16 copy for the weight gradient
+            catb = _bf(M, D2, dev=dev)
+            ops.dequant_fp8_bf16(s.cat, M, D2, D2, lp.cat_scale, D2 // 32, catb, D2)
+        ops.linear_dw_lp(dxb, catb, G.Win, G.bin, rows=M, dy32=dx)
+        dq = _empty(B * Lq, D2, dev=dev)
+        ops.linear_dx_lp(dxb, lp.W.Win, dq, rows=B * Lq, a_rows=qrows, mask=catb, ldmask=D2,
+                         mask_arows=True)
+    else:
+        ops.linear_dw(dx, s.cat, G.Win, G.bin, rows=M)
+        dq = _empty(B * Lq, D2, dev=dev)
+        ops.linear_dx(dx, W.Win, dq, rows=B * Lq, a_rows=qrows, mask=s.cat, ldmask=s.cat.shape[1],
+                      mask_arows=True)
     ops.linear_dw(dq, W.E, G.Wq, G.bq, rows=B * Lq, x_rows=s.q_flat)
     ops.linear_dx(dq, W.Wq, G.E, rows=B * Lq, c_rows=s.q_flat, atomic=True)
     del dq
     if not want_node_grad:
         return None
-    nrows = _rows_index(B, T, 0, Nn, dev)
-    dnode = _empty(B * Nn, W.Win.shape[1], dev=dev)
+    dnode = _empty(B * Nn, D2, dev=dev)
+    if lp is not None:
+        dnodeb = _bf(B * Nn, D2, dev=dev)
+        ops.linear_dx_lp(dxb, lp.W.Win, dnode, dnodeb, rows=B * Nn, a_rows=nrows, mask=catb,
+                         ldmask=D2, mask_arows=True)
+        return dnode, dnodeb
     ops.linear_dx(dx, W.Win, dnode, rows=B * Nn, a_rows=nrows, mask=s.cat, ldmask=s.cat.shape[1],
                   mask_arows=True)
     return dnode
@@ -373,14 +470,18 @@ class MilSaved:
     macro: torch.Tensor = None
     obj: torch.Tensor = None
     rel: Optional[dict] = None
+    lp: object = None
+    macrob: torch.Tensor = None
 
 
 def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb, T_syb: int,
                 mil_out: torch.Tensor, eps: float = 1e-6, rel=None,
-                mil_rel_out: Optional[torch.Tensor] = None) -> MilSaved:
+                mil_rel_out: Optional[torch.Tensor] = None, lp=None) -> MilSaved:
     """MIL_NCE.forward (AttModel_x3.py:352-441): the only_obj branch, plus the relation
     branch (:382-437) when rel = (pos_rel [B,Lp], pos_loc [B,Lp,5], neg_loc [B,Ln,4]).
-    Writes relu(new_macro W_ipt^T + b) into the node rows of the syb stack's cat buffer."""
+    Writes relu(new_macro W_ipt^T + b) into the node rows of the syb stack's cat buffer
+    (bf16 in the low-precision modes: lp = MilLp, whose vis_mlp GEMM reads the bf16 -- or
+    fp8 + block-scale -- region features)."""
     dev = vis_fea.device
     B, Nv, Dv = vis_fea.shape
     Ns = macro_ipt.shape[1]
@@ -393,7 +494,12 @@ def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb
     ops.linear(W.E, W.Ws, W.bs, s.Pf, relu=True, a_rows=s.pos)
     ops.linear(W.E, W.Ws, W.bs, s.Nf, relu=True, a_rows=s.neg)
     s.vv = _empty(B * Nv, Hm, dev=dev)
-    ops.linear(s.vis, W.Wv, W.bv, s.vv, relu=True)
+    s.lp = lp
+    if lp is not None:
+        ops.linear_lp(lp.vis, lp.Wv, W.bv, s.vv, relu=True, x_scale=lp.vis_scale,
+                      w_scale=lp.Wv_scale)
+    else:
+        ops.linear(s.vis, W.Wv, W.bv, s.vv, relu=True)
     s.macro = _empty(B * Ns, Hm, dev=dev)
     ops.linear(W.E, W.Wm, W.bm, s.macro, relu=True, a_rows=macro_ipt.reshape(-1))
     obj = _empty(B * Nv, Hm, dev=dev)
@@ -403,8 +509,14 @@ def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb
     s.obj = obj
     if rel is not None:
         s.rel = _rel_forward(W, s, rel, Ns, Hm, eps, mil_rel_out)
-    ops.linear(s.macro, W.Wipt, W.bipt, cat_syb, relu=True, rows=B * Ns, c_group=Ns,
-               c_stride=T_syb, c_offset=0, ldo=cat_syb.shape[1])
+    if lp is not None:
+        s.macrob = _bf(B * Ns, Hm, dev=dev)
+        ops.cast_bf16(s.macro, B * Ns, Hm, Hm, s.macrob, Hm)
+        ops.linear_lp(s.macrob, lp.Wipt, W.bipt, None, cat_syb, relu=True, rows=B * Ns,
+                      c_group=Ns, c_stride=T_syb, c_offset=0, ldo=cat_syb.shape[1])
+    else:
+        ops.linear(s.macro, W.Wipt, W.bipt, cat_syb, relu=True, rows=B * Ns, c_group=Ns,
+                   c_stride=T_syb, c_offset=0, ldo=cat_syb.shape[1])
     return s
 
 
@@ -440,11 +552,18 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
     B, Nv, Ns, K = s.B, s.Nv, s.Ns, s.K
     Hm = W.Ws.shape[0]
     rel = s.rel
+    lp = s.lp
     dobj = None
     if dnode is not None:
-        ops.linear_dw(dnode, s.macro, G.Wipt, G.bipt, rows=B * Ns)
         dmacro = _empty(B * Ns, Hm, dev=dev)
-        ops.linear_dx(dnode, W.Wipt, dmacro, rows=B * Ns)
+        if lp is not None:  # (fp32, bf16) node gradient from the low-precision stack
+            dnode, dnodeb = dnode
+            ops.linear_dw_lp(dnodeb, s.macrob, G.Wipt, G.bipt, rows=B * Ns, dy32=dnode)
+            ops.linear_dx_lp(dnodeb, lp.Wipt, dmacro, rows=B * Ns)
+            del dnodeb
+        else:
+            ops.linear_dw(dnode, s.macro, G.Wipt, G.bipt, rows=B * Ns)
+            ops.linear_dx(dnode, W.Wipt, dmacro, rows=B * Ns)
         if rel is not None:  # relation rows: grads to the softmax weights and rel features,
             Lp = rel["Lp"]    # and the overwritten previous contents get none
             rel["dwsm"] = torch.zeros(max(B * Lp, 1), device=dev)
@@ -486,7 +605,12 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
     ops.linear_dw(dNf, W.E, G.Ws, G.bs, rows=n, x_rows=s.neg)
     ops.linear_dx(dPf, W.Ws, G.E, rows=n, c_rows=s.pos, atomic=True)
     ops.linear_dx(dNf, W.Ws, G.E, rows=n, c_rows=s.neg, atomic=True)
-    ops.linear_dw(dvv, s.vis, G.Wv, G.bv, rows=B * Nv)
+    if lp is not None:
+        dvvb = _bf(B * Nv, Hm, dev=dev)
+        ops.cast_bf16(dvv, B * Nv, Hm, Hm, dvvb, Hm)
+        ops.linear_dw_lp(dvvb, lp.vis_bf16(), G.Wv, G.bv, rows=B * Nv, dy32=dvv)
+    else:
+        ops.linear_dw(dvv, s.vis, G.Wv, G.bv, rows=B * Nv)
 
 
 # ----------------------------------------------------------------------------- heads
@@ -538,15 +662,109 @@ def heads_backward(Wh: HeadWeights, Gh: HeadWeights, saved, dlc, dlv, dls, d: in
     return df_vis, df_syb
 
 
+# ----------------------------------------------------------------------------- precision
+LP_MODES = ("bf16", "fp8")
+PRECISIONS = ("fp32", "bf16x3") + LP_MODES
+
+
+@dataclass
+class StackLp:
+    """Low-precision operands of one stack: bf16 weight-shadow views, and in fp8 mode the
+    e4m3 input-projection weights + scales that meet the fp8 concat rows (cat_scale)."""
+    W: StackWeights
+    cat_scale: Optional[torch.Tensor] = None
+    Win8: Optional[torch.Tensor] = None
+    Win8_scale: Optional[torch.Tensor] = None
+
+
+@dataclass
+class MilLp:
+    vis: torch.Tensor               # [B*Nv, 2048] bf16, or fp8 (uint8 view) with vis_scale
+    Wv: torch.Tensor
+    Wipt: torch.Tensor
+    vis_scale: Optional[torch.Tensor] = None
+    Wv_scale: Optional[torch.Tensor] = None
+    _vis16: Optional[torch.Tensor] = None
+
+    def vis_bf16(self):
+        """bf16 region features for the vis_mlp weight gradient (fp8 mode: expanded once)."""
+        if self.vis_scale is None:
+            return self.vis
+        if self._vis16 is None:
+            R, D = self.vis.shape
+            self._vis16 = _bf(R, D, dev=self.vis.device)
+            ops.dequant_fp8_bf16(self.vis, R, D, D, self.vis_scale, D // 32, self._vis16, D)
+        return self._vis16
+
+
+class LpShadow:
+    """Low-precision copies of the GEMM weights (BASELINE cfg 3 / cfg 5): a bf16 image of the
+    live parameter range (laid out like the arena, so StackWeights views bind to it; the
+    three GloVe tables are skipped -- their GEMMs stay fp32) and, in fp8 mode, e4m3 + e8m0
+    copies of the two weights that meet the fp8 region features (the visual stack's
+    syb_mlp2, MIL_NCE.vis_mlp). Refreshed lazily when the arena's state key changes (an
+    optimizer step or any in-place edit of the parameters)."""
+
+    def __init__(self, arena, fp8: bool):
+        self.arena, self.fp8 = arena, fp8
+        self.buf, self.key = None, None
+        self.q8 = {}
+
+    def refresh(self):
+        a = self.arena
+        key = a.state_key()
+        if key == self.key:
+            return
+        if self.buf is None or self.buf.device != a.flat.device:
+            self.buf = torch.empty(a.n_live, dtype=torch.bfloat16, device=a.flat.device)
+        lo = 0
+        for t0, t1 in a.table_ranges() + [(a.n_live, a.n_live)]:
+            if t0 > lo:
+                ops.cast_bf16(a.flat[lo:t0], 1, t0 - lo, t0 - lo, self.buf[lo:t0], t0 - lo)
+            lo = max(lo, t1)
+        if self.fp8:
+            for name in ("att_vis_grid.syb_mlp2.weight", "MIL_NCE.vis_mlp.0.weight"):
+                w = a.view(name)
+                N, K = w.shape
+                if name not in self.q8:
+                    self.q8[name] = (torch.empty(N, K, dtype=torch.uint8, device=w.device),
+                                     torch.empty(N, K // 32, dtype=torch.uint8, device=w.device))
+                q, sc = self.q8[name]
+                ops.quant_fp8(w, N, K, K, q, K, sc, K // 32)
+        self.key = key
+
+    def fp8_weight(self, name):
+        q, sc = self.q8[name]
+        return q.view(torch.float8_e4m3fn), sc
+
+
 # ----------------------------------------------------------------------------- model
 class ModelEngine:
-    """Binds arena views once; runs the whole-model forward / backward."""
+    """Binds arena views once; runs the whole-model forward / backward.
+
+    gemm_precision: "fp32" (exact fp32 MFMA everywhere, the north-star tolerance), "bf16x3"
+    (fp32 storage, three bf16 MFMAs per product), "bf16" (BASELINE cfg 3: bf16-resident GEMM
+    operands and bf16 attention storage, fp32 accumulation / residual stream / LN / softmax
+    / loss / Adam), "fp8" (BASELINE cfg 5: "bf16" plus fp8-e4m3 region features, block-scaled,
+    consumed by fp8 MFMA in the visual stack's input projection and MIL_NCE.vis_mlp)."""
 
     def __init__(self, arena, num_blocks: int, hidden: int, heads: int, gemm_precision="fp32"):
+        if gemm_precision not in PRECISIONS:
+            raise ValueError(f"gemm_precision must be one of {PRECISIONS}")
         self.arena = arena
-        self.gemm_precision = gemm_precision  # products of the 128x128 GEMMs (ops.PREC)
+        self.gemm_precision = gemm_precision
         self.nb, self.d, self.H = num_blocks, hidden, heads
+        self._shadow = None
         self.rebind()
+
+    @property
+    def lp_mode(self):
+        return self.gemm_precision in LP_MODES
+
+    def _fp32_kernel_precision(self):
+        """Product precision of the fp32-storage GEMMs (ops.PREC): bf16x3 in that mode,
+        exact fp32 otherwise (incl. the GEMMs the low-precision modes keep in fp32)."""
+        return "bf16x3" if self.gemm_precision == "bf16x3" else "fp32"
 
     def rebind(self):
         a = self.arena
@@ -555,6 +773,7 @@ class ModelEngine:
         self.mil = MilWeights(a)
         self.head = HeadWeights(a)
         self._gbound = None
+        self._shadow = None
 
     def grads(self):
         g = self.arena.ensure_grads()
@@ -565,6 +784,21 @@ class ModelEngine:
             self.gmil = MilWeights(a, grad=True)
             self.ghead = HeadWeights(a, grad=True)
             self._gbound = g
+
+    def lp_weights(self):
+        """(vis StackWeights, syb StackWeights, MilWeights) over the refreshed bf16 shadow."""
+        fp8 = self.gemm_precision == "fp8"
+        if self._shadow is None or self._shadow.fp8 != fp8:
+            self._shadow = LpShadow(self.arena, fp8)
+            self._lpw = None
+        sh = self._shadow
+        sh.refresh()
+        if self._lpw is None or self._lpw[0] is not sh.buf:
+            a = self.arena
+            self._lpw = (sh.buf, StackWeights(a, "att_vis_grid", self.nb, self.d, buf=sh.buf),
+                         StackWeights(a, "att_syb", self.nb, self.d, buf=sh.buf),
+                         MilWeights(a, buf=sh.buf))
+        return self._lpw[1:]
 
     concurrent = True  # False: run both stacks on the caller's stream (serial profiling)
     # backward schedule of the two stacks: "concurrent" = both from the start;
@@ -609,8 +843,44 @@ class ModelEngine:
         return self._side
 
     def forward(self, inp: Dict[str, torch.Tensor], decMask: bool, drop=None):
-        with ops.gemm_precision(self.gemm_precision):
+        with ops.gemm_precision(self._fp32_kernel_precision()):
             return self._forward(inp, decMask, drop)
+
+    def _lp_inputs(self, vis, vis_scale, B, Nv, Dv, Tv, Ts):
+        """Low-precision region features and concat buffers (main stream, before the fork):
+        bf16 mode casts the fp32 features once; fp8 mode takes e4m3 features + e8m0 block
+        scales (vis_scale [B, Nv, Dv/32]) or quantises fp32 ones."""
+        dev = vis.device
+        R = B * Nv
+        if self.gemm_precision == "fp8":
+            if vis.dtype == torch.float8_e4m3fn:
+                if vis_scale is None:
+                    raise ValueError("fp8 region features need vis_fea_scale (e8m0 block scales)")
+                v8 = vis.reshape(R, Dv).view(torch.uint8)
+                vs = vis_scale.reshape(R, Dv // 32)
+            else:
+                v8 = torch.empty(R, Dv, dtype=torch.uint8, device=dev)
+                vs = torch.empty(R, Dv // 32, dtype=torch.uint8, device=dev)
+                ops.quant_fp8(vis.reshape(R, Dv), R, Dv, Dv, v8, Dv, vs, Dv // 32)
+            cat_vis = torch.empty(B * Tv, Dv, dtype=torch.uint8, device=dev)
+            cat_scale = torch.empty(B * Tv, Dv // 32, dtype=torch.uint8, device=dev)
+            ops.copy_rows(v8.view(torch.float32), R, Dv // 4, Dv // 4, cat_vis.view(torch.float32),
+                          Dv // 4, Nv, Tv, 0)
+            ops.copy_rows(vs.view(torch.float32), R, Dv // 128, Dv // 128,
+                          cat_scale.view(torch.float32), Dv // 128, Nv, Tv, 0)
+            vis_lp, vis_sc = v8.view(torch.float8_e4m3fn), vs
+            cat_vis = cat_vis.view(torch.float8_e4m3fn)
+        else:
+            if vis.dtype != torch.float32:
+                raise ValueError("bf16 mode takes fp32 region features")
+            vis_lp = _bf(R, Dv, dev=dev)
+            ops.cast_bf16(vis.reshape(R, Dv), R, Dv, Dv, vis_lp, Dv)
+            cat_vis = _bf(B * Tv, Dv, dev=dev)
+            ops.copy_rows(vis_lp.view(torch.float32), R, Dv // 2, Dv // 2,
+                          cat_vis.view(torch.float32), Dv // 2, Nv, Tv, 0)
+            vis_sc, cat_scale = None, None
+        cat_syb = _bf(B * Ts, Dv, dev=dev)
+        return vis_lp, vis_sc, cat_vis, cat_scale, cat_syb
 
     def _forward(self, inp: Dict[str, torch.Tensor], decMask: bool, drop=None):
         """The two stacks are independent until the heads (AttModel_x3.py:525-541), so the
@@ -625,12 +895,27 @@ class ModelEngine:
         Ns = inp["macro_ipt"].shape[1]
         Tv, Ts = Nv + Lq, Ns + Lq
         main = torch.cuda.current_stream(dev)
+        lp_vis = lp_syb = lp_mil = None
+        if self.lp_mode:
+            wv, ws, wm = self.lp_weights()
+            vis_lp, vis_sc, cat_vis, cat_scale, cat_syb = self._lp_inputs(
+                vis, inp.get("vis_fea_scale"), B, Nv, Dv, Tv, Ts)
+            if self.gemm_precision == "fp8":
+                Win8, Win8_s = self._shadow.fp8_weight("att_vis_grid.syb_mlp2.weight")
+                Wv, Wv_s = self._shadow.fp8_weight("MIL_NCE.vis_mlp.0.weight")
+            else:
+                Win8 = Win8_s = Wv_s = None
+                Wv = wm.Wv
+            lp_vis = StackLp(wv, cat_scale, Win8, Win8_s)
+            lp_syb = StackLp(ws)
+            lp_mil = MilLp(vis_lp, Wv, wm.Wipt, vis_sc, Wv_s)
         s_vis, s_syb = self._streams(dev)
         s_vis.wait_stream(main)
         s_syb.wait_stream(main)
         with torch.cuda.stream(s_syb):
             mil_val = _empty((), dev=dev)
-            cat_syb = _empty(B * Ts, Dv, dev=dev)
+            if lp_syb is None:
+                cat_syb = _empty(B * Ts, Dv, dev=dev)
             rel, mil_rel = None, None
             if "micro_positive_rel_loc" in inp:
                 rel = (inp["micro_positive_rel"], inp["micro_positive_rel_loc"],
@@ -639,16 +924,17 @@ class ModelEngine:
             ms = mil_forward(self.mil, vis, inp["macro_ipt"], inp["macro_obj_loc"],
                              inp["micro_positive_obj"], inp["micro_negative_obj"],
                              inp["micro_obj_mask"], cat_syb, Ts, mil_val, rel=rel,
-                             mil_rel_out=mil_rel)
+                             mil_rel_out=mil_rel, lp=lp_mil)
             ss = stack_forward(self.syb, cat_syb, B, Ns, Lq, inp["q_ipt"], inp["macro_mask"],
                                inp["q_mask"], inp["q_graph"], inp["macro_graph"], decMask, H, d,
-                               drop, SYB_SITES)
+                               drop, SYB_SITES, lp=lp_syb)
         with torch.cuda.stream(s_vis):
-            cat_vis = _empty(B * Tv, Dv, dev=dev)
-            ops.copy_rows(vis.reshape(B * Nv, Dv), B * Nv, Dv, Dv, cat_vis, Dv, Nv, Tv, 0)
+            if lp_vis is None:
+                cat_vis = _empty(B * Tv, Dv, dev=dev)
+                ops.copy_rows(vis.reshape(B * Nv, Dv), B * Nv, Dv, Dv, cat_vis, Dv, Nv, Tv, 0)
             sv = stack_forward(self.vis, cat_vis, B, Nv, Lq, inp["q_ipt"], inp["vis_mask"],
                                inp["q_mask"], inp["q_graph"], None, decMask, H, d, drop,
-                               VIS_SITES)
+                               VIS_SITES, lp=lp_vis)
         main.wait_stream(s_vis)
         main.wait_stream(s_syb)
         for t in (sv.out, ss.out, mil_val) + ((mil_rel,) if mil_rel is not None else ()):
@@ -664,7 +950,7 @@ class ModelEngine:
                 a.offsets["MIL_NCE.ipt_mlp.0.weight"][0])
 
     def backward(self, saved, dlc, dlv, dls, dmil, on_range=None, dmil_rel=None):
-        with ops.gemm_precision(self.gemm_precision):
+        with ops.gemm_precision(self._fp32_kernel_precision()):
             return self._backward(saved, dlc, dlv, dls, dmil, on_range, dmil_rel)
 
     def _backward(self, saved, dlc, dlv, dls, dmil, on_range=None, dmil_rel=None):

@@ -200,14 +200,16 @@ def gemm_lp(*args, **kw):
     _probe.records.append((key, 2.0 * d.M * d.N * d.K, e0, e1))
 
 
-def cast_bf16(x: Tensor, rows: int, cols: int, ldi: int, out: Tensor, ldo: int):
-    call("savqa_cast_bf16", _stream(), _p(x), int(rows), int(cols), int(ldi), _p(out), int(ldo))
+def cast_bf16(x: Tensor, rows: int, cols: int, ldi: int, out: Tensor, ldo: int, group=0,
+              stride=0, offset=0):
+    call("savqa_cast_bf16", _stream(), _p(x), int(rows), int(cols), int(ldi), _p(out), int(ldo),
+         int(group), int(stride), int(offset))
 
 
 def quant_fp8(x: Tensor, rows: int, cols: int, ldi: int, q: Tensor, ldq: int, scale: Tensor,
-              lds: int):
+              lds: int, group=0, stride=0, offset=0):
     call("savqa_quant_fp8", _stream(), _p(x), int(rows), int(cols), int(ldi), _p(q), int(ldq),
-         _p(scale), int(lds))
+         _p(scale), int(lds), int(group), int(stride), int(offset))
 
 
 def dequant_fp8_bf16(q: Tensor, rows: int, cols: int, ldq: int, scale: Tensor, lds: int,
@@ -218,6 +220,44 @@ def dequant_fp8_bf16(q: Tensor, rows: int, cols: int, ldq: int, scale: Tensor, l
 
 def colsum_bf16(X: Tensor, rows: int, cols: int, ldx: int, out: Tensor):
     call("savqa_colsum_bf16", _stream(), _p(X), int(rows), int(cols), int(ldx), _p(out))
+
+
+def linear_lp(X: Tensor, W: Tensor, b: Optional[Tensor], out: Optional[Tensor] = None,
+              outb: Optional[Tensor] = None, *, relu=False, rows: Optional[int] = None,
+              a_rows=None, rowvec=None, rowvec_period=0, resid=None, c_group=0, c_stride=0,
+              c_offset=0, ldo=None, x_scale=None, w_scale=None):
+    """nn.Linear forward on low-precision operands: X [M][K] and W [N][K] both bf16, or both
+    fp8-e4m3 with e8m0 block scales x_scale [M][K/32] / w_scale [N][K/32]; fp32 `out` and/or
+    bf16 `outb` (same row map)."""
+    N, K = W.shape
+    M = rows if rows is not None else (a_rows.numel() if a_rows is not None else X.numel() // K)
+    ld = ldo if ldo is not None else N
+    gemm_lp(X, W, M, N, K, lda=K, ldb=K, b_trans=True, a_rows=a_rows, a_scale=x_scale,
+            lds_a=K // 32, b_scale=w_scale, lds_b=K // 32, C=out, ldc=ld, Cb=outb, ldcb=ld,
+            c_group=c_group, c_stride=c_stride, c_offset=c_offset, bias=b, rowvec=rowvec, ldrv=N,
+            rowvec_period=rowvec_period, resid=resid, ldr=N, relu=relu)
+
+
+def linear_dx_lp(dY: Tensor, W: Tensor, dX: Optional[Tensor] = None,
+                 dXb: Optional[Tensor] = None, *, rows: int, a_rows=None, mask=None, ldmask=0,
+                 mask_arows=False, resid=None):
+    """dX = dY W on bf16 operands (W the bf16 shadow [N][K]); mask: bf16 ReLU gate."""
+    N, K = W.shape
+    gemm_lp(dY, W, rows, K, N, lda=N, ldb=K, a_rows=a_rows, C=dX, ldc=K, Cb=dXb, ldcb=K,
+            mask=mask, ldmask=ldmask, mask_arows=mask_arows, resid=resid, ldr=K)
+
+
+def linear_dw_lp(dY: Tensor, X: Tensor, dW: Tensor, db: Optional[Tensor], *, rows: int,
+                 dy32: Optional[Tensor] = None):
+    """dW += dY^T X on bf16 operands (split-K, atomics); db += colsum(dY) from the fp32 dY
+    when the caller has it (dy32), else from the bf16 one."""
+    N, K = dW.shape
+    gemm_lp(dY, X, N, K, rows, lda=N, ldb=K, a_trans=True, C=dW, ldc=K, atomic=True, split_k=-1)
+    if db is not None:
+        if dy32 is not None:
+            colsum_acc(dy32, rows, N, N, db)
+        else:
+            colsum_bf16(dY, rows, N, N, db)
 
 
 def linear(X: Tensor, W: Tensor, b: Optional[Tensor], out: Tensor, *, relu=False,
@@ -262,11 +302,12 @@ def colsum_acc(X: Tensor, rows: int, cols: int, ldx: int, out: Tensor):
 
 # ------------------------------------------------------------------------------ LN
 def ln_fwd(x: Tensor, gamma: Tensor, beta: Tensor, y: Tensor, mean: Tensor, rden: Tensor,
-           std: Tensor, *, r=None, z_out=None, flag=None, xscale=None, eps=1e-8):
+           std: Tensor, *, r=None, z_out=None, flag=None, xscale=None, eps=1e-8, yb=None):
+    """yb: optional bf16 copy of y (operand of the next low-precision GEMM)."""
     cols = gamma.numel()
     rows = x.numel() // cols
     call("savqa_ln_fwd", _stream(), _p(x), _p(xscale), _p(r), rows, cols, _p(gamma), _p(beta),
-         float(eps), _p(z_out), _p(y), _p(mean), _p(rden), _p(std), _p(flag))
+         float(eps), _p(z_out), _p(y), _p(mean), _p(rden), _p(std), _p(flag), _p(yb))
 
 
 _ln_ws = {}
@@ -286,12 +327,13 @@ def ln_workspace(cols: int, dev) -> Tensor:
 
 
 def ln_bwd(dy: Tensor, z: Tensor, mean: Tensor, rden: Tensor, std: Tensor, gamma: Tensor,
-           dz: Tensor, dgamma: Tensor, dbeta: Tensor, *, dz_add=None):
+           dz: Tensor, dgamma: Tensor, dbeta: Tensor, *, dz_add=None, dzb=None):
+    """dzb: optional bf16 copy of dz (operand of the next low-precision GEMMs)."""
     cols = gamma.numel()
     rows = z.numel() // cols
     ws = ln_workspace(cols, z.device)
     call("savqa_ln_bwd", _stream(), _p(dy), _p(z), _p(mean), _p(rden), _p(std), _p(gamma), rows,
-         cols, _p(dz_add), _p(dz), _p(dgamma), _p(dbeta), _p(ws), ws.numel() * 4)
+         cols, _p(dz_add), _p(dz), _p(dgamma), _p(dbeta), _p(ws), ws.numel() * 4, _p(dzb))
 
 
 def rowflag(X: Tensor, rows: int, cols: int, ldx: int, flag: Tensor):
@@ -300,12 +342,22 @@ def rowflag(X: Tensor, rows: int, cols: int, ldx: int, flag: Tensor):
 
 # ------------------------------------------------------------------------------ attention
 def gattn_fwd(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, o, ldo, att=None, dk=64):
+    """Graph-attention forward; bf16 Q/K/V select the bf16-storage kernels (fp32 math)."""
+    if k.dtype == torch.bfloat16:
+        call("savqa_gattn_fwd_bf16", _stream(), int(q.dtype == torch.bfloat16), _p(q), ldq, _p(k),
+             ldk, _p(v), ldv, _p(G), _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(att))
+        return
     call("savqa_gattn_fwd", _stream(), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G), _p(kflag),
          _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(att))
 
 
 def gattn_bwd(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout, lddo, dq, lddq, dk_,
               lddk, dv, lddv, dk=64):
+    if k.dtype == torch.bfloat16:
+        call("savqa_gattn_bwd_bf16", _stream(), int(q.dtype == torch.bfloat16), _p(q), ldq, _p(k),
+             ldk, _p(v), ldv, _p(G), _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo,
+             _p(dq), lddq, _p(dk_), lddk, _p(dv), lddv)
+        return
     call("savqa_gattn_bwd", _stream(), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G), _p(kflag),
          _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo, _p(dq), lddq, _p(dk_), lddk, _p(dv), lddv)
 

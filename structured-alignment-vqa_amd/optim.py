@@ -52,6 +52,7 @@ class Adam(torch.optim.Optimizer):
                 w.wait()   # this stream waits for this bucket's all-reduce only
             ops.adam(a.flat[lo:hi], g[lo:hi], self.m[lo:hi], self.v[lo:hi], hi - lo, grp["lr"], b1,
                      b2, grp["eps"], bc1, bc2, scale)
+        a.generation += 1  # low-precision weight shadows are stale now
         return loss
 
     @staticmethod

@@ -98,6 +98,7 @@ class ParamArena:
         flat = torch.zeros(self.total, dtype=torch.float32, device=dev)
         self.flat = flat
         self.grad = None  # allocated on first backward (device of flat)
+        self.generation = 0  # bumped by every optimizer update (raw-pointer writes)
         if flat.device.type == "meta":  # layout-only arena (host-side tests)
             return
         with torch.no_grad():
@@ -170,3 +171,18 @@ class ParamArena:
     def zero_grad(self):
         if self.grad is not None:
             self.grad.zero_()
+
+    def state_key(self):
+        """Changes whenever parameter values may have changed: torch in-place edits bump the
+        flat buffer's version counter, optimizer kernels bump `generation`."""
+        return (self.flat.data_ptr(), self.flat._version, self.generation)
+
+    def table_ranges(self):
+        """Arena ranges of the live 407000 x 300 GloVe tables (row-gathered, never GEMM B
+        operands of the low-precision path)."""
+        out = []
+        for n in self.live_names:
+            if n.endswith("syb_emb.weight"):
+                o, shp = self.offsets[n]
+                out.append((o, o + int(torch.Size(shp).numel())))
+        return sorted(out)

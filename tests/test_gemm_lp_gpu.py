@@ -52,9 +52,9 @@ def test_bf16_layouts_bias_relu(lay, M, N, K):
 
 
 @pytest.mark.parametrize("hint", [1, 3, 4])
-@pytest.mark.parametrize("lay,M,N,K", [("NT", 1800, 1536, 512), ("NN", 1304, 1000, 512),
-                                       ("TN", 1304, 1544, 576), ("TT", 704, 1536, 256),
-                                       ("NT", 3700, 512, 2048)])
+@pytest.mark.parametrize("lay,M,N,K", [("NT", 1800, 1536, 512), ("NN", 1304, 1000, 520),
+                                       ("TN", 1304, 1544, 2408), ("TT", 704, 1536, 256),
+                                       ("NT", 3700, 512, 2048), ("TN", 512, 512, 2400)])
 def test_bf16_kernel_variants(hint, lay, M, N, K):
     """Every kernel variant (tile_hint: 128x128 two per CU; 256x256 with a two-slot and
     256x128 with a three-slot LDS-DMA ring, one per CU), incl. M / N edge tiles."""
@@ -74,11 +74,13 @@ def test_bf16_kernel_variants(hint, lay, M, N, K):
     assert torch.equal(Cb.cpu(), C.to(torch.bfloat16).cpu())
 
 
-def test_bf16_dw_split_k_atomic_and_colsum():
+@pytest.mark.parametrize("K", [18688, 2400, 18712])
+def test_bf16_dw_split_k_atomic_and_colsum(K):
     """dW += dY^T X (TN) at the encoder shape with the auto split-K (atomic accumulation
-    into an existing gradient) and the bf16 bias-gradient column sums."""
+    into an existing gradient; K = B*T rows need not fill the last k-tile) and the bf16
+    bias-gradient column sums."""
     O = ops()
-    M, N, K = 512, 1536, 18688          # dW [1536 x 512] over B*T = 18688 rows
+    M, N = 512, 1536                     # dW [1536 x 512] over B*T rows
     dY = bf((K, N), 3)
     X = bf((K, M), 4)
     W0 = torch.randn(N, M, device=dev)
@@ -123,7 +125,7 @@ def test_gemm_lp_rejects_unsupported():
     W = bf((64, 60), 9)
     C = torch.empty(100, 64, device=dev)
     d = O.lp_desc(A, W, 100, 64, 60, lda=60, ldb=60, b_trans=True, C=C, ldc=64)
-    assert not O.lp_supported(d)          # K % 64 != 0
+    assert not O.lp_supported(d)          # K % 8 != 0
     from savqa_amd._lib import SavqaError
     with pytest.raises(SavqaError):
         O.gemm_lp(A, W, 100, 64, 60, lda=60, ldb=60, b_trans=True, C=C, ldc=64)

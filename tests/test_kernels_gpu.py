@@ -259,6 +259,88 @@ def test_graph_attention_fwd_bwd(B, Tq, Tk, kind):
     assert rel(dv.view(B, Tk, D), Vr.grad * mv) < 5e-5
 
 
+@pytest.mark.parametrize("B,Tq,Tk,kind", [(3, 50, 50, "self"), (2, 73, 73, "self"),
+                                           (5, 1, 73, "cross"), (4, 1, 50, "cross"),
+                                           (2, 128, 128, "self"), (3, 17, 33, "cross")])
+def test_graph_attention_bf16_storage(B, Tq, Tk, kind):
+    """bf16-storage attention (savqa_gattn_{fwd,bwd}_bf16; cfg 3 / cfg 5): same fp32 math as the
+    fp32 kernels on the bf16 values, so its outputs equal the fp32 kernels' outputs on the
+    bf16-rounded inputs (O to fp32 rounding, dQ/dK/dV to one bf16 rounding), and both match
+    the fp64 reference of the rounded inputs."""
+    O = ops()
+    H, D = 8, 512
+    bf = torch.bfloat16
+    if kind == "self":
+        qkv = g(B * Tk, 3 * D, seed=50, relu=True).to(bf)
+        Q, K, V = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+        ldq = ldk = ldv = 3 * D
+    else:
+        Q = g(B * Tq, D, seed=51, relu=True).to(bf)
+        kv = g(B * Tk, 2 * D, seed=52, relu=True).to(bf)
+        K, V = kv[:, :D], kv[:, D:]
+        ldq, ldk, ldv = D, 2 * D, 2 * D
+    G = (torch.rand(B, Tq, Tk, generator=torch.Generator().manual_seed(53)) < 0.4).float().to(dev)
+    G[0, :3] = 0.0
+    kf = torch.ones(B, Tk, device=dev)
+    kf[0, 2] = 0.0
+    qf = torch.ones(B, Tq, device=dev)
+    qf[-1, 0] = 0.0
+    Qf, Kf, Vf = (x.float().contiguous() for x in (Q, K, V))
+    o16 = torch.empty(B * Tq, D, device=dev)
+    o32 = torch.empty(B * Tq, D, device=dev)
+    O.gattn_fwd(Q, ldq, K, ldk, V, ldv, G, kf, qf, B, Tq, Tk, H, o16, D)
+    O.gattn_fwd(Qf, D, Kf, D, Vf, D, G, kf, qf, B, Tq, Tk, H, o32, D)
+    assert rel(o16, o32) < 1e-6
+    dO = g(B * Tq, D, seed=54)
+    d16 = [torch.empty(B * n, D, device=dev, dtype=bf) for n in (Tq, Tk, Tk)]
+    d32 = [torch.empty(B * n, D, device=dev) for n in (Tq, Tk, Tk)]
+    O.gattn_bwd(Q, ldq, K, ldk, V, ldv, G, kf, qf, B, Tq, Tk, H, dO, D, d16[0], D, d16[1], D,
+                d16[2], D)
+    O.gattn_bwd(Qf, D, Kf, D, Vf, D, G, kf, qf, B, Tq, Tk, H, dO, D, d32[0], D, d32[1], D, d32[2], D)
+    for a, b_ in zip(d16, d32):
+        assert rel(a.float(), b_.to(bf).float()) < 1e-2   # one bf16 rounding (+ fp32 order)
+        assert rel(a.float(), b_) < 1e-2
+    Qr = Qf.reshape(B, Tq, D).double().cpu().requires_grad_(True)
+    Kr = Kf.reshape(B, Tk, D).double().cpu().requires_grad_(True)
+    Vr = Vf.reshape(B, Tk, D).double().cpu().requires_grad_(True)
+    ref, _ = _attn_ref(Qr, Kr, Vr, G.double().cpu(), kf.double().cpu(), qf.double().cpu())
+    assert rel(o16.view(B, Tq, D), ref) < 2e-5
+    (ref * dO.view(B, Tq, D).double().cpu()).sum().backward()
+    assert rel(d16[0].float().view(B, Tq, D), Qr.grad * (Qr > 0)) < 1e-2
+    assert rel(d16[1].float().view(B, Tk, D), Kr.grad * (Kr > 0)) < 1e-2
+    assert rel(d16[2].float().view(B, Tk, D), Vr.grad * (Vr > 0)) < 1e-2
+
+
+@pytest.mark.parametrize("Tk", [50, 73, 128])
+def test_graph_attention_fp32_query_bf16_kv(Tk):
+    """The decoder's cross-attention in the bf16 mode: fp32 single query (and dQ), bf16 K/V
+    (and dK/dV); equals the fp32 kernels on the bf16-rounded K/V."""
+    O = ops()
+    B, H, D = 6, 8, 512
+    Q = g(B, D, seed=60, relu=True)
+    kv = g(B * Tk, 2 * D, seed=61, relu=True).to(torch.bfloat16)
+    K, V = kv[:, :D], kv[:, D:]
+    Kf, Vf = K.float().contiguous(), V.float().contiguous()
+    G = (torch.rand(B, 1, Tk, generator=torch.Generator().manual_seed(62)) < 0.5).float().to(dev)
+    kf = torch.ones(B, Tk, device=dev)
+    kf[1, 3] = 0.0
+    qf = torch.ones(B, 1, device=dev)
+    o16, o32 = torch.empty(B, D, device=dev), torch.empty(B, D, device=dev)
+    O.gattn_fwd(Q, D, K, 2 * D, V, 2 * D, G, kf, qf, B, 1, Tk, H, o16, D)
+    O.gattn_fwd(Q, D, Kf, D, Vf, D, G, kf, qf, B, 1, Tk, H, o32, D)
+    assert rel(o16, o32) < 1e-6
+    dO = g(B, D, seed=63)
+    dq16, dq32 = torch.empty(B, D, device=dev), torch.empty(B, D, device=dev)
+    dkv16 = torch.empty(B * Tk, 2 * D, device=dev, dtype=torch.bfloat16)
+    dk32, dv32 = torch.empty(B * Tk, D, device=dev), torch.empty(B * Tk, D, device=dev)
+    O.gattn_bwd(Q, D, K, 2 * D, V, 2 * D, G, kf, qf, B, 1, Tk, H, dO, D, dq16, D, dkv16, 2 * D,
+                dkv16[:, D:], 2 * D)
+    O.gattn_bwd(Q, D, Kf, D, Vf, D, G, kf, qf, B, 1, Tk, H, dO, D, dq32, D, dk32, D, dv32, D)
+    assert rel(dq16, dq32) < 1e-6
+    assert rel(dkv16[:, :D].float(), dk32) < 1e-2
+    assert rel(dkv16[:, D:].float(), dv32) < 1e-2
+
+
 def test_graph_build_matches_oracle():
     from oracle import savqa_oracle as OR
     O = ops()
