@@ -28,6 +28,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "QA-samples/sec training (model_v=3, 36 regions × 2048-d) at 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
+FP8_MFMA_PEAK_TFLOPS = 5000.0   # MI355X_MICROARCH.md: ~5 PF dense fp8 (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -138,8 +139,9 @@ WORKLOADS = {
                       "14 q-tokens, 59 nodes, d=512 h=8 L=6, MIL-NCE only_obj topN=5 H=1024, "
                       "914 classes, decMask"),
     "cfg3": dict(d=512, H=8, Nv=36, Ns=59, batch=512, prec="bf16",
-                 desc="cfg3: model_v=3 train step, bf16 GEMM products (fp32 accumulation, fp32 "
-                      "master weights / LN / softmax / loss / Adam), 36 regions x 2048-d, "
+                 desc="cfg3: model_v=3 train step, bf16-resident GEMM operands and attention "
+                      "storage (fp32 accumulation, fp32 residual stream / LN / softmax / loss / "
+                      "master weights / Adam), 36 regions x 2048-d, "
                       "14 q-tokens, 59 nodes, d=512 h=8 L=6, MIL-NCE only_obj topN=5 H=1024, "
                       "914 classes, decMask"),
     "rel": dict(d=512, H=8, Nv=36, Ns=36 + 4 + 36 * 35, batch=4, rel=True, maxlen=1600,
@@ -148,6 +150,14 @@ WORKLOADS = {
                      "4 attributes, 1260 relation nodes: T_syb=1314), 31,500 positive + 31,500 "
                      "negative relation entries per sample, 311 relation categories (R: "
                      "311x1024x1024), d=512 h=8 L=6, H_mil=1024, topN=5, decMask"),
+    "cfg5": dict(d=512, H=8, Nv=36, Ns=59, batch=1024, prec="fp8",
+                 desc="cfg5: model_v=3 train step, fp8-e4m3 region features (per-32 e8m0 block "
+                      "scales, quantised outside the timed region as a loader would ship them) "
+                      "into block-scaled fp8 MFMA (att_vis_grid.syb_mlp2, MIL_NCE.vis_mlp), bf16 "
+                      "GEMM operands and attention storage elsewhere (fp32 accumulation, fp32 "
+                      "residual stream / LN / softmax / loss / master weights / Adam), 36 regions "
+                      "x 2048-d, 14 q-tokens, 59 nodes, d=512 h=8 L=6, MIL-NCE only_obj topN=5 "
+                      "H=1024, 914 classes, decMask"),
     "cfg4": dict(d=1024, H=16, Nv=100, Ns=435, batch=32,
                  desc="cfg4: model_v=3 train step, fp32, 100 regions x 2048-d, 14 q-tokens, "
                       "435-node scene graph (T_vis=114, T_syb=449), d=1024 h=16 (h=12 does not "
@@ -177,8 +187,9 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="samples per GPU (cfg2: 256)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2",
                     help="cfg2 = BASELINE config 2 (fp32, 256/GPU: the metric's workload); cfg3 = "
-                         "config 3 (bf16 GEMM products, 512/GPU); cfg4 = the 100-region / 435-node "
-                         "scene-graph stress shape (d=1024, 16 heads, T_syb=449)")
+                         "config 3 (bf16, 512/GPU); cfg4 = the 100-region / 435-node scene-graph "
+                         "stress shape (d=1024, 16 heads, T_syb=449); cfg5 = config 5 (fp8 region "
+                         "features + bf16, 1024/GPU); rel = the super-node relation branch")
     ap.add_argument("--dropout", type=float, default=0.5,
                     help="dropout_rate (reference training default 0.5, main:466)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -231,11 +242,21 @@ def main():
     else:
         batch = synthetic_batch(B, Nv=Nv, Ns=Ns, seed=1234 + rank, device=dev)
         margs = model_args(batch)
+    fwd_kw = {}
+    if W.get("prec") == "fp8":
+        # the loader ships e4m3 codes + e8m0 block scales (savqa_quant_fp8's layout)
+        R, Dv = B * Nv, batch["vis_fea"].shape[-1]
+        q8 = torch.empty(R, Dv, dtype=torch.uint8, device=dev)
+        s8 = torch.empty(R, Dv // 32, dtype=torch.uint8, device=dev)
+        ops.quant_fp8(batch["vis_fea"].reshape(R, Dv), R, Dv, Dv, q8, Dv, s8, Dv // 32)
+        margs[0] = q8.view(torch.float8_e4m3fn).reshape(B, Nv, Dv)
+        fwd_kw["vis_fea_scale"] = s8.reshape(B, Nv, Dv // 32)
+        del batch["vis_fea"]
 
     def step():
         if reducer:
             reducer.begin()
-        lc, lv, ls, mil, mil_rel = model(*margs, decMask=True, mcb=False)
+        lc, lv, ls, mil, mil_rel = model(*margs, decMask=True, mcb=False, **fwd_kw)
         loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil, with_milnce=True,
                                 mil_nce_rel=mil_rel)
         opt.zero_grad()
@@ -266,7 +287,8 @@ def main():
     value = world * B * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
     fl = train_flops_per_sample(Tv=Nv + 14, Ts=Ns + 14, Nv=Nv, Ns=Ns, d=d)
-    peak = BF16_MFMA_PEAK_TFLOPS if W.get("prec") == "bf16" else FP32_MFMA_PEAK_TFLOPS
+    lp = W.get("prec") in ("bf16", "fp8")
+    peak = BF16_MFMA_PEAK_TFLOPS if lp else FP32_MFMA_PEAK_TFLOPS
 
     roof = None
     if not args.no_roofline:
@@ -282,12 +304,15 @@ def main():
         agg = probe.summary()
         var, (n, flops, ms) = max(agg.items(), key=lambda kv: kv[1][2])
         achieved = (flops / n) / (ms / n * 1e-3) / 1e12
+        kpeak = peak
+        if var.startswith("gemm_lp_kernel"):  # bf16 operands, or fp8 when the key ends ,true>
+            kpeak = FP8_MFMA_PEAK_TFLOPS if var.endswith(",true>") else BF16_MFMA_PEAK_TFLOPS
         allfl = sum(v[1] for v in agg.values())
         allms = sum(v[2] for v in agg.values())
         roof = {"bound": "mfma", "kernel": var, "launches_per_step": n // 2,
                 "avg_launch_us": round(ms / n * 1e3, 2), "flops_per_launch": flops / n,
-                "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4),
+                "achieved": round(achieved, 2), "peak": kpeak, "unit": "TFLOP/s",
+                "frac": round(achieved / kpeak, 4),
                 "traffic": committed_traffic(var),
                 "all_gemm_tflops": round(allfl / (allms * 1e-3) / 1e12, 2),
                 "gemm_ms_per_step": round(allms / 2, 2)}
@@ -300,7 +325,9 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "QA-samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16 (GEMM products; fp32 accumulate)" if W.get("prec") == "bf16" else "fp32",
+            "dtype": {"bf16": "bf16 (GEMM operands; fp32 accumulate)",
+                      "fp8": "fp8-e4m3 region features + bf16 (GEMM operands; fp32 accumulate)"
+                      }.get(W.get("prec"), "fp32"),
             "data": "synthetic (collate_fn tensor contract; random-init weights)",
             "config": {"workload": W["desc"] + f", dropout {args.dropout}",
                        "per_gpu_batch": B, "global_batch": world * B,
