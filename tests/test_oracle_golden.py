@@ -154,11 +154,12 @@ REL_INPUTS = ("vis_fea", "vis_mask", "q_ipt", "q_mask", "q_graph", "macro_ipt", 
 
 
 @pytest.mark.slow
-def test_relation_branch_full_model():
+@pytest.mark.parametrize("case", ["full_rel_b2", "full_rel_sn"])
+def test_relation_branch_full_model(case):
     """MIL-NCE relation branch (only_obj=False, AttModel_x3.py:382-437) end to end: logits,
     mil_nce_obj, mil_nce_rel, loss and every trained gradient (R included) against the
-    reference run on a super-node batch (tests/golden/full_rel_b2.npz)."""
-    g = np.load(os.path.join(GOLD, "full_rel_b2.npz"))
+    reference run on super-node batches (tests/golden/full_rel_{b2,sn}.npz; sn: T_syb=211)."""
+    g = np.load(os.path.join(GOLD, f"{case}.npz"))
     P = hashfill.HashParams(requires_grad=True, num_relations=int(g["num_relations"]))
     inp = {k: torch.from_numpy(g[k]) for k in REL_INPUTS}
     lc, lv, ls, mil, mil_rel = O.attmodel_forward(P, inp, decMask=True, only_obj=False)

@@ -1,7 +1,9 @@
 """MIL-NCE relation branch (only_obj=False, AttModel_x3.py:382-437) on the HIP path against
-the reference's own outputs on a super-node batch (tests/golden/full_rel_b2.npz, produced by
-tools/make_golden.py running the reference): logits, mil_nce_obj, mil_nce_rel, loss and the
-gradients of every trained parameter, MIL_NCE.R included (north-star tolerance 1e-3)."""
+the reference's own outputs on super-node batches (tests/golden/full_rel_{b2,sn}.npz, produced
+by tools/make_golden.py running the reference): logits, mil_nce_obj, mil_nce_rel, loss and
+the gradients of every trained parameter, MIL_NCE.R included (north-star tolerance 1e-3).
+full_rel_sn has T_syb = 211 > 128, so the semantic stack runs the key-tiled attention
+(csrc/attn_flash.hip) inside the parity case."""
 import os
 
 import numpy as np
@@ -24,14 +26,15 @@ def rel(a, b):
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
 
 
-def test_relation_branch_against_reference_golden():
+@pytest.mark.parametrize("case", ["full_rel_b2", "full_rel_sn"])
+def test_relation_branch_against_reference_golden(case):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     torch.backends.cuda.matmul.allow_tf32 = False
     from savqa_amd.AttModel_x3 import AttModel
     from savqa_amd.loss import smoothed_loss
     from savqa_amd.optim import Adam
-    g = np.load(os.path.join(GOLD, "full_rel_b2.npz"))
+    g = np.load(os.path.join(GOLD, f"{case}.npz"))
     m = AttModel(None, 512, 1024, 914, 40, 450, 49, int(g["num_blocks"]), 8, 0.0, 0.0,
                  int(g["num_relations"]), False, device="cuda", init=False)
     with torch.no_grad():

@@ -155,7 +155,19 @@ def full_model_cases(modules_mod, att_mod):
     del model
 
 
+# relation-branch cases: (objects per sample, question lengths). full_rel_sn has a super-node
+# graph of T_syb = 14 + 3 + 14*13 + 12 = 211 > 128 positions, so the key-tiled attention
+# (csrc/attn_flash.hip) runs inside the semantic stack of the parity case.
+RELATION_RUNS = {"full_rel_b2": ([5, 4], [7, 5]),
+                 "full_rel_sn": ([14, 11], [12, 9])}
+
+
 def relation_cases(att_mod):
+    for cname, (nobj, lq) in RELATION_RUNS.items():
+        relation_case(att_mod, cname, nobj, lq)
+
+
+def relation_case(att_mod, cname, nobj, lq):
     """Full model with the MIL-NCE relation branch (only_obj=False, AttModel_x3.py:382-437)
     on a super-node batch (oracle/cases.make_relation_inputs)."""
     nrel = 7
@@ -166,7 +178,8 @@ def relation_cases(att_mod):
                                  0.0, 0.0, nrel, False)
     model.train()
     fill_params(model)
-    inp = cases.make_relation_inputs(2, [5, 4], [7, 5], nrel, tag="relcase")
+    tag = "relcase" if cname == "full_rel_b2" else cname
+    inp = cases.make_relation_inputs(len(nobj), nobj, lq, nrel, tag=tag)
     t = to_t(inp)
     lc, lv, ls, mil, mil_rel = model(
         t["vis_fea"], t["vis_mask"], t["q_ipt"], t["q_mask"], t["q_graph"], t["macro_ipt"],
@@ -199,8 +212,9 @@ def relation_cases(att_mod):
     out["R_used"] = used
     out["R_grad_used"] = model.MIL_NCE.R.grad[torch.from_numpy(used), :4].numpy()  # 4 rows each
     out["grad_names"] = np.array(gnames)
-    np.savez_compressed(os.path.join(OUT, "full_rel_b2.npz"), **out)
-    print("wrote full_rel_b2 loss", float(out["loss"]), "mil_rel", float(out["mil_nce_rel"]))
+    np.savez_compressed(os.path.join(OUT, f"{cname}.npz"), **out)
+    print("wrote", cname, "T_syb", inp["macro_ipt"].shape[1] + inp["q_ipt"].shape[1], "loss",
+          float(out["loss"]), "mil_rel", float(out["mil_nce_rel"]))
     del model
 
 
