@@ -305,7 +305,7 @@ def main():
         var, (n, flops, ms) = max(agg.items(), key=lambda kv: kv[1][2])
         achieved = (flops / n) / (ms / n * 1e-3) / 1e12
         kpeak = peak
-        if var.startswith("gemm_lp_kernel"):  # bf16 operands, or fp8 when the key ends ,true>
+        if var.startswith("gemm_lp"):  # bf16 operands, or fp8 (gemm_lp_kernel<...,true>)
             kpeak = FP8_MFMA_PEAK_TFLOPS if var.endswith(",true>") else BF16_MFMA_PEAK_TFLOPS
         allfl = sum(v[1] for v in agg.values())
         allms = sum(v[2] for v in agg.values())

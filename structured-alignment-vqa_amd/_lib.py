@@ -79,6 +79,7 @@ _SIGS = {
     "savqa_colsum_acc": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
     "savqa_gemm_lp": [c_p, C.POINTER(GemmLpDesc)],
     "savqa_gemm_lp_supported": [C.POINTER(GemmLpDesc)],
+    "savqa_gemm_lp_plan": [C.POINTER(GemmLpDesc), c_p],
     "savqa_cast_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64],
     "savqa_quant_fp8": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64,
                         c_i64],

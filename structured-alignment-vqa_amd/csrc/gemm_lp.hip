@@ -634,6 +634,51 @@ static bool lp_ok(const savqa_gemm_lp_desc& d, const char** msg) {
   return true;
 }
 
+// Launch plan of a supported descriptor: kernel variant (1 = 128x128, two workgroups per
+// CU; 3 = 256x256 BK64 NS2, 4 = 256x128 BK64 NS3 -- one per CU), split-K factor, tiles.
+struct LpPlan {
+  int var, split, nsplit;
+  int64_t tiles, per;
+  int bn;
+};
+
+static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
+  LpPlan p{};
+  const bool fp8 = d.a_type == SAVQA_DT_FP8;
+  // kernel: variants of gemm_lp2_kernel (bf16, one workgroup per CU) when there are enough
+  // tiles to fill the chip, else the 128 x 128 kernel (two per CU); d.tile_hint selects one
+  // explicitly (tests / tuning): 1 = 128x128, 3 = 256x256 BK64 NS2, 4 = 256x128 BK64 NS3
+  // (k-tile 32 with a three-slot ring measured slower: 64-B rows halve each DMA's lines)
+  // measured (tools/lp_bench.py --variants, cfg-3 shapes): the two-per-CU 128 x 128 kernel is
+  // fastest except for the very wide outputs (N = 6144 forward, M = 6144 split-K dW), where
+  // the 256 x 256 tile's halved operand traffic wins by ~10%
+  p.var = 1;
+  if (!fp8) {
+    const bool split = d.split_k > 1 || d.split_k < 0;
+    const int h = d.tile_hint & 255;
+    if (h == 1 || h == 3 || h == 4) p.var = h;
+    else if (d.N >= 4096 || (split && d.M >= 4096 && d.N >= 256)) p.var = 3;
+  }
+  const int bm = p.var == 1 ? 128 : 256;
+  p.bn = p.var == 3 ? 256 : 128;
+  const int bk = fp8 ? 128 : 64;
+  const int slots = p.var == 1 ? lp_slots() : lp_slots() / LP_OCC;
+  p.tiles = ((d.M + bm - 1) / bm) * ((d.N + p.bn - 1) / p.bn);
+  const int64_t nk = (d.K + bk - 1) / bk;
+  p.split = d.split_k > 1 ? d.split_k : 1;
+  if (d.split_k < 0) {  // minimise rounds(s) * (k-tiles per slice + per-block overhead)
+    int64_t best_cost = INT64_MAX;
+    for (int s = 1; s <= 64 && (s == 1 || nk / s >= 4); ++s) {
+      const int64_t rounds = (p.tiles * s + slots - 1) / slots;
+      const int64_t cost = rounds * ((nk + s - 1) / s + 3);
+      if (cost < best_cost) { best_cost = cost; p.split = s; }
+    }
+  }
+  p.per = (nk + p.split - 1) / p.split;
+  p.nsplit = nk > 0 ? (int)((nk + p.per - 1) / p.per) : 1;
+  return p;
+}
+
 }  // namespace savqa
 
 using namespace savqa;
@@ -641,6 +686,18 @@ using namespace savqa;
 extern "C" int savqa_gemm_lp_supported(const savqa_gemm_lp_desc* d) {
   const char* msg = nullptr;
   return d && lp_ok(*d, &msg) ? 1 : 0;
+}
+
+extern "C" int savqa_gemm_lp_plan(const savqa_gemm_lp_desc* d, int32_t* out) {
+  if (!d || !out) return fail(SAVQA_EINVAL, "savqa_gemm_lp_plan: null argument");
+  const char* msg = nullptr;
+  if (!lp_ok(*d, &msg)) return fail(SAVQA_EUNSUP, std::string("savqa_gemm_lp_plan: ") + msg);
+  const LpPlan p = lp_plan(*d);
+  out[0] = p.var;
+  out[1] = p.nsplit;
+  out[2] = (int32_t)(p.tiles * p.nsplit);
+  out[3] = 0;
+  return 0;
 }
 
 extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
@@ -653,44 +710,17 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   if (!lp_ok(d, &msg)) return fail(SAVQA_EUNSUP, std::string("savqa_gemm_lp: ") + msg);
   if (d.c_group <= 0) d.c_group = 0;
   const bool fp8 = d.a_type == SAVQA_DT_FP8;
-  // kernel: variants of gemm_lp2_kernel (bf16, one workgroup per CU) when there are enough
-  // tiles to fill the chip, else the 128 x 128 kernel (two per CU); d.tile_hint selects one
-  // explicitly (tests / tuning): 1 = 128x128, 3 = 256x256 BK64 NS2, 4 = 256x128 BK64 NS3
-  // (k-tile 32 with a three-slot ring measured slower: 64-B rows halve each DMA's lines)
-  // measured (tools/lp_bench.py --variants, cfg-3 shapes): the two-per-CU 128 x 128 kernel is
-  // fastest except for the very wide outputs (N = 6144 forward, M = 6144 split-K dW), where
-  // the 256 x 256 tile's halved operand traffic wins by ~10%
-  int var = 1;
-  if (!fp8) {
-    const bool split = d.split_k > 1 || d.split_k < 0;
-    const int h = d.tile_hint & 255;
-    if (h == 1 || h == 3 || h == 4) var = h;
-    else if (d.N >= 4096 || (split && d.M >= 4096 && d.N >= 256)) var = 3;
-  }
-  const int bm = var == 1 ? 128 : 256, bn = var == 3 ? 256 : 128;
+  const LpPlan p = lp_plan(d);
+  const int var = p.var;
   const int bk = fp8 ? 128 : 64;
-  const int slots = var == 1 ? lp_slots() : lp_slots() / LP_OCC;
-  const int64_t tiles = ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn);
-  const int64_t nk = (d.K + bk - 1) / bk;
-  int split = d.split_k > 1 ? d.split_k : 1;
-  if (d.split_k < 0) {  // minimise rounds(s) * (k-tiles per slice + per-block overhead)
-    int64_t best_cost = INT64_MAX;
-    for (int s = 1; s <= 64 && (s == 1 || nk / s >= 4); ++s) {
-      const int64_t rounds = (tiles * s + slots - 1) / slots;
-      const int64_t cost = rounds * ((nk + s - 1) / s + 3);
-      if (cost < best_cost) { best_cost = cost; split = s; }
-    }
-  }
-  const int64_t per = (nk + split - 1) / split;
-  a.kchunk = per * bk;
-  const int nsplit = nk > 0 ? (int)((nk + per - 1) / per) : 1;
-  a.tiles_n = (int)((d.N + bn - 1) / bn);
+  a.kchunk = p.per * bk;
+  a.tiles_n = (int)((d.N + p.bn - 1) / p.bn);
   a.dbg = d.tile_hint >> 8;
-  a.nblk = (int)tiles;
-  a.ntiles_k = (int)per;
+  a.nblk = (int)p.tiles;
+  a.ntiles_k = (int)p.per;
   if (d.K == 0) a.kchunk = 0;
   hipStream_t s = as_stream(stream);
-  const dim3 grid((unsigned)tiles, (unsigned)nsplit), block(LP_NT);
+  const dim3 grid((unsigned)p.tiles, (unsigned)p.nsplit), block(LP_NT);
   if (var != 1) {
     const dim3 b2(512);
 #define SAVQA_LP2(BN_, WM_, BK_, NS_)                                                              \

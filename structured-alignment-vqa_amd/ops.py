@@ -177,6 +177,19 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
     return d
 
 
+def lp_variant(d) -> str:
+    """Kernel instantiation savqa_gemm_lp launches for d (the name rocprof reports, up to
+    the template arguments that follow from the variant)."""
+    plan = (C.c_int32 * 4)()
+    call("savqa_gemm_lp_plan", C.byref(d), C.cast(plan, C.c_void_p))
+    at, bt = str(bool(d.a_trans)).lower(), str(bool(d.b_trans)).lower()
+    if plan[0] == 3:
+        return f"gemm_lp2_kernel<256,256,2,64,2,{at},{bt}>"
+    if plan[0] == 4:
+        return f"gemm_lp2_kernel<256,128,4,64,3,{at},{bt}>"
+    return f"gemm_lp_kernel<{at},{bt},{str(d.a_type == 2).lower()}>"
+
+
 def lp_supported(d) -> bool:
     return bool(_lib.load().savqa_gemm_lp_supported(C.byref(d)))
 
@@ -192,11 +205,12 @@ def gemm_lp(*args, **kw):
     e0.record()
     call("savqa_gemm_lp", _stream(), C.byref(d))
     e1.record()
-    fp8 = d.a_type == 2
-    key = (f"gemm_lp_kernel<{str(bool(d.a_trans)).lower()},{str(bool(d.b_trans)).lower()},"
-           f"{str(fp8).lower()}>")
+    key = lp_variant(d)
     if _probe.detail:
-        key += f" | {'T' if d.a_trans else 'N'}{'T' if d.b_trans else 'N'} {d.M}x{d.N}x{d.K}"
+        plan = (C.c_int32 * 4)()
+        call("savqa_gemm_lp_plan", C.byref(d), C.cast(plan, C.c_void_p))
+        key += (f" | {'T' if d.a_trans else 'N'}{'T' if d.b_trans else 'N'} {d.M}x{d.N}x{d.K}"
+                f" split{plan[1]} wg{plan[2]}")
     _probe.records.append((key, 2.0 * d.M * d.N * d.K, e0, e1))
 
 

@@ -220,12 +220,34 @@ def _equiv_worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, {s: _equiv_run(world, rank, sparse=s) for s in (True, False)}, None))
+        res = {s: _equiv_run(world, rank, sparse=s) for s in (True, False)}
+        q.put((rank, _to_numpy(res), None))   # by value: the parent reads after we exit
     except Exception:
         import traceback
         q.put((rank, None, traceback.format_exc()))
     finally:
         dist.destroy_process_group()
+
+
+def _to_numpy(x):
+    if isinstance(x, torch.Tensor):
+        return x.numpy()
+    if isinstance(x, dict):
+        return {k: _to_numpy(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_numpy(v) for v in x)
+    return x
+
+
+def _to_torch(x):
+    import numpy as np
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(x)
+    if isinstance(x, dict):
+        return {k: _to_torch(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_torch(v) for v in x)
+    return x
 
 
 def _cmp(a, b):
@@ -261,12 +283,18 @@ def test_two_ranks_on_half_batches_equal_one_rank_on_the_batch():
     procs = [ctx.Process(target=_equiv_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (out, exc)) for r, out, exc in (q.get(timeout=240) for _ in procs))
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    try:
+        res = dict((r, (_to_torch(out), exc)) for r, out, exc in
+                   (q.get(timeout=240) for _ in procs))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
     for r in (0, 1):
         assert res[r][1] is None, res[r][1]
+    for p in procs:
+        assert p.exitcode == 0
     for sparse in (True, False):
         r0, r1 = res[0][0][sparse], res[1][0][sparse]
         worst_g, worst_u = [], []

@@ -1,7 +1,7 @@
 #!/usr/bin/env python
-"""Per-shape GEMM time of one cfg-2 training step (streams serialised, HIP events per
-launch): which GEMMs of the real step run below the standalone rates. Usage:
-python tools/gemm_breakdown.py [batch]"""
+"""Per-shape GEMM time of one training step of a bench.py workload (streams serialised, HIP
+events per launch): which GEMMs of the real step run below the standalone rates. Usage:
+python tools/gemm_breakdown.py [workload (cfg2|cfg3|cfg5|cfg4)] [batch]"""
 import os
 import sys
 
@@ -17,15 +17,18 @@ from savqa_amd.utils import init_params_  # noqa: E402
 
 
 def main():
-    B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    from bench import WORKLOADS
+    wl = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
+    W = WORKLOADS[wl]
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else W["batch"]
     dev = torch.device("cuda", 0)
-    model = AttModel(None, 512, 1024, 914, 40, 450, 49, 6, 8, 0.5, 0.1, 311, True, device=dev,
-                     init=False)
+    model = AttModel(None, W["d"], 1024, 914, 40, 450, 49, 6, W["H"], 0.5, 0.1, 311, True,
+                     device=dev, init=False, gemm_precision=W.get("prec", "fp32"))
     init_params_(model, seed=0)
     model.train()
     model._engine.concurrent = False
     opt = Adam(model, lr=1e-4)
-    batch = synthetic_batch(B, Nv=36, Ns=59, seed=1234, device=dev)
+    batch = synthetic_batch(B, Nv=W["Nv"], Ns=W["Ns"], seed=1234, device=dev)
     margs = model_args(batch)
 
     def step():
@@ -43,7 +46,7 @@ def main():
     ops.set_gemm_probe(None)
     agg = probe.summary()
     tot = sum(v[2] for v in agg.values())
-    print(f"total GEMM {tot:.2f} ms/step, {sum(v[1] for v in agg.values()) / tot / 1e9:.1f} TF")
+    print(f"{wl} B={B}: total GEMM {tot:.2f} ms/step, {sum(v[1] for v in agg.values()) / tot / 1e9:.1f} TF")
     for k, (n, fl, ms) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
         print(f"{ms:8.3f} ms {100 * ms / tot:5.1f}%  n={n:3d}  {fl / ms / 1e9:7.1f} TF  {k}")
 
