@@ -357,8 +357,10 @@ int savqa_mil_bwd(void* stream, const float* Pf, const float* Nf, const float* v
                   const int32_t* mask, int64_t BN, int64_t K, int64_t H, float eps,
                   const float* dobj, const float* dmil, float* dPf, float* dNf, float* dv);
 
-/* macro[b*Ns + loc[b,n]][:] = obj[b*Nv+n][:] for loc >= 0 (AttModel_x3.py:377-380),
- * and its backward dobj[b*Nv+n] = dmacro[b*Ns+loc] (dobj rows with loc < 0 zeroed). */
+/* macro[b*Ns + loc[b,n]][:] = obj[b*Nv+n][:] for 0 <= loc < Ns (AttModel_x3.py:377-380),
+ * and its backward dobj[b*Nv+n] = dmacro[b*Ns+loc] (dobj rows with loc outside [0, Ns)
+ * zeroed). The reference raises IndexError on loc >= Ns; here such a location is never
+ * dereferenced (no write, zero gradient) -- collate.pack rejects it on the host. */
 int savqa_index_put_rows(void* stream, const int64_t* loc, int64_t B, int64_t Nv, int64_t Ns,
                          int64_t H, const float* obj, float* macro);
 int savqa_index_get_rows(void* stream, const int64_t* loc, int64_t B, int64_t Nv, int64_t Ns,

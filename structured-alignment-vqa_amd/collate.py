@@ -170,6 +170,10 @@ def pack(data, relations: Optional[bool] = None,
         return out
 
     locs = rows_of(cols["macro_obj_locs"], 1, T_v, "macro_obj_locs")
+    if any(l.size and int(l.max()) >= T_s for l in locs):
+        # the model would index new_macro_ipt past its T_s rows: the reference's MIL_NCE raises
+        # IndexError there (AttModel_x3.py:377-380); the kernels never dereference such a row
+        raise IndexError(f"collate: a macro_obj_locs entry is >= the {T_s} macro nodes")
     pos = rows_of(cols["micro_positive_nodes_wrd"], topN, T_v, "micro_positive_nodes_wrd")
     neg = rows_of(cols["micro_negative_nodes_wrd"], topN, T_v, "micro_negative_nodes_wrd")
     macro_edges = _edges(cols["macro_edges"], T_s, True)

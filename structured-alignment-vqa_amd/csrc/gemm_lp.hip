@@ -153,6 +153,158 @@ __device__ __forceinline__ i32x8 frag_fp8(const char* img, int base, int lane) {
 
 __device__ __forceinline__ float bf2f(__bf16 v) { return (float)v; }
 
+// Row-major store of G rows of one wave's staged [64][64] image (rows 4(Gh + q) + lane/16,
+// q < G; 4 columns per lane), with every epilogue operand of the G rows loaded BEFORE the
+// first store: a load issued after a store waits for it (vmcnt counts both), so loading
+// per row serialised the whole epilogue on store latency. Requires the vector layout
+// (N % 4 == 0, 16-B / 8-B aligned rows: lp_vec_epilogue). Rows past M and columns past N
+// load a clamped (valid) address and are not stored. MK: 0 none, 1 bf16 mask, 2 fp32 mask.
+template <int G, bool RES, int MK, bool RV>
+__device__ __forceinline__ void lp_rows(const savqa_gemm_lp_desc& d, const char* reg,
+                                         int64_t rbase, int h, int64_t n, bool nok, int64_t nc,
+                                         f4 bv, bool ident, int lane) {
+  const int c = lane & 15;
+  f4 rs[G], rv[G], mk[G];
+#pragma unroll
+  for (int q = 0; q < G; ++q) {
+    const int lr = 4 * (G * h + q) + (lane >> 4);
+    int64_t m = rbase + lr;
+    m = m < d.M ? m : d.M - 1;
+    if constexpr (RES) rs[q] = *reinterpret_cast<const f4*>(d.resid + m * d.ldr + nc);
+    if constexpr (RV)
+      rv[q] = *reinterpret_cast<const f4*>(d.rowvec + (m % d.rowvec_period) * d.ldrv + nc);
+    if constexpr (MK != 0) {
+      const int64_t mr = d.mask_arows ? d.a_rows[m] : m;
+      if constexpr (MK == 1)
+        mk[q] = __builtin_convertvector(
+            *reinterpret_cast<const bf16x4*>(static_cast<const __bf16*>(d.mask) + mr * d.ldmask + nc), f4);
+      else
+        mk[q] = *reinterpret_cast<const f4*>(static_cast<const float*>(d.mask) + mr * d.ldmask + nc);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < G; ++q) {
+    const int lr = 4 * (G * h + q) + (lane >> 4);
+    const int64_t m = rbase + lr;
+    f4 v = *reinterpret_cast<const f4*>(reg + (lr & 63) * 256 + ((c ^ (lr & 15)) * 16));
+    v = v * d.alpha + bv;
+    if constexpr (RV) v += rv[q];
+    if (d.relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+    }
+    if constexpr (MK != 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!(mk[q][r] > 0.f)) v[r] = 0.f;
+    }
+    if constexpr (RES) v += rs[q];
+    if (m < d.M && nok) {
+      int64_t cr = m;
+      if (!ident) {
+        const uint32_t mu = (uint32_t)m, cg = (uint32_t)d.c_group;
+        cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
+      }
+      if (d.C) *reinterpret_cast<f4*>(d.C + cr * d.ldc + n) = v;
+      if (d.Cb)
+        *reinterpret_cast<bf16x4*>(static_cast<__bf16*>(d.Cb) + cr * d.ldcb + n) =
+            __builtin_convertvector(v, bf16x4);
+    }
+  }
+}
+
+// whether every epilogue operand and output allows the vector rows of lp_rows
+__host__ __device__ __forceinline__ bool lp_vec_epilogue(const savqa_gemm_lp_desc& d) {
+  auto al = [](const void* p, int b) { return (((uintptr_t)p) & (b - 1)) == 0; };
+  if (d.N % 4) return false;
+  if (d.rowvec && (d.resid || d.mask)) return false;  // not instantiated: per-row path
+  if (d.C && ((d.ldc & 3) || !al(d.C, 16))) return false;
+  if (d.Cb && ((d.ldcb & 3) || !al(d.Cb, 8))) return false;
+  if (d.resid && ((d.ldr & 3) || !al(d.resid, 16))) return false;
+  if (d.rowvec && ((d.ldrv & 3) || !al(d.rowvec, 16))) return false;
+  if (d.mask && ((d.ldmask & 3) || !al(d.mask, d.mask_type == SAVQA_DT_BF16 ? 8 : 16))) return false;
+  return true;
+}
+
+// Wide row stores for bf16-only outputs: a wave64 store of bf16x4 per lane (8 B) makes the
+// epilogue store-issue-bound (cdna_hip_programming.md T21), so each lane takes 8 consecutive
+// columns (two 16-B chunks of the staged fp32 row) and stores them as one 16-B bf16x8: 8 lanes
+// per 128-B row segment, 8 rows per instruction, 8 instructions per 64-row pass. Optional
+// bf16 ReLU-backward mask (16-B loads in the same map), loaded here or prefetched (PRE).
+__host__ __device__ __forceinline__ bool lp_wide_epilogue(const savqa_gemm_lp_desc& d) {
+  auto al = [](const void* p, int b) { return (((uintptr_t)p) & (b - 1)) == 0; };
+  if (!d.Cb || d.C || d.resid || d.rowvec || d.atomic || d.N % 8) return false;
+  if ((d.ldcb & 7) || !al(d.Cb, 16)) return false;
+  if (d.mask && (d.mask_type != SAVQA_DT_BF16 || (d.ldmask & 7) || !al(d.mask, 16))) return false;
+  return true;
+}
+
+// the mask rows of one lane in the wide map (rows rb + 8q + lane/8, columns col0 + 8(lane%8))
+__device__ __forceinline__ void lp_wide_mask(const savqa_gemm_lp_desc& d, bf16x8 (&mk)[8],
+                                             int64_t rb, int64_t col0, int lane) {
+  const int64_t n = col0 + 8 * (lane & 7);
+  const int64_t nc = n < d.N ? n : d.N - 8;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    int64_t m = rb + 8 * q + (lane >> 3);
+    m = m < d.M ? m : d.M - 1;
+    const int64_t mr = d.mask_arows ? d.a_rows[m] : m;
+    mk[q] = *reinterpret_cast<const bf16x8*>(static_cast<const __bf16*>(d.mask) + mr * d.ldmask + nc);
+  }
+}
+
+template <bool HAVE_MASK>
+__device__ __forceinline__ void lp_pass_wide(const savqa_gemm_lp_desc& d, const char* reg,
+                                             int64_t rb, int64_t col0, bool first_split,
+                                             const bf16x8 (&mk)[8], int lane) {
+  const int c8 = lane & 7, r8 = lane >> 3;
+  const bool ident = d.c_group <= 0;
+  const int64_t n = col0 + 8 * c8;
+  const bool nok = n < d.N;  // N % 8 == 0: a lane's 8 columns are all in or all out
+  const int64_t nc = nok ? n : d.N - 8;
+  f4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  if (first_split && d.bias) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      b0[r] = d.bias[nc + r];
+      b1[r] = d.bias[nc + 4 + r];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int lr = 8 * q + r8;
+    const int64_t m = rb + lr;
+    f4 lo = *reinterpret_cast<const f4*>(reg + lr * 256 + (((2 * c8) ^ (lr & 15)) * 16));
+    f4 hi = *reinterpret_cast<const f4*>(reg + lr * 256 + (((2 * c8 + 1) ^ (lr & 15)) * 16));
+    lo = lo * d.alpha + b0;
+    hi = hi * d.alpha + b1;
+    if (d.relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        lo[r] = fmaxf(lo[r], 0.f);
+        hi[r] = fmaxf(hi[r], 0.f);
+      }
+    }
+    if constexpr (HAVE_MASK) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!((float)mk[q][r] > 0.f)) lo[r] = 0.f;
+        if (!((float)mk[q][4 + r] > 0.f)) hi[r] = 0.f;
+      }
+    }
+    if (m < d.M && nok) {
+      int64_t cr = m;
+      if (!ident) {
+        const uint32_t mu = (uint32_t)m, cg = (uint32_t)d.c_group;
+        cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
+      }
+      const bf16x4 l = __builtin_convertvector(lo, bf16x4), h = __builtin_convertvector(hi, bf16x4);
+      *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(d.Cb) + cr * d.ldcb + n) =
+          bf16x8{l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+    }
+  }
+}
+
 // Epilogue of one wave's TM x 64 output tile (savqa_gemm_lp formula), staged through the
 // wave's own 16 KB of LDS in passes of 64 rows so that the global traffic is whole rows:
 // the swapped-MFMA accumulators (lane: 4 consecutive columns of one row) are written as
@@ -210,6 +362,45 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
         }
         atomicAdd(d.C + cr * d.ldc + n, v);
       }
+    } else if (lp_wide_epilogue(d)) {
+      const int64_t rb = row0 + 64 * pass;
+      bf16x8 mk[8];
+      if (d.mask) {
+        lp_wide_mask(d, mk, rb, col0, lane);
+        lp_pass_wide<true>(d, reg, rb, col0, first_split, mk, lane);
+      } else {
+        lp_pass_wide<false>(d, reg, rb, col0, first_split, mk, lane);
+      }
+    } else if (lp_vec_epilogue(d)) {
+      // 16 lanes per row, 4 rows per instruction, groups of G instructions per pass, each
+      // group's operand loads issued before its stores
+      const int64_t n = col0 + 4 * (lane & 15);
+      const bool nok = n < d.N;  // N % 4 == 0: a lane's 4 columns are all in or all out
+      const int64_t nc = nok ? n : d.N - 4;
+      f4 bv = {0.f, 0.f, 0.f, 0.f};
+      if (first_split && d.bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = d.bias[nc + r];
+      }
+      const bool res = first_split && d.resid, rv = first_split && d.rowvec;
+      const int mk = !d.mask ? 0 : (d.mask_type == SAVQA_DT_BF16 ? 1 : 2);
+      const int64_t rb = row0 + 64 * pass;
+      // (groups of 4 rows when the wave still holds a second pass of accumulators)
+      constexpr int G = FM > 4 ? 4 : 8;
+#define SAVQA_ROWS(R_, M_, V_)                                                  \
+  for (int h = 0; h < 16 / G; ++h) lp_rows<G, R_, M_, V_>(d, reg, rb, h, n, nok, nc, bv, ident, lane)
+      if (rv) {
+        SAVQA_ROWS(false, 0, true);   // the input projection: + position table, no mask / resid
+      } else if (res) {
+        if (mk == 1) SAVQA_ROWS(true, 1, false);
+        else if (mk == 2) SAVQA_ROWS(true, 2, false);
+        else SAVQA_ROWS(true, 0, false);
+      } else {
+        if (mk == 1) SAVQA_ROWS(false, 1, false);
+        else if (mk == 2) SAVQA_ROWS(false, 2, false);
+        else SAVQA_ROWS(false, 0, false);
+      }
+#undef SAVQA_ROWS
     } else {
       // 16 lanes per row, 4 rows per instruction, 16 instructions per pass
       const int c = lane & 15;
@@ -300,7 +491,97 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
   }
 }
 
-template <bool AT, bool BT, bool FP8>
+// Epilogue operands prefetched under the last k-tile's MFMAs (128 x 128 kernel, one 64-row
+// pass per wave): PRE = 1 the fp32 residual (the 16 rows x 4 columns each lane stores,
+// lp_rows' map), PRE = 2 the bf16 ReLU-backward mask of a bf16-only output (optionally through
+// the A-row gather; lp_pass_wide's map).
+// Chosen by the host for non-atomic, unsplit launches in the vector layout with exactly
+// that one operand; their loads then overlap the k-loop instead of following it.
+// (the residual's second 8 rows are loaded at the start of the epilogue, before any store:
+// 16 prefetched f4s beside the accumulators spill)
+template <int PRE>
+struct LpPre {
+  f4 r[PRE == 1 ? 8 : 1];
+  bf16x8 m[PRE == 2 ? 8 : 1];
+
+  __device__ __forceinline__ void load(const savqa_gemm_lp_desc& d, int64_t row0, int64_t col0,
+                                       int lane) {
+    const int64_t n = col0 + 4 * (lane & 15);
+    const int64_t nc = n < d.N ? n : d.N - 4;
+    if constexpr (PRE == 1) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        int64_t m = row0 + 4 * q + (lane >> 4);
+        m = m < d.M ? m : d.M - 1;
+        r[q] = *reinterpret_cast<const f4*>(d.resid + m * d.ldr + nc);
+      }
+    }
+    if constexpr (PRE == 2) lp_wide_mask(d, this->m, row0, col0, lane);
+  }
+};
+
+template <int PRE>
+__device__ __forceinline__ void lp_epilogue_pre(const savqa_gemm_lp_desc& d, f4 (&acc)[4][4],
+                                                char* reg, int64_t row0, int64_t col0,
+                                                const LpPre<PRE>& pre, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int lr = 16 * i + (lane & 15);
+      *reinterpret_cast<f4*>(reg + lr * 256 + (((4 * j + g) ^ (lr & 15)) * 16)) = acc[i][j];
+    }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is complete
+  __builtin_amdgcn_wave_barrier();
+  if constexpr (PRE == 2) {
+    lp_pass_wide<true>(d, reg, row0, col0, true, pre.m, lane);
+    return;
+  }
+  const bool ident = d.c_group <= 0;
+  const int64_t n = col0 + 4 * c;
+  const bool nok = n < d.N;
+  const int64_t nc = nok ? n : d.N - 4;
+  f4 bv = {0.f, 0.f, 0.f, 0.f};
+  if (d.bias) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = d.bias[nc + r];
+  }
+  f4 r2[PRE == 1 ? 8 : 1];
+  if constexpr (PRE == 1) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      int64_t m = row0 + 4 * (q + 8) + (lane >> 4);
+      m = m < d.M ? m : d.M - 1;
+      r2[q] = *reinterpret_cast<const f4*>(d.resid + m * d.ldr + nc);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int lr = 4 * q + (lane >> 4);
+    const int64_t m = row0 + lr;
+    f4 v = *reinterpret_cast<const f4*>(reg + lr * 256 + ((c ^ (lr & 15)) * 16));
+    v = v * d.alpha + bv;
+    if (d.relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+    }
+    if constexpr (PRE == 1) v += q < 8 ? pre.r[q & 7] : r2[q & 7];
+    if (m < d.M && nok) {
+      int64_t cr = m;
+      if (!ident) {
+        const uint32_t mu = (uint32_t)m, cg = (uint32_t)d.c_group;
+        cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
+      }
+      if (d.C) *reinterpret_cast<f4*>(d.C + cr * d.ldc + n) = v;
+      if (d.Cb)
+        *reinterpret_cast<bf16x4*>(static_cast<__bf16*>(d.Cb) + cr * d.ldcb + n) =
+            __builtin_convertvector(v, bf16x4);
+    }
+  }
+}
+
+template <bool AT, bool BT, bool FP8, int PRE>
 __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   const savqa_gemm_lp_desc& d = args.d;
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * LP_IMG];
@@ -328,6 +609,10 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  LpPre<PRE> pre;
+  if constexpr (PRE != 0) {
+    if (nt == 0) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
+  }
 
   // fp8 block scales of this lane's rows: A rows (m), B rows (n), block k/32 + g
   int sca[4], scb[4];
@@ -372,6 +657,8 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
       if (kt + 1 < nt) {  // next k-tile into the other buffer (read one barrier ago)
         stage(smem + ((kt + 1) & 1) * 2 * LP_IMG, kt + 1);
         load_scales(kt + 1);
+      } else if constexpr (PRE != 0) {  // last k-tile: epilogue operands under its MFMAs
+        pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
       }
       if constexpr (FP8) {
         i32x8 a[4], b[4];
@@ -406,7 +693,10 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
 
   // ---------------------------------------------------------------- epilogue
   __syncthreads();  // every wave's last k-tile reads are done: LDS is free
-  lp_epilogue<4, 4>(d, acc, smem + wave * 16384, m0 + wm * 64, n0 + wn * 64, first_split, lane);
+  if constexpr (PRE != 0)
+    lp_epilogue_pre<PRE>(d, acc, smem + wave * 16384, m0 + wm * 64, n0 + wn * 64, pre, lane);
+  else
+    lp_epilogue<4, 4>(d, acc, smem + wave * 16384, m0 + wm * 64, n0 + wn * 64, first_split, lane);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -737,15 +1027,27 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
     if (var == 3) SAVQA_LP2(256, 2, 64, 2);
     else SAVQA_LP2(128, 4, 64, 3);
 #undef SAVQA_LP2
-  } else if (fp8)
-    hipLaunchKernelGGL((gemm_lp_kernel<false, true, true>), grid, block, 0, s, a);
-  else if (!d.a_trans && d.b_trans)
-    hipLaunchKernelGGL((gemm_lp_kernel<false, true, false>), grid, block, 0, s, a);
-  else if (!d.a_trans && !d.b_trans)
-    hipLaunchKernelGGL((gemm_lp_kernel<false, false, false>), grid, block, 0, s, a);
-  else if (d.a_trans && !d.b_trans)
-    hipLaunchKernelGGL((gemm_lp_kernel<true, false, false>), grid, block, 0, s, a);
-  else
-    hipLaunchKernelGGL((gemm_lp_kernel<true, true, false>), grid, block, 0, s, a);
+  } else if (fp8) {
+    hipLaunchKernelGGL((gemm_lp_kernel<false, true, true, 0>), grid, block, 0, s, a);
+  } else {
+    // epilogue operand prefetched under the last k-tile (LpPre): one residual or one bf16
+    // mask, nothing else to load, whole tiles (no split), vector layout
+    int pre = 0;
+    if (p.nsplit == 1 && !d.atomic && !d.rowvec && lp_vec_epilogue(d)) {
+      if (d.resid && !d.mask) pre = 1;
+      else if (d.mask && lp_wide_epilogue(d)) pre = 2;
+    }
+#define SAVQA_LP1(AT_, BT_)                                                                   \
+  do {                                                                                        \
+    if (pre == 1) hipLaunchKernelGGL((gemm_lp_kernel<AT_, BT_, false, 1>), grid, block, 0, s, a); \
+    else if (pre == 2) hipLaunchKernelGGL((gemm_lp_kernel<AT_, BT_, false, 2>), grid, block, 0, s, a); \
+    else hipLaunchKernelGGL((gemm_lp_kernel<AT_, BT_, false, 0>), grid, block, 0, s, a);     \
+  } while (0)
+    if (!d.a_trans && d.b_trans) SAVQA_LP1(false, true);
+    else if (!d.a_trans && !d.b_trans) SAVQA_LP1(false, false);
+    else if (d.a_trans && !d.b_trans) SAVQA_LP1(true, false);
+    else SAVQA_LP1(true, true);
+#undef SAVQA_LP1
+  }
   return check_launch("savqa_gemm_lp");
 }

@@ -265,7 +265,7 @@ __global__ void index_put_rows_kernel(const int64_t* __restrict__ loc, int64_t N
   const int64_t b = blockIdx.x;
   for (int64_t n = 0; n < Nv; ++n) {
     const int64_t l = loc[b * Nv + n];
-    if (l < 0) continue;
+    if (l < 0 || l >= Ns) continue;  // LOC_PAD; an out-of-range location writes nothing
     for (int64_t c = threadIdx.x; c < H; c += blockDim.x)
       macro[(b * Ns + l) * H + c] = obj[(b * Nv + n) * H + c];
     __syncthreads();
@@ -279,7 +279,7 @@ __global__ void index_get_rows_kernel(const int64_t* __restrict__ loc, int64_t N
   const int64_t b = bn / Nv;
   const int64_t l = loc[bn];
   for (int64_t c = threadIdx.x; c < H; c += blockDim.x)
-    dobj[bn * H + c] = l >= 0 ? dmacro[(b * Ns + l) * H + c] : 0.f;
+    dobj[bn * H + c] = (l >= 0 && l < Ns) ? dmacro[(b * Ns + l) * H + c] : 0.f;
 }
 
 // ------------------------------------------------------------------ loss

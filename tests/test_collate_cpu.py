@@ -129,3 +129,22 @@ def test_pack_plan_expands_to_reference(name):
         g = gold[f"{name}:{k}"]
         assert res[k].dtype == g.dtype and res[k].shape == g.shape, k
         assert np.array_equal(res[k], g), k
+
+
+
+def test_object_location_past_the_macro_nodes_raises():
+    """A macro_obj_locs entry >= the padded macro-node count is an IndexError in the
+    reference's MIL_NCE (AttModel_x3.py:377-380); pack() raises it on the host (the kernels
+    never dereference such a row)."""
+    from savqa_amd.collate import pack
+    data = ocol.make_samples(3, fea_dim=8, topN=3, tag="loc", edge_cases=False)
+    T_s = max(np.asarray(d[1]).reshape(-1).shape[0] for d in data)
+    s = list(data[0])
+    locs = np.asarray(s[2], dtype=np.int64).reshape(-1).copy()
+    locs[0] = T_s
+    s[2] = locs
+    with pytest.raises(IndexError):
+        pack([tuple(s), data[1], data[2]])
+    locs[0] = T_s - 1
+    s[2] = locs
+    pack([tuple(s), data[1], data[2]])

@@ -119,6 +119,94 @@ def test_bf16_epilogues_rows_mask_resid_rowvec():
     assert (C[untouched] == 7.0).all()
 
 
+@pytest.mark.parametrize("hint", [1, 3, 4])
+@pytest.mark.parametrize("mtype,arows,resid,rowvec", [
+    ("bf16", False, False, False), ("bf16", True, True, False), ("f32", False, True, False),
+    (None, False, True, False), (None, False, False, True)])
+def test_bf16_vector_epilogue_prefetched_rows(hint, mtype, arows, resid, rowvec):
+    """The vector epilogue (N % 4 == 0, aligned rows: every operand of a group of rows is
+    loaded before its stores) for each operand combination the training step uses -- ReLU-
+    backward mask (bf16 / fp32, direct or through the A-row gather), residual, position
+    rows -- with fp32 + bf16 outputs through a c_group row map, M / N edge tiles (N = 264:
+    a lane group past N), on every kernel variant."""
+    O = ops()
+    M, N, K, T, G = 1300, 264, 192, 50, 14
+    src = bf((1500, K), 15)
+    rows = torch.randperm(1500, device=dev)[:M].contiguous() if arows else None
+    A = src if arows else src[:M].contiguous()
+    W = bf((N, K), 16)
+    mrows = 1500 if arows else M
+    mask = None
+    if mtype == "bf16":
+        mask = bf((mrows, N), 17)
+    elif mtype == "f32":
+        mask = torch.randn(mrows, N, device=dev)
+    R = torch.randn(M, N, device=dev) if resid else None
+    rv = torch.randn(T, N, device=dev) if rowvec else None
+    bias = torch.randn(N, device=dev)
+    Cn = M // G * T + T
+    C = torch.full((Cn, N), 7.0, device=dev)
+    Cb = torch.full((Cn, N), 7.0, device=dev, dtype=torch.bfloat16)
+    O.gemm_lp(A, W, M, N, K, lda=K, ldb=K, b_trans=True, a_rows=rows, C=C, ldc=N, Cb=Cb,
+              ldcb=N, c_group=G, c_stride=T, c_offset=3, bias=bias, rowvec=rv, ldrv=N,
+              rowvec_period=T, resid=R, ldr=N, mask=mask, ldmask=N, mask_arows=arows,
+              relu=mask is None, tile_hint=hint)
+    m = torch.arange(M, device=dev)
+    Ad = (src[rows] if arows else A).double()
+    v = Ad @ W.double().t() + bias.double()
+    if rv is not None:
+        v = v + rv.double()[m % T]
+    if mask is None:
+        v = torch.relu(v)
+    else:
+        mk = (mask[rows] if arows else mask).double()
+        v = torch.where(mk > 0, v, torch.zeros_like(v))
+    if R is not None:
+        v = v + R.double()
+    crow = (m // G) * T + m % G + 3
+    assert rel(C[crow], v) < 2e-5
+    assert torch.equal(Cb[crow].cpu(), C[crow].to(torch.bfloat16).cpu())
+    untouched = torch.ones(Cn, dtype=torch.bool, device=dev)
+    untouched[crow] = False
+    assert (C[untouched] == 7.0).all() and (Cb[untouched].float() == 7.0).all()
+
+
+@pytest.mark.parametrize("hint", [1, 3, 4])
+@pytest.mark.parametrize("mask,arows,N", [(False, False, 264), (True, False, 264), (True, True, 136),
+                                          (True, False, 2048)])
+def test_bf16_only_output_wide_stores(hint, mask, arows, N):
+    """bf16-only outputs (the forward's ReLU activations, the FFN's masked dX) take the wide
+    epilogue: 8 columns per lane, 16-B bf16 stores and 16-B mask loads (prefetched under the
+    last k-tile on the 128 x 128 kernel), through a c_group row map, M / N edge tiles."""
+    O = ops()
+    M, K, T, G = 1300, 320, 50, 14
+    src = bf((1500, K), 25)
+    rows = torch.randperm(1500, device=dev)[:M].contiguous() if arows else None
+    A = src if arows else src[:M].contiguous()
+    W = bf((N, K), 26)
+    mk = bf((1500 if arows else M, N), 27) if mask else None
+    bias = torch.randn(N, device=dev)
+    Cn = M // G * T + T
+    Cb = torch.full((Cn, N), 7.0, device=dev, dtype=torch.bfloat16)
+    O.gemm_lp(A, W, M, N, K, lda=K, ldb=K, b_trans=True, a_rows=rows, Cb=Cb, ldcb=N, c_group=G,
+              c_stride=T, c_offset=3, bias=bias, mask=mk, ldmask=N, mask_arows=arows,
+              relu=not mask, tile_hint=hint)
+    m = torch.arange(M, device=dev)
+    Ad = (src[rows] if arows else A).double()
+    v = Ad @ W.double().t() + bias.double()
+    if mask:
+        v = torch.where((mk[rows] if arows else mk).double() > 0, v, torch.zeros_like(v))
+    else:
+        v = torch.relu(v)
+    crow = (m // G) * T + m % G + 3
+    assert rel(Cb[crow].float(), v) < 8e-3            # bf16 rounding of the output
+    assert torch.equal(Cb[crow].cpu(), v.float().to(torch.bfloat16).cpu()) or \
+        float((Cb[crow].double() - v).abs().max()) <= float(v.abs().max()) * 2 ** -8
+    untouched = torch.ones(Cn, dtype=torch.bool, device=dev)
+    untouched[crow] = False
+    assert (Cb[untouched].float() == 7.0).all()
+
+
 def test_gemm_lp_rejects_unsupported():
     O = ops()
     A = bf((100, 60), 8)

@@ -23,7 +23,7 @@ def test_training_step_captured_into_a_hip_graph(prec):
                  init=False, gemm_precision=prec)
     init_params_(m, seed=5)
     m.train()
-    batch = synthetic_batch(16, Nv=36, Lq=14, Ns=30, topN=5, num_classes=40, seed=9,
+    batch = synthetic_batch(16, Nv=36, Lq=14, Ns=40, topN=5, num_classes=40, seed=9,
                             device="cuda")
     args = model_args(batch)
     opt = Adam(m, lr=1e-3)
@@ -58,9 +58,14 @@ def test_training_step_captured_into_a_hip_graph(prec):
         a.generation += 1
 
     st = save()
-    step()
-    torch.cuda.synchronize()
-    eager_p, eager_loss = a.flat[:a.n_live].clone(), float(out["loss"])
+    eager = []
+    for _ in range(2):   # the eager step twice from the same state (determinism check)
+        load(st)
+        torch.cuda.synchronize()
+        step()
+        torch.cuda.synchronize()
+        eager.append((a.flat[:a.n_live].clone(), a.grad.clone(), float(out["loss"])))
+    eager_p, eager_g, eager_loss = eager[0]
 
     load(st)
     torch.cuda.synchronize()
@@ -74,10 +79,28 @@ def test_training_step_captured_into_a_hip_graph(prec):
         torch.cuda.synchronize()
         g.replay()
         torch.cuda.synchronize()
-        rep.append((a.flat[:a.n_live].clone(), float(static_loss)))
-    for p, loss in rep:
+        rep.append((a.flat[:a.n_live].clone(), a.grad.clone(), float(static_loss)))
+
+    def rel(x, y):
+        return float((x - y).abs().max() / y.abs().max())
+
+    def worst(x, y):
+        out = []
+        for n in a.live_names:
+            o, shp = a.offsets[n]
+            yy = y[o:o + shp.numel()]
+            e = float((x[o:o + shp.numel()] - yy).abs().max() / yy.abs().max().clamp_min(1e-30))
+            out.append((e, n))
+        return sorted(out, reverse=True)[:12]
+
+    diag = {"eager_p": rel(eager[1][0], eager_p), "eager_g": rel(eager[1][1], eager_g),
+            "rep_p": rel(rep[1][0], rep[0][0]), "rep_g": rel(rep[1][1], rep[0][1]),
+            "rep_vs_eager_p": rel(rep[0][0], eager_p), "rep_vs_eager_g": rel(rep[0][1], eager_g),
+            "worst_g": worst(rep[0][1], eager_g), "worst_eager_g": worst(eager[1][1], eager_g)}
+    print("graph-capture diagnostics:", diag)
+    for p, gr, loss in rep:
         assert abs(loss - eager_loss) <= 1e-5 * abs(eager_loss), (loss, eager_loss)
-        d = (p - eager_p).abs().max() / eager_p.abs().max()
-        assert float(d) <= 1e-5, float(d)
+        assert rel(gr, eager_g) <= 1e-5, diag
+        assert rel(p, eager_p) <= 1e-5, diag
         assert not torch.equal(p, st[0][:a.n_live])   # the replay did update the parameters
-    assert float((rep[0][0] - rep[1][0]).abs().max() / rep[0][0].abs().max()) <= 1e-5
+    assert diag["rep_p"] <= 1e-5, diag

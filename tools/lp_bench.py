@@ -39,7 +39,16 @@ def bf16_case(lay, m, n, k, out, hint=0):
         A, B = torch.randn(k, m, device=dev).to(BF), torch.randn(k, n, device=dev).to(BF)
         kw = dict(lda=m, ldb=n, a_trans=True)
         ref = lambda: torch.mm(A.t(), B)
-    if out == "bf16":
+    if out == "bf16mask":   # the ReLU-backward dX of the FFN: bf16 out, bf16 mask
+        Cb = torch.empty(m, n, device=dev, dtype=BF)
+        mk = torch.randn(m, n, device=dev).to(BF)
+        f = lambda: ops.gemm_lp(A, B, m, n, k, Cb=Cb, ldcb=n, mask=mk, ldmask=n, tile_hint=hint,
+                                **kw)
+    elif out == "f32resid":  # FFN conv2 forward / dX with the residual: fp32 out + resid
+        C = torch.empty(m, n, device=dev)
+        R = torch.randn(m, n, device=dev)
+        f = lambda: ops.gemm_lp(A, B, m, n, k, C=C, ldc=n, resid=R, ldr=n, tile_hint=hint, **kw)
+    elif out == "bf16":
         Cb = torch.empty(m, n, device=dev, dtype=BF)
         f = lambda: ops.gemm_lp(A, B, m, n, k, Cb=Cb, ldcb=n, relu=True, tile_hint=hint, **kw)
     elif out == "atomic":
@@ -75,7 +84,9 @@ def main():
              ("dx ffn2", "NN", Ms, 2048, 512, "bf16"), ("dx ffn1", "NN", Ms, 512, 2048, "f32"),
              ("dx qkv", "NN", Ms, 512, 1536, "f32"), ("dx kv", "NN", Ms, 512, 6144, "f32"),
              ("dw qkv", "TN", 1536, 512, Ms, "atomic"), ("dw ffn1", "TN", 2048, 512, Ms, "atomic"),
-             ("dw ffn2", "TN", 512, 2048, Ms, "atomic"), ("dw kv", "TN", 6144, 512, Ms, "atomic")]
+             ("dw ffn2", "TN", 512, 2048, Ms, "atomic"), ("dw kv", "TN", 6144, 512, Ms, "atomic"),
+             ("dx ffn2 m", "NN", Ms, 2048, 512, "bf16mask"), ("fwd ffn2 r", "NT", Ms, 512, 2048, "f32resid"),
+             ("dx ffn1 r", "NN", Ms, 512, 2048, "f32resid")]
     hints = [0] + ([1, 3, 4] if "--variants" in sys.argv else [])
     if "--dbg" in sys.argv:  # v3 as is / without MFMAs / without k-loop DMAs
         hints = [3, 3 + 256, 3 + 512, 4, 4 + 256, 4 + 512]
@@ -91,7 +102,7 @@ def main():
         for _ in range(3):  # interleaved rounds (rule 24), min
             for h in hints:
                 ts[h].append(timeit(fs[h][0]))
-        line = f"{name:10s} {lay} {m:6d}x{n:5d}x{k:6d} {out:6s}"
+        line = f"{name:10s} {lay} {m:6d}x{n:5d}x{k:6d} {out:8s}"
         for h in hints:
             t1 = min(ts[h])
             tot_t[h] += t1
