@@ -164,15 +164,20 @@ WORKLOADS = {
                       "divide d=1024) L=6, MIL-NCE only_obj topN=5 H=1024, 914 classes, decMask"),
 }
 
-ROOFLINE_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                             "r01_bench_roofline.json")
+PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+# committed PMC passes of each workload's bench command (tools/profile_round.sh)
+ROOFLINE_JSON = {"cfg2": "r02_cfg2_roofline.json", "cfg3": "r02_cfg3_roofline.json",
+                 "cfg5": "r02_cfg5_roofline.json"}
 
 
-def committed_traffic(variant):
+def committed_traffic(variant, workload="cfg2"):
     """HBM bytes per launch of `variant` from the committed PMC passes of this command
     (tools/summarize_prof.py: 2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected), or None."""
+    name = ROOFLINE_JSON.get(workload)
+    if name is None:
+        return None
     try:
-        with open(ROOFLINE_JSON) as f:
+        with open(os.path.join(PROFILES, name)) as f:
             t = json.load(f)["traffic"].get(variant)
         return None if t is None else round(t["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError):
@@ -313,7 +318,7 @@ def main():
                 "avg_launch_us": round(ms / n * 1e3, 2), "flops_per_launch": flops / n,
                 "achieved": round(achieved, 2), "peak": kpeak, "unit": "TFLOP/s",
                 "frac": round(achieved / kpeak, 4),
-                "traffic": committed_traffic(var),
+                "traffic": committed_traffic(var, args.workload),
                 "all_gemm_tflops": round(allfl / (allms * 1e-3) / 1e12, 2),
                 "gemm_ms_per_step": round(allms / 2, 2)}
 

@@ -130,7 +130,8 @@ int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* d);
 int savqa_gemm_lp_supported(const savqa_gemm_lp_desc* d);
 /* The launch plan savqa_gemm_lp would use for *d (no launch): out[0] = kernel variant
  * (1: 128x128 tile, two workgroups per CU; 3: 256x256; 4: 256x128 -- one per CU),
- * out[1] = K slices, out[2] = workgroups, out[3] = 0. */
+ * out[1] = K slices, out[2] = workgroups, out[3] = epilogue operand prefetched under the
+ * last k-tile (variant 1: 0 none, 1 the residual, 2 the bf16 mask). */
 int savqa_gemm_lp_plan(const savqa_gemm_lp_desc* d, int32_t* out);
 
 /* Conversions feeding the low-precision operands (output row of input row r: ro(r) =

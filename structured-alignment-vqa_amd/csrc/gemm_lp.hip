@@ -930,6 +930,7 @@ struct LpPlan {
   int var, split, nsplit;
   int64_t tiles, per;
   int bn;
+  int pre;  // gemm_lp_kernel's epilogue-operand prefetch (LpPre): 0 none, 1 resid, 2 bf16 mask
 };
 
 static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
@@ -966,6 +967,13 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
   }
   p.per = (nk + p.split - 1) / p.split;
   p.nsplit = nk > 0 ? (int)((nk + p.per - 1) / p.per) : 1;
+  // epilogue operand prefetched under the last k-tile (LpPre): one residual or one bf16
+  // mask, nothing else to load, whole tiles (no split), vector layout
+  p.pre = 0;
+  if (p.var == 1 && !fp8 && p.nsplit == 1 && !d.atomic && !d.rowvec && lp_vec_epilogue(d)) {
+    if (d.resid && !d.mask) p.pre = 1;
+    else if (d.mask && lp_wide_epilogue(d)) p.pre = 2;
+  }
   return p;
 }
 
@@ -986,7 +994,7 @@ extern "C" int savqa_gemm_lp_plan(const savqa_gemm_lp_desc* d, int32_t* out) {
   out[0] = p.var;
   out[1] = p.nsplit;
   out[2] = (int32_t)(p.tiles * p.nsplit);
-  out[3] = 0;
+  out[3] = p.pre;
   return 0;
 }
 
@@ -1030,13 +1038,7 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   } else if (fp8) {
     hipLaunchKernelGGL((gemm_lp_kernel<false, true, true, 0>), grid, block, 0, s, a);
   } else {
-    // epilogue operand prefetched under the last k-tile (LpPre): one residual or one bf16
-    // mask, nothing else to load, whole tiles (no split), vector layout
-    int pre = 0;
-    if (p.nsplit == 1 && !d.atomic && !d.rowvec && lp_vec_epilogue(d)) {
-      if (d.resid && !d.mask) pre = 1;
-      else if (d.mask && lp_wide_epilogue(d)) pre = 2;
-    }
+    const int pre = p.pre;
 #define SAVQA_LP1(AT_, BT_)                                                                   \
   do {                                                                                        \
     if (pre == 1) hipLaunchKernelGGL((gemm_lp_kernel<AT_, BT_, false, 1>), grid, block, 0, s, a); \

@@ -187,7 +187,7 @@ def lp_variant(d) -> str:
         return f"gemm_lp2_kernel<256,256,2,64,2,{at},{bt}>"
     if plan[0] == 4:
         return f"gemm_lp2_kernel<256,128,4,64,3,{at},{bt}>"
-    return f"gemm_lp_kernel<{at},{bt},{str(d.a_type == 2).lower()}>"
+    return f"gemm_lp_kernel<{at},{bt},{str(d.a_type == 2).lower()},{plan[3]}>"
 
 
 def lp_supported(d) -> bool:
