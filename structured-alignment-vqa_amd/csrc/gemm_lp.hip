@@ -61,7 +61,8 @@ struct LpArgs {
   int tiles_n, ntiles_k;  // k-tiles per split slice
   int64_t kchunk;         // elements of k per split slice
   int nblk;               // tiles (grid.x)
-  int dbg;                // diagnostics: 1 = skip the MFMAs, 2 = skip the k-loop DMAs
+  int dbg;                // diagnostics (bits): 1 = skip the MFMAs, 2 = skip the k-loop DMAs,
+                          // 4 = skip the epilogue (gemm_lp3_kernel)
 };
 
 // Per-lane LDS-DMA sources of one operand, resolved once per workgroup.
@@ -226,6 +227,12 @@ __host__ __device__ __forceinline__ bool lp_vec_epilogue(const savqa_gemm_lp_des
   return true;
 }
 
+// Output column of staged-image column c (0..63) of a wave tile whose two 32-column halves
+// start at col0 and col_hi (col_hi = col0 + 32 for a contiguous 64-column wave tile).
+__device__ __forceinline__ int64_t ecol(int64_t col0, int64_t col_hi, int c) {
+  return c < 32 ? col0 + c : col_hi + (c - 32);
+}
+
 // Wide row stores for bf16-only outputs: a wave64 store of bf16x4 per lane (8 B) makes the
 // epilogue store-issue-bound (cdna_hip_programming.md T21), so each lane takes 8 consecutive
 // columns (two 16-B chunks of the staged fp32 row) and stores them as one 16-B bf16x8: 8 lanes
@@ -241,8 +248,9 @@ __host__ __device__ __forceinline__ bool lp_wide_epilogue(const savqa_gemm_lp_de
 
 // the mask rows of one lane in the wide map (rows rb + 8q + lane/8, columns col0 + 8(lane%8))
 __device__ __forceinline__ void lp_wide_mask(const savqa_gemm_lp_desc& d, bf16x8 (&mk)[8],
-                                             int64_t rb, int64_t col0, int lane) {
-  const int64_t n = col0 + 8 * (lane & 7);
+                                             int64_t rb, int64_t col0, int lane,
+                                             int64_t col_hi = -1) {
+  const int64_t n = ecol(col0, col_hi < 0 ? col0 + 32 : col_hi, 8 * (lane & 7));
   const int64_t nc = n < d.N ? n : d.N - 8;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -256,10 +264,11 @@ __device__ __forceinline__ void lp_wide_mask(const savqa_gemm_lp_desc& d, bf16x8
 template <bool HAVE_MASK>
 __device__ __forceinline__ void lp_pass_wide(const savqa_gemm_lp_desc& d, const char* reg,
                                              int64_t rb, int64_t col0, bool first_split,
-                                             const bf16x8 (&mk)[8], int lane) {
+                                             const bf16x8 (&mk)[8], int lane,
+                                             int64_t col_hi = -1) {
   const int c8 = lane & 7, r8 = lane >> 3;
   const bool ident = d.c_group <= 0;
-  const int64_t n = col0 + 8 * c8;
+  const int64_t n = ecol(col0, col_hi < 0 ? col0 + 32 : col_hi, 8 * c8);
   const bool nok = n < d.N;  // N % 8 == 0: a lane's 8 columns are all in or all out
   const int64_t nc = nok ? n : d.N - 8;
   f4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
@@ -317,7 +326,9 @@ __device__ __forceinline__ void lp_pass_wide(const savqa_gemm_lp_desc& d, const 
 template <int FM, int FN>
 __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&acc)[FM][FN],
                                             char* reg, int64_t row0, int64_t col0,
-                                            bool first_split, int lane) {
+                                            bool first_split, int lane, int64_t rstep = 64,
+                                            int64_t col_hi = -1) {
+  if (col_hi < 0) col_hi = col0 + 32;
   static_assert(FN == 4, "wave tiles are 64 columns wide");
   const int g = lane >> 4;
   const bool ident = d.c_group <= 0;
@@ -336,10 +347,10 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
     __builtin_amdgcn_wave_barrier();
     if (d.atomic) {
       // one float per lane: row q, column lane (256 contiguous bytes per atomic instruction)
-      const int64_t n = col0 + lane;
+      const int64_t n = ecol(col0, col_hi, lane);
       const float bv = (first_split && d.bias && n < d.N) ? d.bias[n] : 0.f;
       for (int q = 0; q < 64; ++q) {
-        const int64_t m = row0 + 64 * pass + q;
+        const int64_t m = row0 + rstep * pass + q;
         if (m >= d.M) break;
         float v = *reinterpret_cast<const float*>(reg + q * 256 + ((((lane >> 2) ^ (q & 15)) * 16)) +
                                                   (lane & 3) * 4);
@@ -363,18 +374,18 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
         atomicAdd(d.C + cr * d.ldc + n, v);
       }
     } else if (lp_wide_epilogue(d)) {
-      const int64_t rb = row0 + 64 * pass;
+      const int64_t rb = row0 + rstep * pass;
       bf16x8 mk[8];
       if (d.mask) {
-        lp_wide_mask(d, mk, rb, col0, lane);
-        lp_pass_wide<true>(d, reg, rb, col0, first_split, mk, lane);
+        lp_wide_mask(d, mk, rb, col0, lane, col_hi);
+        lp_pass_wide<true>(d, reg, rb, col0, first_split, mk, lane, col_hi);
       } else {
-        lp_pass_wide<false>(d, reg, rb, col0, first_split, mk, lane);
+        lp_pass_wide<false>(d, reg, rb, col0, first_split, mk, lane, col_hi);
       }
     } else if (lp_vec_epilogue(d)) {
       // 16 lanes per row, 4 rows per instruction, groups of G instructions per pass, each
       // group's operand loads issued before its stores
-      const int64_t n = col0 + 4 * (lane & 15);
+      const int64_t n = ecol(col0, col_hi, 4 * (lane & 15));
       const bool nok = n < d.N;  // N % 4 == 0: a lane's 4 columns are all in or all out
       const int64_t nc = nok ? n : d.N - 4;
       f4 bv = {0.f, 0.f, 0.f, 0.f};
@@ -384,7 +395,7 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
       }
       const bool res = first_split && d.resid, rv = first_split && d.rowvec;
       const int mk = !d.mask ? 0 : (d.mask_type == SAVQA_DT_BF16 ? 1 : 2);
-      const int64_t rb = row0 + 64 * pass;
+      const int64_t rb = row0 + rstep * pass;
       // (groups of 4 rows when the wave still holds a second pass of accumulators)
       constexpr int G = FM > 4 ? 4 : 8;
 #define SAVQA_ROWS(R_, M_, V_)                                                  \
@@ -404,7 +415,7 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
     } else {
       // 16 lanes per row, 4 rows per instruction, 16 instructions per pass
       const int c = lane & 15;
-      const int64_t n = col0 + 4 * c;
+      const int64_t n = ecol(col0, col_hi, 4 * c);
       const bool full = n + 4 <= d.N;
       f4 bv = {0.f, 0.f, 0.f, 0.f};
       if (first_split && d.bias) {
@@ -414,7 +425,7 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
 #pragma unroll 4
       for (int q = 0; q < 16; ++q) {
         const int lr = 4 * q + (lane >> 4);
-        const int64_t m = row0 + 64 * pass + lr;
+        const int64_t m = row0 + rstep * pass + lr;
         if (m >= d.M || n >= d.N) continue;
         f4 v = *reinterpret_cast<const f4*>(reg + lr * 256 + ((c ^ (lr & 15)) * 16));
         v = v * d.alpha + bv;
@@ -878,6 +889,172 @@ __global__ __launch_bounds__(512, 1) void gemm_lp2_kernel(LpArgs args) {
   lp_epilogue<FM, FN>(d, acc, smem + wave * 16384, m0 + wm * TM, n0 + wn * TN, first_split, lane);
 }
 
+// ---------------------------------------------------------------------------------------
+// 256 x 256 bf16 tile in the 8-phase structure (cdna_hip_programming.md "The 256^2 8-phase
+// template"): 512 threads = 8 waves, one workgroup per CU, k-tile 64, two LDS buffers of four
+// 16-KB half images each (A rows 0-127 / 128-255, B columns 0-127 / 128-255; every half image
+// has the format of the 128 x 128 kernel's operand image, so the fragment reads are shared).
+// A k-tile is 4 phases; phase q computes block quadrant (i, j) = (0,0), (0,1), (1,1), (1,0) --
+// each wave a 64 x 32 piece of it (rows wm*64 of A half i, columns wn*32 of B half j), 16
+// MFMAs -- so a phase reads ONE A half and ONE B half, and consecutive phases share a
+// register subtile (phase 0 reads A(0) + B(0), 1 B(1), 2 A(1), 3 B(0)). Each phase also
+// LDS-DMAs one half of the NEXT k-tile in the order A0, B0, B1, A1, i.e. the order the next
+// k-tile's phases first read them, and waits (counted vmcnt) only for the half the next
+// phase reads: two halves stay in flight across every barrier. Per phase: subtile ds_reads,
+// one half-tile DMA, vmcnt, barrier, lgkmcnt(0), 16 MFMAs at raised priority, barrier.
+// RAW: a half is read one phase after the wait that retired it; WAR: a half is restaged
+// >= 1 phase (and an lgkmcnt(0)) after its last read in the previous k-tile -- both also
+// hold with the two wave rows staggered by one barrier (the row behind waits for its part of
+// a half before the barrier the row ahead reads after; it retires its last reads of a half
+// before the barrier after which the row ahead restages it).
+template <bool T>
+struct LpHalf {
+  const char* p[2];
+  int koff[2];
+  int64_t step;
+
+  __device__ __forceinline__ void setup(const void* base, int64_t ld,
+                                        const int64_t* __restrict__ rows, int64_t r0, int64_t lim,
+                                        int64_t kbeg, int wave, int lane) {
+    const char* b = static_cast<const char*>(base);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int ins = 2 * wave + u;  // 16 instructions x 1 KB = one 16-KB half image
+      if constexpr (!T) {
+        const int r = 8 * ins + (lane >> 3);
+        const int lc = (lane & 7) ^ rswz<false>(r);
+        int64_t m = r0 + r;
+        m = m < lim ? m : lim - 1;
+        const int64_t rr = rows ? rows[m] : m;
+        p[u] = b + (rr * ld + kbeg) * 2 + lc * 16;
+        koff[u] = lc * 8;
+      } else {
+        const int r = 4 * ins + (lane >> 4);
+        const int lc = (lane & 15) ^ (2 * th(r));
+        int64_t c = r0 + lc * 8;
+        c = c + 8 <= lim ? c : lim - 8;
+        p[u] = b + ((kbeg + r) * ld + c) * 2;
+        koff[u] = r;
+      }
+    }
+    step = T ? (int64_t)64 * ld * 2 : LP_KB;
+  }
+
+  __device__ __forceinline__ void issue(char* img, int wave, int64_t t, int krem) const {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      glds16(krem >= 64 || koff[u] < krem ? (const void*)(p[u] + t * step) : (const void*)g_lp_zero,
+             (lds_void*)(img + (2 * wave + u) * 1024));
+  }
+};
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(512, 1) void gemm_lp3_kernel(LpArgs args) {
+  const savqa_gemm_lp_desc& d = args.d;
+  __shared__ __attribute__((aligned(1024))) char smem[8 * LP_IMG];  // 2 x {A0, A1, B0, B1}
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int t = xcd_remap(blockIdx.x, args.nblk);
+  const int tn = t % args.tiles_n, tm = t / args.tiles_n;
+  const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
+  const int64_t kbeg = (int64_t)blockIdx.y * args.kchunk;
+  const int64_t kend = min(d.K, kbeg + args.kchunk);
+  const int nt = (int)((kend - kbeg + 63) / 64);
+  const int krem = (int)(kend - kbeg - (int64_t)(nt - 1) * 64);  // k of the last k-tile
+  const bool first_split = blockIdx.y == 0;
+
+  LpHalf<AT> sa[2];
+  LpHalf<!BT> sb[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    sa[h].setup(d.A, d.lda, AT ? nullptr : d.a_rows, m0 + 128 * h, d.M, kbeg, wave, lane);
+    sb[h].setup(d.B, d.ldb, nullptr, n0 + 128 * h, d.N, kbeg, wave, lane);
+  }
+  // half image slots within a buffer: A0 0, A1 1, B0 2, B1 3; DMA order A0, B0, B1, A1
+  auto stage = [&](int q, int buf, int64_t kt) {
+    const int kr = kt + 1 == nt ? krem : 64;
+    char* base = smem + buf * 4 * LP_IMG;
+    if (q == 0) sa[0].issue(base + 0 * LP_IMG, wave, kt, kr);
+    else if (q == 1) sb[0].issue(base + 2 * LP_IMG, wave, kt, kr);
+    else if (q == 2) sb[1].issue(base + 3 * LP_IMG, wave, kt, kr);
+    else sa[1].issue(base + 1 * LP_IMG, wave, kt, kr);
+  };
+
+  f4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) stage(q, 0, 0);
+    wait_vm<4>();  // A0 and B0 of k-tile 0 landed (B1, A1 in flight)
+    __builtin_amdgcn_s_barrier();
+    // the two wave rows run one barrier apart, so on every SIMD one wave issues its MFMAs
+    // while the other reads its next subtile (each barrier interval: reads | MFMAs)
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+    bf16x8 a[4][2], b[2][2];
+    for (int kt = 0; kt < nt; ++kt) {
+      const char* img = smem + (kt & 1) * 4 * LP_IMG;
+      const bool pf = kt + 1 < nt;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = (q == 0 || q == 1) ? 0 : 1;
+        const int j = (q == 0 || q == 3) ? 0 : 1;
+        if (q == 0 || q == 2) {
+#pragma unroll
+          for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+              a[fi][kk] = frag_bf16<AT>(img + i * LP_IMG, wm * 64 + 16 * fi, kk, lane);
+        }
+        if (q != 2) {
+#pragma unroll
+          for (int fj = 0; fj < 2; ++fj)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+              b[fj][kk] = frag_bf16<!BT>(img + (2 + j) * LP_IMG, wn * 32 + 16 * fj, kk, lane);
+        }
+        if (pf && !(args.dbg & 2)) {
+          stage(q, (kt + 1) & 1, kt + 1);
+          wait_vm<4>();  // the half the next phase reads has landed
+        } else {
+          wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this phase's subtile is in VGPRs
+        __builtin_amdgcn_s_setprio(1);
+        if (!(args.dbg & 1)) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+              for (int fj = 0; fj < 2; ++fj)
+                acc[4 * i + fi][2 * j + fj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    b[fj][kk], a[fi][kk], acc[4 * i + fi][2 * j + fj], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered rows
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // (every DMA retired in the last k-tile; its last phase ended with a barrier after the
+  // final ds_reads were waited for, so LDS is free)
+  __syncthreads();
+  if (args.dbg & 4) {  // diagnostics: no epilogue (one store keeps the k-loop alive)
+    if (acc[0][0][0] == 12345.f && d.C) d.C[0] = acc[7][3][3];
+    return;
+  }
+  lp_epilogue<8, 4>(d, acc, smem + wave * 16384, m0 + wm * 64, n0 + wn * 32, first_split, lane,
+                    128, n0 + 128 + wn * 32);
+}
+
 static int lp_slots() {
   static int cached[64] = {0};
   int dev = 0;
@@ -941,17 +1118,23 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
   // explicitly (tests / tuning): 1 = 128x128, 3 = 256x256 BK64 NS2, 4 = 256x128 BK64 NS3
   // (k-tile 32 with a three-slot ring measured slower: 64-B rows halve each DMA's lines)
   // measured (tools/lp_bench.py --variants, cfg-3 shapes): the two-per-CU 128 x 128 kernel is
-  // fastest except for the very wide outputs (N = 6144 forward, M = 6144 split-K dW), where
-  // the 256 x 256 tile's halved operand traffic wins by ~10%
+  // fastest except for the very wide outputs (N = 6144 forward, M = 6144 split-K dW) and the
+  // wide dX of the FFN (NN, N = 2048), where the 8-phase 256 x 256 kernel (5) wins by 1-11%
+  // (the NS2 256 x 256 kernel (3) by ~10% over 128 x 128 on the first two). Diagnostic builds
+  // of kernel 5 (tile_hint bits 8-10: no MFMA / no k-loop DMA / no epilogue) at the K = 512
+  // shapes: the epilogue's HBM writes are ~30% of a launch and are not overlapped (one
+  // workgroup per CU), which is why the two-per-CU kernel stays ahead there.
   p.var = 1;
   if (!fp8) {
     const bool split = d.split_k > 1 || d.split_k < 0;
     const int h = d.tile_hint & 255;
-    if (h == 1 || h == 3 || h == 4) p.var = h;
-    else if (d.N >= 4096 || (split && d.M >= 4096 && d.N >= 256)) p.var = 3;
+    if (h == 1 || h == 3 || h == 4 || h == 5) p.var = h;
+    else if (d.N >= 4096 || (split && d.M >= 4096 && d.N >= 256) ||
+             (!d.a_trans && !d.b_trans && d.N >= 2048 && d.M >= 8192))
+      p.var = 5;
   }
   const int bm = p.var == 1 ? 128 : 256;
-  p.bn = p.var == 3 ? 256 : 128;
+  p.bn = (p.var == 3 || p.var == 5) ? 256 : 128;
   const int bk = fp8 ? 128 : 64;
   const int slots = p.var == 1 ? lp_slots() : lp_slots() / LP_OCC;
   p.tiles = ((d.M + bm - 1) / bm) * ((d.N + p.bn - 1) / p.bn);
@@ -1019,7 +1202,17 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   if (d.K == 0) a.kchunk = 0;
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)p.tiles, (unsigned)p.nsplit), block(LP_NT);
-  if (var != 1) {
+  if (var == 5) {
+    const dim3 b3(512);
+    if (!d.a_trans && d.b_trans)
+      hipLaunchKernelGGL((gemm_lp3_kernel<false, true>), grid, b3, 0, s, a);
+    else if (!d.a_trans)
+      hipLaunchKernelGGL((gemm_lp3_kernel<false, false>), grid, b3, 0, s, a);
+    else if (!d.b_trans)
+      hipLaunchKernelGGL((gemm_lp3_kernel<true, false>), grid, b3, 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_lp3_kernel<true, true>), grid, b3, 0, s, a);
+  } else if (var != 1) {
     const dim3 b2(512);
 #define SAVQA_LP2(BN_, WM_, BK_, NS_)                                                              \
   do {                                                                                             \

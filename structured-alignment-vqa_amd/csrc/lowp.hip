@@ -152,6 +152,48 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const __bf16* __restri
                            (part[2][threadIdx.x] + part[3][threadIdx.x]));
 }
 
+// Wide form (cols % 8 == 0, 16-B aligned rows): each lane sums 8 consecutive columns with
+// 16-B loads (a wave covers 512 columns of a row), the 4 waves of a block take interleaved
+// rows of its row chunk, and fold through LDS before one atomicAdd per column and block.
+// (The 2-B-per-lane form above ran the bias-gradient sums at ~2.3 TB/s.)
+typedef __bf16 cs_bf16x8 __attribute__((ext_vector_type(8)));
+__global__ __launch_bounds__(256) void colsum_bf16_wide_kernel(const __bf16* __restrict__ X,
+                                                               int64_t rows, int64_t cols,
+                                                               int64_t ldx, int64_t rchunk,
+                                                               float* __restrict__ out) {
+  __shared__ float part[4][512];
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 512 + 8 * lane;
+  const int64_t r0 = (int64_t)blockIdx.y * rchunk;
+  const int64_t r1 = min(rows, r0 + rchunk);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    int64_t r = r0 + sl;
+    for (; r + 12 < r1; r += 16) {  // four rows in flight per lane
+      cs_bf16x8 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = *reinterpret_cast<const cs_bf16x8*>(X + (r + 4 * u) * ldx + c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += (float)v[u][j];
+    }
+    for (; r < r1; r += 4) {
+      const cs_bf16x8 v = *reinterpret_cast<const cs_bf16x8*>(X + r * ldx + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[sl][8 * lane + j] = s[j];
+  __syncthreads();
+  for (int k = threadIdx.x; k < 512; k += 256) {
+    const int64_t cc = (int64_t)blockIdx.x * 512 + k;
+    if (cc < cols) atomicAdd(&out[cc], (part[0][k] + part[1][k]) + (part[2][k] + part[3][k]));
+  }
+}
+
 static unsigned grid_for(int64_t n) {
   int64_t b = (n + 255) / 256;
   return (unsigned)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
@@ -200,6 +242,17 @@ extern "C" int savqa_dequant_fp8_bf16(void* stream, const void* q, int64_t rows,
 extern "C" int savqa_colsum_bf16(void* stream, const void* X, int64_t rows, int64_t cols, int64_t ldx,
                                  float* out) {
   if (rows <= 0 || cols <= 0) return 0;
+  if (cols % 8 == 0 && ldx % 8 == 0 && (((uintptr_t)X) & 15) == 0) {
+    const int64_t cb = (cols + 511) / 512;
+    int64_t chunks = (2048 + cb - 1) / cb;
+    int64_t rchunk = (rows + chunks - 1) / chunks;
+    if (rchunk < 64) rchunk = 64;
+    chunks = (rows + rchunk - 1) / rchunk;
+    hipLaunchKernelGGL(colsum_bf16_wide_kernel, dim3((unsigned)cb, (unsigned)chunks), dim3(256), 0,
+                       as_stream(stream), static_cast<const __bf16*>(X), rows, cols, ldx, rchunk,
+                       out);
+    return check_launch("savqa_colsum_bf16");
+  }
   const int64_t cb = (cols + 63) / 64;
   int64_t chunks = (2048 + cb - 1) / cb;
   int64_t rchunk = (rows + chunks - 1) / chunks;

@@ -51,7 +51,7 @@ def test_bf16_layouts_bias_relu(lay, M, N, K):
     assert torch.equal(Cb.cpu(), C.to(torch.bfloat16).cpu())
 
 
-@pytest.mark.parametrize("hint", [1, 3, 4])
+@pytest.mark.parametrize("hint", [1, 3, 4, 5])
 @pytest.mark.parametrize("lay,M,N,K", [("NT", 1800, 1536, 512), ("NN", 1304, 1000, 520),
                                        ("TN", 1304, 1544, 2408), ("TT", 704, 1536, 256),
                                        ("NT", 3700, 512, 2048), ("TN", 512, 512, 2400)])
@@ -74,8 +74,9 @@ def test_bf16_kernel_variants(hint, lay, M, N, K):
     assert torch.equal(Cb.cpu(), C.to(torch.bfloat16).cpu())
 
 
+@pytest.mark.parametrize("hint", [0, 5])
 @pytest.mark.parametrize("K", [18688, 2400, 18712])
-def test_bf16_dw_split_k_atomic_and_colsum(K):
+def test_bf16_dw_split_k_atomic_and_colsum(K, hint):
     """dW += dY^T X (TN) at the encoder shape with the auto split-K (atomic accumulation
     into an existing gradient; K = B*T rows need not fill the last k-tile) and the bf16
     bias-gradient column sums."""
@@ -86,7 +87,7 @@ def test_bf16_dw_split_k_atomic_and_colsum(K):
     W0 = torch.randn(N, M, device=dev)
     dW = W0.clone()
     O.gemm_lp(dY, X, N, M, K, lda=N, ldb=M, a_trans=True, b_trans=False, C=dW, ldc=M,
-              atomic=True, split_k=-1)
+              atomic=True, split_k=-1, tile_hint=hint)
     ref = W0.double() + dY.double().t() @ X.double()
     assert rel(dW - W0, ref - W0.double()) < 2e-5
     cs = torch.ones(N, device=dev)
@@ -119,7 +120,7 @@ def test_bf16_epilogues_rows_mask_resid_rowvec():
     assert (C[untouched] == 7.0).all()
 
 
-@pytest.mark.parametrize("hint", [1, 3, 4])
+@pytest.mark.parametrize("hint", [1, 3, 4, 5])
 @pytest.mark.parametrize("mtype,arows,resid,rowvec", [
     ("bf16", False, False, False), ("bf16", True, True, False), ("f32", False, True, False),
     (None, False, True, False), (None, False, False, True)])
@@ -171,7 +172,7 @@ def test_bf16_vector_epilogue_prefetched_rows(hint, mtype, arows, resid, rowvec)
     assert (C[untouched] == 7.0).all() and (Cb[untouched].float() == 7.0).all()
 
 
-@pytest.mark.parametrize("hint", [1, 3, 4])
+@pytest.mark.parametrize("hint", [1, 3, 4, 5])
 @pytest.mark.parametrize("mask,arows,N", [(False, False, 264), (True, False, 264), (True, True, 136),
                                           (True, False, 2048)])
 def test_bf16_only_output_wide_stores(hint, mask, arows, N):
@@ -205,6 +206,19 @@ def test_bf16_only_output_wide_stores(hint, mask, arows, N):
     untouched = torch.ones(Cn, dtype=torch.bool, device=dev)
     untouched[crow] = False
     assert (Cb[untouched].float() == 7.0).all()
+
+
+@pytest.mark.parametrize("rows,cols,ld", [(5, 520, 520), (37376, 2048, 2048), (1000, 300, 300),
+                                           (777, 512, 1024)])
+def test_colsum_bf16_shapes(rows, cols, ld):
+    """Bias-gradient column sums of bf16 rows: the 16-B wide kernel (cols % 8 == 0) incl. a
+    partial 512-column block, short row chunks and a strided view, and the 2-B fallback."""
+    O = ops()
+    X = bf((rows, ld), 31)
+    out = torch.full((cols,), 0.5, device=dev)
+    O.colsum_bf16(X, rows, cols, ld, out)
+    ref = X[:, :cols].double().sum(0) + 0.5
+    assert rel(out, ref) < 1e-5
 
 
 def test_gemm_lp_rejects_unsupported():

@@ -87,10 +87,10 @@ def main():
              ("dw ffn2", "TN", 512, 2048, Ms, "atomic"), ("dw kv", "TN", 6144, 512, Ms, "atomic"),
              ("dx ffn2 m", "NN", Ms, 2048, 512, "bf16mask"), ("fwd ffn2 r", "NT", Ms, 512, 2048, "f32resid"),
              ("dx ffn1 r", "NN", Ms, 512, 2048, "f32resid")]
-    hints = [0] + ([1, 3, 4] if "--variants" in sys.argv else [])
-    if "--dbg" in sys.argv:  # v3 as is / without MFMAs / without k-loop DMAs
-        hints = [3, 3 + 256, 3 + 512, 4, 4 + 256, 4 + 512]
-        cases = cases[1:2] + cases[6:7] + cases[10:11]
+    hints = [0] + ([1, 3, 5] if "--variants" in sys.argv else [])
+    if "--dbg" in sys.argv:  # v5 as is / without MFMAs / without k-loop DMAs / no epilogue
+        hints = [5, 5 + 256, 5 + 512, 5 + 1024, 5 + 256 + 1024]
+        cases = cases[1:4] + cases[6:7] + cases[10:11]
     tot_f = 0.0
     tot_t = {h: 0.0 for h in hints}
     for name, lay, m, n, k, out in cases:
