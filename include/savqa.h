@@ -93,8 +93,9 @@ int savqa_gemm_plan(const savqa_gemm_desc* d, int32_t* out);
  *   a_type / b_type: SAVQA_DT_BF16 or SAVQA_DT_FP8 (OCP e4m3fn). fp8 needs both operands
  *   fp8, a_trans = 0, b_trans = 1, K % 128 == 0, and e8m0 block scales a_scale[m][k/32]
  *   (row stride lds_a bytes) / b_scale[n][k/32]: value = e4m3 * 2^(scale - 127)
- *   (v_mfma_scale_f32_16x16x128_f8f6f4). bf16 needs K % 8 == 0, 16-B aligned operands
- *   with ld % 8 == 0, and M % 8 == 0 (a_trans) / N % 8 == 0 (b_trans = 0).
+ *   (v_mfma_scale_f32_16x16x128_f8f6f4). bf16 needs K % 8 == 0 (unless both operands are
+ *   k-major: a_trans = 1, b_trans = 0), 16-B aligned operands with ld % 8 == 0, and M % 8 == 0
+ *   (a_trans) / N % 8 == 0 (b_trans = 0).
  *   v = acc*alpha + bias[n] + rowvec[(m % rowvec_period)*ldrv + n]  (bias/rowvec/resid:
  *       first K slice only) ; v = relu ? max(v,0) : v ;
  *   v = (mask && !(mask[mr*ldmask+n] > 0)) ? 0 : v   mr = mask_arows ? a_rows[m] : m
@@ -124,6 +125,9 @@ typedef struct savqa_gemm_lp_desc {
     float alpha;
     int32_t relu, atomic, split_k;
     int32_t tile_hint;  /* 0 = library's choice; 1..5 force a kernel variant (gemm_lp.hip) */
+    const int64_t* c_rows;  /* atomic only: output row of m is c_rows[m] (scatter-add) */
+    int64_t n_store;        /* atomic only, > 0: columns >= n_store are not stored (an operand
+                               zero-padded to a multiple of 8 columns, C rows n_store wide) */
 } savqa_gemm_lp_desc;
 
 int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* d);
@@ -141,7 +145,10 @@ int savqa_gemm_lp_plan(const savqa_gemm_lp_desc* d, int32_t* out);
  *   savqa_quant_fp8: per row r and 32-column block b: s = e8m0 scale making max|x| <= 448,
  *     q[ro(r)*ldq + c] = e4m3fn(x / 2^(s-127)) (round to nearest even), scale[ro(r)*lds + b]
  *     = s; cols % 32 == 0
- *   savqa_dequant_fp8_bf16: out = bf16(q * 2^(s-127))  (the backward's bf16 copy) */
+ *   savqa_dequant_fp8_bf16: out = bf16(q * 2^(s-127))  (the backward's bf16 copy)
+ *   savqa_gather_rows_bf16: out[r*ldo + c] = bf16(table[ids[r]*ldt + c]) for c < cols, 0 for
+ *     cols <= c < ldo (GloVe rows of a token list, zero-padded to a multiple of 8 columns:
+ *     the K = 300 embedding GEMMs of the low-precision modes) */
 int savqa_cast_bf16(void* stream, const float* in, int64_t rows, int64_t cols, int64_t ldi,
                     void* out, int64_t ldo, int64_t group, int64_t stride, int64_t offset);
 int savqa_quant_fp8(void* stream, const float* in, int64_t rows, int64_t cols, int64_t ldi,
@@ -152,6 +159,8 @@ int savqa_dequant_fp8_bf16(void* stream, const void* q, int64_t rows, int64_t co
 /* out[c] += sum_r X[r*ldx + c] over a bf16 X (bias gradients of the low-precision GEMMs) */
 int savqa_colsum_bf16(void* stream, const void* X, int64_t rows, int64_t cols, int64_t ldx,
                       float* out);
+int savqa_gather_rows_bf16(void* stream, const float* table, int64_t ldt, const int64_t* ids,
+                           int64_t n, int64_t cols, void* out, int64_t ldo);
 
 /* out[c] += sum_r X[r*ldx + c]  (bias gradients of every Linear above) */
 int savqa_colsum_acc(void* stream, const float* X, int64_t rows, int64_t cols, int64_t ldx, float* out);
@@ -357,6 +366,10 @@ int savqa_mil_fwd(void* stream, const float* Pf, const float* Nf, const float* v
 int savqa_mil_bwd(void* stream, const float* Pf, const float* Nf, const float* v,
                   const int32_t* mask, int64_t BN, int64_t K, int64_t H, float eps,
                   const float* dobj, const float* dmil, float* dPf, float* dNf, float* dv);
+/* The same with bf16 dPf / dNf (the operands of the low-precision modes' embedding GEMMs). */
+int savqa_mil_bwd_bf16(void* stream, const float* Pf, const float* Nf, const float* v,
+                       const int32_t* mask, int64_t BN, int64_t K, int64_t H, float eps,
+                       const float* dobj, const float* dmil, void* dPf, void* dNf, float* dv);
 
 /* macro[b*Ns + loc[b,n]][:] = obj[b*Nv+n][:] for 0 <= loc < Ns (AttModel_x3.py:377-380),
  * and its backward dobj[b*Nv+n] = dmacro[b*Ns+loc] (dobj rows with loc outside [0, Ns)

@@ -59,6 +59,7 @@ class GemmLpDesc(C.Structure):
         ("alpha", c_f),
         ("relu", c_i32), ("atomic", c_i32), ("split_k", c_i32),
         ("tile_hint", c_i32),
+        ("c_rows", c_p), ("n_store", c_i64),
     ]
 
 
@@ -85,6 +86,7 @@ _SIGS = {
                         c_i64],
     "savqa_dequant_fp8_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64],
     "savqa_colsum_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
+    "savqa_gather_rows_bf16": [c_p, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64],
     "savqa_ln_fwd": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p,
                      c_p],
     "savqa_ln_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p,
@@ -128,6 +130,8 @@ _SIGS = {
     "savqa_copy_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64],
     "savqa_mil_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_p],
     "savqa_mil_bwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_p, c_p, c_p],
+    "savqa_mil_bwd_bf16": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_p, c_p,
+                           c_p],
     "savqa_index_put_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "savqa_index_get_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "savqa_loss_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f, c_p, c_i32, c_p, c_p, c_p, c_p],

@@ -354,7 +354,7 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
         if (m >= d.M) break;
         float v = *reinterpret_cast<const float*>(reg + q * 256 + ((((lane >> 2) ^ (q & 15)) * 16)) +
                                                   (lane & 3) * 4);
-        if (n >= d.N) continue;
+        if (n >= d.N || (d.n_store > 0 && n >= d.n_store)) continue;
         v = v * d.alpha + bv;
         if (first_split && d.rowvec) v += d.rowvec[(m % d.rowvec_period) * d.ldrv + n];
         if (d.relu) v = fmaxf(v, 0.f);
@@ -367,7 +367,9 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
         }
         if (first_split && d.resid) v += d.resid[m * d.ldr + n];
         int64_t cr = m;
-        if (!ident) {
+        if (d.c_rows) {
+          cr = d.c_rows[m];
+        } else if (!ident) {
           const uint32_t mu = (uint32_t)m, cg = (uint32_t)d.c_group;
           cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
         }
@@ -1081,6 +1083,7 @@ static bool lp_ok(const savqa_gemm_lp_desc& d, const char** msg) {
   if (d.a_type != d.b_type) return no("a_type != b_type");
   if (!fp8 && d.a_type != SAVQA_DT_BF16) return no("operand type must be bf16 or fp8");
   if (d.atomic && d.Cb) return no("bf16 output with atomic accumulation");
+  if ((d.c_rows || d.n_store > 0) && !d.atomic) return no("c_rows / n_store need atomic = 1");
   if ((d.split_k > 1 || d.split_k < 0) && (!d.atomic || !d.C)) return no("split-K needs atomic fp32 C");
   if (d.a_rows && d.a_trans) return no("a_rows needs a_trans = 0");
   if (d.mask && d.mask_arows && !d.a_rows) return no("mask_arows needs a_rows");
@@ -1093,7 +1096,8 @@ static bool lp_ok(const savqa_gemm_lp_desc& d, const char** msg) {
     if (d.lda % 16 || d.ldb % 16) return no("fp8 needs ld % 16 == 0");
     if (!d.a_scale || !d.b_scale) return no("fp8 needs block scales");
   } else {
-    if (d.K % 8) return no("bf16 needs K % 8 == 0");
+    // 16-B granules run along k only in k-contiguous (R image) operands
+    if (d.K % 8 && (!d.a_trans || d.b_trans)) return no("bf16 needs K % 8 == 0");
     if (d.lda % 8 || d.ldb % 8) return no("bf16 needs ld % 8 == 0");
     if (d.a_trans && d.M % 8) return no("a_trans needs M % 8 == 0");
     if (!d.b_trans && d.N % 8) return no("b_trans = 0 needs N % 8 == 0");
@@ -1129,7 +1133,7 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
     const bool split = d.split_k > 1 || d.split_k < 0;
     const int h = d.tile_hint & 255;
     if (h == 1 || h == 3 || h == 4 || h == 5) p.var = h;
-    else if (d.N >= 4096 || (split && d.M >= 4096 && d.N >= 256) ||
+    else if (d.N >= 4096 || (split && d.a_trans && d.M >= 4096 && d.N >= 256) ||
              (!d.a_trans && !d.b_trans && d.N >= 2048 && d.M >= 8192))
       p.var = 5;
   }

@@ -7,6 +7,9 @@
 
 namespace savqa {
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
@@ -194,6 +197,36 @@ __global__ __launch_bounds__(256) void colsum_bf16_wide_kernel(const __bf16* __r
   }
 }
 
+// GloVe rows of a token list into a zero-padded bf16 matrix: one wave per output row, each
+// lane 4 consecutive columns (16-B fp32 loads when the table rows allow, 8-B bf16 stores).
+__global__ __launch_bounds__(256) void gather_rows_bf16_kernel(const float* __restrict__ table,
+                                                               int64_t ldt,
+                                                               const int64_t* __restrict__ ids,
+                                                               int64_t n, int64_t cols,
+                                                               __bf16* __restrict__ out,
+                                                               int64_t ldo, bool vec) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int lane = threadIdx.x & 63;
+  const float* src = table + ids[r] * ldt;
+  __bf16* dst = out + r * ldo;
+  for (int64_t c = 4 * lane; c < ldo; c += 256) {
+    float v[4];
+    if (vec && c + 4 <= cols) {
+      const f4v t = *reinterpret_cast<const f4v*>(src + c);
+      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = c + j < cols ? src[c + j] : 0.f;
+    }
+    if (c + 4 <= ldo) {
+      *reinterpret_cast<bf16x4v*>(dst + c) = bf16x4v{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    } else {
+      for (int j = 0; c + j < ldo; ++j) dst[c + j] = (__bf16)v[j];
+    }
+  }
+}
+
 static unsigned grid_for(int64_t n) {
   int64_t b = (n + 255) / 256;
   return (unsigned)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
@@ -261,4 +294,17 @@ extern "C" int savqa_colsum_bf16(void* stream, const void* X, int64_t rows, int6
   hipLaunchKernelGGL(colsum_bf16_kernel, dim3((unsigned)cb, (unsigned)chunks), dim3(256), 0,
                      as_stream(stream), static_cast<const __bf16*>(X), rows, cols, ldx, rchunk, out);
   return check_launch("savqa_colsum_bf16");
+}
+
+extern "C" int savqa_gather_rows_bf16(void* stream, const float* table, int64_t ldt,
+                                      const int64_t* ids, int64_t n, int64_t cols, void* out,
+                                      int64_t ldo) {
+  if (n <= 0) return 0;
+  if (cols <= 0 || ldo < cols || (ldo & 3) || (((uintptr_t)out) & 7))
+    return fail(SAVQA_EINVAL, "savqa_gather_rows_bf16: need 0 < cols <= ldo, ldo % 4 == 0, 8-B aligned out");
+  const bool vec = (ldt & 3) == 0 && (((uintptr_t)table) & 15) == 0;
+  hipLaunchKernelGGL(gather_rows_bf16_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0,
+                     as_stream(stream), table, ldt, ids, n, cols, static_cast<__bf16*>(out), ldo,
+                     vec);
+  return check_launch("savqa_gather_rows_bf16");
 }

@@ -170,11 +170,21 @@ __global__ void mean_reduce_kernel(const float* __restrict__ x, int64_t n, float
   }
 }
 
+__device__ __forceinline__ void mil_store4(float* p, const float4& v) {
+  *reinterpret_cast<float4*>(p) = v;
+}
+__device__ __forceinline__ void mil_store4(__bf16* p, const float4& v) {
+  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+  *reinterpret_cast<b4*>(p) = b4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+}
+
+// TO: element type of dPf / dNf (float, or bf16 for the low-precision modes' GEMMs)
+template <typename TO>
 __global__ __launch_bounds__(256) void mil_bwd_kernel(
     const float* __restrict__ Pf, const float* __restrict__ Nf, const float* __restrict__ v,
     const int32_t* __restrict__ mask, int64_t BN, int K, int H, float eps,
-    const float* __restrict__ dobj, const float* __restrict__ dmil, float* __restrict__ dPf,
-    float* __restrict__ dNf, float* __restrict__ dv) {
+    const float* __restrict__ dobj, const float* __restrict__ dmil, TO* __restrict__ dPf,
+    TO* __restrict__ dNf, float* __restrict__ dv) {
   const int lane = threadIdx.x & 63;
   const int64_t bn = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (bn >= BN) return;
@@ -243,8 +253,8 @@ __global__ __launch_bounds__(256) void mil_bwd_kernel(
       dn.y = qq.y > 0.f ? dsn[k] * vv.y : 0.f;
       dn.z = qq.z > 0.f ? dsn[k] * vv.z : 0.f;
       dn.w = qq.w > 0.f ? dsn[k] * vv.w : 0.f;
-      reinterpret_cast<float4*>(dPf + off)[i] = dp;
-      reinterpret_cast<float4*>(dNf + off)[i] = dn;
+      mil_store4(dPf + off + 4 * i, dp);
+      mil_store4(dNf + off + 4 * i, dn);
       acc.x += dsp[k] * pp.x + dsn[k] * qq.x;
       acc.y += dsp[k] * pp.y + dsn[k] * qq.y;
       acc.z += dsp[k] * pp.z + dsn[k] * qq.z;
@@ -548,9 +558,22 @@ extern "C" int savqa_mil_bwd(void* stream, const float* Pf, const float* Nf, con
   if (BN <= 0) return 0;
   if (K <= 0 || K > MIL_KMAX || H % 4 != 0)
     return fail(SAVQA_EUNSUP, "savqa_mil_bwd: need 1 <= topN <= 16 and H % 4 == 0");
-  hipLaunchKernelGGL(mil_bwd_kernel, dim3((BN + 3) / 4), dim3(256), 0, as_stream(stream), Pf, Nf, v,
-                     mask, BN, (int)K, (int)H, eps, dobj, dmil, dPf, dNf, dv);
+  hipLaunchKernelGGL(mil_bwd_kernel<float>, dim3((BN + 3) / 4), dim3(256), 0, as_stream(stream), Pf,
+                     Nf, v, mask, BN, (int)K, (int)H, eps, dobj, dmil, dPf, dNf, dv);
   return check_launch("savqa_mil_bwd");
+}
+
+extern "C" int savqa_mil_bwd_bf16(void* stream, const float* Pf, const float* Nf, const float* v,
+                                  const int32_t* mask, int64_t BN, int64_t K, int64_t H, float eps,
+                                  const float* dobj, const float* dmil, void* dPf, void* dNf,
+                                  float* dv) {
+  if (BN <= 0) return 0;
+  if (K <= 0 || K > MIL_KMAX || H % 4 != 0)
+    return fail(SAVQA_EUNSUP, "savqa_mil_bwd_bf16: need 1 <= topN <= 16 and H % 4 == 0");
+  hipLaunchKernelGGL(mil_bwd_kernel<__bf16>, dim3((BN + 3) / 4), dim3(256), 0, as_stream(stream), Pf,
+                     Nf, v, mask, BN, (int)K, (int)H, eps, dobj, dmil,
+                     static_cast<__bf16*>(dPf), static_cast<__bf16*>(dNf), dv);
+  return check_launch("savqa_mil_bwd_bf16");
 }
 
 extern "C" int savqa_index_put_rows(void* stream, const int64_t* loc, int64_t B, int64_t Nv,

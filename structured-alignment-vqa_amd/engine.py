@@ -472,6 +472,7 @@ class MilSaved:
     rel: Optional[dict] = None
     lp: object = None
     macrob: torch.Tensor = None
+    Eg: Optional[list] = None      # low-precision modes: gathered bf16 GloVe rows (pos, neg)
 
 
 def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb, T_syb: int,
@@ -491,17 +492,34 @@ def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb
                  loc=loc.reshape(-1), mask=omask, vis=vis_fea.reshape(B * Nv, Dv))
     s.Pf = _empty(B * Nv * K, Hm, dev=dev)
     s.Nf = _empty(B * Nv * K, Hm, dev=dev)
-    ops.linear(W.E, W.Ws, W.bs, s.Pf, relu=True, a_rows=s.pos)
-    ops.linear(W.E, W.Ws, W.bs, s.Nf, relu=True, a_rows=s.neg)
     s.vv = _empty(B * Nv, Hm, dev=dev)
     s.lp = lp
+    if lp is not None and rel is None:
+        # low-precision modes: the object-word rows of the GloVe table gathered once into
+        # zero-padded bf16 matrices (kept for the weight gradient), K = 304 bf16 GEMMs
+        s.Eg = []
+        for ids, out in ((s.pos, s.Pf), (s.neg, s.Nf)):
+            eg = _bf(ids.numel(), GLOVE_PAD, dev=dev)
+            ops.gather_rows_bf16(W.E, ids, GLOVE_D, eg)
+            ops.linear_lp(eg, lp.Ws, W.bs, out, relu=True)
+            s.Eg.append(eg)
+    else:
+        ops.linear(W.E, W.Ws, W.bs, s.Pf, relu=True, a_rows=s.pos)
+        ops.linear(W.E, W.Ws, W.bs, s.Nf, relu=True, a_rows=s.neg)
     if lp is not None:
         ops.linear_lp(lp.vis, lp.Wv, W.bv, s.vv, relu=True, x_scale=lp.vis_scale,
                       w_scale=lp.Wv_scale)
     else:
         ops.linear(s.vis, W.Wv, W.bv, s.vv, relu=True)
     s.macro = _empty(B * Ns, Hm, dev=dev)
-    ops.linear(W.E, W.Wm, W.bm, s.macro, relu=True, a_rows=macro_ipt.reshape(-1))
+    if lp is not None:  # (forward only: new_macro_ipt is detached, AttModel_x3.py:354)
+        ids = macro_ipt.reshape(-1)
+        em = _bf(ids.numel(), GLOVE_PAD, dev=dev)
+        ops.gather_rows_bf16(W.E, ids, GLOVE_D, em)
+        ops.linear_lp(em, lp.Wm, W.bm, s.macro, relu=True)
+        del em
+    else:
+        ops.linear(W.E, W.Wm, W.bm, s.macro, relu=True, a_rows=macro_ipt.reshape(-1))
     obj = _empty(B * Nv, Hm, dev=dev)
     ws = _empty(B * Nv, dev=dev)
     ops.mil_fwd(s.Pf, s.Nf, s.vv, omask, B * Nv, K, Hm, eps, obj, ws, mil_out)
@@ -597,14 +615,28 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
         ops.rowscale_mask(drelf, None, rel["relf"], B * Lp, Hm, drelf)  # ReLU of syb_mlp
         ops.linear_dw(drelf, W.E, G.Ws, G.bs, rows=B * Lp, x_rows=rel["pos_rel"])
         ops.linear_dx(drelf, W.Ws, G.E, rows=B * Lp, c_rows=rel["pos_rel"], atomic=True)
-    dPf, dNf = torch.empty_like(s.Pf), torch.empty_like(s.Nf)
     dvv = torch.empty_like(s.vv)
-    ops.mil_bwd(s.Pf, s.Nf, s.vv, s.mask, B * Nv, K, Hm, eps, dobj, dmil, dPf, dNf, dvv)
     n = B * Nv * K
-    ops.linear_dw(dPf, W.E, G.Ws, G.bs, rows=n, x_rows=s.pos)
-    ops.linear_dw(dNf, W.E, G.Ws, G.bs, rows=n, x_rows=s.neg)
-    ops.linear_dx(dPf, W.Ws, G.E, rows=n, c_rows=s.pos, atomic=True)
-    ops.linear_dx(dNf, W.Ws, G.E, rows=n, c_rows=s.neg, atomic=True)
+    if s.Eg is not None:
+        # bf16 dPf / dNf straight from the MIL-NCE backward; dW = dP^T Eg and the table
+        # scatter dE[ids] += dP Ws on the 304-column padded operands (pad columns not stored)
+        dPb = _bf(n, Hm, dev=dev)
+        dNb = _bf(n, Hm, dev=dev)
+        ops.mil_bwd_bf16(s.Pf, s.Nf, s.vv, s.mask, B * Nv, K, Hm, eps, dobj, dmil, dPb, dNb, dvv)
+        for dY, ids, eg in ((dPb, s.pos, s.Eg[0]), (dNb, s.neg, s.Eg[1])):
+            ops.gemm_lp(dY, eg, Hm, GLOVE_PAD, n, lda=Hm, ldb=GLOVE_PAD, a_trans=True, C=G.Ws,
+                        ldc=GLOVE_D, atomic=True, split_k=-1, n_store=GLOVE_D)
+            ops.colsum_bf16(dY, n, Hm, Hm, G.bs)
+            ops.gemm_lp(dY, lp.Ws, n, GLOVE_PAD, Hm, lda=Hm, ldb=GLOVE_PAD, C=G.E, ldc=GLOVE_D,
+                        atomic=True, split_k=-1, c_rows=ids, n_store=GLOVE_D)
+        del dPb, dNb
+    else:
+        dPf, dNf = torch.empty_like(s.Pf), torch.empty_like(s.Nf)
+        ops.mil_bwd(s.Pf, s.Nf, s.vv, s.mask, B * Nv, K, Hm, eps, dobj, dmil, dPf, dNf, dvv)
+        ops.linear_dw(dPf, W.E, G.Ws, G.bs, rows=n, x_rows=s.pos)
+        ops.linear_dw(dNf, W.E, G.Ws, G.bs, rows=n, x_rows=s.neg)
+        ops.linear_dx(dPf, W.Ws, G.E, rows=n, c_rows=s.pos, atomic=True)
+        ops.linear_dx(dNf, W.Ws, G.E, rows=n, c_rows=s.neg, atomic=True)
     if lp is not None:
         dvvb = _bf(B * Nv, Hm, dev=dev)
         ops.cast_bf16(dvv, B * Nv, Hm, Hm, dvvb, Hm)
@@ -677,6 +709,10 @@ class StackLp:
     Win8_scale: Optional[torch.Tensor] = None
 
 
+GLOVE_D = 300
+GLOVE_PAD = 304   # the 300-d GloVe rows zero-padded to a multiple of 8 bf16 (16-B granules)
+
+
 @dataclass
 class MilLp:
     vis: torch.Tensor               # [B*Nv, 2048] bf16, or fp8 (uint8 view) with vis_scale
@@ -685,6 +721,8 @@ class MilLp:
     vis_scale: Optional[torch.Tensor] = None
     Wv_scale: Optional[torch.Tensor] = None
     _vis16: Optional[torch.Tensor] = None
+    Ws: Optional[torch.Tensor] = None   # MIL_NCE.syb_mlp / marco_mlp weights, bf16 [1024, 304]
+    Wm: Optional[torch.Tensor] = None
 
     def vis_bf16(self):
         """bf16 region features for the vis_mlp weight gradient (fp8 mode: expanded once)."""
@@ -705,10 +743,13 @@ class LpShadow:
     syb_mlp2, MIL_NCE.vis_mlp). Refreshed lazily when the arena's state key changes (an
     optimizer step or any in-place edit of the parameters)."""
 
+    PADDED = ("MIL_NCE.syb_mlp.0.weight", "MIL_NCE.marco_mlp.0.weight")
+
     def __init__(self, arena, fp8: bool):
         self.arena, self.fp8 = arena, fp8
         self.buf, self.key = None, None
         self.q8 = {}
+        self.pad = {}
 
     def refresh(self):
         a = self.arena
@@ -722,6 +763,14 @@ class LpShadow:
             if t0 > lo:
                 ops.cast_bf16(a.flat[lo:t0], 1, t0 - lo, t0 - lo, self.buf[lo:t0], t0 - lo)
             lo = max(lo, t1)
+        # the two weights that meet GloVe rows (K = 300): bf16 copies with rows zero-padded
+        # to 304 columns (the pad is written once, at allocation)
+        for name in self.PADDED:
+            w = a.view(name)
+            N, K = w.shape
+            if name not in self.pad:
+                self.pad[name] = torch.zeros(N, GLOVE_PAD, dtype=torch.bfloat16, device=w.device)
+            ops.cast_bf16(w, N, K, K, self.pad[name], GLOVE_PAD)
         if self.fp8:
             for name in ("att_vis_grid.syb_mlp2.weight", "MIL_NCE.vis_mlp.0.weight"):
                 w = a.view(name)
@@ -908,7 +957,9 @@ class ModelEngine:
                 Wv = wm.Wv
             lp_vis = StackLp(wv, cat_scale, Win8, Win8_s)
             lp_syb = StackLp(ws)
-            lp_mil = MilLp(vis_lp, Wv, wm.Wipt, vis_sc, Wv_s)
+            pad = self._shadow.pad
+            lp_mil = MilLp(vis_lp, Wv, wm.Wipt, vis_sc, Wv_s, Ws=pad["MIL_NCE.syb_mlp.0.weight"],
+                           Wm=pad["MIL_NCE.marco_mlp.0.weight"])
         s_vis, s_syb = self._streams(dev)
         s_vis.wait_stream(main)
         s_syb.wait_stream(main)

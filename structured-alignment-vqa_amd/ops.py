@@ -157,7 +157,8 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
             b_trans=False, a_rows=None, a_scale=None, lds_a=0, b_scale=None, lds_b=0, C=None,
             ldc=0, Cb=None, ldcb=0, c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None,
             ldrv=0, rowvec_period=0, resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False,
-            alpha=1.0, relu=False, atomic=False, split_k=1, tile_hint=0):
+            alpha=1.0, relu=False, atomic=False, split_k=1, tile_hint=0, c_rows=None,
+            n_store=0):
     """savqa_gemm_lp_desc for bf16 / fp8 operands (include/savqa.h)."""
     d = _lib.GemmLpDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
@@ -174,6 +175,7 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
     d.alpha = float(alpha)
     d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
     d.tile_hint = int(tile_hint)
+    d.c_rows, d.n_store = _p(c_rows), int(n_store)
     return d
 
 
@@ -230,6 +232,13 @@ def dequant_fp8_bf16(q: Tensor, rows: int, cols: int, ldq: int, scale: Tensor, l
                      out: Tensor, ldo: int):
     call("savqa_dequant_fp8_bf16", _stream(), _p(q), int(rows), int(cols), int(ldq), _p(scale),
          int(lds), _p(out), int(ldo))
+
+
+def gather_rows_bf16(table: Tensor, ids: Tensor, cols: int, out: Tensor):
+    """out[r, :cols] = bf16(table[ids[r], :cols]); out[r, cols:] = 0 (savqa_gather_rows_bf16)."""
+    n = ids.numel()
+    call("savqa_gather_rows_bf16", _stream(), _p(table), int(table.stride(0)), _p(ids), int(n),
+         int(cols), _p(out), int(out.stride(0)))
 
 
 def colsum_bf16(X: Tensor, rows: int, cols: int, ldx: int, out: Tensor):
@@ -448,6 +457,12 @@ def copy_rows(src, rows, cols, lds, dst, ldd, group=0, stride=0, offset=0):
 def mil_fwd(Pf, Nf, v, mask, BN, K, H, eps, obj, ws, mil_out):
     call("savqa_mil_fwd", _stream(), _p(Pf), _p(Nf), _p(v), _p(mask), BN, K, H, float(eps),
          _p(obj), _p(ws), _p(mil_out))
+
+
+def mil_bwd_bf16(Pf, Nf, v, mask, BN, K, H, eps, dobj, dmil, dPf, dNf, dv):
+    """mil_bwd with bf16 dPf / dNf (savqa_mil_bwd_bf16)."""
+    call("savqa_mil_bwd_bf16", _stream(), _p(Pf), _p(Nf), _p(v), _p(mask), BN, K, H, float(eps),
+         _p(dobj), _p(dmil), _p(dPf), _p(dNf), _p(dv))
 
 
 def mil_bwd(Pf, Nf, v, mask, BN, K, H, eps, dobj, dmil, dPf, dNf, dv):

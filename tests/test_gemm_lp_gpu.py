@@ -221,6 +221,45 @@ def test_colsum_bf16_shapes(rows, cols, ld):
     assert rel(out, ref) < 1e-5
 
 
+def test_gather_rows_bf16_zero_padded():
+    """GloVe rows of a token list into a 304-column bf16 matrix (the K = 300 embedding GEMMs
+    of the low-precision modes): bf16 of the rows, pad columns zero."""
+    O = ops()
+    table = torch.randn(1000, 300, device=dev)
+    ids = torch.randint(0, 1000, (517,), device=dev)
+    out = torch.full((517, 304), 3.0, device=dev, dtype=torch.bfloat16)
+    O.gather_rows_bf16(table, ids, 300, out)
+    assert torch.equal(out[:, :300].cpu(), table[ids].to(torch.bfloat16).cpu())
+    assert (out[:, 300:].float() == 0).all()
+
+
+@pytest.mark.parametrize("hint", [0, 1, 5])
+def test_lp_scatter_rows_and_n_store(hint):
+    """Atomic scatter-add into indexed rows (c_rows: the GloVe-table gradient, duplicate ids
+    add up) of a 304-column product whose pad columns are not stored (n_store = 300, C rows
+    300 wide), and the padded weight gradient dW[:, :300] += dY^T Eg (a_trans)."""
+    O = ops()
+    n, H = 1500, 256
+    dY = bf((n, H), 41)
+    W = torch.zeros(H, 304, device=dev, dtype=torch.bfloat16)
+    W[:, :300] = bf((H, 300), 42)
+    ids = torch.randint(0, 700, (n,), device=dev)
+    C0 = torch.randn(700, 300, device=dev)
+    C = C0.clone()
+    O.gemm_lp(dY, W, n, 304, H, lda=H, ldb=304, C=C, ldc=300, atomic=True, split_k=-1, c_rows=ids,
+              n_store=300, tile_hint=hint)
+    ref = C0.double().index_add(0, ids, dY.double() @ W[:, :300].double())
+    assert rel(C, ref) < 2e-5
+    Eg = torch.zeros(n, 304, device=dev, dtype=torch.bfloat16)
+    Eg[:, :300] = bf((n, 300), 43)
+    G0 = torch.randn(H, 300, device=dev)
+    G = G0.clone()
+    O.gemm_lp(dY, Eg, H, 304, n, lda=H, ldb=304, a_trans=True, C=G, ldc=300, atomic=True,
+              split_k=-1, n_store=300, tile_hint=hint)
+    ref = G0.double() + dY.double().t() @ Eg[:, :300].double()
+    assert rel(G - G0, ref - G0.double()) < 2e-5
+
+
 def test_gemm_lp_rejects_unsupported():
     O = ops()
     A = bf((100, 60), 8)
