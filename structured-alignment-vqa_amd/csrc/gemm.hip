@@ -533,55 +533,158 @@ __device__ __forceinline__ void sk_load4(const float* __restrict__ P, int64_t ld
   }
 }
 
-template <bool AT, bool BT, int NW>
+// Branch-free loads of whole k-groups (every k in range, the lane's row / column clamped to a
+// valid one and its values masked at use): the guarded sk_load4 above branches per element,
+// and hipcc then waits vmcnt(0) at every join -- it serialised the skinny kernels' loads
+// (63-75 s_waitcnt vmcnt(0) per kernel body, one global round trip per load). The guarded
+// form now only runs the (at most one) partial group at the end of K.
+//   KCONTIG: value(x, k) = base[k] with base = P + r(x) * ld (VEC: one b128 load)
+//   else:    value(x, k) = base[k * ld] with base = P + x (4 coalesced scalars)
+template <bool KCONTIG, bool VEC>
+__device__ __forceinline__ void sk_full4(const float* __restrict__ base, int64_t ld, int64_t k,
+                                         float (&v)[4]) {
+  if constexpr (KCONTIG) {
+    if constexpr (VEC) {
+      const f4 t = *reinterpret_cast<const f4*>(base + k);
+      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = base[k + j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = base[(k + j) * ld];
+  }
+}
+
+// D-slot register ring over ng whole k-groups starting at g0: a steady loop whose body is
+// straight-line (every slot's MFMAs, then its reload D groups ahead), so hipcc's counted
+// vmcnt waits for exactly the slot it consumes; guards only in the drain. Fewer than D
+// groups: all loads first, then the MFMAs (one round trip).
+template <int D, class LD, class MM>
+__device__ __forceinline__ void sk_ring(int64_t g0, int ng, float (&a)[D][4], float (&b)[D][4],
+                                        LD&& load, MM&& mma) {
+  if (ng >= D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) load(g0 + u, a[u], b[u]);
+    int it = 0;
+    for (; it + 2 * D <= ng; it += D) {
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        mma(a[u], b[u]);
+        load(g0 + it + D + u, a[u], b[u]);
+        // keep slot order: left alone, the scheduler hoists every MFMA above every reload
+        // and the loop then waits vmcnt(0) at its head
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      mma(a[u], b[u]);
+      if (it + D + u < ng) load(g0 + it + D + u, a[u], b[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+      if (it + D + u < ng) mma(a[u], b[u]);
+  } else {
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+      if (u < ng) load(g0 + u, a[u], b[u]);
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+      if (u < ng) mma(a[u], b[u]);
+  }
+}
+
+// per-lane operand base of sk_full4 (row / column clamped into range)
+template <bool KCONTIG>
+__device__ __forceinline__ const float* sk_base(const float* P, int64_t ld,
+                                                const int64_t* __restrict__ rows, int64_t x,
+                                                int64_t xlim) {
+  const int64_t xc = x < xlim ? x : xlim - 1;
+  if constexpr (KCONTIG) return P + (rows ? rows[xc] : xc) * ld;
+  else return P + xc;
+}
+
+template <bool AT, bool BT, int NW, bool AV, bool BV>
 __global__ __launch_bounds__(64 * NW) void gemm_skinny_kernel(savqa_gemm_desc d, int tiles_n,
                                                                    int avec, int bvec) {
   __shared__ float red[NW][32][33];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the wave index in an SGPR: every k-range bound below is then wave-uniform to the
+  // compiler, so the ring's guards are scalar branches, not exec masks (an exec-masked guard
+  // makes hipcc wait vmcnt(0) at its join and serialises the loads)
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int t = blockIdx.x;
   const int64_t m0 = (int64_t)(t / tiles_n) * 32, n0 = (int64_t)(t % tiles_n) * 32;
   // this wave's k range, in whole 8-k groups
   const int64_t ngrp = (d.K + 7) / 8;
   const int64_t g0 = ngrp * w / NW, g1 = ngrp * (w + 1) / NW;
+  const int64_t gf = min(g1, max(g0, d.K / 8));  // [g0, gf): groups wholly inside K
   const int i = lane & 31, q = lane >> 5;
   const int64_t am = m0 + i, bn = n0 + i;
   const int64_t* arows = d.a_rows;  // !AT: gather on m; AT: gather on k
   const int64_t* brows = d.b_rows;  // BT: gather on n; !BT: gather on k
+  // k-row gathers (AT a_rows / !BT b_rows) keep the guarded per-element loads
+  const bool kgather = (AT && arows) || (!BT && brows);
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   float cs = 0.f;  // colsum_a partial (AT): sum over this wave's k of A(m0 + i, k), half q
-  float a[SK_DEPTH][2][4], b[SK_DEPTH][2][4];
-  auto load_pair = [&](int64_t gg, float (&aa)[2][4], float (&bb)[2][4]) {
+  // out-of-range rows / columns (clamped loads) contribute zeros: masked here, at the use,
+  // so no load result is needed before the MFMA that consumes it
+  const bool aok = am < d.M, bok = bn < d.N;
+  auto mma = [&](const float (&aa)[4], const float (&bb)[4]) {
+    float x[4], y[4];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t k = (gg + u) * 8 + 4 * q;
-      const int64_t kl = gg + u < g1 ? d.K : 0;  // groups past this wave's range load zeros
-      sk_load4<!AT>(d.A, d.lda, arows, am, d.M, k, kl, avec, aa[u]);
-      sk_load4<BT>(d.B, d.ldb, brows, bn, d.N, k, kl, bvec, bb[u]);
+    for (int j = 0; j < 4; ++j) {
+      x[j] = aok ? aa[j] : 0.f;
+      y[j] = bok ? bb[j] : 0.f;
     }
+    cs += (x[0] + x[1]) + (x[2] + x[3]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[s], y[s], acc, 0, 0, 0);
   };
-  auto mma_pair = [&](const float (&aa)[2][4], const float (&bb)[2][4]) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      cs += (aa[u][0] + aa[u][1]) + (aa[u][2] + aa[u][3]);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(aa[u][s], bb[u][s], acc, 0, 0, 0);
+  if (!kgather) {
+    const float* ab = sk_base<!AT>(d.A, d.lda, AT ? nullptr : arows, am, d.M);
+    const float* bb_ = sk_base<BT>(d.B, d.ldb, BT ? brows : nullptr, bn, d.N);
+    constexpr int D = 4;  // k-groups in flight per wave (a ring of compile-time slots)
+    float a[D][4], b[D][4];
+    auto load = [&](int64_t g, float (&aa)[4], float (&bx)[4]) {
+      const int64_t k = g * 8 + 4 * q;
+      sk_full4<!AT, AV>(ab, d.lda, k, aa);
+      sk_full4<BT, BV>(bb_, d.ldb, k, bx);
+    };
+    sk_ring<D>(g0, (int)(gf - g0), a, b, load, mma);
+    if (gf < g1) {  // the partial group at the end of K (one wave at most)
+      float aa[4], bx[4];
+      const int64_t k = gf * 8 + 4 * q;
+      sk_load4<!AT>(d.A, d.lda, arows, am, d.M, k, d.K, avec, aa);
+      sk_load4<BT>(d.B, d.ldb, brows, bn, d.N, k, d.K, bvec, bx);
+      mma(aa, bx);
     }
-  };
-  // SK_DEPTH group pairs in flight: the k range of a wave is short (K/8), so global-load
-  // latency, not the MFMAs, bounds these launches; a ring of register buffers with
-  // compile-time slots keeps SK_DEPTH loads outstanding while the oldest is consumed
-  const int npair = (int)((g1 - g0 + 1) / 2);
+  } else {
+    float a[SK_DEPTH][2][4], b[SK_DEPTH][2][4];
+    auto load_pair = [&](int64_t gg, float (&aa)[2][4], float (&bb)[2][4]) {
 #pragma unroll
-  for (int q2 = 0; q2 < SK_DEPTH; ++q2)
-    if (q2 < npair) load_pair(g0 + 2 * q2, a[q2], b[q2]);
-  for (int pi = 0; pi < npair; pi += SK_DEPTH) {
+      for (int u = 0; u < 2; ++u) {
+        const int64_t k = (gg + u) * 8 + 4 * q;
+        const int64_t kl = gg + u < g1 ? d.K : 0;  // groups past this wave's range load zeros
+        sk_load4<!AT>(d.A, d.lda, arows, am, d.M, k, kl, avec, aa[u]);
+        sk_load4<BT>(d.B, d.ldb, brows, bn, d.N, k, kl, bvec, bb[u]);
+      }
+    };
+    const int npair = (int)((g1 - g0 + 1) / 2);
 #pragma unroll
-    for (int q2 = 0; q2 < SK_DEPTH; ++q2) {
-      if (pi + q2 < npair) {
-        mma_pair(a[q2], b[q2]);
-        if (pi + q2 + SK_DEPTH < npair) load_pair(g0 + 2 * (pi + q2 + SK_DEPTH), a[q2], b[q2]);
+    for (int q2 = 0; q2 < SK_DEPTH; ++q2)
+      if (q2 < npair) load_pair(g0 + 2 * q2, a[q2], b[q2]);
+    for (int pi = 0; pi < npair; pi += SK_DEPTH) {
+#pragma unroll
+      for (int q2 = 0; q2 < SK_DEPTH; ++q2) {
+        if (pi + q2 < npair) {
+          mma(a[q2][0], b[q2][0]);
+          mma(a[q2][1], b[q2][1]);
+          if (pi + q2 + SK_DEPTH < npair) load_pair(g0 + 2 * (pi + q2 + SK_DEPTH), a[q2], b[q2]);
+        }
       }
     }
   }
@@ -621,41 +724,67 @@ __global__ __launch_bounds__(64 * NW) void gemm_skinny_kernel(savqa_gemm_desc d,
 // operand, 4 coalesced scalars otherwise; accumulator row 4q + r, column i.
 constexpr int SK16_DEPTH = 4;
 
-template <bool AT, bool BT, int NW>
+template <bool AT, bool BT, int NW, bool AV, bool BV>
 __global__ __launch_bounds__(64 * NW) void gemm_skinny16_kernel(savqa_gemm_desc d,
                                                                      int tiles_n, int avec,
                                                                      int bvec) {
   __shared__ float red[NW][16][17];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int t = blockIdx.x;
   const int64_t m0 = (int64_t)(t / tiles_n) * 16, n0 = (int64_t)(t % tiles_n) * 16;
   const int64_t ngrp = (d.K + 15) / 16;
   const int64_t g0 = ngrp * w / NW, g1 = ngrp * (w + 1) / NW;
+  const int64_t gf = min(g1, max(g0, d.K / 16));  // [g0, gf): groups wholly inside K
   const int i = lane & 15, q = lane >> 4;
   const int64_t am = m0 + i, bn = n0 + i;
+  const bool kgather = (AT && d.a_rows) || (!BT && d.b_rows);
   f4 acc = {0.f, 0.f, 0.f, 0.f};
   float cs = 0.f;
-  float a[SK16_DEPTH][4], b[SK16_DEPTH][4];
-  auto load = [&](int64_t gg, float (&aa)[4], float (&bb)[4]) {
+  const bool aok = am < d.M, bok = bn < d.N;  // clamped loads masked at the use
+  auto mma = [&](const float (&aa)[4], const float (&bb)[4]) {
+    float x[4], y[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[j] = aok ? aa[j] : 0.f;
+      y[j] = bok ? bb[j] : 0.f;
+    }
+    cs += (x[0] + x[1]) + (x[2] + x[3]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], y[s], acc, 0, 0, 0);
+  };
+  auto load_guarded = [&](int64_t gg, float (&aa)[4], float (&bb)[4]) {
     const int64_t k = gg * 16 + 4 * q;
     sk_load4<!AT>(d.A, d.lda, d.a_rows, am, d.M, k, d.K, avec, aa);
     sk_load4<BT>(d.B, d.ldb, d.b_rows, bn, d.N, k, d.K, bvec, bb);
   };
-  auto mma = [&](const float (&aa)[4], const float (&bb)[4]) {
-    cs += (aa[0] + aa[1]) + (aa[2] + aa[3]);
+  if (!kgather) {
+    const float* ab = sk_base<!AT>(d.A, d.lda, AT ? nullptr : d.a_rows, am, d.M);
+    const float* bb_ = sk_base<BT>(d.B, d.ldb, BT ? d.b_rows : nullptr, bn, d.N);
+    float a[SK16_DEPTH][4], b[SK16_DEPTH][4];
+    auto load = [&](int64_t gg, float (&aa)[4], float (&bx)[4]) {
+      const int64_t k = gg * 16 + 4 * q;
+      sk_full4<!AT, AV>(ab, d.lda, k, aa);
+      sk_full4<BT, BV>(bb_, d.ldb, k, bx);
+    };
+    sk_ring<SK16_DEPTH>(g0, (int)(gf - g0), a, b, load, mma);
+    if (gf < g1) {
+      float aa[4], bx[4];
+      load_guarded(gf, aa, bx);
+      mma(aa, bx);
+    }
+  } else {
+    float a[SK16_DEPTH][4], b[SK16_DEPTH][4];
+    const int ng = (int)(g1 - g0);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[s], bb[s], acc, 0, 0, 0);
-  };
-  const int ng = (int)(g1 - g0);
+    for (int q2 = 0; q2 < SK16_DEPTH; ++q2)
+      if (q2 < ng) load_guarded(g0 + q2, a[q2], b[q2]);
+    for (int pi = 0; pi < ng; pi += SK16_DEPTH) {
 #pragma unroll
-  for (int q2 = 0; q2 < SK16_DEPTH; ++q2)
-    if (q2 < ng) load(g0 + q2, a[q2], b[q2]);
-  for (int pi = 0; pi < ng; pi += SK16_DEPTH) {
-#pragma unroll
-    for (int q2 = 0; q2 < SK16_DEPTH; ++q2) {
-      if (pi + q2 < ng) {
-        mma(a[q2], b[q2]);
-        if (pi + q2 + SK16_DEPTH < ng) load(g0 + pi + q2 + SK16_DEPTH, a[q2], b[q2]);
+      for (int q2 = 0; q2 < SK16_DEPTH; ++q2) {
+        if (pi + q2 < ng) {
+          mma(a[q2], b[q2]);
+          if (pi + q2 + SK16_DEPTH < ng) load_guarded(g0 + pi + q2 + SK16_DEPTH, a[q2], b[q2]);
+        }
       }
     }
   }
@@ -687,6 +816,15 @@ __global__ __launch_bounds__(64 * NW) void gemm_skinny16_kernel(savqa_gemm_desc 
     }
   }
 }
+
+// skinny launches: the operands' vector-load eligibility picks the instantiation
+#define SAVQA_SK_LAUNCH(K_, AT_, BT_)                                                          \
+  do {                                                                                         \
+    if (avec && bvec) hipLaunchKernelGGL((K_<AT_, BT_, SK_WAVES, true, true>), g, b, 0, s, d, tn, avec, bvec);    \
+    else if (avec) hipLaunchKernelGGL((K_<AT_, BT_, SK_WAVES, true, false>), g, b, 0, s, d, tn, avec, bvec);      \
+    else if (bvec) hipLaunchKernelGGL((K_<AT_, BT_, SK_WAVES, false, true>), g, b, 0, s, d, tn, avec, bvec);      \
+    else hipLaunchKernelGGL((K_<AT_, BT_, SK_WAVES, false, false>), g, b, 0, s, d, tn, avec, bvec);               \
+  } while (0)
 
 static int slots_per_launch() {
   // 2 workgroups per CU (launch bounds / LDS); the CU count of the current device
@@ -864,17 +1002,17 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   } else if (p.tile == 16) {
     const int tn = p.gg.tiles_n;
     const dim3 g(p.grid_x), b(64 * SK_WAVES);
-    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
-    else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<false, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
-    else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny16_kernel<true, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
-    else hipLaunchKernelGGL((gemm_skinny16_kernel<true, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+    if (!d.a_trans && d.b_trans) SAVQA_SK_LAUNCH(gemm_skinny16_kernel, false, true);
+    else if (!d.a_trans) SAVQA_SK_LAUNCH(gemm_skinny16_kernel, false, false);
+    else if (!d.b_trans) SAVQA_SK_LAUNCH(gemm_skinny16_kernel, true, false);
+    else SAVQA_SK_LAUNCH(gemm_skinny16_kernel, true, true);
   } else {
     const dim3 g(p.grid_x), b(64 * SK_WAVES);
     const int tn = p.gg.tiles_n;
-    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
-    else if (!d.a_trans) hipLaunchKernelGGL((gemm_skinny_kernel<false, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
-    else if (!d.b_trans) hipLaunchKernelGGL((gemm_skinny_kernel<true, false, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
-    else hipLaunchKernelGGL((gemm_skinny_kernel<true, true, SK_WAVES>), g, b, 0, s, d, tn, avec, bvec);
+    if (!d.a_trans && d.b_trans) SAVQA_SK_LAUNCH(gemm_skinny_kernel, false, true);
+    else if (!d.a_trans) SAVQA_SK_LAUNCH(gemm_skinny_kernel, false, false);
+    else if (!d.b_trans) SAVQA_SK_LAUNCH(gemm_skinny_kernel, true, false);
+    else SAVQA_SK_LAUNCH(gemm_skinny_kernel, true, true);
   }
   return check_launch("savqa_gemm");
 }

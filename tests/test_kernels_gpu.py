@@ -122,7 +122,8 @@ def test_gemm_dw_auto_split(N, K, rows):
     assert rel(dW, dW0.double() + dY.double().t() @ X.double()) < 1e-5
 
 
-@pytest.mark.parametrize("M,N,K", [(33, 65, 37), (256, 512, 2048), (256, 914, 1024), (1, 7, 3)])
+@pytest.mark.parametrize("M,N,K", [(33, 65, 37), (256, 512, 2048), (256, 914, 1024), (1, 7, 3),
+                                   (512, 512, 520), (16, 1024, 256)])
 @pytest.mark.parametrize("at,bt", [(False, True), (False, False), (True, False), (True, True)])
 def test_gemm_skinny_layouts(M, N, K, at, bt):
     """Few-tile problems run the skinny kernel (32x32 tiles, K split over 8 waves): every
