@@ -124,7 +124,9 @@ __device__ __forceinline__ void row_forward(const AttnArgs& a, int b, int i, int
 template <int KB>
 __global__ __launch_bounds__(256) void gattn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int bh = blockIdx.x;
+  // XCD-aware (common.h xcd_remap): the H heads of a sample run on one XCD, so its graph
+  // rows come from HBM once per L2 instead of once per head
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);
   const int b = bh / a.H, h = bh % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float* Ks = sm;
@@ -185,7 +187,9 @@ __global__ __launch_bounds__(256) void gattn_fwd_kernel(AttnArgs a) {
 template <int KB>
 __global__ __launch_bounds__(256) void gattn_bwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int bh = blockIdx.x;
+  // XCD-aware (common.h xcd_remap): the H heads of a sample run on one XCD, so its graph
+  // rows come from HBM once per L2 instead of once per head
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);
   const int b = bh / a.H, h = bh % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int PLD = a.Tk + 1;
@@ -420,7 +424,9 @@ __device__ __forceinline__ void preload_graph(const A& a, int b, int i0, int g, 
 template <int NJT, typename T>
 __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgsT<T> a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int bh = blockIdx.x;
+  // XCD-aware (common.h xcd_remap): the H heads of a sample run on one XCD, so its graph
+  // rows come from HBM once per L2 instead of once per head
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);
   const int b = bh / a.H, h = bh % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = lane & 15, g = lane >> 4;
@@ -509,7 +515,9 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgsT<T> a) {
 template <int NJT, typename T>
 __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgsT<T> a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int bh = blockIdx.x;
+  // XCD-aware (common.h xcd_remap): the H heads of a sample run on one XCD, so its graph
+  // rows come from HBM once per L2 instead of once per head
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);
   const int b = bh / a.H, h = bh % a.H;
   const int nw = blockDim.x >> 6;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

@@ -71,7 +71,9 @@ __global__ __launch_bounds__(256) void gattn_fwd_flash_kernel(AttnArgs a, float*
                                                              int nqt) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int nw = blockDim.x >> 6;
-  const int qt = blockIdx.x % nqt, bh = blockIdx.x / nqt;
+  // XCD-aware: the tiles of a (sample, head) and the heads of a sample share an XCD's L2
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = bid % nqt, bh = bid / nqt;
   const int b = bh / a.H, h = bh % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = lane & 15, g = lane >> 4;
@@ -206,7 +208,9 @@ __global__ __launch_bounds__(256) void gattn_bwd_kv_flash_kernel(AttnArgs a,
                                                                 int nkt2) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int nw = blockDim.x >> 6;
-  const int kt = blockIdx.x % nkt2, bh = blockIdx.x / nkt2;
+  // XCD-aware: the tiles of a (sample, head) and the heads of a sample share an XCD's L2
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kt = bid % nkt2, bh = bid / nkt2;
   const int b = bh / a.H, h = bh % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = lane & 15, g = lane >> 4;
@@ -308,7 +312,9 @@ __global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
                                                                int nqt) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int nw = blockDim.x >> 6;
-  const int qt = blockIdx.x % nqt, bh = blockIdx.x / nqt;
+  // XCD-aware: the tiles of a (sample, head) and the heads of a sample share an XCD's L2
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = bid % nqt, bh = bid / nqt;
   const int b = bh / a.H, h = bh % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = lane & 15, g = lane >> 4;
