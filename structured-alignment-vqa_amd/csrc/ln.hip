@@ -99,6 +99,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 // (one row's loads in flight per wave left every wave waiting on HBM latency).
 constexpr int LN_BWD_WAVES = 8;
 constexpr int LN_SLOTS = 16;
+// grid cap: 1024 / 2048 blocks with 32 / 64 slots measured slower standalone (18688 x 512:
+// 22.9 us = 5.0 TB/s at 512 blocks / 16 slots; 25.1 / 27.9 / 41.9 us) and equal in-step
+constexpr int LN_BWD_BLOCKS = 512;
 
 template <int NV, bool ADD>
 struct LnBwdRow {
@@ -286,7 +289,7 @@ extern "C" int savqa_ln_bwd(void* stream, const float* dy, const float* z, const
   if (!ws || ws_bytes < savqa_ln_bwd_workspace_bytes(cols) || ((uintptr_t)ws & 15))
     return fail(SAVQA_EINVAL, "savqa_ln_bwd: workspace missing, too small or not 16-B aligned");
   int64_t blocks = (rows + LN_BWD_WAVES - 1) / LN_BWD_WAVES;
-  if (blocks > 512) blocks = 512;
+  if (blocks > LN_BWD_BLOCKS) blocks = LN_BWD_BLOCKS;
   const dim3 g((unsigned)blocks), b(64 * LN_BWD_WAVES);
   hipStream_t st = as_stream(stream);
   switch (cols / 256) {

@@ -88,6 +88,9 @@ def main():
              ("dx ffn2 m", "NN", Ms, 2048, 512, "bf16mask"), ("fwd ffn2 r", "NT", Ms, 512, 2048, "f32resid"),
              ("dx ffn1 r", "NN", Ms, 512, 2048, "f32resid")]
     hints = [0] + ([1, 3, 5] if "--variants" in sys.argv else [])
+    if "--square" in sys.argv:  # structure check at 8192^3 / 4096^3 (cdna guide's reference shapes)
+        hints = [1, 3, 5]
+        cases = [(f"sq{n}", lay, n, n, n, "bf16") for n in (4096, 8192) for lay in ("NT", "NN", "TN")]
     if "--dbg" in sys.argv:  # v5 as is / without MFMAs / without k-loop DMAs / no epilogue
         hints = [5, 5 + 256, 5 + 512, 5 + 1024, 5 + 256 + 1024]
         cases = cases[1:4] + cases[6:7] + cases[10:11]
@@ -111,7 +114,8 @@ def main():
     for h in hints:
         print(f"bf16 total v{h}: {tot_f/tot_t[h]/1e12:.1f} TF over the cfg-3 encoder shapes",
               flush=True)
-    for name, m, n, k in (("fp8 vis in", 1024 * 50, 512, 2048), ("fp8 vis_mlp", 1024 * 36, 1024, 2048)):
+    for name, m, n, k in (() if "--square" in sys.argv else
+                          (("fp8 vis in", 1024 * 50, 512, 2048), ("fp8 vis_mlp", 1024 * 36, 1024, 2048))):
         f, g = fp8_case(m, n, k)
         fl = 2.0 * m * n * k
         t1, t2 = timeit(f), timeit(g)
