@@ -67,6 +67,10 @@ class _Tar:
             self._fid, self._pid = tarfile.open(self.path), os.getpid()
         return self._fid.extractfile(member).read()
 
+    def __getstate__(self):
+        # spawned loader workers get the index, never the parent's open handle
+        return {"path": self.path, "members": self.members, "_fid": None, "_pid": None}
+
 
 class GQADataset_super_node(tud.Dataset):
     """onlyobj:41-99 constructor; opt carries data_dir_azure, maxlen, gt_relation_fn,

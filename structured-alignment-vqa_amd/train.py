@@ -143,6 +143,9 @@ def gqa_loaders(args, rank):
     with open(os.path.join(args.data_dir_azure, args.obj_vocab_fn)) as fid:
         args.bg_class = len(fid.readlines()) + 1
     out = {}
+    # Workers forked from a process whose HIP runtime (and its threads) is live can
+    # inherit a held lock and stall; once the device is up they are spawned instead.
+    ctx = "spawn" if args.num_workers > 0 and torch.cuda.is_initialized() else None
     for split in ("train", "val"):
         ds = cls(split, args, getattr(args, f"fea_tar_fn_{split}"),
                                    getattr(args, f"q_tar_fn_{split}"),
@@ -150,7 +153,7 @@ def gqa_loaders(args, rank):
         sampler = tud.distributed.DistributedSampler(ds, num_replicas=args.world_size, rank=rank)
         out[split] = tud.DataLoader(ds, batch_size=args.batch_size, num_workers=args.num_workers,
                                     drop_last=True, collate_fn=pack, sampler=sampler,
-                                    pin_memory=True)
+                                    pin_memory=True, multiprocessing_context=ctx)
     return out
 
 

@@ -102,3 +102,21 @@ def test_relation_reader_items_pack_like_the_reference_collate(tmp_path):
     got = _expand(pack(kept))
     for k in ref:
         assert np.array_equal(ref[k], got[k]), k
+
+
+def test_spawned_loader_workers(tmp_path):
+    """Once the device is initialised train.gqa_loaders spawns its workers instead of
+    forking them: the dataset (tar index without the parent's handle) and collate.pack
+    must cross a spawn boundary and yield the same batches as in-process loading."""
+    import torch.utils.data as tud
+    from savqa_amd.gqa import GQADataset_super_node
+    from savqa_amd.collate import pack
+    fx.write_dataset(str(tmp_path), n_questions=16)
+    ds = _dataset(str(tmp_path), dict(with_loc=True, pred_rel=False, topN=5))
+    ds[0]  # opens the tar handle in this process; it must not be pickled
+    kw = dict(batch_size=4, drop_last=True, collate_fn=pack, shuffle=False)
+    here = [pk.B for pk in tud.DataLoader(ds, num_workers=0, **kw)]
+    there = [pk.B for pk in tud.DataLoader(ds, num_workers=2, multiprocessing_context="spawn",
+                                           **kw)]
+    assert isinstance(ds, GQADataset_super_node)
+    assert here == there and len(here) > 0
