@@ -351,20 +351,34 @@ __device__ __forceinline__ void strip_dots(const f4v (&x)[4], const float* y, in
   }
 }
 
-// Cooperative stage of K_h and V_h rows [0, TK) into LDS (zero rows past Tk): every
-// thread issues its b128 loads back to back, so the workgroup waits one latency.
+// Cooperative stage of K_h and V_h rows [0, TK) into LDS (zero rows past Tk). Batches of
+// SKV_BATCH loads per thread are issued back to back from clamped (always valid) rows and
+// only then stored, so a batch costs one memory latency (a guarded load in a rolled loop
+// waited for every iteration's loads in turn: 4 round trips per workgroup at T = 73).
+constexpr int SKV_BATCH = 4;
 template <int TK, class A>
 __device__ __forceinline__ void stage_kv_tiles(const A& a, int b, int h, float* Ks, float* Vs) {
-  for (int idx = threadIdx.x; idx < TK * 16; idx += blockDim.x) {
-    const int j = idx >> 4, c4 = (idx & 15) * 4;
-    f4v kv = {0.f, 0.f, 0.f, 0.f}, vv = kv;
-    if (j < a.Tk) {
+  for (int base = threadIdx.x; base < TK * 16; base += SKV_BATCH * blockDim.x) {
+    f4v kv[SKV_BATCH], vv[SKV_BATCH];
+#pragma unroll
+    for (int u = 0; u < SKV_BATCH; ++u) {
+      const int idx = base + u * blockDim.x;
+      const int j = min(idx >> 4, a.Tk - 1), c4 = (idx & 15) * 4;
       const int64_t row = (int64_t)b * a.Tk + j;
-      kv = ldx4(a.k + row * a.ldk + h * ATT_DK + c4);
-      vv = ldx4(a.v + row * a.ldv + h * ATT_DK + c4);
+      kv[u] = ldx4(a.k + row * a.ldk + h * ATT_DK + c4);
+      vv[u] = ldx4(a.v + row * a.ldv + h * ATT_DK + c4);
     }
-    *reinterpret_cast<f4v*>(&Ks[j * ATT_KLD + c4]) = kv;
-    *reinterpret_cast<f4v*>(&Vs[j * ATT_KLD + c4]) = vv;
+#pragma unroll
+    for (int u = 0; u < SKV_BATCH; ++u) {
+      const int idx = base + u * blockDim.x;
+      if (idx < TK * 16) {
+        const int j = idx >> 4, c4 = (idx & 15) * 4;
+        const bool ok = j < a.Tk;
+        const f4v z = {0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4v*>(&Ks[j * ATT_KLD + c4]) = ok ? kv[u] : z;
+        *reinterpret_cast<f4v*>(&Vs[j * ATT_KLD + c4]) = ok ? vv[u] : z;
+      }
+    }
   }
 }
 
@@ -395,11 +409,12 @@ __device__ __forceinline__ float strip_row_forward(const f4v (&s)[NJT], int r, c
     sum += e;
   }
   sum = row16_sum(sum);
+  const float rsum = 1.f / sum;  // one division per row (the elements multiply)
   float nrm = 0.f;
 #pragma unroll
   for (int jt = 0; jt < NJT; ++jt) {
     const int j = jt * 16 + col;
-    aa[jt] = x[jt] / sum;
+    aa[jt] = x[jt] * rsum;
     gg[jt] = j < Tk ? gpre[jt] : 0.f;
     bm[jt] = gg[jt] * aa[jt];
     nrm += fabsf(bm[jt]);
@@ -445,7 +460,8 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgsT<T> a) {
   float* Vs = Ks + TK * ATT_KLD;            // [TK][ATT_KLD]
   float* Pw = Vs + TK * ATT_KLD + w * TK * WLD;
 #endif
-  stage_kv_tiles<TK>(a, b, h, Ks, Vs);
+  // strip operands, graph and flags first, then the K/V staging: every load of the
+  // workgroup's first phase is in flight together
   f4v qa[4];
   {
     const int iq = min(i0 + col, a.Tq - 1);
@@ -458,6 +474,7 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgsT<T> a) {
   float kf[NJT];
 #pragma unroll
   for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[(int64_t)b * a.Tk + min(jt * 16 + col, a.Tk - 1)];
+  stage_kv_tiles<TK>(a, b, h, Ks, Vs);
   __syncthreads();  // K/V staged
   f4v s[NJT];
   strip_dots_lds<NJT>(qa, Ks, col, g, s);
@@ -472,12 +489,12 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgsT<T> a) {
     const int ic = min(i, a.Tq - 1);
     float aa[NJT], gg[NJT], bm[NJT];
     const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
-    const float sden = fmaxf(nrm, 1e-12f);
+    const float rsd = 1.f / fmaxf(nrm, 1e-12f);
     const float qf = a.qflag[(int64_t)b * a.Tq + ic];
 #pragma unroll
     for (int jt = 0; jt < NJT; ++jt) {
       const int j = jt * 16 + col;
-      const float n = bm[jt] / sden;
+      const float n = bm[jt] * rsd;
       const bool ok = i < a.Tq && j < a.Tk;
       if (a.att && ok) a.att[(((int64_t)h * a.B + b) * a.Tq + i) * a.Tk + j] = n;
       pv[jt][r] = ok ? n * qf : 0.f;
@@ -532,8 +549,8 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgsT<T> a) {
   const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
   const int hd = h * ATT_DK;
 
-  stage_kv_tiles<TK>(a, b, h, Ks, Vs);
-  // ---- phase 1: strips
+  // ---- phase 1: strips (strip operands, graph and flags are loaded before the K/V
+  // staging, so all of the phase's loads are in flight together)
   {
     f4v qa[4], oa[4];
     const int iq = min(i0 + col, a.Tq - 1);
@@ -549,6 +566,7 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgsT<T> a) {
     float kf[NJT];
 #pragma unroll
     for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[kb + min(jt * 16 + col, a.Tk - 1)];
+    stage_kv_tiles<TK>(a, b, h, Ks, Vs);
     __syncthreads();  // K/V staged
     f4v s[NJT], dp[NJT];
     strip_dots_lds<NJT>(qa, Ks, col, g, s);
@@ -562,6 +580,7 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgsT<T> a) {
       float aa[NJT], gg[NJT], bm[NJT];
       const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
       const float sden = fmaxf(nrm, 1e-12f);
+      const float rsd = 1.f / sden;
       const float qf = a.qflag[qb + ic];
       float dn[NJT], t1 = 0.f;
 #pragma unroll
@@ -570,12 +589,12 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgsT<T> a) {
         t1 += dn[jt] * bm[jt];
       }
       t1 = row16_sum(t1);
-      const float dnrm = nrm >= 1e-12f ? -t1 / (sden * sden) : 0.f;
+      const float dnrm = nrm >= 1e-12f ? -t1 * (rsd * rsd) : 0.f;
       float da[NJT], t2 = 0.f;
 #pragma unroll
       for (int jt = 0; jt < NJT; ++jt) {
         const float sg = bm[jt] > 0.f ? 1.f : (bm[jt] < 0.f ? -1.f : 0.f);
-        const float dbm = dn[jt] / sden + dnrm * sg;
+        const float dbm = dn[jt] * rsd + dnrm * sg;
         da[jt] = dbm * gg[jt];
         t2 += da[jt] * aa[jt];
       }
@@ -587,7 +606,7 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgsT<T> a) {
         float ds = aa[jt] * (da[jt] - t2);
         if (kf[jt] == 0.f) ds = 0.f;
         dsv[jt][r] = ok ? ds * 0.125f : 0.f;
-        pv[jt][r] = ok ? bm[jt] / sden * qf : 0.f;
+        pv[jt][r] = ok ? bm[jt] * rsd * qf : 0.f;
       }
     }
 #pragma unroll

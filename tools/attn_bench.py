@@ -26,26 +26,34 @@ def timeit(fn, iters=20):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bf16", action="store_true", help="bf16 Q/K/V storage (cfg-3 mode)")
+    ap.add_argument("--B", type=int, default=256)
+    ap.add_argument("--T", type=int, nargs="*", default=[73, 50])
+    args = ap.parse_args()
     H, dk = 8, 64
     d = H * dk
-    for B, T in ((256, 73), (256, 50)):
-        qkv = torch.randn(B * T, 3 * d, device=dev).relu_()
+    dt = torch.bfloat16 if args.bf16 else torch.float32
+    for B, T in ((args.B, t) for t in args.T):
+        qkv = torch.randn(B * T, 3 * d, device=dev).relu_().to(dt)
         G = (torch.rand(B, T, T, device=dev) < 0.3).float()
         flag = torch.ones(B * T, device=dev)
         o = torch.empty(B * T, d, device=dev)
         dout = torch.randn(B * T, d, device=dev)
-        dqkv = torch.zeros(B * T, 3 * d, device=dev)
+        dqkv = torch.zeros(B * T, 3 * d, device=dev, dtype=dt)
         f = lambda: ops.gattn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag,
                                   flag, B, T, T, H, o, d)
         g = lambda: ops.gattn_bwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag,
                                   flag, B, T, T, H, dout, d, dqkv, 3 * d, dqkv[:, d:], 3 * d,
                                   dqkv[:, 2 * d:], 3 * d)
         tf, tb = timeit(f), timeit(g)
-        fb = B * T * 3 * d * 4 + B * T * T * 4 + B * T * d * 4
-        bb = B * T * 4 * d * 4 + B * T * T * 4 + B * T * 3 * d * 4
+        es = 2 if args.bf16 else 4  # Q/K/V/dQ/dK/dV element size; O, dO, graph fp32
+        fb = B * T * 3 * d * es + B * T * T * 4 + B * T * d * 4
+        bb = B * T * 3 * d * es + B * T * d * 4 + B * T * T * 4 + B * T * 3 * d * es
         ffl = B * H * 4 * T * T * dk
         bfl = B * H * 10 * T * T * dk
-        print(f"B={B} T={T}: fwd {tf*1e6:7.1f} us {fb/tf/1e9:6.0f} GB/s {ffl/tf/1e12:5.1f} TF | "
+        print(f"{dt} B={B} T={T}: fwd {tf*1e6:7.1f} us {fb/tf/1e9:6.0f} GB/s {ffl/tf/1e12:5.1f} TF | "
               f"bwd {tb*1e6:7.1f} us {bb/tb/1e9:6.0f} GB/s {bfl/tb/1e12:5.1f} TF", flush=True)
 
 

@@ -91,6 +91,11 @@ def main():
     if "--square" in sys.argv:  # structure check at 8192^3 / 4096^3 (cdna guide's reference shapes)
         hints = [1, 3, 5]
         cases = [(f"sq{n}", lay, n, n, n, "bf16") for n in (4096, 8192) for lay in ("NT", "NN", "TN")]
+    if "--msweep" in sys.argv:  # wave quantisation: the same shapes at whole-round row counts
+        hints = [1, 3, 4, 5]
+        cases = [(f"m{m}", lay, m, n, k, out) for m in (32768, 37376, 40960)
+                 for lay, n, k, out in (("NT", 512, 2048, "f32"), ("NN", 512, 2048, "f32"),
+                                        ("NT", 2048, 512, "bf16"), ("NN", 2048, 512, "bf16"))]
     if "--dbg" in sys.argv:  # v5 as is / without MFMAs / without k-loop DMAs / no epilogue
         hints = [5, 5 + 256, 5 + 512, 5 + 1024, 5 + 256 + 1024]
         cases = cases[1:4] + cases[6:7] + cases[10:11]
