@@ -52,6 +52,23 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   return base + (bid >> 3);
 }
 
+// (tile, k-slice) of a split-K launch (grid = tiles x slices), XCD-aware over the WHOLE grid
+// in slice-major order: each XCD runs a contiguous run of (slice, tile) items, i.e. whole
+// k-slices, so a slice's operand rows are fetched into one XCD's L2 and shared by every tile
+// of that slice there. (Remapping only the tile index gave every XCD the same tiles of
+// every slice: each XCD then streamed all k-slices of its tiles' operand columns, and the
+// N-side operand was fetched by all eight L2s.) Unsplit launches: xcd_remap of the tile.
+__device__ __forceinline__ void split_remap(int nblk, int& tile, int& slice) {
+  if (gridDim.y == 1) {
+    tile = xcd_remap(blockIdx.x, nblk);
+    slice = 0;
+    return;
+  }
+  const int item = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+  slice = item / gridDim.x;
+  tile = item - slice * gridDim.x;
+}
+
 // Dropout keep bits (nn.Dropout sites of the path, AttModel_x3.py:71-72, 102, 147, 227, 274,
 // 482-500). torch's Philox stream cannot be reproduced bit-for-bit, so the library defines
 // its own counter-based stream: element idx of dropout site `site` under step seed `seed`

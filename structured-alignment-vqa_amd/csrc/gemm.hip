@@ -366,10 +366,11 @@ __global__ __launch_bounds__(GEMM_NT, GEMM_OCC) __attribute__((amdgpu_waves_per_
   int64_t kbeg, kend;
   bool first_split, atomic;
   if (bid < gg.full) {
-    t = xcd_remap(bid, gg.full);
-    kbeg = (int64_t)blockIdx.y * gg.kchunk;
+    int slice;  // (split launches have no tail: grid.x == gg.full)
+    split_remap(gg.full, t, slice);
+    kbeg = (int64_t)slice * gg.kchunk;
     kend = min(d.K, kbeg + gg.kchunk);
-    first_split = blockIdx.y == 0;
+    first_split = slice == 0;
     atomic = d.atomic || gridDim.y > 1;
   } else {
     const int u = bid - gg.full;

@@ -231,10 +231,11 @@ __global__ __launch_bounds__(GEMM_NT, 2) void gemm_bf16_kernel(savqa_gemm_desc d
   int64_t kbeg, kend;
   bool first_split, atomic;
   if (bid < gg.full) {
-    t = xcd_remap(bid, gg.full);
-    kbeg = (int64_t)blockIdx.y * gg.kchunk;
+    int slice;
+    split_remap(gg.full, t, slice);
+    kbeg = (int64_t)slice * gg.kchunk;
     kend = min(d.K, kbeg + gg.kchunk);
-    first_split = blockIdx.y == 0;
+    first_split = slice == 0;
     atomic = d.atomic || gridDim.y > 1;
   } else {
     const int u = bid - gg.full;

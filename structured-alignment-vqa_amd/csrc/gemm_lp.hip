@@ -61,8 +61,12 @@ struct LpArgs {
   int tiles_n, ntiles_k;  // k-tiles per split slice
   int64_t kchunk;         // elements of k per split slice
   int nblk;               // tiles (grid.x)
-  int dbg;                // diagnostics (bits): 1 = skip the MFMAs, 2 = skip the k-loop DMAs,
-                          // 4 = skip the epilogue (gemm_lp3_kernel)
+  // tail split (gemm_lp_kernel, unsplit launches): blocks >= full take the last tiles, from
+  // tail_t0 on, in tail_f k-slices of tail_kchunk each, accumulated atomically into C
+  int full, tail_t0, tail_f;
+  int64_t tail_kchunk;
+  int dbg;                // diagnostics (bits): 1 = skip the MFMAs (bf16), 2 = skip the k-loop
+                          // DMAs, 4 = skip the epilogue (gemm_lp_kernel, gemm_lp3_kernel)
 };
 
 // Per-lane LDS-DMA sources of one operand, resolved once per workgroup.
@@ -327,7 +331,7 @@ template <int FM, int FN>
 __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&acc)[FM][FN],
                                             char* reg, int64_t row0, int64_t col0,
                                             bool first_split, int lane, int64_t rstep = 64,
-                                            int64_t col_hi = -1) {
+                                            int64_t col_hi = -1, bool tail_atomic = false) {
   if (col_hi < 0) col_hi = col0 + 32;
   static_assert(FN == 4, "wave tiles are 64 columns wide");
   const int g = lane >> 4;
@@ -345,7 +349,7 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
       }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is complete
     __builtin_amdgcn_wave_barrier();
-    if (d.atomic) {
+    if (d.atomic || tail_atomic) {
       // one float per lane: row q, column lane (256 contiguous bytes per atomic instruction)
       const int64_t n = ecol(col0, col_hi, lane);
       const float bv = (first_split && d.bias && n < d.N) ? d.bias[n] : 0.f;
@@ -601,15 +605,26 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int t = xcd_remap(blockIdx.x, args.nblk);
+  int t, slice;
+  int64_t kbeg, kend;
+  const bool tail = (int)blockIdx.x >= args.full;  // tail-split block (atomic epilogue)
+  if (!tail) {
+    split_remap(args.full, t, slice);
+    kbeg = (int64_t)slice * args.kchunk;
+    kend = min(d.K, kbeg + args.kchunk);
+  } else {
+    const int u = blockIdx.x - args.full;
+    slice = u % args.tail_f;
+    t = args.tail_t0 + u / args.tail_f;
+    kbeg = (int64_t)slice * args.tail_kchunk;
+    kend = min(d.K, kbeg + args.tail_kchunk);
+  }
   const int tn = t % args.tiles_n, tm = t / args.tiles_n;
   const int64_t m0 = (int64_t)tm * LP_TILE, n0 = (int64_t)tn * LP_TILE;
-  const int64_t kbeg = (int64_t)blockIdx.y * args.kchunk;
-  const int64_t kend = min(d.K, kbeg + args.kchunk);
   constexpr int BKE = FP8 ? 128 : 64;  // k elements per k-tile
   const int nt = (int)((kend - kbeg + BKE - 1) / BKE);
   const int krem = (int)(kend - kbeg - (int64_t)(nt - 1) * BKE);  // k of the last k-tile
-  const bool first_split = blockIdx.y == 0;
+  const bool first_split = slice == 0;
   const int esz = FP8 ? 1 : 2;
 
   LpStage<AT, FP8> sa;
@@ -624,7 +639,7 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   LpPre<PRE> pre;
   if constexpr (PRE != 0) {
-    if (nt == 0) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
+    if (nt == 0 && !tail) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
   }
 
   // fp8 block scales of this lane's rows: A rows (m), B rows (n), block k/32 + g
@@ -668,10 +683,10 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
         for (int i = 0; i < 4; ++i) { sca_c[i] = sca[i]; scb_c[i] = scb[i]; }
       }
       if (kt + 1 < nt) {  // next k-tile into the other buffer (read one barrier ago)
-        stage(smem + ((kt + 1) & 1) * 2 * LP_IMG, kt + 1);
+        if (!(args.dbg & 2)) stage(smem + ((kt + 1) & 1) * 2 * LP_IMG, kt + 1);
         load_scales(kt + 1);
       } else if constexpr (PRE != 0) {  // last k-tile: epilogue operands under its MFMAs
-        pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
+        if (!tail) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
       }
       if constexpr (FP8) {
         i32x8 a[4], b[4];
@@ -688,6 +703,7 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
       } else {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
+          if (args.dbg & 1) break;
           bf16x8 a[4], b[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) a[i] = frag_bf16<AT>(ia, wm * 64 + 16 * i, kk, lane);
@@ -706,7 +722,14 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
 
   // ---------------------------------------------------------------- epilogue
   __syncthreads();  // every wave's last k-tile reads are done: LDS is free
-  if constexpr (PRE != 0)
+  if (args.dbg & 4) {  // diagnostics: no epilogue (one store keeps the k-loop alive)
+    if (acc[0][0][0] == 12345.f && d.C) d.C[0] = acc[3][3][3];
+    return;
+  }
+  if (tail)
+    lp_epilogue<4, 4>(d, acc, smem + wave * 16384, m0 + wm * 64, n0 + wn * 64, first_split, lane,
+                      64, -1, true);
+  else if constexpr (PRE != 0)
     lp_epilogue_pre<PRE>(d, acc, smem + wave * 16384, m0 + wm * 64, n0 + wn * 64, pre, lane);
   else
     lp_epilogue<4, 4>(d, acc, smem + wave * 16384, m0 + wm * 64, n0 + wn * 64, first_split, lane);
@@ -816,14 +839,15 @@ __global__ __launch_bounds__(512, 1) void gemm_lp2_kernel(LpArgs args) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int t = xcd_remap(blockIdx.x, args.nblk);
+  int t, slice;
+  split_remap(args.nblk, t, slice);
   const int tn = t % args.tiles_n, tm = t / args.tiles_n;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int64_t kbeg = (int64_t)blockIdx.y * args.kchunk;
+  const int64_t kbeg = (int64_t)slice * args.kchunk;
   const int64_t kend = min(d.K, kbeg + args.kchunk);
   const int nt = (int)((kend - kbeg + BK - 1) / BK);
   const int krem = (int)(kend - kbeg - (int64_t)(nt - 1) * BK);  // k of the last k-tile
-  const bool first_split = blockIdx.y == 0;
+  const bool first_split = slice == 0;
 
   Lp2Stage<AT, BM, BK> sa;
   Lp2Stage<!BT, BN, BK> sb;
@@ -957,14 +981,15 @@ __global__ __launch_bounds__(512, 1) void gemm_lp3_kernel(LpArgs args) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 2, wn = wave & 3;
-  const int t = xcd_remap(blockIdx.x, args.nblk);
+  int t, slice;
+  split_remap(args.nblk, t, slice);
   const int tn = t % args.tiles_n, tm = t / args.tiles_n;
   const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
-  const int64_t kbeg = (int64_t)blockIdx.y * args.kchunk;
+  const int64_t kbeg = (int64_t)slice * args.kchunk;
   const int64_t kend = min(d.K, kbeg + args.kchunk);
   const int nt = (int)((kend - kbeg + 63) / 64);
   const int krem = (int)(kend - kbeg - (int64_t)(nt - 1) * 64);  // k of the last k-tile
-  const bool first_split = blockIdx.y == 0;
+  const bool first_split = slice == 0;
 
   LpHalf<AT> sa[2];
   LpHalf<!BT> sb[2];
@@ -1112,6 +1137,10 @@ struct LpPlan {
   int64_t tiles, per;
   int bn;
   int pre;  // gemm_lp_kernel's epilogue-operand prefetch (LpPre): 0 none, 1 resid, 2 bf16 mask
+  // tail split (variant 1, unsplit): tiles [tail_t0, tiles) in tail_f k-slices, rows
+  // [zero_row0, M) of C zero-filled first; tail_f = 1: none
+  int tail_f;
+  int64_t tail_t0, tail_per, zero_row0;
 };
 
 static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
@@ -1161,6 +1190,39 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
     if (d.resid && !d.mask) p.pre = 1;
     else if (d.mask && lp_wide_epilogue(d)) p.pre = 2;
   }
+  // Tail split (as savqa_gemm's): the tiles of the last, partial round of workgroups are split
+  // over K (zero-filled C, atomic fp32 adds, bias / residual / row vector on slice 0) so that
+  // they spread over all CUs instead of leaving most of them idle for a whole tile. Needs a
+  // linear epilogue into fp32 C only (no ReLU, no bf16 copy), identity row map, and C not
+  // overlapping the residual.
+  p.tail_f = 1;
+  p.tail_t0 = p.tiles;
+  p.tail_per = p.per;
+  p.zero_row0 = -1;
+  bool tail_ok = p.var == 1 && p.nsplit == 1 && !d.atomic && d.C && !d.Cb && !d.relu &&
+                 d.c_group <= 0 && !d.c_rows && d.ldc >= d.N && d.tile_hint == 0;
+  if (tail_ok && d.resid) {
+    const char* c0 = (const char*)d.C;
+    const char* c1 = (const char*)(d.C + (d.M - 1) * d.ldc + d.N);
+    const char* r0 = (const char*)d.resid;
+    const char* r1 = (const char*)(d.resid + (d.M - 1) * d.ldr + d.N);
+    if (r0 < c1 && c0 < r1) tail_ok = false;
+  }
+  if (tail_ok && p.tiles > slots) {
+    const int64_t tn = (d.N + p.bn - 1) / p.bn;
+    int64_t r = p.tiles % slots;
+    r = (r + tn - 1) / tn * tn;  // whole rows of tiles: one contiguous zero-fill
+    if (r > 0 && r < p.tiles) {
+      int64_t f = slots / r;
+      if (f > nk / 4) f = nk / 4;
+      if (f >= 2) {
+        p.tail_per = (nk + f - 1) / f;
+        p.tail_f = (int)((nk + p.tail_per - 1) / p.tail_per);
+        p.tail_t0 = p.tiles - r;
+        p.zero_row0 = (p.tail_t0 / tn) * bm;
+      }
+    }
+  }
   return p;
 }
 
@@ -1180,7 +1242,7 @@ extern "C" int savqa_gemm_lp_plan(const savqa_gemm_lp_desc* d, int32_t* out) {
   const LpPlan p = lp_plan(*d);
   out[0] = p.var;
   out[1] = p.nsplit;
-  out[2] = (int32_t)(p.tiles * p.nsplit);
+  out[2] = (int32_t)(p.tail_t0 * p.nsplit + (p.tiles - p.tail_t0) * p.tail_f);
   out[3] = p.pre;
   return 0;
 }
@@ -1203,9 +1265,18 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   a.dbg = d.tile_hint >> 8;
   a.nblk = (int)p.tiles;
   a.ntiles_k = (int)p.per;
+  a.full = (int)p.tail_t0;
+  a.tail_t0 = (int)p.tail_t0;
+  a.tail_f = p.tail_f;
+  a.tail_kchunk = p.tail_per * bk;
   if (d.K == 0) a.kchunk = 0;
   hipStream_t s = as_stream(stream);
-  const dim3 grid((unsigned)p.tiles, (unsigned)p.nsplit), block(LP_NT);
+  if (p.zero_row0 >= 0 &&
+      hipMemset2DAsync(d.C + p.zero_row0 * d.ldc, d.ldc * sizeof(float), 0, d.N * sizeof(float),
+                       d.M - p.zero_row0, s) != hipSuccess)
+    return fail(SAVQA_EUNSUP, "savqa_gemm_lp: tail zero-fill failed");
+  const dim3 grid((unsigned)(p.tail_t0 + (p.tiles - p.tail_t0) * p.tail_f), (unsigned)p.nsplit),
+      block(LP_NT);
   if (var == 5) {
     const dim3 b3(512);
     if (!d.a_trans && d.b_trans)

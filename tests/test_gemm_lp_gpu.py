@@ -332,3 +332,87 @@ def test_fp8_scaled_mfma_gemm(M, N, K):
     assert float(err) < 1e-4
     # and the quantisation itself stays within e4m3's half-ulp (2^-4 relative) per element
     assert rel(_dequant(qx, sx), X.cpu()) < 2 ** -4
+
+
+def _lp_plan(O, d):
+    import ctypes as C
+    from savqa_amd import _lib
+    plan = (C.c_int32 * 4)()
+    assert _lib.load().savqa_gemm_lp_plan(C.byref(d), C.cast(plan, C.c_void_p)) == 0
+    return list(plan)
+
+
+@pytest.mark.parametrize("lay,epi,ldc_pad", [("NT", "resid", 0), ("NN", "bias", 8),
+                                             ("NT", "rowvec", 0), ("NN", "resid_bias", 16)])
+def test_bf16_tail_split_last_round(lay, epi, ldc_pad):
+    """Tail split: the tiles of the last, partial round of workgroups (M = 18688, N = 512:
+    584 tiles over 512 slots) are split over K with atomic fp32 adds into a zero-filled C;
+    bias / residual / row vector are added by slice 0 only, and a strided C (ldc > N) keeps
+    its other columns."""
+    O = ops()
+    M, N, K = 18688, 512, 2048
+    bt = lay[1] == "T"
+    A = bf((M, K), 31)
+    B = bf((N, K) if bt else (K, N), 32)
+    ldc = N + ldc_pad
+    Cfull = torch.full((M, ldc), 7.0, device=dev)
+    C = Cfull[:, :N]
+    kw = {}
+    ref = A.double() @ (B.t() if bt else B).double()
+    if "resid" in epi:
+        R = torch.randn(M, N, device=dev)
+        kw.update(resid=R, ldr=N)
+        ref = ref + R.double()
+    if "bias" in epi:
+        bias = torch.randn(N, device=dev)
+        kw.update(bias=bias)
+        ref = ref + bias.double()
+    if epi == "rowvec":
+        P = 73
+        rv = torch.randn(P, N, device=dev)
+        kw.update(rowvec=rv, ldrv=N, rowvec_period=P)
+        ref = ref + rv.double().repeat(M // P + 1, 1)[:M]
+    d = O.lp_desc(A, B, M, N, K, lda=K, ldb=K if bt else N, b_trans=bt, C=C, ldc=ldc, **kw)
+    plan = _lp_plan(O, d)
+    tiles = ((M + 127) // 128) * (N // 128)  # 146 x 4
+    assert plan[0] == 1 and plan[1] == 1 and plan[2] > tiles, plan  # tail blocks present
+    O.gemm_lp(A, B, M, N, K, lda=K, ldb=K if bt else N, b_trans=bt, C=C, ldc=ldc, **kw)
+    torch.cuda.synchronize()
+    err = float((C.double() - ref).abs().max() / ref.abs().max())
+    assert err < 2e-5, err
+    if ldc_pad:
+        assert bool((Cfull[:, N:] == 7.0).all())
+
+
+def test_fp8_tail_split_last_round():
+    """fp8 block-scaled GEMM at cfg 5's region-feature shape (51200 x 512 x 2048: 1600 tiles,
+    a 64-tile last round split over K) against fp64 on the dequantised operands."""
+    O = ops()
+    M, N, K = 51200, 512, 2048
+    g = torch.Generator(device=dev).manual_seed(5)
+    X = torch.randn(M, K, generator=g, device=dev).clamp_min(0)
+    W = torch.randn(N, K, generator=g, device=dev) / K ** 0.5
+    qx = torch.empty(M, K, dtype=torch.uint8, device=dev)
+    sx = torch.empty(M, K // 32, dtype=torch.uint8, device=dev)
+    qw = torch.empty(N, K, dtype=torch.uint8, device=dev)
+    sw = torch.empty(N, K // 32, dtype=torch.uint8, device=dev)
+    O.quant_fp8(X, M, K, K, qx, K, sx, K // 32)
+    O.quant_fp8(W, N, K, K, qw, K, sw, K // 32)
+    bias = torch.randn(N, device=dev)
+    C = torch.empty(M, N, device=dev)
+    kw = dict(lda=K, ldb=K, b_trans=True, a_scale=sx, lds_a=K // 32, b_scale=sw,
+              lds_b=K // 32, C=C, ldc=N, bias=bias)
+    plan = _lp_plan(O, O.lp_desc(qx.view(torch.float8_e4m3fn), qw.view(torch.float8_e4m3fn),
+                                 M, N, K, **kw))
+    assert plan[2] > 1600, plan
+    O.gemm_lp(qx.view(torch.float8_e4m3fn), qw.view(torch.float8_e4m3fn), M, N, K, **kw)
+
+    def deq(q, s):  # e4m3 value x 2^(e8m0 - 127), per 32-column block, on the GPU
+        v = q.view(torch.float8_e4m3fn).double()
+        return v * torch.pow(2.0, s.double() - 127).repeat_interleave(32, 1)
+
+    Xd, Wd = deq(qx, sx), deq(qw, sw)
+    ref = Xd @ Wd.t() + bias.double()
+    row_scale = (Xd.abs() @ Wd.abs().t()).amax(1, keepdim=True)
+    err = float(((C.double() - ref).abs() / row_scale.clamp_min(1e-30)).max())
+    assert err < 1e-4, err

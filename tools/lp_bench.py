@@ -96,7 +96,10 @@ def main():
         cases = [(f"m{m}", lay, m, n, k, out) for m in (32768, 37376, 40960)
                  for lay, n, k, out in (("NT", 512, 2048, "f32"), ("NN", 512, 2048, "f32"),
                                         ("NT", 2048, 512, "bf16"), ("NN", 2048, 512, "bf16"))]
-    if "--dbg" in sys.argv:  # v5 as is / without MFMAs / without k-loop DMAs / no epilogue
+    if "--dbg1" in sys.argv:  # 128x128 kernel as is / no MFMAs / no k-loop DMAs / no epilogue
+        hints = [1, 1 + 256, 1 + 512, 1 + 1024, 1 + 256 + 1024, 1 + 256 + 512]
+        cases = [cases[i] for i in (1, 2, 5, 10, 13)]
+    elif "--dbg" in sys.argv:  # v5 as is / without MFMAs / without k-loop DMAs / no epilogue
         hints = [5, 5 + 256, 5 + 512, 5 + 1024, 5 + 256 + 1024]
         cases = cases[1:4] + cases[6:7] + cases[10:11]
     tot_f = 0.0
