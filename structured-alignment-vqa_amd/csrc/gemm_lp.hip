@@ -1194,7 +1194,10 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
   // over K (zero-filled C, atomic fp32 adds, bias / residual / row vector on slice 0) so that
   // they spread over all CUs instead of leaving most of them idle for a whole tile. Needs a
   // linear epilogue into fp32 C only (no ReLU, no bf16 copy), identity row map, and C not
-  // overlapping the residual.
+  // overlapping the residual. Only for long K (>= 64 k-tiles): the atomic epilogue costs about
+  // a third of a K = 512 launch (diagnostic builds), and with the zero-fill it made the K = 2048
+  // step shapes 20-40 % slower (tools/lp_bench.py); at K = 6144 (dX of the decoder K/V
+  // projection) it is 8-10 % faster.
   p.tail_f = 1;
   p.tail_t0 = p.tiles;
   p.tail_per = p.per;
@@ -1208,7 +1211,7 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
     const char* r1 = (const char*)(d.resid + (d.M - 1) * d.ldr + d.N);
     if (r0 < c1 && c0 < r1) tail_ok = false;
   }
-  if (tail_ok && p.tiles > slots) {
+  if (tail_ok && p.tiles > slots && nk >= 64) {
     const int64_t tn = (d.N + p.bn - 1) / p.bn;
     int64_t r = p.tiles % slots;
     r = (r + tn - 1) / tn * tn;  // whole rows of tiles: one contiguous zero-fill
