@@ -96,7 +96,8 @@ def main():
         cases = [(f"m{m}", lay, m, n, k, out) for m in (32768, 37376, 40960)
                  for lay, n, k, out in (("NT", 512, 2048, "f32"), ("NN", 512, 2048, "f32"),
                                         ("NT", 2048, 512, "bf16"), ("NN", 2048, 512, "bf16"))]
-    if "--dbg1" in sys.argv:  # 128x128 kernel as is / no MFMAs / no k-loop DMAs / no epilogue
+    if "--dbg1" in sys.argv:  # 128x128 kernel as is / no MFMAs / no DMAs / no epilogue (needs a
+        # diagnostic build: the tile_hint >> 8 bits tested in gemm_lp_kernel as in gemm_lp3_kernel)
         hints = [1, 1 + 256, 1 + 512, 1 + 1024, 1 + 256 + 1024, 1 + 256 + 512]
         cases = [cases[i] for i in (1, 2, 5, 10, 13)]
     elif "--dbg" in sys.argv:  # v5 as is / without MFMAs / without k-loop DMAs / no epilogue
