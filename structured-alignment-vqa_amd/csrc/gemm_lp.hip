@@ -65,8 +65,9 @@ struct LpArgs {
   // tail_t0 on, in tail_f k-slices of tail_kchunk each, accumulated atomically into C
   int full, tail_t0, tail_f;
   int64_t tail_kchunk;
-  int dbg;                // diagnostics (bits): 1 = skip the MFMAs (bf16), 2 = skip the k-loop
-                          // DMAs, 4 = skip the epilogue (gemm_lp_kernel, gemm_lp3_kernel)
+  int dbg;                // diagnostics (bits): 1 = skip the MFMAs, 2 = skip the k-loop DMAs,
+                          // 4 = skip the epilogue (gemm_lp3_kernel; the 128x128 kernel's
+                          // breakdown in DESIGN.md came from a build with the same bits)
 };
 
 // Per-lane LDS-DMA sources of one operand, resolved once per workgroup.
@@ -607,7 +608,9 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   const int wm = wave >> 1, wn = wave & 1;
   int t, slice;
   int64_t kbeg, kend;
-  const bool tail = (int)blockIdx.x >= args.full;  // tail-split block (atomic epilogue)
+  // tail-split block (atomic epilogue); the host never pairs a tail split with an epilogue
+  // prefetch (PRE), so those instantiations carry no tail code (it cost them 20 % when present)
+  const bool tail = PRE == 0 && (int)blockIdx.x >= args.full;
   if (!tail) {
     split_remap(args.full, t, slice);
     kbeg = (int64_t)slice * args.kchunk;
@@ -683,7 +686,7 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
         for (int i = 0; i < 4; ++i) { sca_c[i] = sca[i]; scb_c[i] = scb[i]; }
       }
       if (kt + 1 < nt) {  // next k-tile into the other buffer (read one barrier ago)
-        if (!(args.dbg & 2)) stage(smem + ((kt + 1) & 1) * 2 * LP_IMG, kt + 1);
+        stage(smem + ((kt + 1) & 1) * 2 * LP_IMG, kt + 1);
         load_scales(kt + 1);
       } else if constexpr (PRE != 0) {  // last k-tile: epilogue operands under its MFMAs
         if (!tail) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
@@ -703,7 +706,6 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
       } else {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          if (args.dbg & 1) break;
           bf16x8 a[4], b[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) a[i] = frag_bf16<AT>(ia, wm * 64 + 16 * i, kk, lane);
@@ -722,10 +724,6 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
 
   // ---------------------------------------------------------------- epilogue
   __syncthreads();  // every wave's last k-tile reads are done: LDS is free
-  if (args.dbg & 4) {  // diagnostics: no epilogue (one store keeps the k-loop alive)
-    if (acc[0][0][0] == 12345.f && d.C) d.C[0] = acc[3][3][3];
-    return;
-  }
   if (tail)
     lp_epilogue<4, 4>(d, acc, smem + wave * 16384, m0 + wm * 64, n0 + wn * 64, first_split, lane,
                       64, -1, true);
@@ -1223,6 +1221,7 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
         p.tail_f = (int)((nk + p.tail_per - 1) / p.tail_per);
         p.tail_t0 = p.tiles - r;
         p.zero_row0 = (p.tail_t0 / tn) * bm;
+        p.pre = 0;  // the prefetching instantiations have no tail path
       }
     }
   }
