@@ -706,6 +706,333 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgsT<T> a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// bf16 MFMA strip kernels (bf16 training modes, cfg 3 / cfg 5). Same workgroup / wave /
+// strip structure and the same fp32 softmax -> graph -> L1 chain (and adjoint) as the fp32
+// kernels above, but the products run on bf16 matrix cores and every LDS image is bf16:
+//   S = Q K^T, dP = dO V^T     v_mfma_f32_16x16x32_bf16, 2 per 16x16 tile (Q, K, V are bf16
+//                              already: exact products, fp32 sums; dO is rounded to bf16);
+//   O = P V, dV = P^T dO,      v_mfma_f32_16x16x16_bf16, one per 16 k (P and dS rounded to
+//   dK = dS^T Q, dQ = dS K     bf16, as a bf16 attention's second GEMM does).
+// The fp32 kernels issue 4x (S) / 4x (phase 2) as many 16x16x4 MFMAs; halving the LDS
+// images (K/V staging, P^T / dS^T) doubles the workgroups per CU (T = 73 backward: 53.7 KB ->
+// 26.9 KB), which is what hides this latency-bound kernel's global loads.
+// Both MFMA forms take operand k-sets by lane group (A[m = l&15][k in set(l>>4)],
+// B[k in set(l>>4)][n = l&15], D[4(l>>4)+r][l&15]); A and B always use the same set, so the
+// inner products are exact whatever the hardware's k order inside a set.
+typedef __bf16 att_bf16x8 __attribute__((ext_vector_type(8)));
+typedef short att_s4 __attribute__((ext_vector_type(4)));
+constexpr int ATT_KLB = 72;  // staged K/V row (bf16): 144 B, conflict-free 16-B reads by 16 rows
+
+__device__ __forceinline__ f4v mfma_bf32(att_bf16x8 a, att_bf16x8 b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f4v mfma_bf16(att_bf16x4 a, att_bf16x4 b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(att_s4, a),
+                                                   __builtin_bit_cast(att_s4, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ att_bf16x8 cat8(att_bf16x4 lo, att_bf16x4 hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ att_bf16x4 ldb4(const __bf16* p) {
+  return *reinterpret_cast<const att_bf16x4*>(p);
+}
+__device__ __forceinline__ att_bf16x8 ldb8_lds(const __bf16* p) {
+  return *reinterpret_cast<const att_bf16x8*>(p);
+}
+// strip operand: 8 consecutive d (32c + 8g ..) of a bf16 row / of an fp32 row rounded to bf16
+__device__ __forceinline__ att_bf16x8 strip8(const __bf16* p) { return cat8(ldb4(p), ldb4(p + 4)); }
+__device__ __forceinline__ att_bf16x8 strip8(const float* p) {
+  return cat8(__builtin_convertvector(ld4(p), att_bf16x4), __builtin_convertvector(ld4(p + 4), att_bf16x4));
+}
+
+// K_h, V_h rows [0, TK) of sample b into bf16 LDS images [TK][ATT_KLB] (zero rows past Tk);
+// batched like stage_kv_tiles (all loads of a batch issued before any store)
+template <int TK>
+__device__ __forceinline__ void stage_kv_bf(const AttnArgsT<__bf16>& a, int b, int h, __bf16* Ks,
+                                            __bf16* Vs) {
+  for (int base = threadIdx.x; base < TK * 16; base += SKV_BATCH * blockDim.x) {
+    att_bf16x4 kv[SKV_BATCH], vv[SKV_BATCH];
+#pragma unroll
+    for (int u = 0; u < SKV_BATCH; ++u) {
+      const int idx = base + u * blockDim.x;
+      const int j = min(idx >> 4, a.Tk - 1), c4 = (idx & 15) * 4;
+      const int64_t row = (int64_t)b * a.Tk + j;
+      kv[u] = ldb4(a.k + row * a.ldk + h * ATT_DK + c4);
+      vv[u] = ldb4(a.v + row * a.ldv + h * ATT_DK + c4);
+    }
+#pragma unroll
+    for (int u = 0; u < SKV_BATCH; ++u) {
+      const int idx = base + u * blockDim.x;
+      if (idx < TK * 16) {
+        const int j = idx >> 4, c4 = (idx & 15) * 4;
+        const bool ok = j < a.Tk;
+        const att_bf16x4 z = {};
+        *reinterpret_cast<att_bf16x4*>(&Ks[j * ATT_KLB + c4]) = ok ? kv[u] : z;
+        *reinterpret_cast<att_bf16x4*>(&Vs[j * ATT_KLB + c4]) = ok ? vv[u] : z;
+      }
+    }
+  }
+}
+
+// acc[jt] = X_strip . Y_tile(jt)^T over d = 64 (Y staged bf16 in LDS)
+template <int NJT>
+__device__ __forceinline__ void strip_dots_bf(const att_bf16x8 (&x)[2], const __bf16* Ys, int col,
+                                              int g, f4v (&acc)[NJT]) {
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt) {
+    const __bf16* yr = Ys + (jt * 16 + col) * ATT_KLB + 8 * g;
+    f4v s = {0.f, 0.f, 0.f, 0.f};
+    s = mfma_bf32(x[0], ldb8_lds(yr), s);
+    s = mfma_bf32(x[1], ldb8_lds(yr + 32), s);
+    acc[jt] = s;
+  }
+}
+
+__device__ __forceinline__ att_bf16x4 pack4(f4v v) { return __builtin_convertvector(v, att_bf16x4); }
+
+template <int NJT>
+__global__ __launch_bounds__(512) void gattn_fwd_mfma_bf_kernel(AttnArgsT<__bf16> a) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);  // heads of a sample on one XCD
+  const int b = bh / a.H, h = bh % a.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = w * 16;
+  constexpr int TK = NJT * 16;
+  constexpr int WLB = 20;                  // per-wave P^T image [TK][16 + 4] bf16
+  __bf16* Ks = smb;                        // [TK][ATT_KLB]
+  __bf16* Vs = Ks + TK * ATT_KLB;          // [TK][ATT_KLB]
+  __bf16* Pw = Vs + TK * ATT_KLB + w * TK * WLB;
+  att_bf16x8 qa[2];
+  {
+    const int iq = min(i0 + col, a.Tq - 1);
+    const __bf16* qr = a.q + ((int64_t)b * a.Tq + iq) * a.ldq + h * ATT_DK + 8 * g;
+    qa[0] = strip8(qr);
+    qa[1] = strip8(qr + 32);
+  }
+  float gp[4][NJT];
+  preload_graph<NJT>(a, b, i0, g, col, gp);
+  float kf[NJT];
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[(int64_t)b * a.Tk + min(jt * 16 + col, a.Tk - 1)];
+  stage_kv_bf<TK>(a, b, h, Ks, Vs);
+  __syncthreads();  // K/V staged
+  f4v s[NJT];
+  strip_dots_bf<NJT>(qa, Ks, col, g, s);
+  f4v pv[NJT];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 4 * g + r;
+    const int ic = min(i, a.Tq - 1);
+    float aa[NJT], gg[NJT], bm[NJT];
+    const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
+    const float rsd = 1.f / fmaxf(nrm, 1e-12f);
+    const float qf = a.qflag[(int64_t)b * a.Tq + ic];
+#pragma unroll
+    for (int jt = 0; jt < NJT; ++jt) {
+      const int j = jt * 16 + col;
+      const float n = bm[jt] * rsd;
+      const bool ok = i < a.Tq && j < a.Tk;
+      if (a.att && ok) a.att[(((int64_t)h * a.B + b) * a.Tq + i) * a.Tk + j] = n;
+      pv[jt][r] = ok ? n * qf : 0.f;
+    }
+  }
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt)
+    *reinterpret_cast<att_bf16x4*>(&Pw[(jt * 16 + col) * WLB + 4 * g]) = pack4(pv[jt]);
+  __builtin_amdgcn_wave_barrier();  // this wave's P^T strip written (wave-private image)
+  // O strip = P V: A[m = i][k = j] = P^T[j][i], B[k = j][n = d] = V[j][d]; k = 16 jc + 4g + t
+  f4v o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int jc = 0; jc < NJT; ++jc) {
+    const int j = jc * 16 + 4 * g;
+    const att_bf16x4 pa = {Pw[j * WLB + col], Pw[(j + 1) * WLB + col], Pw[(j + 2) * WLB + col],
+                           Pw[(j + 3) * WLB + col]};
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const __bf16* vc = Vs + j * ATT_KLB + dt * 16 + col;
+      const att_bf16x4 vb = {vc[0], vc[ATT_KLB], vc[2 * ATT_KLB], vc[3 * ATT_KLB]};
+      o[dt] = mfma_bf16(pa, vb, o[dt]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 4 * g + r;
+    if (i < a.Tq) {
+      float* orow = a.o + ((int64_t)b * a.Tq + i) * a.ldo + h * ATT_DK + col;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) orow[dt * 16] = o[dt][r];
+    }
+  }
+}
+
+template <int NJT>
+__global__ __launch_bounds__(512) void gattn_bwd_mfma_bf_kernel(AttnArgsT<__bf16> a) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);  // heads of a sample on one XCD
+  const int b = bh / a.H, h = bh % a.H;
+  const int nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = w * 16;
+  constexpr int TK = NJT * 16;
+  // P^T / dS^T row stride (bf16): 16 nw + 8 keeps the 8-B row reads of 16 rows on disjoint
+  // bank pairs and the scalar column reads of the 4 lane groups on disjoint bank ranges
+  const int PLB = 16 * nw + 8;
+  __bf16* Pt = smb;              // [TK][PLB]  P^T                    (phase 2)
+  __bf16* dSt = smb + TK * PLB;  // [TK][PLB]  dS^T (scaled by 1/8, masked)
+  __bf16* Ks = smb;              // [TK][ATT_KLB] K_h, V_h for phase 1 (aliases Pt / dSt)
+  __bf16* Vs = smb + TK * ATT_KLB;
+  const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
+  const int hd = h * ATT_DK;
+
+  // ---- phase 1: strips
+  {
+    att_bf16x8 qa[2], oa[2];
+    const int iq = min(i0 + col, a.Tq - 1);
+    const __bf16* qr = a.q + (qb + iq) * a.ldq + hd + 8 * g;
+    const float* orr = a.dout + (qb + iq) * a.lddo + hd + 8 * g;
+    qa[0] = strip8(qr);
+    qa[1] = strip8(qr + 32);
+    oa[0] = strip8(orr);
+    oa[1] = strip8(orr + 32);
+    float gp[4][NJT];
+    preload_graph<NJT>(a, b, i0, g, col, gp);
+    float kf[NJT];
+#pragma unroll
+    for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[kb + min(jt * 16 + col, a.Tk - 1)];
+    stage_kv_bf<TK>(a, b, h, Ks, Vs);
+    __syncthreads();  // K/V staged
+    f4v s[NJT], dp[NJT];
+    strip_dots_bf<NJT>(qa, Ks, col, g, s);
+    strip_dots_bf<NJT>(oa, Vs, col, g, dp);
+    __syncthreads();  // every wave is done with K/V: the region becomes P^T / dS^T
+    f4v pv[NJT], dsv[NJT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * g + r;
+      const int ic = min(i, a.Tq - 1);
+      float aa[NJT], gg[NJT], bm[NJT];
+      const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
+      const float sden = fmaxf(nrm, 1e-12f);
+      const float rsd = 1.f / sden;
+      const float qf = a.qflag[qb + ic];
+      float dn[NJT], t1 = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        dn[jt] = dp[jt][r] * qf;
+        t1 += dn[jt] * bm[jt];
+      }
+      t1 = row16_sum(t1);
+      const float dnrm = nrm >= 1e-12f ? -t1 * (rsd * rsd) : 0.f;
+      float da[NJT], t2 = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        const float sg = bm[jt] > 0.f ? 1.f : (bm[jt] < 0.f ? -1.f : 0.f);
+        const float dbm = dn[jt] * rsd + dnrm * sg;
+        da[jt] = dbm * gg[jt];
+        t2 += da[jt] * aa[jt];
+      }
+      t2 = row16_sum(t2);
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        const int j = jt * 16 + col;
+        const bool ok = i < a.Tq && j < a.Tk;
+        float ds = aa[jt] * (da[jt] - t2);
+        if (kf[jt] == 0.f) ds = 0.f;
+        dsv[jt][r] = ok ? ds * 0.125f : 0.f;
+        pv[jt][r] = ok ? bm[jt] * rsd * qf : 0.f;
+      }
+    }
+#pragma unroll
+    for (int jt = 0; jt < NJT; ++jt) {
+      *reinterpret_cast<att_bf16x4*>(&Pt[(jt * 16 + col) * PLB + i0 + 4 * g]) = pack4(pv[jt]);
+      *reinterpret_cast<att_bf16x4*>(&dSt[(jt * 16 + col) * PLB + i0 + 4 * g]) = pack4(dsv[jt]);
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: 16x16 output tiles, grouped (tensor, 16-column block dt) as in the fp32
+  // kernel: [0,4) dV = P^T dO, [4,8) dK = dS^T Q (k = query), [8,12) dQ = dS K (k = key);
+  // one 16x16x16 MFMA per 16 k, k = 16 kc + 4g + t
+  const int nitems = 8 * NJT + 4 * nw;
+  const int it0 = nitems * w / nw, it1 = nitems * (w + 1) / nw;
+  int cur = -1;
+  att_bf16x4 bcol[8];  // B rows k = 16 kc + 4g + t of column dt*16 + col (kc < 8)
+  for (int it = it0; it < it1; ++it) {
+    int grp, tile;
+    if (it < 8 * NJT) {
+      grp = it / NJT;
+      tile = it - grp * NJT;
+    } else {
+      grp = 8 + (it - 8 * NJT) / nw;
+      tile = (it - 8 * NJT) % nw;
+    }
+    const int dt = grp & 3;
+    const int dcol = hd + dt * 16 + col;
+    if (grp != cur) {  // wave-uniform
+      cur = grp;
+      const __bf16* src = grp < 8 ? a.q : a.k;  // dO (fp32) for grp < 4
+      const int64_t ld = grp < 4 ? a.lddo : (grp < 8 ? a.ldq : a.ldk);
+      const int64_t base = grp < 8 ? qb : kb;
+      const int lim = grp < 8 ? a.Tq : a.Tk;
+      const int nk = grp < 8 ? nw : NJT;
+#pragma unroll
+      for (int kc = 0; kc < 8; ++kc) {
+        if (kc < nk) {
+          float t4[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int64_t off = (base + min(kc * 16 + 4 * g + t, lim - 1)) * ld + dcol;
+            t4[t] = grp < 4 ? a.dout[off] : (float)src[off];
+          }
+          bcol[kc] = pack4(f4v{t4[0], t4[1], t4[2], t4[3]});
+        }
+      }
+    }
+    // ReLU-mask values of this tile's 4 output rows, fetched before the MFMAs (clamped rows)
+    float mk[4];
+    {
+      const __bf16* msrc = grp < 4 ? a.v : (grp < 8 ? a.k : a.q);
+      const int64_t mld = grp < 4 ? a.ldv : (grp < 8 ? a.ldk : a.ldq);
+      const int64_t base = grp < 8 ? kb : qb;
+      const int lim = grp < 8 ? a.Tk : a.Tq;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mk[r] = (float)msrc[(base + min(tile * 16 + 4 * g + r, lim - 1)) * mld + dcol];
+    }
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+    if (grp < 8) {
+      const bool isv = grp < 4;
+      const __bf16* arow = (isv ? Pt : dSt) + (tile * 16 + col) * PLB + 4 * g;
+#pragma unroll
+      for (int kc = 0; kc < 8; ++kc)
+        if (kc < nw) acc = mfma_bf16(ldb4(arow + kc * 16), bcol[kc], acc);
+      __bf16* dst = isv ? a.dv : a.dk;
+      const int64_t dld = isv ? a.lddv : a.lddk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = tile * 16 + 4 * g + r;
+        if (j < a.Tk) dst[(kb + j) * dld + dcol] = (__bf16)(mk[r] > 0.f ? acc[r] : 0.f);
+      }
+    } else {
+#pragma unroll
+      for (int kc = 0; kc < NJT; ++kc) {
+        const __bf16* ac = dSt + (kc * 16 + 4 * g) * PLB + tile * 16 + col;
+        const att_bf16x4 av = {ac[0], ac[PLB], ac[2 * PLB], ac[3 * PLB]};
+        acc = mfma_bf16(av, bcol[kc], acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = tile * 16 + 4 * g + r;
+        if (i < a.Tq) a.dq[(qb + i) * a.lddq + dcol] = (__bf16)(mk[r] > 0.f ? acc[r] : 0.f);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Single-query path (T_q = 1: the decoder cross-attention, one query token per sample).
 // One wave per (b, h); 16 lanes per key row (lane = (key slot kk = lane>>4, float4 chunk
 // c = lane&15)), so every K/V load instruction reads 4 whole 256-B rows (coalesced) and
@@ -941,6 +1268,19 @@ static int launch_fwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const ch
 #else
     const size_t lds = sizeof(float) * ((size_t)2 * njt * 16 * ATT_KLD + (size_t)nw * njt * 16 * 20);
 #endif
+    if constexpr (sizeof(T) == 2) {
+      // bf16 MFMA kernels: bf16 K/V images + per-wave bf16 P^T images
+      const size_t ldsb = 2 * ((size_t)2 * njt * 16 * ATT_KLB + (size_t)nw * njt * 16 * 20);
+      switch (njt) {
+#define SAVQA_FWD_CASE(N)                                                                       \
+  case N:                                                                                       \
+    hipLaunchKernelGGL((gattn_fwd_mfma_bf_kernel<N>), dim3(B * H), dim3(64 * nw), ldsb, s, a);  \
+    break;
+        SAVQA_FWD_CASE(1) SAVQA_FWD_CASE(2) SAVQA_FWD_CASE(3) SAVQA_FWD_CASE(4)
+        SAVQA_FWD_CASE(5) SAVQA_FWD_CASE(6) SAVQA_FWD_CASE(7) SAVQA_FWD_CASE(8)
+#undef SAVQA_FWD_CASE
+      }
+    } else {
     switch (njt) {
 #define SAVQA_FWD_CASE(N)                                                                      \
   case N:                                                                                      \
@@ -949,6 +1289,7 @@ static int launch_fwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const ch
       SAVQA_FWD_CASE(1) SAVQA_FWD_CASE(2) SAVQA_FWD_CASE(3) SAVQA_FWD_CASE(4)
       SAVQA_FWD_CASE(5) SAVQA_FWD_CASE(6) SAVQA_FWD_CASE(7) SAVQA_FWD_CASE(8)
 #undef SAVQA_FWD_CASE
+    }
     }
     }
   } else {
@@ -985,6 +1326,19 @@ static int launch_bwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const ch
     if constexpr (std::is_same<TQ, TKV>::value) {
     using T = TKV;
     const int njt = (Tk + 15) / 16, nw = (Tq + 15) / 16;
+    if constexpr (sizeof(T) == 2) {
+      // bf16 MFMA kernels: bf16 K/V staging aliased with the bf16 P^T / dS^T images
+      const size_t ldsb = 2 * 2 * (size_t)njt * 16 * (size_t)std::max(16 * nw + 8, ATT_KLB);
+      switch (njt) {
+#define SAVQA_BWD_CASE(N)                                                                       \
+  case N:                                                                                       \
+    hipLaunchKernelGGL((gattn_bwd_mfma_bf_kernel<N>), dim3(B * H), dim3(64 * nw), ldsb, s, a);  \
+    break;
+        SAVQA_BWD_CASE(1) SAVQA_BWD_CASE(2) SAVQA_BWD_CASE(3) SAVQA_BWD_CASE(4)
+        SAVQA_BWD_CASE(5) SAVQA_BWD_CASE(6) SAVQA_BWD_CASE(7) SAVQA_BWD_CASE(8)
+#undef SAVQA_BWD_CASE
+      }
+    } else {
     const size_t lds = sizeof(float) * 2 * (size_t)njt * 16 * (size_t)std::max(16 * nw + 4, ATT_KLD);
     switch (njt) {
 #define SAVQA_BWD_CASE(N)                                                                      \
@@ -994,6 +1348,7 @@ static int launch_bwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const ch
       SAVQA_BWD_CASE(1) SAVQA_BWD_CASE(2) SAVQA_BWD_CASE(3) SAVQA_BWD_CASE(4)
       SAVQA_BWD_CASE(5) SAVQA_BWD_CASE(6) SAVQA_BWD_CASE(7) SAVQA_BWD_CASE(8)
 #undef SAVQA_BWD_CASE
+    }
     }
     }
     return check_launch(who);

@@ -264,10 +264,13 @@ def test_graph_attention_fwd_bwd(B, Tq, Tk, kind):
                                            (5, 1, 73, "cross"), (4, 1, 50, "cross"),
                                            (2, 128, 128, "self"), (3, 17, 33, "cross")])
 def test_graph_attention_bf16_storage(B, Tq, Tk, kind):
-    """bf16-storage attention (savqa_gattn_{fwd,bwd}_bf16; cfg 3 / cfg 5): same fp32 math as the
-    fp32 kernels on the bf16 values, so its outputs equal the fp32 kernels' outputs on the
-    bf16-rounded inputs (O to fp32 rounding, dQ/dK/dV to one bf16 rounding), and both match
-    the fp64 reference of the rounded inputs."""
+    """bf16-storage attention (savqa_gattn_{fwd,bwd}_bf16; cfg 3 / cfg 5) against the fp32
+    kernels and the fp64 reference on the bf16-rounded inputs. T_q = 1 (single-query kernels):
+    the same fp32 math, so O equals the fp32 kernel's to fp32 rounding. T_q > 1 (bf16 MFMA
+    strip kernels): S = QK^T is exact (bf16 products, fp32 sums) and the softmax / graph / L1
+    chain is fp32, but P, dS and dO enter their second products rounded to bf16 (as in a bf16
+    attention), so O is within a few bf16 ulps (tolerance 4e-3 relative Frobenius, ~1 ulp =
+    3.9e-3 per element, averaged down over 64-term sums); dQ/dK/dV carry one more rounding."""
     O = ops()
     H, D = 8, 512
     bf = torch.bfloat16
@@ -291,7 +294,8 @@ def test_graph_attention_bf16_storage(B, Tq, Tk, kind):
     o32 = torch.empty(B * Tq, D, device=dev)
     O.gattn_fwd(Q, ldq, K, ldk, V, ldv, G, kf, qf, B, Tq, Tk, H, o16, D)
     O.gattn_fwd(Qf, D, Kf, D, Vf, D, G, kf, qf, B, Tq, Tk, H, o32, D)
-    assert rel(o16, o32) < 1e-6
+    tol_o = 1e-6 if Tq == 1 else 4e-3
+    assert rel(o16, o32) < tol_o
     dO = g(B * Tq, D, seed=54)
     d16 = [torch.empty(B * n, D, device=dev, dtype=bf) for n in (Tq, Tk, Tk)]
     d32 = [torch.empty(B * n, D, device=dev) for n in (Tq, Tk, Tk)]
@@ -305,7 +309,7 @@ def test_graph_attention_bf16_storage(B, Tq, Tk, kind):
     Kr = Kf.reshape(B, Tk, D).double().cpu().requires_grad_(True)
     Vr = Vf.reshape(B, Tk, D).double().cpu().requires_grad_(True)
     ref, _ = _attn_ref(Qr, Kr, Vr, G.double().cpu(), kf.double().cpu(), qf.double().cpu())
-    assert rel(o16.view(B, Tq, D), ref) < 2e-5
+    assert rel(o16.view(B, Tq, D), ref) < (2e-5 if Tq == 1 else 4e-3)
     (ref * dO.view(B, Tq, D).double().cpu()).sum().backward()
     assert rel(d16[0].float().view(B, Tq, D), Qr.grad * (Qr > 0)) < 1e-2
     assert rel(d16[1].float().view(B, Tk, D), Kr.grad * (Kr > 0)) < 1e-2
