@@ -713,9 +713,9 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgsT<T> a) {
 //                              already: exact products, fp32 sums; dO is rounded to bf16);
 //   O = P V, dV = P^T dO,      v_mfma_f32_16x16x16_bf16, one per 16 k (P and dS rounded to
 //   dK = dS^T Q, dQ = dS K     bf16, as a bf16 attention's second GEMM does).
-// The fp32 kernels issue 4x (S) / 4x (phase 2) as many 16x16x4 MFMAs; halving the LDS
-// images (K/V staging, P^T / dS^T) doubles the workgroups per CU (T = 73 backward: 53.7 KB ->
-// 26.9 KB), which is what hides this latency-bound kernel's global loads.
+// The fp32 kernels issue 8x (S) / 4x (phase 2) as many 16x16x4 MFMAs. bf16 LDS images halve
+// the footprint, which buys both more workgroups per CU (T = 73 backward: 3 instead of 2,
+// VGPR-limited) and keeping K / V staged through the backward's phase 2 (50 KB).
 // Both MFMA forms take operand k-sets by lane group (A[m = l&15][k in set(l>>4)],
 // B[k in set(l>>4)][n = l&15], D[4(l>>4)+r][l&15]); A and B always use the same set, so the
 // inner products are exact whatever the hardware's k order inside a set.
@@ -881,10 +881,13 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf_kernel(AttnArgsT<__bf16
   // P^T / dS^T row stride (bf16): 16 nw + 8 keeps the 8-B row reads of 16 rows on disjoint
   // bank pairs and the scalar column reads of the 4 lane groups on disjoint bank ranges
   const int PLB = 16 * nw + 8;
-  __bf16* Pt = smb;              // [TK][PLB]  P^T                    (phase 2)
-  __bf16* dSt = smb + TK * PLB;  // [TK][PLB]  dS^T (scaled by 1/8, masked)
-  __bf16* Ks = smb;              // [TK][ATT_KLB] K_h, V_h for phase 1 (aliases Pt / dSt)
+  // K_h / V_h stay staged through phase 2 (not aliased by the P^T / dS^T images): dQ's B
+  // operand and the dK / dV ReLU masks are LDS reads instead of global round trips (T = 73:
+  // 50 KB, still 3 workgroups per CU, which the 114 VGPRs limit anyway; -17 % vs aliasing)
+  __bf16* Ks = smb;                // [TK][ATT_KLB]
   __bf16* Vs = smb + TK * ATT_KLB;
+  __bf16* Pt = Vs + TK * ATT_KLB;  // [TK][PLB]  P^T
+  __bf16* dSt = Pt + TK * PLB;     // [TK][PLB]  dS^T (scaled by 1/8, masked)
   const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
   const int hd = h * ATT_DK;
 
@@ -908,7 +911,6 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf_kernel(AttnArgsT<__bf16
     f4v s[NJT], dp[NJT];
     strip_dots_bf<NJT>(qa, Ks, col, g, s);
     strip_dots_bf<NJT>(oa, Vs, col, g, dp);
-    __syncthreads();  // every wave is done with K/V: the region becomes P^T / dS^T
     f4v pv[NJT], dsv[NJT];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -979,6 +981,13 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf_kernel(AttnArgsT<__bf16
       const int64_t base = grp < 8 ? qb : kb;
       const int lim = grp < 8 ? a.Tq : a.Tk;
       const int nk = grp < 8 ? nw : NJT;
+      if (grp >= 8) {  // dQ = dS K: K columns from the staged image
+#pragma unroll
+        for (int kc = 0; kc < NJT; ++kc) {
+          const __bf16* kcp = Ks + (kc * 16 + 4 * g) * ATT_KLB + dt * 16 + col;
+          bcol[kc] = att_bf16x4{kcp[0], kcp[ATT_KLB], kcp[2 * ATT_KLB], kcp[3 * ATT_KLB]};
+        }
+      } else
 #pragma unroll
       for (int kc = 0; kc < 8; ++kc) {
         if (kc < nk) {
@@ -999,6 +1008,11 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf_kernel(AttnArgsT<__bf16
       const int64_t mld = grp < 4 ? a.ldv : (grp < 8 ? a.ldk : a.ldq);
       const int64_t base = grp < 8 ? kb : qb;
       const int lim = grp < 8 ? a.Tk : a.Tq;
+      if (grp < 8) {  // dV / dK rows: masks of the staged V / K
+        const __bf16* mc = (grp < 4 ? Vs : Ks) + (tile * 16 + 4 * g) * ATT_KLB + dt * 16 + col;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mk[r] = (float)mc[r * ATT_KLB];
+      } else
 #pragma unroll
       for (int r = 0; r < 4; ++r) mk[r] = (float)msrc[(base + min(tile * 16 + 4 * g + r, lim - 1)) * mld + dcol];
     }
@@ -1327,8 +1341,8 @@ static int launch_bwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const ch
     using T = TKV;
     const int njt = (Tk + 15) / 16, nw = (Tq + 15) / 16;
     if constexpr (sizeof(T) == 2) {
-      // bf16 MFMA kernels: bf16 K/V staging aliased with the bf16 P^T / dS^T images
-      const size_t ldsb = 2 * 2 * (size_t)njt * 16 * (size_t)std::max(16 * nw + 8, ATT_KLB);
+      // bf16 MFMA kernels: bf16 K/V images kept next to the bf16 P^T / dS^T images
+      const size_t ldsb = 2 * 2 * (size_t)njt * 16 * (size_t)(16 * nw + 8 + ATT_KLB);
       switch (njt) {
 #define SAVQA_BWD_CASE(N)                                                                       \
   case N:                                                                                       \
