@@ -1109,6 +1109,29 @@ __device__ __forceinline__ void q1_forward(const A& a, int b, int hd, int kk, in
   nrm = rows4_sum(nr);
 }
 
+// 4 consecutive outputs of one lane: one 16-B (fp32) / 8-B (bf16) store when the row is
+// vector-aligned (vec: wave-uniform), else 4 element stores (4 / 8 x the store instructions)
+__device__ __forceinline__ void stx4(float* p, f4v v, bool vec) {
+  if (vec) {
+    *reinterpret_cast<f4v*>(p) = v;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p[e] = v[e];
+  }
+}
+__device__ __forceinline__ void stx4(__bf16* p, f4v v, bool vec) {
+  if (vec) {
+    *reinterpret_cast<att_bf16x4*>(p) = __builtin_convertvector(v, att_bf16x4);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p[e] = (__bf16)v[e];
+  }
+}
+template <typename T>
+__device__ __forceinline__ bool vec_rows(const T* p, int64_t ld) {
+  return (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & (4 * sizeof(T) - 1)) == 0;
+}
+
 template <int NIT, typename TQ, typename TKV>
 __global__ __launch_bounds__(256) void gattn_fwd_q1_kernel(AttnArgsT<TQ, TKV> a) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1135,11 +1158,7 @@ __global__ __launch_bounds__(256) void gattn_fwd_q1_kernel(AttnArgsT<TQ, TKV> a)
     }
   }
   o = xrow_sum(o);
-  if (kk == 0) {
-    float* orow = a.o + (int64_t)b * a.ldo + hd + 4 * c;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) orow[e] = o[e];
-  }
+  if (kk == 0) stx4(a.o + (int64_t)b * a.ldo + hd + 4 * c, o, vec_rows(a.o, a.ldo));
 }
 
 template <int NIT, typename TQ, typename TKV>
@@ -1173,6 +1192,7 @@ __global__ __launch_bounds__(256) void gattn_bwd_q1_kernel(AttnArgsT<TQ, TKV> a)
   t1 = rows4_sum(t1);
   const float dnrm = nrm >= 1e-12f ? -t1 / (sden * sden) : 0.f;
   float t2 = 0.f;
+  const bool vk = vec_rows(a.dk, a.lddk), vv = vec_rows(a.dv, a.lddv);
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const float sg = bm[it] > 0.f ? 1.f : (bm[it] < 0.f ? -1.f : 0.f);
@@ -1196,21 +1216,22 @@ __global__ __launch_bounds__(256) void gattn_bwd_q1_kernel(AttnArgsT<TQ, TKV> a)
       const f4v v4 = ldx4(a.v + row * a.ldv + hd + 4 * c);
       dq += ds * k4;
       if (ok) {
-        TKV* dkr = a.dk + row * a.lddk + hd + 4 * c;
-        TKV* dvr = a.dv + row * a.lddv + hd + 4 * c;
+        f4v gk, gv;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          stx1(dkr + e, k4[e] > 0.f ? ds * q4[e] : 0.f);
-          stx1(dvr + e, v4[e] > 0.f ? pj * do4[e] : 0.f);
+          gk[e] = k4[e] > 0.f ? ds * q4[e] : 0.f;
+          gv[e] = v4[e] > 0.f ? pj * do4[e] : 0.f;
         }
+        stx4(a.dk + row * a.lddk + hd + 4 * c, gk, vk);
+        stx4(a.dv + row * a.lddv + hd + 4 * c, gv, vv);
       }
     }
   }
   dq = xrow_sum(dq);
   if (kk == 0) {
-    TQ* dqr = a.dq + (int64_t)b * a.lddq + hd + 4 * c;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) stx1(dqr + e, q4[e] > 0.f ? dq[e] : 0.f);
+    for (int e = 0; e < 4; ++e) dq[e] = q4[e] > 0.f ? dq[e] : 0.f;
+    stx4(a.dq + (int64_t)b * a.lddq + hd + 4 * c, dq, vec_rows(a.dq, a.lddq));
   }
 }
 

@@ -31,7 +31,11 @@ def main():
     ap.add_argument("--bf16", action="store_true", help="bf16 Q/K/V storage (cfg-3 mode)")
     ap.add_argument("--B", type=int, default=256)
     ap.add_argument("--T", type=int, nargs="*", default=[73, 50])
+    ap.add_argument("--q1", action="store_true",
+                    help="decoder cross-attention: one fp32 query per sample, K/V of T rows")
     args = ap.parse_args()
+    if args.q1:
+        return q1_main(args)
     H, dk = 8, 64
     d = H * dk
     dt = torch.bfloat16 if args.bf16 else torch.float32
@@ -55,6 +59,30 @@ def main():
         bfl = B * H * 10 * T * T * dk
         print(f"{dt} B={B} T={T}: fwd {tf*1e6:7.1f} us {fb/tf/1e9:6.0f} GB/s {ffl/tf/1e12:5.1f} TF | "
               f"bwd {tb*1e6:7.1f} us {bb/tb/1e9:6.0f} GB/s {bfl/tb/1e12:5.1f} TF", flush=True)
+
+
+def q1_main(args):
+    """T_q = 1 kernels (gattn_{fwd,bwd}_q1): bytes = K, V read + dK, dV written (+ q, o)."""
+    H, dk = 8, 64
+    d = H * dk
+    dt = torch.bfloat16 if args.bf16 else torch.float32
+    es = 2 if args.bf16 else 4
+    for B, T in ((args.B, t) for t in args.T):
+        q = torch.randn(B, d, device=dev).relu_()
+        kv = torch.randn(B * T, 2 * d, device=dev).relu_().to(dt)
+        G = (torch.rand(B, 1, T, device=dev) < 0.3).float()
+        kf, qf = torch.ones(B * T, device=dev), torch.ones(B, device=dev)
+        o, dout = torch.empty(B, d, device=dev), torch.randn(B, d, device=dev)
+        dq = torch.empty(B, d, device=dev)
+        dkv = torch.empty(B * T, 2 * d, device=dev, dtype=dt)
+        f = lambda: ops.gattn_fwd(q, d, kv, 2 * d, kv[:, d:], 2 * d, G, kf, qf, B, 1, T, H, o, d)
+        g = lambda: ops.gattn_bwd(q, d, kv, 2 * d, kv[:, d:], 2 * d, G, kf, qf, B, 1, T, H, dout,
+                                  d, dq, d, dkv, 2 * d, dkv[:, d:], 2 * d)
+        tf, tb = timeit(f), timeit(g)
+        fb = B * T * 2 * d * es
+        bb = 2 * B * T * 2 * d * es
+        print(f"q1 {dt} B={B} Tk={T}: fwd {tf*1e6:7.1f} us {fb/tf/1e9:6.0f} GB/s | "
+              f"bwd {tb*1e6:7.1f} us {bb/tb/1e9:6.0f} GB/s", flush=True)
 
 
 if __name__ == "__main__":
