@@ -1161,8 +1161,12 @@ __global__ __launch_bounds__(256) void gattn_fwd_q1_kernel(AttnArgsT<TQ, TKV> a)
   if (kk == 0) stx4(a.o + (int64_t)b * a.ldo + hd + 4 * c, o, vec_rows(a.o, a.ldo));
 }
 
+// bf16 K/V: capped at 128 VGPRs (4 waves per SIMD, so all B*H waves of cfg 3 are resident at
+// once instead of 1.33 rounds at 3 per SIMD); the cap's spills are cheaper than the lost
+// occupancy there (bf16 T = 73: 94 -> 72 us) but not for fp32 K/V (55 -> 65 us: uncapped)
 template <int NIT, typename TQ, typename TKV>
-__global__ __launch_bounds__(256) void gattn_bwd_q1_kernel(AttnArgsT<TQ, TKV> a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(TKV) == 2 ? 4 : 1)))
+void gattn_bwd_q1_kernel(AttnArgsT<TQ, TKV> a) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int bh = blockIdx.x * 4 + w;
   if (bh >= a.B * a.H) return;
