@@ -221,8 +221,10 @@ int savqa_gattn_bwd(void* stream, const float* q, int64_t ldq, const float* k, i
 /* bf16-storage variants (BASELINE cfg 3 / cfg 5 bf16 attention core): K / V and dK / dV are
  * bf16 (rows 8-B aligned, ld % 4 == 0), Q / dQ are bf16 if q_bf16 else fp32 (the decoder's
  * single query; mixed types need T_q = 1); O, dO, G and the flags stay fp32 and the softmax /
- * graph / L1 chain and all products run in fp32 (MFMA strip kernels for T_q > 1, the
- * single-query kernels for T_q = 1; T_k <= 128). */
+ * graph / L1 chain runs in fp32. T_q > 1 (q_bf16 = 1): bf16 MFMA strip kernels -- S = QK^T and
+ * dP = dO V^T on bf16 operands (dO rounded to bf16), PV / P^T dO / dS^T Q / dS K with P and dS
+ * rounded to bf16, fp32 accumulation. T_q = 1: the single-query kernels, fp32 products on the
+ * bf16 values. T_k <= 128. */
 int savqa_gattn_fwd_bf16(void* stream, int32_t q_bf16, const void* q, int64_t ldq, const void* k,
                          int64_t ldk, const void* v, int64_t ldv, const float* G,
                          const float* kflag, const float* qflag, int64_t B, int64_t Tq,
