@@ -144,12 +144,13 @@ WORKLOADS = {
                       "master weights / Adam), 36 regions x 2048-d, "
                       "14 q-tokens, 59 nodes, d=512 h=8 L=6, MIL-NCE only_obj topN=5 H=1024, "
                       "914 classes, decMask"),
-    "rel": dict(d=512, H=8, Nv=36, Ns=36 + 4 + 36 * 35, batch=4, rel=True, maxlen=1600,
-                desc="relation mode (only_obj=False, submit.py:76 'with relations'): model_v=3 "
-                     "train step, fp32, 36 regions, super-node graph of 1300 nodes (36 objects, "
-                     "4 attributes, 1260 relation nodes: T_syb=1314), 31,500 positive + 31,500 "
-                     "negative relation entries per sample, 311 relation categories (R: "
-                     "311x1024x1024), d=512 h=8 L=6, H_mil=1024, topN=5, decMask"),
+    "rel": dict(d=512, H=8, Nv=36, Ns=36 + 4 + 36 * 35, batch=4, rel=True, maxlen=1600, hm=64,
+                desc="relation mode (only_obj=False, submit.py:76 'with relations', :87 maxlen "
+                     "1600, :101 hidden_size_mil 64): model_v=3 train step, fp32, 36 regions, "
+                     "super-node graph of 1300 nodes (36 objects, 4 attributes, 1260 relation "
+                     "nodes: T_syb=1314), 31,500 positive + 31,500 negative relation entries per "
+                     "sample, 311 relation categories (R: 311x64x64), d=512 h=8 L=6, H_mil=64, "
+                     "topN=5, decMask"),
     "cfg5": dict(d=512, H=8, Nv=36, Ns=59, batch=1024, prec="fp8",
                  desc="cfg5: model_v=3 train step, fp8-e4m3 region features (per-32 e8m0 block "
                       "scales, quantised outside the timed region as a loader would ship them) "
@@ -229,7 +230,8 @@ def main():
     W = WORKLOADS[args.workload]
     B = args.batch or W["batch"]
     d, H, Nv, Ns = W["d"], W["H"], W["Nv"], W["Ns"]
-    model = AttModel(None, d, 1024, 914, 40, W.get("maxlen", 450), 49, 6, H, args.dropout, 0.1, 311,
+    hm = W.get("hm", 1024)  # hidden_size_mil (submit.py:101: 1024 objects-only, 64 with relations)
+    model = AttModel(None, d, hm, 914, 40, W.get("maxlen", 450), 49, 6, H, args.dropout, 0.1, 311,
                      not W.get("rel", False), device=dev, init=False,
                      gemm_precision=W.get("prec", "fp32"))
     init_params_(model, seed=0)  # identical on every rank (same seed), like a broadcast
@@ -239,7 +241,7 @@ def main():
     opt = Adam(model, lr=1e-4)
     reducer = GradReducer(model._arena) if world > 1 else None
     if reducer:
-        model.attach_reducer(reducer)
+        model.attach_reducer(reducer, batch_size=B)
     if W.get("rel"):
         from savqa_amd.data import model_args_rel, synthetic_relation_batch
         batch = synthetic_relation_batch(B, Nv=Nv, seed=1234 + rank, device=dev)
@@ -291,7 +293,7 @@ def main():
 
     value = world * B * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
-    fl = train_flops_per_sample(Tv=Nv + 14, Ts=Ns + 14, Nv=Nv, Ns=Ns, d=d)
+    fl = train_flops_per_sample(Tv=Nv + 14, Ts=Ns + 14, Nv=Nv, Ns=Ns, d=d, Hm=hm)
     lp = W.get("prec") in ("bf16", "fp8")
     peak = BF16_MFMA_PEAK_TFLOPS if lp else FP32_MFMA_PEAK_TFLOPS
 

@@ -51,15 +51,15 @@ const char* savqa_last_error(void);
  * Non-atomic launches with a linear epilogue (relu=0, beta=0, C not aliasing resid) may
  * split the last partial wave of tiles over K internally (zero-fill + atomics): results
  * then differ from a single-pass launch only in fp32 summation order.
- * prec (128x128-tile launches; the skinny kernel stays fp32): 1 = operands rounded to
- * bf16 while they are staged in LDS, v_mfma_f32_32x32x16_bf16, fp32 accumulate and
- * epilogue (BASELINE cfg 3's bf16 training); 3 = each operand split into bf16 hi + lo
- * (lo = bf16(x - hi)) and a*b ~ ah*bh + ah*bl + al*bh: ~2^-16 relative per product.
+ * prec (128x128-tile launches; the skinny kernel stays fp32): 3 = each operand split into
+ * bf16 hi + lo (lo = bf16(x - hi)) and a*b ~ ah*bh + ah*bl + al*bh on
+ * v_mfma_f32_32x32x16_bf16: ~2^-16 relative per product (the "bf16x3" mode). The bf16
+ * training mode (BASELINE cfg 3) uses savqa_gemm_lp on bf16-resident operands instead.
  * ------------------------------------------------------------------------ */
 typedef struct savqa_gemm_desc {
     int64_t M, N, K;
     const float* A; int64_t lda; int32_t a_trans;
-    int32_t prec;      /* products: 0 fp32 MFMA (exact), 1 bf16 MFMA (cfg 3), 3 3xbf16 split */
+    int32_t prec;      /* products: 0 fp32 MFMA (exact), 3 3xbf16 split */
     const int64_t* a_rows;
     const float* B; int64_t ldb; int32_t b_trans; int32_t _pad1;
     const int64_t* b_rows;

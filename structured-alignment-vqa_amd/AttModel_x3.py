@@ -133,8 +133,8 @@ class AttModel_syb(nn.Module):
 
 
 class MIL_NCE(nn.Module):
-    """AttModel_x3.py:285-443 (only_obj branch runs in the engine; the relation branch
-    :382-440 is the next scope row and raises)."""
+    """AttModel_x3.py:285-443 (parameters; both the only_obj branch :352-380 and the relation
+    branch :382-440 run inside AttModel's engine -- engine.mil_forward / csrc/rel.hip)."""
 
     def __init__(self, glove, hidden_size, dropout_rate, num_relations, only_obj, _init=True):
         super().__init__()
@@ -233,6 +233,7 @@ class AttModel(nn.Module):
         super().__init__()
         self.only_obj = only_obj
         self.num_classes = num_classes
+        self.maxlen_q = maxlen_q
         self.hidden_size = hidden_size
         self.num_blocks = num_blocks
         self.num_heads = num_heads
@@ -269,11 +270,16 @@ class AttModel(nn.Module):
         object.__setattr__(self, "_engine", ModelEngine(self._arena, num_blocks, hidden_size,
                                                         num_heads, gemm_precision))
 
-    def attach_reducer(self, reducer):
+    def attach_reducer(self, reducer, batch_size: Optional[int] = None):
         """Stream the data-parallel gradient all-reduce out of the backward (ddp.GradReducer).
         The two stacks' syb_emb tables only get question-token rows (AttModel_x3.py:96-99,
-        :216-219), so they are exchanged by rows (ddp.GradReducer.add_sparse_table)."""
+        :216-219), so they are exchanged by rows (ddp.GradReducer.add_sparse_table).
+        batch_size (the per-rank batch every rank is configured with): the row lists are then
+        padded to the static bound batch_size * maxlen_q, so no rank waits for the others'
+        counts in the forward (without it the counts are agreed on the host each step)."""
         object.__setattr__(self, "_reducer", reducer)
+        object.__setattr__(self, "_rows_cap", None if batch_size is None
+                           else int(batch_size) * int(self.maxlen_q))
         self._engine.multi_rank = reducer is not None and getattr(reducer, "world", 1) > 1
         if reducer is not None and getattr(reducer, "world", 1) > 1:
             for pre in ("att_vis_grid", "att_syb"):
@@ -335,7 +341,7 @@ class AttModel(nn.Module):
         anchor = self._arena_anchor()
         red = self.__dict__.get("_reducer")
         if red is not None and anchor is not None:
-            red.set_rows(tensors[2])     # q_ipt: the stack tables' touched rows
+            red.set_rows(tensors[2], cap=self.__dict__.get("_rows_cap"))  # q_ipt: touched rows
         lc, lv, ls, mil, mil_rel = _AttModelFn.apply(self, bool(decMask), drop, anchor, *tensors)
         return lc, lv, ls, mil, (mil_rel if not self.only_obj else 0)
 

@@ -1,4 +1,4 @@
-// Shared pieces of the graph-attention kernels (attn.hip: T <= 128 full-row kernels,
+// Shared pieces of the graph-attention kernels (attn.hip: T <= 128 MFMA strip / single-query kernels,
 // attn_flash.hip: key-tiled kernels for long sequences). gfx950 only.
 #pragma once
 #include "common.h"
@@ -7,7 +7,6 @@ namespace savqa {
 
 constexpr int ATT_DK = 64;
 constexpr int ATT_KLD = 68;  // padded K/V row (floats), 16-B aligned
-constexpr int ATT_RB = 4;    // query rows per wave per pass
 constexpr float ATT_MASKED = -4294967296.0f;  // fp32(-2**32 + 1)
 
 // TQ / TKV: storage types of Q, dQ and of K, V, dK, dV (float, or __bf16 in the bf16

@@ -1,11 +1,12 @@
-// bf16-MFMA GEMM for the 128x128-tile shapes (v_mfma_f32_32x32x16_bf16, fp32 accumulate).
+// 3xbf16-MFMA GEMM for the 128x128-tile shapes (v_mfma_f32_32x32x16_bf16, fp32 accumulate):
+// the "bf16x3" precision mode (savqa_gemm_desc.prec = 3).
 //
 // Same operator, operand layouts, epilogues and launch grid as gemm_f32_kernel (gemm.hip);
 // only the products run on the bf16 matrix path (16x the fp32 MFMA rate per clock):
-//   prec 1 (SAVQA_PREC_BF16):   a*b ~ bf16(a)*bf16(b)                    (BASELINE cfg 3)
-//   prec 3 (SAVQA_PREC_BF16X3): a = ah + al, b = bh + bl (ah = bf16(a), al = bf16(a - ah)),
-//                               a*b ~ ah*bh + ah*bl + al*bh  (three MFMAs, ~2^-16 relative
-//                               per product; fp32 storage and accumulation throughout)
+//   a = ah + al, b = bh + bl (ah = bf16(a), al = bf16(a - ah)), a*b ~ ah*bh + ah*bl + al*bh
+//   (three MFMAs, ~2^-16 relative per product; fp32 storage and accumulation throughout).
+// (The plain bf16 training mode, BASELINE cfg 3, runs on bf16-RESIDENT operands in
+// gemm_lp.hip; the P template parameter below only ever takes 3 in the library.)
 // Operands stay fp32 in HBM: each 128x32 tile is loaded as float4s, converted while it is
 // staged, and kept in LDS as [row][k] bf16 planes (hi, and lo for prec 3) with 80-B rows,
 // so every MFMA fragment (8 consecutive k of one row) is ONE conflict-free ds_read_b128,
@@ -311,10 +312,7 @@ int savqa_launch_gemm_bf16(const savqa_gemm_desc& d, const savqa::GemmGrid& gg, 
   const dim3 g(grid_x, nsplit), b(GEMM_NT);
 #define SAVQA_BF_LAUNCH(AT, BT)                                                              \
   do {                                                                                       \
-    if (d.prec == 3)                                                                         \
-      hipLaunchKernelGGL((gemm_bf16_kernel<AT, BT, 3>), g, b, 0, s, d, gg, avec, bvec);      \
-    else                                                                                     \
-      hipLaunchKernelGGL((gemm_bf16_kernel<AT, BT, 1>), g, b, 0, s, d, gg, avec, bvec);      \
+    hipLaunchKernelGGL((gemm_bf16_kernel<AT, BT, 3>), g, b, 0, s, d, gg, avec, bvec);        \
   } while (0)
   if (!d.a_trans && d.b_trans) SAVQA_BF_LAUNCH(false, true);
   else if (!d.a_trans && !d.b_trans) SAVQA_BF_LAUNCH(false, false);

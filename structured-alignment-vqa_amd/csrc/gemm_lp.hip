@@ -65,10 +65,15 @@ struct LpArgs {
   // tail_t0 on, in tail_f k-slices of tail_kchunk each, accumulated atomically into C
   int full, tail_t0, tail_f;
   int64_t tail_kchunk;
-  int dbg;                // diagnostics (bits): 1 = skip the MFMAs, 2 = skip the k-loop DMAs,
-                          // 4 = skip the epilogue (gemm_lp3_kernel; the 128x128 kernel's
-                          // breakdown in DESIGN.md came from a build with the same bits)
+  int dbg;                // diagnostic builds only (SAVQA_LP_DIAG=1, tools/lp_bench.py --dbg):
+                          // 1 = skip the MFMAs, 2 = skip the k-loop DMAs, 4 = skip the
+                          // epilogue; production builds compile every test of it away
 };
+
+#ifndef SAVQA_LP_DIAG
+#define SAVQA_LP_DIAG 0
+#endif
+__device__ __forceinline__ int lp_dbg(const LpArgs& a) { return SAVQA_LP_DIAG ? a.dbg : 0; }
 
 // Per-lane LDS-DMA sources of one operand, resolved once per workgroup.
 //   R image: instruction u of wave w covers tile rows 8(4w+u) .. +7; lane L -> row
@@ -880,13 +885,13 @@ __global__ __launch_bounds__(512, 1) void gemm_lp2_kernel(LpArgs args) {
       const char* ia = smem + cur * STAGE;
       const char* ib = ia + IMG_A;
       const int nxt = kt + NS - 1;
-      if (nxt < nt && args.dbg != 2) {  // into slot nxt % NS, last read in iteration kt-1
+      if (nxt < nt && lp_dbg(args) != 2) {  // into slot nxt % NS, last read in iteration kt-1
         const int sl = cur == 0 ? NS - 1 : cur - 1;
         stage(smem + sl * STAGE, nxt);
       }
 #pragma unroll
       for (int kk = 0; kk < BK / 32; ++kk) {
-        if (args.dbg == 1) break;
+        if (lp_dbg(args) == 1) break;
         bf16x8 a[FM], b[FN];
 #pragma unroll
         for (int i = 0; i < FM; ++i) a[i] = frag2<AT, BM, BK>(ia, wm * TM + 16 * i, kk, lane);
@@ -1042,7 +1047,7 @@ __global__ __launch_bounds__(512, 1) void gemm_lp3_kernel(LpArgs args) {
             for (int kk = 0; kk < 2; ++kk)
               b[fj][kk] = frag_bf16<!BT>(img + (2 + j) * LP_IMG, wn * 32 + 16 * fj, kk, lane);
         }
-        if (pf && !(args.dbg & 2)) {
+        if (pf && !(lp_dbg(args) & 2)) {
           stage(q, (kt + 1) & 1, kt + 1);
           wait_vm<4>();  // the half the next phase reads has landed
         } else {
@@ -1051,7 +1056,7 @@ __global__ __launch_bounds__(512, 1) void gemm_lp3_kernel(LpArgs args) {
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this phase's subtile is in VGPRs
         __builtin_amdgcn_s_setprio(1);
-        if (!(args.dbg & 1)) {
+        if (!(lp_dbg(args) & 1)) {
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -1072,7 +1077,7 @@ __global__ __launch_bounds__(512, 1) void gemm_lp3_kernel(LpArgs args) {
   // (every DMA retired in the last k-tile; its last phase ended with a barrier after the
   // final ds_reads were waited for, so LDS is free)
   __syncthreads();
-  if (args.dbg & 4) {  // diagnostics: no epilogue (one store keeps the k-loop alive)
+  if (lp_dbg(args) & 4) {  // diagnostics: no epilogue (one store keeps the k-loop alive)
     if (acc[0][0][0] == 12345.f && d.C) d.C[0] = acc[7][3][3];
     return;
   }
@@ -1264,7 +1269,7 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   const int bk = fp8 ? 128 : 64;
   a.kchunk = p.per * bk;
   a.tiles_n = (int)((d.N + p.bn - 1) / p.bn);
-  a.dbg = d.tile_hint >> 8;
+  a.dbg = SAVQA_LP_DIAG ? d.tile_hint >> 8 : 0;
   a.nblk = (int)p.tiles;
   a.ntiles_k = (int)p.per;
   a.full = (int)p.tail_t0;

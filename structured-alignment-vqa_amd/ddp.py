@@ -27,7 +27,7 @@ Works with any torch.distributed backend (gloo on CPU tensors for the host tests
 """
 from __future__ import annotations
 
-from typing import List
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -57,13 +57,17 @@ class GradReducer:
     optimizer can update each bucket as soon as ITS all-reduce lands (Adam of the early
     buckets overlaps the all-reduce of the last ones)."""
 
-    def __init__(self, arena, bucket_mb: float = 64.0, group=None):
+    def __init__(self, arena, bucket_mb: float = 64.0, group=None, filler: int = 400000):
         self.arena = arena
         self.group = group
+        # padding row of the static-cap set_rows lists (any row of every sparse table; the
+        # default is the PAD token's row, AttModel_x3.py:13)
+        self.filler = int(filler)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        # host-side metadata exchange (the per-rank id counts of set_rows): a gloo group on
-        # CPU tensors, so agreeing on a size never synchronises a GPU stream. Created here,
-        # where every rank constructs its reducer (new_group is collective).
+        # host-side metadata exchange (the per-rank id counts of set_rows without a static
+        # cap): a gloo group on CPU tensors, so agreeing on a size never synchronises a GPU
+        # stream. Created here, where every rank constructs its reducer (new_group is
+        # collective).
         self.meta = None
         if self.world > 1:
             self.meta = group if dist.get_backend(group) == "gloo" else dist.new_group(
@@ -91,25 +95,36 @@ class GradReducer:
         self._rows = None
         self.rows_exchanged = 0
 
-    def set_rows(self, ids: torch.Tensor):
+    def set_rows(self, ids: torch.Tensor, cap: Optional[int] = None):
         """This step's touched rows of the sparse tables (any integer tensor): all-gathered
         now, async, while the forward runs. Ranks may hold different numbers of ids (the
-        collate pads questions to each batch's own longest one, so q_ipt is ragged across
-        ranks): the counts are agreed on the host first (gloo, no GPU synchronisation) and
-        every rank pads its ids to the largest count with a duplicate of one of its own ids
-        (duplicates are exchanged once). Several calls before the backward (e.g. several
+        collate pads questions to each batch's own longest one, and drops bad samples, so
+        q_ipt is ragged across ranks); every rank pads its list to one common length:
+          * cap given (the static bound every rank shares, e.g. batch_size * maxlen_q: see
+            AttModel.attach_reducer): padded to `cap` with the fixed filler row (ctor) -- no
+            host exchange at all. A filler row nobody touched has a zero gradient on every
+            rank, so exchanging it changes nothing. More than `cap` ids raise.
+          * cap None: the counts are agreed on the host first (gloo, no GPU synchronisation,
+            but one host rendezvous of the ranks per call) and the lists padded to the largest.
+        Duplicates are exchanged once. Several calls before the backward (e.g. several
         forwards) accumulate: the union of their rows is exchanged."""
         if self.world <= 1 or not self.sparse:
             return
         ids = ids.reshape(-1).to(torch.int64).contiguous()
         n = ids.numel()
-        cnt = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world)]
-        dist.all_gather(cnt, torch.tensor([n], dtype=torch.int64), group=self.meta)
-        cap = max(int(c) for c in cnt)
+        if cap is not None:
+            cap = int(cap)
+            if n > cap:
+                raise ValueError(f"GradReducer.set_rows: {n} row ids exceed the static cap {cap} "
+                                 "(batch_size * maxlen_q); raise maxlen_q")
+        else:
+            cnt = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world)]
+            dist.all_gather(cnt, torch.tensor([n], dtype=torch.int64), group=self.meta)
+            cap = max(int(c) for c in cnt)
         if cap == 0:
             return
         if n < cap:
-            fill = ids[:1] if n > 0 else torch.zeros(1, dtype=torch.int64, device=ids.device)
+            fill = torch.full((1,), self.filler, dtype=torch.int64, device=ids.device)
             ids = torch.cat([ids, fill.expand(cap - n)])
         outs = [torch.empty_like(ids) for _ in range(self.world)]
         w = dist.all_gather(outs, ids, group=self.group, async_op=True)

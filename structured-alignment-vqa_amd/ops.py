@@ -80,10 +80,10 @@ class GemmProbe:
 
 _probe = None
 
-# Product precision of the 128x128-tile GEMMs (savqa_gemm_desc.prec): 0 = fp32 MFMA (exact
-# fp32, the default), 1 = bf16 MFMA with fp32 accumulation (BASELINE cfg 3), 3 = 3xbf16
-# split products. Set per model (AttModel(..., gemm_precision=...)) via gemm_precision().
-PREC = {"fp32": 0, "bf16": 1, "bf16x3": 3}
+# Product precision of the fp32-storage 128x128-tile GEMMs (savqa_gemm_desc.prec): 0 = fp32
+# MFMA (exact fp32, the default), 3 = 3xbf16 split products. Set per model (AttModel(...,
+# gemm_precision="bf16x3")) via gemm_precision(); the bf16 / fp8 modes use gemm_lp instead.
+PREC = {"fp32": 0, "bf16x3": 3}
 _prec = 0
 
 
@@ -189,6 +189,8 @@ def lp_variant(d) -> str:
         return f"gemm_lp2_kernel<256,256,2,64,2,{at},{bt}>"
     if plan[0] == 4:
         return f"gemm_lp2_kernel<256,128,4,64,3,{at},{bt}>"
+    if plan[0] == 5:
+        return f"gemm_lp3_kernel<{at},{bt}>"
     return f"gemm_lp_kernel<{at},{bt},{str(d.a_type == 2).lower()},{plan[3]}>"
 
 

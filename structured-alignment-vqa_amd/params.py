@@ -173,9 +173,13 @@ class ParamArena:
             self.grad.zero_()
 
     def state_key(self):
-        """Changes whenever parameter values may have changed: torch in-place edits bump the
-        flat buffer's version counter, optimizer kernels bump `generation`."""
-        return (self.flat.data_ptr(), self.flat._version, self.generation)
+        """Changes whenever parameter values may have changed: torch in-place edits of the flat
+        buffer bump its version counter, optimizer kernels bump `generation`, and in-place
+        writes through the Parameters themselves (load_state_dict's copy_, init_params_, any
+        stock torch optimizer) bump each Parameter's OWN version counter -- `p.data = view`
+        does not share the flat buffer's -- so their sum is part of the key."""
+        return (self.flat.data_ptr(), self.flat._version, self.generation,
+                sum(p._version for p in self.params.values()))
 
     def table_ranges(self):
         """Arena ranges of the live 407000 x 300 GloVe tables (row-gathered, never GEMM B

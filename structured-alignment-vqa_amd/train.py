@@ -183,8 +183,7 @@ def main(gpu_rank, args):
     opt = Adam(model, lr=args.lr)
     reducer = GradReducer(model._arena) if args.world_size > 1 else None
     if reducer:
-        model.attach_reducer(reducer)
-    loss_meter, mil_meter = AverageMeter(), AverageMeter()
+        model.attach_reducer(reducer, batch_size=args.batch_size)
     result = {}
 
     def batches(seed0, split="train"):
@@ -205,6 +204,8 @@ def main(gpu_rank, args):
                                                device=dev)
 
     for epoch in range(args.num_epochs):
+        # main:261-266: both meters restart every epoch
+        loss_meter, loss_rank_meter = AverageMeter(), AverageMeter()
         for i, batch in enumerate(batches(1000 * epoch + 7919 * rank)):
             if reducer:
                 reducer.begin()
@@ -212,16 +213,23 @@ def main(gpu_rank, args):
             opt.zero_grad()
             loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil,
                                     with_milnce=args.with_MILNCE_loss, mil_nce_rel=mil_rel)
+            B = batch["answer"].shape[0]
+            # main:326-329 / :358-361: the MIL-NCE loss term, metered every step whether or not
+            # it enters the loss (--with_MILNCE_loss)
+            mil_loss = -mil.detach() - (mil_rel.detach() if mil_rel is not None else 0.0)
+            loss_rank_meter.update(mil_loss, B)
             loss.backward()
             opt.step(reducer=reducer)
-            if (i + 1) % args.log_steps == 0 or i + 1 == args.steps_per_epoch:
-                loss_meter.update(float(loss), batch["answer"].shape[0])
-                mil_meter.update(-float(mil) - (float(mil_rel) if mil_rel is not None else 0.0),
-                                 batch["answer"].shape[0])
-                if rank == 0:
-                    logging.info('Time %s, Epoch [%d/%d], Step [%d/%d], Loss: %.5f, MIL NCE Loss: %.5f, '
-                                 'Avg Loss: %.5f', datetime.datetime.now(), epoch + 1, args.num_epochs,
-                                 i + 1, args.steps_per_epoch, float(loss), -float(mil), loss_meter.avg)
+            # main:368: every step. The values stay device scalars (the meters' sums are device
+            # tensors), so the per-step update adds no host synchronisation; they are read on
+            # the log steps only.
+            loss_meter.update(loss.detach(), B)
+            if rank == 0 and ((i + 1) % args.log_steps == 0 or i + 1 == args.steps_per_epoch):
+                # main:370-377 (its "Epoch [e/num_epochs + 1]" counter kept as the reference prints it)
+                logging.info('Time %s, Epoch [%d/%d], Step [%d/%d], Loss: %s, MIL NCE Loss: %s, '
+                             'Avg Loss: %s, Avg MILNCE_loss: %s', datetime.datetime.now(), epoch + 1,
+                             args.num_epochs + 1, i + 1, args.steps_per_epoch, float(loss),
+                             float(mil_loss), float(loss_meter.avg), float(loss_rank_meter.avg))
         if gqa and hasattr(loaders["train"].sampler, "set_epoch"):
             loaders["train"].sampler.set_epoch(epoch + 1)
         # main:380-382: eval on the validation split, then on the training split
@@ -231,7 +239,8 @@ def main(gpu_rank, args):
         val_loss, corr, cnt, acc = gather_metrics(val, args.world_size, dev)
         train_loss, corr_t, cnt_t, acc_t = gather_metrics(trn, args.world_size, dev)
         if rank == 0:
-            result = {"epoch": epoch + 1, "train_loss": loss_meter.avg, "val_loss": val_loss,
+            result = {"epoch": epoch + 1, "train_loss": float(loss_meter.avg),
+                      "train_mil_loss": float(loss_rank_meter.avg), "val_loss": val_loss,
                       "accuracy": acc, "correct": corr, "cnt": cnt,
                       "train_eval_loss": train_loss, "train_accuracy": acc_t,
                       "train_correct": corr_t, "train_cnt": cnt_t}

@@ -133,9 +133,10 @@ def test_sparse_table_rows_exchange_equals_dense_gloo_world2():
         assert pos == n
 
 
-def _ragged_worker(rank, world, port, q):
+def _ragged_worker(rank, world, port, q, static_cap=False):
     """Ranks with different question lengths (the collate pads to each batch's own longest
-    question), two forwards before one backward, and declarations that leave a gap."""
+    question), two forwards before one backward, and declarations that leave a gap.
+    static_cap: the lists are padded to a bound every rank knows (no host count exchange)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -155,11 +156,21 @@ def _ragged_worker(rank, world, port, q):
     dense = g.clone()
     dist.all_reduce(dense)
     arena = types.SimpleNamespace(grad=g.clone())
-    red = GradReducer(arena, bucket_mb=0.001)
+    red = GradReducer(arena, bucket_mb=0.001, filler=rows - 1)
     red.add_sparse_table(t0, t1, width)
     red.begin()
-    red.set_rows(ids_a)
-    red.set_rows(ids_b)                 # second forward: its rows join the union
+    if static_cap:
+        red.meta = None                 # no host metadata group: a count exchange would fail
+        red.set_rows(ids_a, cap=3 * 10)
+        red.set_rows(ids_b, cap=2 * 8)  # second forward: its rows join the union
+        try:
+            red.set_rows(ids_a, cap=4)
+            raise AssertionError("ids beyond the cap must raise")
+        except ValueError:
+            pass
+    else:
+        red.set_rows(ids_a)
+        red.set_rows(ids_b)             # second forward: its rows join the union
     red.reduce_range(0, 100, True)
     red.reduce_range(250, n, True)      # [100, 250) never declared
     works, scale = red.drain()
@@ -171,14 +182,17 @@ def _ragged_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_ragged_rows_accumulated_forwards_and_coverage_gap_gloo_world2():
+@pytest.mark.parametrize("static_cap", [False, True])
+def test_ragged_rows_accumulated_forwards_and_coverage_gap_gloo_world2(static_cap):
     """ragged q_ipt across ranks must not desynchronise the id all-gather; rows of
     every forward since begin() are exchanged; an undeclared span is all-reduced densely
-    before Adam instead of being updated with the local gradient."""
+    before Adam instead of being updated with the local gradient. static_cap: the
+    per-forward host count exchange is replaced by padding to a bound every rank shares."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ragged_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_ragged_worker, args=(r, 2, port, q, static_cap))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

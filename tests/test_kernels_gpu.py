@@ -440,11 +440,11 @@ def test_adam_matches_oracle():
     assert rel(p, P["x"]) < 1e-6
 
 
-@pytest.mark.parametrize("prec,tol", [(1, 2e-2), (3, 1e-4)])
+@pytest.mark.parametrize("prec,tol", [(3, 1e-4)])
 @pytest.mark.parametrize("lay", ["NT", "NN", "TN"])
 @pytest.mark.parametrize("M,N,K", [(2048, 2048, 512), (4100, 1280, 520), (2100, 1536, 96)])
 def test_gemm_bf16_paths(prec, tol, lay, M, N, K):
-    """bf16 (prec 1, BASELINE cfg 3) and 3xbf16 (prec 3) MFMA GEMMs against fp64, with the
+    """3xbf16 (prec 3, the "bf16x3" mode) MFMA GEMMs against fp64, with the
     same epilogues as the fp32 path (bias+ReLU forward, residual dX, split-K dW with the
     bias-gradient column sums), including edge tiles and k tails."""
     O = ops()

@@ -155,31 +155,45 @@ def full_model_cases(modules_mod, att_mod):
     del model
 
 
-# relation-branch cases: (objects per sample, question lengths). full_rel_sn has a super-node
-# graph of T_syb = 14 + 3 + 14*13 + 12 = 211 > 128 positions, so the key-tiled attention
-# (csrc/attn_flash.hip) runs inside the semantic stack of the parity case.
-RELATION_RUNS = {"full_rel_b2": ([5, 4], [7, 5]),
-                 "full_rel_sn": ([14, 11], [12, 9])}
+# relation-branch cases: (objects per sample, question lengths, options). full_rel_sn has a
+# super-node graph of T_syb = 14 + 3 + 14*13 + 12 = 211 > 128 positions, so the key-tiled
+# attention (csrc/attn_flash.hip) runs inside the semantic stack of the parity case.
+# full_rel_big is the reference's own relation configuration (submit.py:87 maxlen 1600,
+# :101 hidden_size_mil 64) at the benched super-node size: 36 objects -> T_syb = 36 + 3 +
+# 36*35 + 14 = 1313 positions, 311 relation categories, up to 8 listed relations per object
+# pair (~5.7k positive entries), 6 encoder/decoder blocks (the reference hard-codes 6 in its
+# forwards, AttModel_x3.py:127-139; its per-entry Python loop :421-436 dominates the CPU time).
+RELATION_RUNS = {"full_rel_b2": ([5, 4], [7, 5], {}),
+                 "full_rel_sn": ([14, 11], [12, 9], {}),
+                 "full_rel_big": ([36], [14], dict(hidden_mil=64, num_blocks=6, nrel=311,
+                                                   max_rel_per_pair=8, maxlen=1600))}
 
 
-def relation_cases(att_mod):
-    for cname, (nobj, lq) in RELATION_RUNS.items():
-        relation_case(att_mod, cname, nobj, lq)
+def relation_cases(att_mod, only=None):
+    for cname, (nobj, lq, opt) in RELATION_RUNS.items():
+        if only is None or cname in only:
+            relation_case(att_mod, cname, nobj, lq, **opt)
 
 
-def relation_case(att_mod, cname, nobj, lq):
+def relation_case(att_mod, cname, nobj, lq, hidden_mil=None, num_blocks=None, nrel=7,
+                  max_rel_per_pair=2, maxlen=None):
     """Full model with the MIL-NCE relation branch (only_obj=False, AttModel_x3.py:382-437)
     on a super-node batch (oracle/cases.make_relation_inputs)."""
-    nrel = 7
+    import time
+    hidden_mil = hidden_mil or CFG["hidden_mil"]
+    num_blocks = num_blocks or CFG["num_blocks"]
+    maxlen = maxlen or CFG["maxlen"]
     glove = types.SimpleNamespace(vectors=torch.zeros(8, 300))
     with torch.no_grad():
-        model = att_mod.AttModel(glove, CFG["hidden"], CFG["hidden_mil"], CFG["num_classes"],
-                                 CFG["maxlen_q"], CFG["maxlen"], CFG["maxlen_v"], CFG["num_blocks"], CFG["heads"],
+        model = att_mod.AttModel(glove, CFG["hidden"], hidden_mil, CFG["num_classes"],
+                                 CFG["maxlen_q"], maxlen, CFG["maxlen_v"], num_blocks, CFG["heads"],
                                  0.0, 0.0, nrel, False)
     model.train()
     fill_params(model)
     tag = "relcase" if cname == "full_rel_b2" else cname
-    inp = cases.make_relation_inputs(len(nobj), nobj, lq, nrel, tag=tag)
+    inp = cases.make_relation_inputs(len(nobj), nobj, lq, nrel, tag=tag,
+                                     max_rel_per_pair=max_rel_per_pair)
+    t0 = time.time()
     t = to_t(inp)
     lc, lv, ls, mil, mil_rel = model(
         t["vis_fea"], t["vis_mask"], t["q_ipt"], t["q_mask"], t["q_graph"], t["macro_ipt"],
@@ -194,7 +208,8 @@ def relation_case(att_mod, cname, nobj, lq):
     out.update(logits_concat=lc.detach().numpy(), logits_vis=lv.detach().numpy(),
                logits_syb=ls.detach().numpy(), mil_nce_obj=np.float32(mil.item()),
                mil_nce_rel=np.float32(mil_rel.item()), loss=np.float32(loss.item()),
-               num_relations=np.int32(nrel), num_blocks=np.int32(CFG["num_blocks"]))
+               num_relations=np.int32(nrel), num_blocks=np.int32(num_blocks),
+               hidden_mil=np.int32(hidden_mil), maxlen=np.int32(maxlen))
     gnames = []
     for name, p in model.named_parameters():
         if p.grad is None:
@@ -214,7 +229,8 @@ def relation_case(att_mod, cname, nobj, lq):
     out["grad_names"] = np.array(gnames)
     np.savez_compressed(os.path.join(OUT, f"{cname}.npz"), **out)
     print("wrote", cname, "T_syb", inp["macro_ipt"].shape[1] + inp["q_ipt"].shape[1], "loss",
-          float(out["loss"]), "mil_rel", float(out["mil_nce_rel"]))
+          float(out["loss"]), "mil_rel", float(out["mil_nce_rel"]), "entries",
+          int((inp["micro_positive_rel_loc"][..., 3] >= 0).sum()), f"{time.time() - t0:.1f}s")
     del model
 
 
@@ -372,6 +388,8 @@ def main():
         full_model_cases(modules_mod, att_mod)
     if "rel" in which:
         relation_cases(att_mod)
+    if "rel_big" in which:  # only the large relation case (minutes of reference CPU time)
+        relation_cases(att_mod, only=("full_rel_big",))
     if "collate" in which:
         collate_cases()
     if "reader" in which:
