@@ -156,6 +156,10 @@ int savqa_quant_fp8(void* stream, const float* in, int64_t rows, int64_t cols, i
                     int64_t stride, int64_t offset);
 int savqa_dequant_fp8_bf16(void* stream, const void* q, int64_t rows, int64_t cols, int64_t ldq,
                            const uint8_t* scale, int64_t lds, void* out, int64_t ldo);
+/* out[r*ldo + c] = float(in[r*ldi + c]) over bf16 rows (exact): the fp32 Q/K/V the key-tiled
+ * attention reads when a low-precision mode meets a sequence longer than 128 */
+int savqa_widen_bf16(void* stream, const void* in, int64_t rows, int64_t cols, int64_t ldi,
+                     float* out, int64_t ldo);
 /* out[c] += sum_r X[r*ldx + c] over a bf16 X (bias gradients of the low-precision GEMMs) */
 int savqa_colsum_bf16(void* stream, const void* X, int64_t rows, int64_t cols, int64_t ldx,
                       float* out);
@@ -420,6 +424,20 @@ int savqa_scale_by(void* stream, const float* in, const float* scale, int64_t n,
 int savqa_adam(void* stream, float* p, const float* g, float* m, float* v, int64_t n,
                float lr, float beta1, float beta2, float eps, float bc1, float bc2,
                float grad_scale);
+
+/* Row-tracked tables (the three 407000 x 300 GloVe tables, AttModel_x3.py:36-41, :168-171,
+ * :295): flags[r] bit 0 = row r has Adam state (touched at some step), bit 1 = row
+ * r was touched since the last savqa_zero_rows (its gradient may be non-zero).
+ *   savqa_mark_rows: flags[ids[i]] |= 2 (ids outside [0, nrows) ignored)
+ *   savqa_zero_rows: g row r = 0 and bit 1 cleared, for every row with bit 1
+ *   savqa_adam_rows: the savqa_adam update on every row with bit 0 or 1 (g read only with
+ *     bit 1, else 0), then bit 0 set on rows with bit 1. Rows with neither bit are exactly
+ *     what torch.optim.Adam would leave unchanged (m = v = 0, g = 0): skipping them is exact. */
+int savqa_mark_rows(void* stream, const int64_t* ids, int64_t n, int64_t nrows, uint8_t* flags);
+int savqa_zero_rows(void* stream, float* g, int64_t width, int64_t nrows, uint8_t* flags);
+int savqa_adam_rows(void* stream, float* p, const float* g, float* m, float* v, int64_t width,
+                    int64_t nrows, uint8_t* flags, float lr, float beta1, float beta2, float eps,
+                    float bc1, float bc2, float grad_scale);
 
 /* ------------------------------------------------------------------------
  * Batch collation. Replaces the host-side padding of

@@ -183,15 +183,25 @@ class CompactBilinearPooling(nn.Module):
 
 
 class _AttModelFn(torch.autograd.Function):
+    """The whole AttModel.forward as one autograd node. Its inputs are the batch tensors AND
+    every live Parameter: the backward writes the parameter gradients straight into the
+    flat gradient arena (the Parameters' .grad views) and returns None for them, but having
+    the Parameters as inputs puts their AccumulateGrad nodes into the graph, so everything
+    that hooks gradient accumulation sees each parameter become ready after the backward:
+    torch's DistributedDataParallel (main:203, find_unused_parameters=True) then averages
+    the arena's gradients in place (its bucket copies read and write .grad), and
+    register_post_accumulate_grad_hook users run as usual."""
+
     @staticmethod
-    def forward(ctx, model, decMask, drop, anchor, *tensors):
+    def forward(ctx, model, decMask, drop, ntensors, *args):
+        tensors = args[:ntensors]
         inp = dict(zip(_INPUT_NAMES + _REL_NAMES, tensors))
         if model.__dict__.get("_vis_scale") is not None:
             inp["vis_fea_scale"] = model._vis_scale
         (lc, lv, ls, mil, mil_rel), saved = model._engine.forward(inp, decMask, drop)
         ctx.model = model
         ctx.saved = saved
-        ctx.ntensors = len(tensors)
+        ctx.nargs = len(args)
         ctx.rel = mil_rel is not None
         if mil_rel is None:
             mil_rel = torch.zeros((), device=mil.device)
@@ -215,7 +225,7 @@ class _AttModelFn(torch.autograd.Function):
                                z(dmil, ()), on_range=red.reduce_range if red else None,
                                dmil_rel=z(dmil_rel, ()) if ctx.rel else None)
         ctx.saved = None
-        return (None, None, None, None) + (None,) * ctx.ntensors
+        return (None, None, None, None) + (None,) * ctx.nargs
 
 
 _INPUT_NAMES = ("vis_fea", "vis_mask", "q_ipt", "q_mask", "q_graph", "macro_ipt", "macro_mask",
@@ -280,8 +290,9 @@ class AttModel(nn.Module):
         object.__setattr__(self, "_reducer", reducer)
         object.__setattr__(self, "_rows_cap", None if batch_size is None
                            else int(batch_size) * int(self.maxlen_q))
-        self._engine.multi_rank = reducer is not None and getattr(reducer, "world", 1) > 1
-        if reducer is not None and getattr(reducer, "world", 1) > 1:
+        active = reducer is not None and getattr(reducer, "active", getattr(reducer, "world", 1) > 1)
+        self._engine.multi_rank = active
+        if active:
             for pre in ("att_vis_grid", "att_syb"):
                 o, shp = self._arena.offsets[f"{pre}.syb_emb.weight"]
                 reducer.add_sparse_table(o, o + shp.numel(), shp[1])
@@ -338,11 +349,12 @@ class AttModel(nn.Module):
                                  i64(micro_negative_rel_loc))
             self._check_relation_locs(tensors[-2], tensors[-1], vis_fea.shape[1],
                                       macro_ipt.shape[1], tensors[-3].shape[1])
-        anchor = self._arena_anchor()
+        live = self._live_params()
         red = self.__dict__.get("_reducer")
-        if red is not None and anchor is not None:
+        if red is not None and live:
             red.set_rows(tensors[2], cap=self.__dict__.get("_rows_cap"))  # q_ipt: touched rows
-        lc, lv, ls, mil, mil_rel = _AttModelFn.apply(self, bool(decMask), drop, anchor, *tensors)
+        lc, lv, ls, mil, mil_rel = _AttModelFn.apply(self, bool(decMask), drop, len(tensors),
+                                                     *tensors, *live)
         return lc, lv, ls, mil, (mil_rel if not self.only_obj else 0)
 
     def _check_relation_locs(self, pos, neg, n_obj, n_macro, n_rel):
@@ -368,9 +380,11 @@ class AttModel(nn.Module):
             raise IndexError("relation location out of range (objects / categories "
                              f"< {nrel} / macro nodes / positive words)")
 
-    def _arena_anchor(self):
-        # any parameter that requires grad links the autograd node into the graph
-        for p in self.cls.parameters():
-            if p.requires_grad and torch.is_grad_enabled():
-                return p
-        return None
+    def _live_params(self):
+        """The live Parameters (those the backward writes gradients for) when a graph is being
+        recorded, else () -- they link the autograd node to their AccumulateGrad nodes."""
+        if not torch.is_grad_enabled():
+            return ()
+        a = self._arena
+        live = [a.params[n] for n in a.live_names]
+        return tuple(p for p in live if p.requires_grad)

@@ -82,6 +82,11 @@ _SIGS = {
     "savqa_gemm_lp_supported": [C.POINTER(GemmLpDesc)],
     "savqa_gemm_lp_plan": [C.POINTER(GemmLpDesc), c_p],
     "savqa_cast_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64],
+    "savqa_widen_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64],
+    "savqa_mark_rows": [c_p, c_p, c_i64, c_i64, c_p],
+    "savqa_zero_rows": [c_p, c_p, c_i64, c_i64, c_p],
+    "savqa_adam_rows": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_f, c_f, c_f, c_f, c_f, c_f,
+                        c_f],
     "savqa_quant_fp8": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64,
                         c_i64],
     "savqa_dequant_fp8_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64],

@@ -29,22 +29,20 @@
 
 namespace savqa {
 
-constexpr int GEMM_OCC = 2;   // workgroups (= waves per SIMD) per CU
+// Workgroups (= waves per SIMD) per CU the launch bounds ask for (VGPRs capped at 512 / OCC;
+// 40 KB of LDS per workgroup admits 3), and the slots per CU the launch planner counts per
+// round (split-K factors, the tail split of the last partial round).
+#ifndef SAVQA_GEMM_OCC
+#define SAVQA_GEMM_OCC 3
+#endif
+#ifndef SAVQA_GEMM_PLAN_OCC
+#define SAVQA_GEMM_PLAN_OCC 3
+#endif
+constexpr int GEMM_OCC = SAVQA_GEMM_OCC;
+constexpr int GEMM_PLAN_OCC = SAVQA_GEMM_PLAN_OCC;
 constexpr int GEMM_BK = 16;   // k-tile; 16 beats 32 on the K=512 step shapes (shorter prologue)
 constexpr int GEMM_BK_DW = 16;  // k-tile of the dW layouts (A = dY^T, K = B*T rows); 32 no better
 
-// Main loop: 1 = three LDS stages with the next k-tile's MFMA fragments read into a second
-// register set while the current one's MFMAs run (no LDS wait between a barrier and the
-// MFMAs); 0 = two stages, fragments read after each barrier (round 1-2 structure).
-#ifndef SAVQA_GEMM_PIPE
-#define SAVQA_GEMM_PIPE 1
-#endif
-// Epilogue: 1 = the C tile staged through LDS and written as whole 16-B row segments (four
-// per lane per 512-B row pair), its operands (residual / mask / row vector) loaded for the
-// whole tile before the first store; 0 = per-fragment element stores (round 1-2).
-#ifndef SAVQA_GEMM_LDS_EPI
-#define SAVQA_GEMM_LDS_EPI 1
-#endif
 
 // MFMA of the 128x128 path: v_mfma_f32_16x16x4_f32 (fp32 in, fp32 accumulate, 64
 // FLOP/clk/SIMD), 16-row fragments, 4 accumulator VGPRs each. A fragment's operand lane
@@ -342,119 +340,6 @@ __device__ __forceinline__ void gemm_mainloop(
 #undef SAVQA_GEMM_LOAD
 }
 
-// Three-stage main loop (SAVQA_GEMM_PIPE): per k-tile t, after ONE barrier,
-//   fetch the MFMA fragments of tile t+1 (LDS stage (t+1)%3, stored in step t-1) into the
-//   idle register set, store the staged tile t+2 into stage (t+2)%3 (last read in step t-2),
-//   issue the global loads of tile t+3, then run tile t's MFMAs from the other register set,
-// so a wave goes from the barrier straight into its MFMAs: the fragment reads of the next
-// tile and the staging traffic are issued ahead of them and land underneath.
-template <int BM, int BN, int BK, bool AT, bool BT>
-__device__ __forceinline__ void gemm_fetch_frags(const float* __restrict__ As,
-                                                 const float* __restrict__ Bs, int wm, int wn,
-                                                 int lane,
-                                                 float (&a)[GemmCfg<BM, BN, BK, AT, BT>::FM][4],
-                                                 float (&b)[GemmCfg<BM, BN, BK, AT, BT>::FN][4]) {
-  using G = GemmCfg<BM, BN, BK, AT, BT>;
-#pragma unroll
-  for (int i = 0; i < G::FM; ++i) G::OA::template fetch<typename G::MI>(As, wm * G::WM, i, 0, lane, a[i]);
-#pragma unroll
-  for (int j = 0; j < G::FN; ++j) G::OB::template fetch<typename G::MI>(Bs, wn * G::WN, j, 0, lane, b[j]);
-}
-
-template <int BM, int BN, int BK, bool AT, bool BT>
-__device__ __forceinline__ void gemm_mma_frags(
-    const float (&a)[GemmCfg<BM, BN, BK, AT, BT>::FM][4],
-    const float (&b)[GemmCfg<BM, BN, BK, AT, BT>::FN][4],
-    typename GemmCfg<BM, BN, BK, AT, BT>::Acc (&acc)[GemmCfg<BM, BN, BK, AT, BT>::FM][GemmCfg<BM, BN, BK, AT, BT>::FN]) {
-  using G = GemmCfg<BM, BN, BK, AT, BT>;
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int i = 0; i < G::FM; ++i)
-#pragma unroll
-      for (int j = 0; j < G::FN; ++j) acc[i][j] = G::MI::mma(a[i][s], b[j][s], acc[i][j]);
-}
-
-template <int BM, int BN, int BK, bool AT, bool BT, int MODE>
-__device__ __forceinline__ void gemm_mainloop_pipe(
-    const savqa_gemm_desc& d, float* smem, int64_t m0, int64_t n0, int64_t kbeg, int64_t kend,
-    int ntiles,
-    typename GemmCfg<BM, BN, BK, AT, BT>::Acc (&acc)[GemmCfg<BM, BN, BK, AT, BT>::FM][GemmCfg<BM, BN, BK, AT, BT>::FN],
-    bool do_cs, f4 (&cs)[GemmCfg<BM, BN, BK, AT, BT>::OA::ITERS]) {
-  using G = GemmCfg<BM, BN, BK, AT, BT>;
-  using OA = typename G::OA;
-  using OB = typename G::OB;
-  static_assert(BK == G::MI::KCH, "one fragment read per operand row per k-tile");
-  constexpr int STAGE = OA::SIZE + OB::SIZE;
-  OA la;
-  OB lb;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const bool agk = AT && d.a_rows, bgk = !BT && d.b_rows;  // MODE 3: k-row gathers
-  if constexpr (MODE != 0) {
-    la.setup_fast(d.A, d.lda, AT ? nullptr : d.a_rows, m0, d.M, tid);
-    lb.setup_fast(d.B, d.ldb, BT ? d.b_rows : nullptr, n0, d.N, tid);
-    if (MODE == 3 && agk) la.setup_kg(d.lda, tid);
-    if (MODE == 3 && bgk) lb.setup_kg(d.ldb, tid);
-  }
-  auto load = [&](int64_t k0) {
-    if (MODE == 1 || (MODE == 2 && k0 + BK <= kend)) {
-      la.load_fast(d.lda, k0);
-      lb.load_fast(d.ldb, k0);
-    } else if (MODE == 3 && k0 + BK <= kend) {
-      if (agk) la.load_fast_kg(d.lda, d.a_rows, k0, tid);
-      else la.load_fast(d.lda, k0);
-      if (bgk) lb.load_fast_kg(d.ldb, d.b_rows, k0, tid);
-      else lb.load_fast(d.ldb, k0);
-    } else {
-      la.load_slow(d.A, d.lda, d.a_rows, d.M, m0, k0, kend, tid);
-      lb.load_slow(d.B, d.ldb, d.b_rows, d.N, n0, k0, kend, tid);
-    }
-  };
-  auto stage_of = [&](int t) { return smem + (t % 3) * STAGE; };
-  auto put = [&](int t) {
-    float* st = stage_of(t);
-    if (do_cs) la.accum(cs);  // colsum_a: the staged A tile summed over its k rows
-    la.store(st, tid);
-    lb.store(st + OA::SIZE, tid);
-  };
-  load(kbeg);
-  put(0);
-  if (ntiles > 1) {
-    load(kbeg + BK);
-    put(1);
-  }
-  if (ntiles > 2) load(kbeg + 2 * BK);
-  float fa0[G::FM][4], fb0[G::FN][4], fa1[G::FM][4], fb1[G::FN][4];
-  __syncthreads();
-  gemm_fetch_frags<BM, BN, BK, AT, BT>(stage_of(0), stage_of(0) + OA::SIZE, wm, wn, lane, fa0, fb0);
-  // two k-tiles per trip, so each register set has a fixed name (no runtime-indexed arrays)
-  for (int t = 0; t < ntiles; t += 2) {
-    __syncthreads();
-    if (t + 1 < ntiles)
-      gemm_fetch_frags<BM, BN, BK, AT, BT>(stage_of(t + 1), stage_of(t + 1) + OA::SIZE, wm, wn,
-                                           lane, fa1, fb1);
-    if (t + 2 < ntiles) {
-      put(t + 2);
-      if (t + 3 < ntiles) load(kbeg + (int64_t)(t + 3) * BK);
-    }
-    gemm_mma_frags<BM, BN, BK, AT, BT>(fa0, fb0, acc);
-    if (t + 1 >= ntiles) break;
-    __syncthreads();
-    if (t + 2 < ntiles)
-      gemm_fetch_frags<BM, BN, BK, AT, BT>(stage_of(t + 2), stage_of(t + 2) + OA::SIZE, wm, wn,
-                                           lane, fa0, fb0);
-    if (t + 3 < ntiles) {
-      put(t + 3);
-      if (t + 4 < ntiles) load(kbeg + (int64_t)(t + 4) * BK);
-    }
-    gemm_mma_frags<BM, BN, BK, AT, BT>(fa1, fb1, acc);
-  }
-  __syncthreads();  // every wave's last fragment reads are done: the caller reuses smem
-}
-
 // colsum_a fold (bias gradient of a dW GEMM): every thread's staged-A partials share one
 // column group q = tid % PER (GEMM_NT is a multiple of PER); rows of threads write plain
 // LDS rows and one thread per column sums them (LDS float atomics serialise: ~us per block)
@@ -477,120 +362,12 @@ __device__ __forceinline__ void cs_fold(const f4 (&cs)[ITERS], float* smem, int6
   }
 }
 
-// LDS-staged epilogue (SAVQA_GEMM_LDS_EPI): the waves write their accumulators into a
-// [BM][BN + 4] fp32 image of the C tile (ds_write_b32, conflict-free: the two rows a 32-lane
-// half covers are 4 rows = 16 banks apart), then every thread owns one 4-column group of
-// 16 rows (32 threads per 512-B row) and finishes them as whole 16-B segments: one float4 of
-// bias per thread, the residual / row vector and the mask loaded for all 16 rows before the
-// first store (vmcnt counts stores too: a load behind a store waits for it), one 16-B store
-// (or four contiguous float atomics) per row. A wave instruction then covers two whole 512-B
-// rows instead of the fragment layout's four 64-B pieces, with a quarter of the store
-// instructions. `vec`: every row pointer of C / residual / row vector / mask is 16-B aligned
-// (host check); otherwise the same loop runs element by element.
-template <int BM, int BN>
-__device__ __forceinline__ void gemm_epilogue_lds(
-    const savqa_gemm_desc& d, float* smem, const f4 (&acc)[BM / 32][BN / 32], int64_t m0,
-    int64_t n0, bool first_split, bool atomic, bool vec) {
-  using MI = GemmMi;
-  constexpr int FM = BM / 32, FN = BN / 32, WM = BM / 2, WN = BN / 2;
-  constexpr int CLD = BN + 4;
-  constexpr int CG = BN / 4;                 // 4-column groups per row
-  constexpr int RSTEP = GEMM_NT / CG;        // rows per pass
-  constexpr int NP = BM / RSTEP;             // rows per thread
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < MI::NACC; ++r)
-        smem[(wm * WM + i * MI::FR + MI::row(r, lane)) * CLD + wn * WN + j * MI::FR + MI::col(lane)] =
-            acc[i][j][r];
-  __syncthreads();
-  const int cg = threadIdx.x % CG, rr = threadIdx.x / CG;
-  const int64_t n = n0 + 4 * cg;
-  if (n >= d.N) return;
-  const bool full = n + 3 < d.N;
-  const bool vfull = vec && full;
-  const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
-  f4 bv = {0.f, 0.f, 0.f, 0.f};
-  if (first_split && d.bias) {
-    if (vfull) bv = *reinterpret_cast<const f4*>(d.bias + n);
-    else
-      for (int e = 0; e < 4; ++e) bv[e] = n + e < d.N ? d.bias[n + e] : 0.f;
-  }
-  // X: the residual (or, without one, the row vector); Y: the mask (keep where > 0)
-  const bool use_res = first_split && d.resid != nullptr;
-  const bool use_rv = first_split && d.rowvec != nullptr;
-  const bool x_is_rv = !use_res && use_rv;
-  const bool has_x = use_res || use_rv;
-  f4 X[NP], Y[NP];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int64_t m = min(m0 + rr + p * RSTEP, d.M - 1);
-    const float* xp = nullptr;
-    if (use_res) xp = d.resid + m * d.ldr + n;
-    else if (use_rv) xp = d.rowvec + (int64_t)((uint32_t)m % (uint32_t)d.rowvec_period) * d.ldrv + n;
-    X[p] = f4{0.f, 0.f, 0.f, 0.f};
-    if (has_x) {
-      if (vfull) X[p] = *reinterpret_cast<const f4*>(xp);
-      else
-        for (int e = 0; e < 4; ++e) X[p][e] = n + e < d.N ? xp[e] : 0.f;
-    }
-    Y[p] = f4{1.f, 1.f, 1.f, 1.f};
-    if (d.mask) {
-      const int64_t mr = d.mask_arows ? d.a_rows[m] : m;
-      const float* mp = d.mask + mr * d.ldmask + n;
-      if (vfull) Y[p] = *reinterpret_cast<const f4*>(mp);
-      else
-        for (int e = 0; e < 4; ++e) Y[p][e] = n + e < d.N ? mp[e] : 0.f;
-    }
-  }
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int r = rr + p * RSTEP;
-    const int64_t m = m0 + r;
-    if (m >= d.M) break;
-    const EpiRow er = epi_row(d, m, ident);
-    f4 v = *reinterpret_cast<const f4*>(&smem[r * CLD + 4 * cg]) * d.alpha + bv;
-    if (use_res && use_rv) {  // both (unused by the model): the row vector read inline
-      for (int e = 0; e < 4; ++e)
-        if (n + e < d.N) v[e] += d.rowvec[er.pr * d.ldrv + n + e];
-    } else if (x_is_rv) {
-      v += X[p];
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (d.relu) v[e] = fmaxf(v[e], 0.f);
-      v[e] *= er.rs;
-      if (!(Y[p][e] > 0.f)) v[e] = 0.f;
-    }
-    if (use_res) v += X[p];
-    float* cp = er.crow + n;
-    if (atomic) {
-      for (int e = 0; e < 4; ++e)
-        if (n + e < d.N) atomicAdd(cp + e, v[e]);
-    } else if (d.beta != 0.f) {
-      for (int e = 0; e < 4; ++e)
-        if (n + e < d.N) cp[e] = v[e] + d.beta * cp[e];
-    } else if (vfull) {
-      *reinterpret_cast<f4*>(cp) = v;
-    } else {
-      for (int e = 0; e < 4; ++e)
-        if (n + e < d.N) cp[e] = v[e];
-    }
-  }
-}
-
 template <int BM, int BN, int BK, bool AT, bool BT>
 __global__ __launch_bounds__(GEMM_NT, GEMM_OCC) __attribute__((amdgpu_waves_per_eu(GEMM_OCC, GEMM_OCC))) void gemm_f32_kernel(savqa_gemm_desc d, GemmGrid gg,
-                                                             int avec, int bvec, int evec) {
+                                                             int avec, int bvec) {
   using G = GemmCfg<BM, BN, BK, AT, BT>;
   constexpr int FM = G::FM, FN = G::FN, WM = G::WM, WN = G::WN;
-  constexpr int MAIN_LDS = (SAVQA_GEMM_PIPE ? 3 : 2) * (G::OA::SIZE + G::OB::SIZE);
-  constexpr int EPI_LDS = SAVQA_GEMM_LDS_EPI ? BM * (BN + 4) : 0;
-  __shared__ __attribute__((aligned(16))) float smem[MAIN_LDS > EPI_LDS ? MAIN_LDS : EPI_LDS];
+  __shared__ __attribute__((aligned(16))) float smem[2 * (G::OA::SIZE + G::OB::SIZE)];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -637,40 +414,20 @@ __global__ __launch_bounds__(GEMM_NT, GEMM_OCC) __attribute__((amdgpu_waves_per_
 #pragma unroll
   for (int it = 0; it < G::OA::ITERS; ++it) cs[it] = f4{0.f, 0.f, 0.f, 0.f};
   if (ntiles > 0) {
-#if SAVQA_GEMM_PIPE
-#define SAVQA_MAINLOOP gemm_mainloop_pipe
-#else
-#define SAVQA_MAINLOOP gemm_mainloop
-#endif
     if (mode == 1)
-      SAVQA_MAINLOOP<BM, BN, BK, AT, BT, 1>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      gemm_mainloop<BM, BN, BK, AT, BT, 1>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     else if (mode == 2)
-      SAVQA_MAINLOOP<BM, BN, BK, AT, BT, 2>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      gemm_mainloop<BM, BN, BK, AT, BT, 2>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     else if (mode == 3)
-      SAVQA_MAINLOOP<BM, BN, BK, AT, BT, 3>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      gemm_mainloop<BM, BN, BK, AT, BT, 3>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     else
-      SAVQA_MAINLOOP<BM, BN, BK, AT, BT, 0>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
-#undef SAVQA_MAINLOOP
+      gemm_mainloop<BM, BN, BK, AT, BT, 0>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
   }
   if constexpr (AT) {
     if (do_cs) {  // block-uniform; smem is free after the main loop's last barrier
       cs_fold<G::OA::PER, G::OA::ITERS, BM>(cs, smem, m0, d);
     }
   }
-#if SAVQA_GEMM_LDS_EPI
-  if (ntiles == 0) {
-    // a slice without k-tiles never ran the main loop's barriers: nothing to stage
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  }
-  if constexpr (AT) {
-    if (do_cs) __syncthreads();  // cs_fold's smem rows are read before the C image lands
-  }
-  gemm_epilogue_lds<BM, BN>(d, smem, acc, m0, n0, first_split, atomic, evec != 0);
-  return;
-#endif
 
   // ---------------------------------------------------------------- epilogue
   const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
@@ -1090,7 +847,7 @@ static int slots_per_launch() {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
-    cached[dev] = GEMM_OCC * cus;
+    cached[dev] = GEMM_PLAN_OCC * cus;
   }
   return cached[dev];
 }
@@ -1122,15 +879,6 @@ using namespace savqa;
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// 16-B row segments in the LDS-staged epilogue: every row pointer it forms must be aligned
-static int epi_vec(const savqa_gemm_desc& d) {
-  const bool c = aligned16(d.C) && d.ldc % 4 == 0;
-  const bool b = !d.bias || aligned16(d.bias);
-  const bool r = !d.resid || (aligned16(d.resid) && d.ldr % 4 == 0);
-  const bool v = !d.rowvec || (aligned16(d.rowvec) && d.ldrv % 4 == 0);
-  const bool m = !d.mask || (aligned16(d.mask) && d.ldmask % 4 == 0);
-  return c && b && r && v && m;
-}
 
 // skinny shapes with fewer 32x32 tiles than this run on 16x16 tiles (measured: 256x512
 // outputs (128 tiles) 1.25-1.55x faster at K=2048, 256x914 (232) slower; thresholds 192 /
@@ -1221,7 +969,7 @@ template <int BM, int BN, int BK, bool AT, bool BT>
 static void launch_gemm(const savqa_gemm_desc& d, const GemmPlan& p, hipStream_t s, int avec,
                         int bvec) {
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, AT, BT>), dim3(p.grid_x, p.nsplit), dim3(GEMM_NT),
-                     0, s, d, p.gg, avec, bvec, epi_vec(d));
+                     0, s, d, p.gg, avec, bvec);
 }
 
 template <int BM, int BN, int BK>

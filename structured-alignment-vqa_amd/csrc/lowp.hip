@@ -73,6 +73,24 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict_
   }
 }
 
+// out[r*ldo + c] = float(in[r*ldi + c]): exact widening of bf16 rows (the fp32 operands the
+// key-tiled attention takes in the low-precision modes at T > 128)
+__global__ __launch_bounds__(256) void widen_bf16_kernel(const __bf16* __restrict__ in, int64_t rows,
+                                                         int64_t cols, int64_t ldi,
+                                                         float* __restrict__ out, int64_t ldo, int vec) {
+  const int64_t per_row = vec ? cols / 4 : cols;
+  const int64_t n = rows * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / per_row, c = i - r * per_row;
+    if (vec) {
+      const bf16x4 v = *reinterpret_cast<const bf16x4*>(in + r * ldi + 4 * c);
+      *reinterpret_cast<f4v*>(out + r * ldo + 4 * c) = __builtin_convertvector(v, f4v);
+    } else {
+      out[r * ldo + c] = (float)in[r * ldi + c];
+    }
+  }
+}
+
 // one wave per (row, 64 32-column blocks): lane = block, 32 values each
 __global__ __launch_bounds__(256) void quant_fp8_kernel(const float* __restrict__ in, int64_t rows,
                                                         int64_t cols, int64_t ldi,
@@ -246,6 +264,17 @@ extern "C" int savqa_cast_bf16(void* stream, const float* in, int64_t rows, int6
   hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), in, rows,
                      cols, ldi, static_cast<__bf16*>(out), ldo, vec, RowMap{group, stride, offset});
   return check_launch("savqa_cast_bf16");
+}
+
+extern "C" int savqa_widen_bf16(void* stream, const void* in, int64_t rows, int64_t cols,
+                                int64_t ldi, float* out, int64_t ldo) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const int vec = (cols % 4 == 0) && (ldi % 4 == 0) && (ldo % 4 == 0) &&
+                  (((uintptr_t)in) & 7) == 0 && (((uintptr_t)out) & 15) == 0;
+  const int64_t n = rows * (vec ? cols / 4 : cols);
+  hipLaunchKernelGGL(widen_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream),
+                     static_cast<const __bf16*>(in), rows, cols, ldi, out, ldo, vec);
+  return check_launch("savqa_widen_bf16");
 }
 
 extern "C" int savqa_quant_fp8(void* stream, const float* in, int64_t rows, int64_t cols, int64_t ldi,

@@ -481,6 +481,98 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
 }
 
+
+// ------------------------------------------------------------------ row-tracked tables
+// The three 407000 x 300 GloVe tables (AttModel_x3.py:36-41, :168-171, :295) receive gradient
+// rows only for the token ids of the step. Per table row a flag byte: bit 0 = the row has
+// Adam state (it was touched at some step), bit 1 = the row was touched since the last
+// zero_rows (its gradient may be non-zero). A never-touched row has m = v = 0 and g = 0, so
+// torch.optim.Adam leaves p, m and v exactly unchanged there: skipping it is bit-exact. A row
+// with state but no gradient this step still decays (g = 0 is not read).
+constexpr int ROW_EVER = 1, ROW_CUR = 2;
+
+__global__ __launch_bounds__(256) void mark_rows_kernel(const int64_t* __restrict__ ids, int64_t n,
+                                                        int64_t nrows, uint8_t* __restrict__ flags) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = ids[i];
+    if (r >= 0 && r < nrows) flags[r] |= ROW_CUR;  // every writer stores old | CUR: no race
+  }
+}
+
+// One wave per 64 rows: lane l reads flag byte (r0 + l); the wave then walks the flagged rows
+// of its group (ballot), each row as `width` floats spread over the 64 lanes (float4 when the
+// row is 16-B aligned).
+template <bool VEC>
+__device__ __forceinline__ void zero_row(float* __restrict__ row, int64_t width, int lane) {
+  if (VEC) {
+    adam_f4* r4 = reinterpret_cast<adam_f4*>(row);
+    for (int64_t c = lane; c < width / 4; c += 64) r4[c] = adam_f4{0.f, 0.f, 0.f, 0.f};
+  } else {
+    for (int64_t c = lane; c < width; c += 64) row[c] = 0.f;
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void zero_rows_kernel(float* __restrict__ g, int64_t width,
+                                                        int64_t nrows, uint8_t* __restrict__ flags) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (r0 >= nrows) return;
+  const int64_t r = r0 + lane;
+  const uint8_t f = r < nrows ? flags[r] : 0;
+  uint64_t todo = __ballot((f & ROW_CUR) != 0);
+  while (todo) {
+    const int l = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    zero_row<VEC>(g + (r0 + l) * width, width, lane);
+  }
+  if (f & ROW_CUR) flags[r] = f & ~ROW_CUR;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void adam_rows_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        int64_t width, int64_t nrows,
+                                                        uint8_t* __restrict__ flags, float b1, float b2,
+                                                        float eps, float step_size, float sbc2,
+                                                        float gs) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (r0 >= nrows) return;
+  const int64_t r = r0 + lane;
+  const uint8_t f = r < nrows ? flags[r] : 0;
+  uint64_t todo = __ballot(f != 0);
+  const uint64_t cur = __ballot((f & ROW_CUR) != 0);
+  while (todo) {
+    const int l = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    const int64_t o = (r0 + l) * width;
+    const bool has_g = (cur >> l) & 1;
+    if (VEC) {
+      adam_f4* P = reinterpret_cast<adam_f4*>(p + o);
+      const adam_f4* G = reinterpret_cast<const adam_f4*>(g + o);
+      adam_f4* M = reinterpret_cast<adam_f4*>(m + o);
+      adam_f4* V = reinterpret_cast<adam_f4*>(v + o);
+      for (int64_t c = lane; c < width / 4; c += 64) {
+        adam_f4 pp = P[c], mm = M[c], vv = V[c];
+        const adam_f4 gg = has_g ? G[c] : adam_f4{0.f, 0.f, 0.f, 0.f};
+        adam4(pp, gg, mm, vv, b1, b2, eps, step_size, sbc2, gs);
+        P[c] = pp; M[c] = mm; V[c] = vv;
+      }
+    } else {
+      for (int64_t c = lane; c < width; c += 64) {
+        const float gx = has_g ? g[o + c] * gs : 0.f;
+        float mm = m[o + c], vv = v[o + c];
+        mm = mm + (1.f - b1) * (gx - mm);
+        vv = b2 * vv + (1.f - b2) * gx * gx;
+        const float den = sqrtf(vv) / sbc2 + eps;
+        m[o + c] = mm; v[o + c] = vv;
+        p[o + c] = p[o + c] - step_size * (mm / den);
+      }
+    }
+  }
+  if (f & ROW_CUR) flags[r] = f | ROW_EVER;
+}
 }  // namespace savqa
 
 using namespace savqa;
@@ -628,6 +720,48 @@ extern "C" int savqa_adam(void* stream, float* p, const float* g, float* m, floa
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr,
                      beta1, beta2, eps, step_size, sbc2, grad_scale);
   return check_launch("savqa_adam");
+}
+
+static unsigned rows_grid(int64_t nrows) { return (unsigned)((nrows + 255) / 256); }
+
+extern "C" int savqa_mark_rows(void* stream, const int64_t* ids, int64_t n, int64_t nrows,
+                               uint8_t* flags) {
+  if (n <= 0) return 0;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(mark_rows_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), ids, n, nrows,
+                     flags);
+  return check_launch("savqa_mark_rows");
+}
+
+extern "C" int savqa_zero_rows(void* stream, float* g, int64_t width, int64_t nrows, uint8_t* flags) {
+  if (nrows <= 0) return 0;
+  if (width % 4 == 0 && (((uintptr_t)g) & 15) == 0)
+    hipLaunchKernelGGL(zero_rows_kernel<true>, dim3(rows_grid(nrows)), dim3(256), 0,
+                       as_stream(stream), g, width, nrows, flags);
+  else
+    hipLaunchKernelGGL(zero_rows_kernel<false>, dim3(rows_grid(nrows)), dim3(256), 0,
+                       as_stream(stream), g, width, nrows, flags);
+  return check_launch("savqa_zero_rows");
+}
+
+extern "C" int savqa_adam_rows(void* stream, float* p, const float* g, float* m, float* v,
+                               int64_t width, int64_t nrows, uint8_t* flags, float lr,
+                               float beta1, float beta2, float eps, float bc1, float bc2,
+                               float grad_scale) {
+  if (nrows <= 0) return 0;
+  const float step_size = lr / bc1, sbc2 = sqrtf(bc2);
+  const bool vec = width % 4 == 0 && ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) |
+                                        ((uintptr_t)v)) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(adam_rows_kernel<true>, dim3(rows_grid(nrows)), dim3(256), 0,
+                       as_stream(stream), p, g, m, v, width, nrows, flags, beta1, beta2, eps,
+                       step_size, sbc2, grad_scale);
+  else
+    hipLaunchKernelGGL(adam_rows_kernel<false>, dim3(rows_grid(nrows)), dim3(256), 0,
+                       as_stream(stream), p, g, m, v, width, nrows, flags, beta1, beta2, eps,
+                       step_size, sbc2, grad_scale);
+  return check_launch("savqa_adam_rows");
 }
 
 extern "C" int savqa_rowscale_mask(void* stream, const float* in, const float* rowscale,

@@ -57,19 +57,23 @@ class GradReducer:
     optimizer can update each bucket as soon as ITS all-reduce lands (Adam of the early
     buckets overlaps the all-reduce of the last ones)."""
 
-    def __init__(self, arena, bucket_mb: float = 64.0, group=None, filler: int = 400000):
+    def __init__(self, arena, bucket_mb: float = 64.0, group=None, filler: int = 400000,
+                 force: bool = False):
         self.arena = arena
         self.group = group
         # padding row of the static-cap set_rows lists (any row of every sparse table; the
         # default is the PAD token's row, AttModel_x3.py:13)
         self.filler = int(filler)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # active: the exchange runs (world > 1; `force` runs every collective at world 1 too --
+        # the single-GPU RCCL test of the streamed path)
+        self.active = self.world > 1 or bool(force)
         # host-side metadata exchange (the per-rank id counts of set_rows without a static
         # cap): a gloo group on CPU tensors, so agreeing on a size never synchronises a GPU
         # stream. Created here, where every rank constructs its reducer (new_group is
         # collective).
         self.meta = None
-        if self.world > 1:
+        if self.active:
             self.meta = group if dist.get_backend(group) == "gloo" else dist.new_group(
                 ranks=None if group is None else dist.get_process_group_ranks(group),
                 backend="gloo")
@@ -79,6 +83,7 @@ class GradReducer:
         self.sparse: List = []      # [(lo, hi, width)] arena ranges exchanged by rows
         self._ids = None            # (all_gather work, [world] id tensors) of this step
         self._rows = None           # (sorted ids, first-occurrence mask, source position)
+        self._rows_done = set()     # arena offsets of the tables exchanged by rows this step
         self.rows_exchanged = 0     # tables exchanged by rows in the current step
 
     def add_sparse_table(self, lo: int, hi: int, width: int):
@@ -88,7 +93,13 @@ class GradReducer:
         self.sparse.append((int(lo), int(hi), int(width)))
         self.sparse.sort()
 
+    def rows_tracked(self, offset: int) -> bool:
+        """Whether the table starting at arena `offset` is exchanged by rows (its touched-row
+        flags then get the union of every rank's ids, so Adam may update it row by row)."""
+        return self.active and offset in self._rows_done
+
     def begin(self):
+        self._rows_done = set()
         self.works = []
         self.pending = {}
         self._ids = None
@@ -108,7 +119,7 @@ class GradReducer:
             but one host rendezvous of the ranks per call) and the lists padded to the largest.
         Duplicates are exchanged once. Several calls before the backward (e.g. several
         forwards) accumulate: the union of their rows is exchanged."""
-        if self.world <= 1 or not self.sparse:
+        if not self.active or not self.sparse:
             return
         ids = ids.reshape(-1).to(torch.int64).contiguous()
         n = ids.numel()
@@ -180,6 +191,10 @@ class GradReducer:
             return
         ids, first, src = self._rows
         table = self.arena.grad[t0:t1].view(-1, width)
+        mark = getattr(self.arena, "mark_table_rows", None)
+        if mark is not None:  # rows other ranks touched get a gradient here too
+            mark(t0, ids)
+        self._rows_done.add(t0)
         buf = table.index_select(0, ids)
         buf.mul_(first.unsqueeze(1).to(buf.dtype))
         w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
@@ -187,7 +202,7 @@ class GradReducer:
         self.rows_exchanged += 1
 
     def reduce_range(self, start: int, end: int, flush: bool = False):
-        if self.world <= 1:
+        if not self.active:
             return
         end = min(int(end), self.arena.grad.numel())
         start = int(start)
@@ -216,7 +231,7 @@ class GradReducer:
 
     def drain(self):
         """Issue what is pending; return ([(work, lo, hi)...] in issue order, 1/world)."""
-        if self.world <= 1:
+        if not self.active:
             return [], 1.0
         self._flush_all()
         works, self.works = self.works, []

@@ -62,6 +62,7 @@ class StackWeights:
 
     def __init__(self, arena, pre: str, num_blocks: int, d: int, grad: bool = False, buf=None):
         v, sp = _views(arena, grad, buf)
+        self.arena, self.table = arena, f"{pre}.syb_emb.weight"
         self.E = v(f"{pre}.syb_emb.weight")
         self.Wq, self.bq = v(f"{pre}.syb_mlp.0.weight"), v(f"{pre}.syb_mlp.0.bias")
         self.Win, self.bin = v(f"{pre}.syb_mlp2.weight"), v(f"{pre}.syb_mlp2.bias")
@@ -100,6 +101,7 @@ class MilWeights:
     def __init__(self, arena, grad=False, buf=None):
         v, _ = _views(arena, grad, buf)
         m = "MIL_NCE"
+        self.arena, self.table = arena, f"{m}.syb_emb.weight"
         live = f"{m}.R" in arena.live_names
         self.R = v(f"{m}.R") if (live or (not grad and buf is None)) else None  # relations only
         self.E = v(f"{m}.syb_emb.weight")
@@ -140,6 +142,7 @@ class StackSaved:
     sites: tuple = (-1, 4, 5)
     lp: object = None
     x6b: torch.Tensor = None
+    kv32: torch.Tensor = None      # fp32 copy of a bf16 kv for the key-tiled attention (T > 128)
 
 
 # dropout sites (site ids of the library's counter-hash masks, include/savqa.h)
@@ -216,8 +219,18 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
             Lb = lp.W.enc[i]
             qkv = _bf(M, 3 * d, dev=dev)
             ops.linear_lp(xb, Lb["Wqkv"], L["bqkv"], None, qkv, relu=True)
-            ops.gattn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag, flag, B,
-                          T, T, H, o, d)
+            if ops.use_flash(T, T):
+                # the key-tiled kernels read fp32 Q/K/V: widen the bf16 projections (exact) and
+                # keep the fp32 copy for the backward
+                qkv32 = _empty(M, 3 * d, dev=dev)
+                ops.widen_bf16(qkv, M, 3 * d, 3 * d, qkv32, 3 * d)
+                ast = _empty(B * H * T * 4, dev=dev)
+                ops.gattn_fwd_flash(qkv32, 3 * d, qkv32[:, d:], 3 * d, qkv32[:, 2 * d:], 3 * d, G,
+                                    flag, flag, B, T, T, H, o, d, ast)
+                e.update(ast=ast, qkv32=qkv32)
+            else:
+                ops.gattn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag, flag,
+                              B, T, T, H, o, d)
         else:
             qkv = _empty(M, 3 * d, dev=dev)
             ops.linear(x, L["Wqkv"], L["bqkv"], qkv, relu=True)
@@ -255,6 +268,9 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
     if lp is not None:
         s.kv = _bf(M, 2 * nb * d, dev=dev)
         ops.linear_lp(xb, lp.W.Wkv, W.bkv, None, s.kv, relu=True)
+        if ops.use_flash(1, T):  # fp32 K/V for the key-tiled decoder cross-attention
+            s.kv32 = _empty(M, 2 * nb * d, dev=dev)
+            ops.widen_bf16(s.kv, M, 2 * nb * d, 2 * nb * d, s.kv32, 2 * nb * d)
     else:
         s.kv = _empty(M, 2 * nb * d, dev=dev)
         ops.linear(x, W.Wkv, W.bkv, s.kv, relu=True)
@@ -274,7 +290,9 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
         ops.linear(d1, L["Wqc"], L["bqc"], qc, relu=True)
         oc = _empty(B, d, dev=dev)
         kvi = s.kv[:, 2 * i * d:]
-        if lp is None and ops.use_flash(1, T):
+        if ops.use_flash(1, T):
+            if s.kv32 is not None:
+                kvi = s.kv32[:, 2 * i * d:]
             ast = _empty(B * H * 4, dev=dev)
             ops.gattn_fwd_flash(qc, d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6, f1, B,
                                 1, T, H, oc, d, ast)
@@ -318,6 +336,8 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
     lp = s.lp
     ddec = dout
     dkv = (_bf if lp is not None else _empty)(M, 2 * nb * d, dev=dev)
+    # key-tiled kernels write fp32 dK/dV: into an fp32 buffer, rounded to bf16 after the loop
+    dkv_att = _empty(M, 2 * nb * d, dev=dev) if s.kv32 is not None else dkv
     for i in reversed(range(nb)):
         L, Lg, e = W.dec[i], G.dec[i], s.dec[i]
         # feed-forward
@@ -333,8 +353,10 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         dzc = _empty(B, d, dev=dev)
         ops.ln_bwd(dd2, e["zc"], *e["stc"], L["gc"], dzc, Lg["gc"], Lg["bc"])
         dqc = _empty(B, d, dev=dev)
-        kvi, dkvi = s.kv[:, 2 * i * d:], dkv[:, 2 * i * d:]
+        kvi, dkvi = s.kv[:, 2 * i * d:], dkv_att[:, 2 * i * d:]
         if "ast" in e:
+            if s.kv32 is not None:
+                kvi = s.kv32[:, 2 * i * d:]
             ops.gattn_bwd_flash(e["qc"], d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6,
                                 e["f1"], B, 1, T, H, dzc, d, e["ast"], dqc, d, dkvi,
                                 2 * nb * d, dkvi[:, d:], 2 * nb * d)
@@ -357,6 +379,9 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         mark(f"dec_feed_forward_{i - 1}.normalization.gamma" if i > 0 else "dec_emb.lookup_table")
     ops.dec_init_bwd(ddec, B, d, 2, math.sqrt(d), G.dec_emb, G.dec_pos, drop=s.drop,
                      site=s.sites[2])
+    if dkv_att is not dkv:
+        ops.cast_bf16(dkv_att, M, 2 * nb * d, 2 * nb * d, dkv, 2 * nb * d)
+        del dkv_att
     # all decoder K/V projections at once
     dx = _empty(M, d, dev=dev)
     if lp is not None:
@@ -395,9 +420,14 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         qkv = e["qkv"]
         dqkv = (_bf if lp is not None else _empty)(M, 3 * d, dev=dev)
         if "ast" in e:
-            ops.gattn_bwd_flash(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, Gm, e["flag"],
-                                e["flag"], B, T, T, H, dz1, d, e["ast"], dqkv, 3 * d,
-                                dqkv[:, d:], 3 * d, dqkv[:, 2 * d:], 3 * d)
+            q32 = e.get("qkv32", qkv)
+            dq32 = dqkv if lp is None else _empty(M, 3 * d, dev=dev)
+            ops.gattn_bwd_flash(q32, 3 * d, q32[:, d:], 3 * d, q32[:, 2 * d:], 3 * d, Gm, e["flag"],
+                                e["flag"], B, T, T, H, dz1, d, e["ast"], dq32, 3 * d,
+                                dq32[:, d:], 3 * d, dq32[:, 2 * d:], 3 * d)
+            if dq32 is not dqkv:
+                ops.cast_bf16(dq32, M, 3 * d, 3 * d, dqkv, 3 * d)
+                del dq32
         else:
             ops.gattn_bwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, Gm, e["flag"],
                           e["flag"], B, T, T, H, dz1, d, dqkv, 3 * d, dqkv[:, d:], 3 * d,
@@ -438,6 +468,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
                       mask_arows=True)
     ops.linear_dw(dq, W.E, G.Wq, G.bq, rows=B * Lq, x_rows=s.q_flat)
     ops.linear_dx(dq, W.Wq, G.E, rows=B * Lq, c_rows=s.q_flat, atomic=True)
+    G.arena.mark_rows(G.table, s.q_flat)  # the table's gradient rows of this step
     del dq
     if not want_node_grad:
         return None
@@ -615,6 +646,7 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
         ops.rowscale_mask(drelf, None, rel["relf"], B * Lp, Hm, drelf)  # ReLU of syb_mlp
         ops.linear_dw(drelf, W.E, G.Ws, G.bs, rows=B * Lp, x_rows=rel["pos_rel"])
         ops.linear_dx(drelf, W.Ws, G.E, rows=B * Lp, c_rows=rel["pos_rel"], atomic=True)
+        G.arena.mark_rows(G.table, rel["pos_rel"])
     dvv = torch.empty_like(s.vv)
     n = B * Nv * K
     if s.Eg is not None:
@@ -637,6 +669,9 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
         ops.linear_dw(dNf, W.E, G.Ws, G.bs, rows=n, x_rows=s.neg)
         ops.linear_dx(dPf, W.Ws, G.E, rows=n, c_rows=s.pos, atomic=True)
         ops.linear_dx(dNf, W.Ws, G.E, rows=n, c_rows=s.neg, atomic=True)
+    # the table's gradient rows of this step: the positive / negative object words
+    G.arena.mark_rows(G.table, s.pos)
+    G.arena.mark_rows(G.table, s.neg)
     if lp is not None:
         dvvb = _bf(B * Nv, Hm, dev=dev)
         ops.cast_bf16(dvv, B * Nv, Hm, Hm, dvvb, Hm)

@@ -224,6 +224,11 @@ def cast_bf16(x: Tensor, rows: int, cols: int, ldi: int, out: Tensor, ldo: int, 
          int(group), int(stride), int(offset))
 
 
+def widen_bf16(x: Tensor, rows: int, cols: int, ldi: int, out: Tensor, ldo: int):
+    """out = float(x) over bf16 rows (savqa_widen_bf16)."""
+    call("savqa_widen_bf16", _stream(), _p(x), int(rows), int(cols), int(ldi), _p(out), int(ldo))
+
+
 def quant_fp8(x: Tensor, rows: int, cols: int, ldi: int, q: Tensor, ldq: int, scale: Tensor,
               lds: int, group=0, stride=0, offset=0):
     call("savqa_quant_fp8", _stream(), _p(x), int(rows), int(cols), int(ldi), _p(q), int(ldq),
@@ -541,6 +546,20 @@ def rel_loss_bwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cum, wsm, dwsm, st, d
 
 def axpby(x, y, n, a, b, out):
     call("savqa_axpby", _stream(), _p(x), _p(y), int(n), float(a), float(b), _p(out))
+
+
+def mark_rows(ids, nrows, flags):
+    call("savqa_mark_rows", _stream(), _p(ids), int(ids.numel()), int(nrows), _p(flags))
+
+
+def zero_rows(g, width, nrows, flags):
+    call("savqa_zero_rows", _stream(), _p(g), int(width), int(nrows), _p(flags))
+
+
+def adam_rows(p, g, m, v, width, nrows, flags, lr, beta1, beta2, eps, bc1, bc2, grad_scale=1.0):
+    call("savqa_adam_rows", _stream(), _p(p), _p(g), _p(m), _p(v), int(width), int(nrows),
+         _p(flags), float(lr), float(beta1), float(beta2), float(eps), float(bc1), float(bc2),
+         float(grad_scale))
 
 
 def adam(p, g, m, v, n, lr, beta1, beta2, eps, bc1, bc2, grad_scale=1.0):

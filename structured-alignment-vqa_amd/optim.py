@@ -3,11 +3,14 @@
 One HIP launch updates every live parameter: the arena keeps them contiguous, and the
 gradient all-reduce's 1/world scaling is folded into the same pass (grad_scale).
 Parameters that never receive a gradient (the reference's Adam skips grad=None) lie
-outside the live range and are untouched.
+outside the live range and are untouched. The three 407000 x 300 GloVe tables run row by
+row (savqa_adam_rows): rows never touched have m = v = 0 and no gradient, where
+torch.optim.Adam's update is exactly zero, so they are skipped bit-exactly.
 """
 from __future__ import annotations
 
 import torch
+import torch.distributed as dist
 
 from . import ops
 
@@ -44,16 +47,61 @@ class Adam(torch.optim.Optimizer):
         bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
         ranges = [(None, 0, a.n_live)]
         scale = self.grad_scale
-        if reducer is not None and reducer.world > 1:
+        active = reducer is not None and getattr(reducer, "active", reducer.world > 1)
+        if active:
             works, scale = reducer.drain()
             ranges = works + self._coverage_gaps(reducer, works, a.n_live)
+        rows = self._row_tables(reducer if active else None)
+        lr, eps = grp["lr"], grp["eps"]
         for w, lo, hi in ranges:
             if w is not None:
                 w.wait()   # this stream waits for this bucket's all-reduce only
-            ops.adam(a.flat[lo:hi], g[lo:hi], self.m[lo:hi], self.v[lo:hi], hi - lo, grp["lr"], b1,
-                     b2, grp["eps"], bc1, bc2, scale)
+            for plo, phi in self._dense_pieces(lo, hi, rows):
+                ops.adam(a.flat[plo:phi], g[plo:phi], self.m[plo:phi], self.v[plo:phi], phi - plo,
+                         lr, b1, b2, eps, bc1, bc2, scale)
+        # row-tracked tables last: every bucket covering them has been waited for by now
+        for n in rows:
+            o, shp = a.offsets[n]
+            e = o + shp.numel()
+            ops.adam_rows(a.flat[o:e], g[o:e], self.m[o:e], self.v[o:e], shp[1], shp[0],
+                          a.row_flags[n], lr, b1, b2, eps, bc1, bc2, scale)
+        for n in a.row_flags:
+            if n not in rows:
+                a.mark_all_rows(n)  # updated densely: every row may hold Adam state now
         a.generation += 1  # low-precision weight shadows are stale now
         return loss
+
+    def _row_tables(self, reducer):
+        """Tables whose Adam runs row by row this step. The touched-row flags are
+        set by the engine's backward from the token ids; a table is row-updated only when
+        those flags cover every row whose gradient can be non-zero: on one rank always; with
+        GradReducer only the tables it exchanges by rows (it flags the union of all ranks'
+        ids); under another data-parallel exchange (e.g. torch DDP) none -- the all-reduced
+        gradient has rows other ranks touched."""
+        a = self.arena
+        if not a.row_flags:
+            return ()
+        if reducer is not None:
+            return tuple(n for n in a.row_flags if reducer.rows_tracked(a.offsets[n][0]))
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return ()
+        return tuple(a.row_flags)
+
+    def _dense_pieces(self, lo, hi, rows):
+        """[lo, hi) minus the row-tracked tables."""
+        a = self.arena
+        out = []
+        for n in sorted(rows, key=lambda n: a.offsets[n][0]):
+            o, shp = a.offsets[n]
+            e = o + shp.numel()
+            if e <= lo or o >= hi:
+                continue
+            if o > lo:
+                out.append((lo, o))
+            lo = e
+        if hi > lo:
+            out.append((lo, hi))
+        return out
 
     @staticmethod
     def _coverage_gaps(reducer, works, n_live):
@@ -76,5 +124,6 @@ class Adam(torch.optim.Optimizer):
         return extra
 
     def zero_grad(self, set_to_none: bool = False):
-        # keep the arena views attached; zero the live gradient range in one memset
+        # keep the arena views attached; zero the live gradient range (the row-tracked tables:
+        # only the rows touched since the last zero)
         self.arena.zero_grad()

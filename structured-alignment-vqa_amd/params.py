@@ -24,6 +24,10 @@ import torch.nn as nn
 
 ALIGN = 64
 
+# The 407000 x 300 GloVe tables (AttModel_x3.py:36-41, :168-171, :295): only the rows of the
+# step's token ids receive gradient, so their zero-fill and Adam run row by row.
+ROW_TABLES = ("att_vis_grid.syb_emb.weight", "att_syb.syb_emb.weight", "MIL_NCE.syb_emb.weight")
+
 
 def _live_order(num_blocks: int, only_obj: bool = True) -> List[str]:
     """Live parameter names in backward-completion order (see module docstring). With the
@@ -99,6 +103,10 @@ class ParamArena:
         self.flat = flat
         self.grad = None  # allocated on first backward (device of flat)
         self.generation = 0  # bumped by every optimizer update (raw-pointer writes)
+        # row tracking of the GloVe tables (savqa_mark_rows / savqa_zero_rows / savqa_adam_rows):
+        # name -> uint8 flag per row (bit 0: has Adam state, bit 1: touched since the last zero)
+        self.row_tracking = True
+        self.row_flags: Dict[str, torch.Tensor] = {}
         if flat.device.type == "meta":  # layout-only arena (host-side tests)
             return
         with torch.no_grad():
@@ -139,6 +147,7 @@ class ParamArena:
         self.flat = new
         if self.grad is not None and self.grad.device != new.device:
             self.grad = None
+            self.row_flags = {}  # recreated with the gradient (optimizer state restarts too)
         self._bind()
         for n in self.live_names:
             self.params[n].grad = None
@@ -160,7 +169,43 @@ class ParamArena:
             self.grad.zero_()
             for n in self.live_names:
                 self.params[n].grad = self.view(n, self.grad)
+            self._clear_touched()
+        if self.row_tracking and not self.row_flags:
+            for n in ROW_TABLES:
+                if n in self.offsets and n in set(self.live_names):
+                    self.row_flags[n] = torch.zeros(self.offsets[n][1][0], dtype=torch.uint8,
+                                                    device=self.flat.device)
         return self.grad
+
+    # ------------------------------------------------------------------ row tracking
+    def table_width(self, name: str) -> int:
+        return int(self.offsets[name][1][1])
+
+    def mark_rows(self, name: str, ids: torch.Tensor):
+        """Flag the rows `ids` of table `name` as touched this step (gradient rows written)."""
+        f = self.row_flags.get(name)
+        if f is not None:
+            from . import ops
+            ops.mark_rows(ids, f.numel(), f)
+
+    def mark_table_rows(self, offset: int, ids: torch.Tensor):
+        """mark_rows for the table that starts at arena offset `offset` (ddp's row exchange)."""
+        for n, f in self.row_flags.items():
+            if self.offsets[n][0] == offset:
+                self.mark_rows(n, ids)
+
+    def mark_all_rows(self, name: str):
+        """Every row of `name` has (or may have) Adam state: after a dense update."""
+        f = self.row_flags.get(name)
+        if f is not None:
+            f.fill_(1)
+
+    def _clear_touched(self):
+        # the whole gradient was just zeroed densely: clear the touched bits with it
+        from . import ops
+        for n, f in self.row_flags.items():
+            o, shp = self.offsets[n]
+            ops.zero_rows(self.grad[o:o + shp.numel()], shp[1], shp[0], f)
 
     def gview(self, name: str) -> torch.Tensor:
         return self.view(name, self.grad)
@@ -169,8 +214,20 @@ class ParamArena:
         return self.span(first, last, shape, self.grad)
 
     def zero_grad(self):
-        if self.grad is not None:
-            self.grad.zero_()
+        """Zero the live gradient range: one memset per dense span, and only the rows touched
+        since the last zero in the row-tracked tables."""
+        if self.grad is None:
+            return
+        from . import ops
+        lo = 0
+        for n, f in sorted(self.row_flags.items(), key=lambda kv: self.offsets[kv[0]][0]):
+            o, shp = self.offsets[n]
+            if o > lo:
+                self.grad[lo:o].zero_()
+            ops.zero_rows(self.grad[o:o + shp.numel()], shp[1], shp[0], f)
+            lo = o + shp.numel()
+        if lo < self.grad.numel():
+            self.grad[lo:].zero_()
 
     def state_key(self):
         """Changes whenever parameter values may have changed: torch in-place edits of the flat

@@ -1,8 +1,13 @@
-"""The engine's streamed gradient declarations (per layer, per backward phase) tile the
-live range of the arena, and the per-bucket Adam (opt.step(reducer=...)) equals one
-Adam launch over the whole range -- on one GPU, with a recording stand-in for the
-all-reduce (world=2 semantics without a second rank; RCCL itself is exercised by
-bench.py --gpus N and the gloo tests)."""
+"""Data-parallel training on one GPU:
+  * the engine's streamed gradient declarations (per layer, per backward phase) tile the live
+    range of the arena, and the per-bucket Adam (opt.step(reducer=...)) equals one Adam launch
+    over the whole range (a recording stand-in for the all-reduce);
+  * RCCL itself: a 1-rank "nccl" process group with GradReducer(force=True) issues every
+    collective of the streamed path (bucket all-reduces from the side streams, the row-sparse
+    table exchange, per-bucket Adam) on the GPU;
+  * 1 rank on B == 2 ranks (gloo, same GPU) on B/2 through GradReducer, and through torch's own
+    DistributedDataParallel(find_unused_parameters=True) + torch.optim.Adam as main:203/:206
+    wrap the model."""
 import pytest
 import torch
 
@@ -34,7 +39,7 @@ def test_streamed_ranges_tile_live_range_and_bucketed_adam_matches():
 
     class Recorder(GradReducer):
         def __init__(self, arena):
-            self.arena, self.group, self.world = arena, None, 2
+            self.arena, self.group, self.world, self.active = arena, None, 2, True
             self.bucket = 1 << 18
             self.works, self.pending, self.log = [], {}, []
             self.sparse, self._ids, self._rows = [], None, None
@@ -177,10 +182,14 @@ def _digest(arena, t):
     return out
 
 
-def _equiv_run(world, rank, steps=2, sparse=True):
-    """`steps` full training steps (forward, loss, backward, streamed GradReducer, per-bucket
-    Adam) on this rank's contiguous shard of the 8-sample batch; returns per step the
-    gradient Adam consumed (summed / world) and the parameters after the step."""
+def _equiv_run(world, rank, steps=2, sparse=True, mode="reducer"):
+    """`steps` full training steps on this rank's contiguous shard of the 8-sample batch;
+    returns per step the gradient the optimizer consumed (averaged over ranks) and the
+    parameters after the step.
+      mode "reducer": forward, loss, backward, streamed GradReducer, per-bucket savqa Adam;
+      mode "ddp": the reference's own wrapping (main:203/:206/:363-366) --
+        DistributedDataParallel(model, find_unused_parameters=True), torch.optim.Adam over
+        model.parameters(), loss.backward(), optimizer.step()."""
     from savqa_amd.data import model_args
     from savqa_amd.ddp import GradReducer
     from savqa_amd.loss import smoothed_loss
@@ -190,37 +199,50 @@ def _equiv_run(world, rank, steps=2, sparse=True):
     n = 8 // world
     batch = {k: v[rank * n:(rank + 1) * n] for k, v in full.items()}
     red = None
-    if world > 1:
-        red = GradReducer(m._arena, bucket_mb=1.0)
-        m.attach_reducer(red)      # multi_rank: the gated enc4 backward schedule is on
-        assert m._engine.vis_gate() is not None
-        if not sparse:
-            red.sparse = []
-    opt = Adam(m, lr=1e-4)
+    net = m
+    if mode == "ddp":
+        net = torch.nn.parallel.DistributedDataParallel(m, find_unused_parameters=True)
+        opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    else:
+        if world > 1:
+            red = GradReducer(m._arena, bucket_mb=1.0)
+            m.attach_reducer(red)      # multi_rank: the gated enc4 backward schedule is on
+            assert m._engine.vis_gate() is not None
+            if not sparse:
+                red.sparse = []
+        opt = Adam(m, lr=1e-4)
     a = m._arena
     rec = []
     for _ in range(steps):
         if red:
             red.begin()
-        lc, lv, ls, mil, _ = m(*model_args(batch), decMask=True, mcb=False)
+        lc, lv, ls, mil, _ = net(*model_args(batch), decMask=True, mcb=False)
         loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil)
         opt.zero_grad()
         loss.backward()
-        opt.step(reducer=red)
+        if mode == "ddp":
+            opt.step()
+            scale = 1          # DDP averaged the gradients in place
+        else:
+            opt.step(reducer=red)
+            scale = world      # the reducer sums; Adam folds in 1/world
         torch.cuda.synchronize()
-        g = a.grad[:a.n_live] / world
+        g = a.grad[:a.n_live] / scale
         rec.append((_digest(a, g), _digest(a, a.flat[:a.n_live])))
     return rec
 
 
-def _equiv_worker(rank, world, port, q):
+def _equiv_worker(rank, world, port, q, mode="reducer"):
     import os
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = {s: _equiv_run(world, rank, sparse=s) for s in (True, False)}
+        if mode == "ddp":
+            res = {True: _equiv_run(world, rank, mode="ddp")}
+        else:
+            res = {s: _equiv_run(world, rank, sparse=s) for s in (True, False)}
         q.put((rank, _to_numpy(res), None))   # by value: the parent reads after we exit
     except Exception:
         import traceback
@@ -258,7 +280,8 @@ def _cmp(a, b):
     return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
 
 
-def test_two_ranks_on_half_batches_equal_one_rank_on_the_batch():
+@pytest.mark.parametrize("mode", ["reducer", "ddp"])
+def test_two_ranks_on_half_batches_equal_one_rank_on_the_batch(mode):
     """SURVEY 4 / main:203,363 (DistributedDataParallel): the same global batch gives the same
     update on 1 rank and on 2 ranks with B/2 each -- 2 training steps through the full path
     (forward, loss, backward with the gated enc4 schedule, streamed bucketed all-reduce,
@@ -268,7 +291,11 @@ def test_two_ranks_on_half_batches_equal_one_rank_on_the_batch():
     2-step updates to 1e-3 (Adam divides by sqrt(v), so near-zero gradient entries amplify
     rounding; the key-projection biases have an exactly-zero true gradient -- softmax shift
     invariance -- and their Adam update is rounding noise in every implementation, so they
-    are left out)."""
+    are left out).
+    mode "ddp": the same with the model wrapped exactly as the reference wraps it --
+    DistributedDataParallel(model, find_unused_parameters=True) and torch.optim.Adam
+    (main:203/:206) -- instead of GradReducer + the fused Adam: the gradients reach DDP's
+    hooks through the Parameters' AccumulateGrad nodes and DDP averages the arena in place."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import socket
@@ -280,7 +307,7 @@ def test_two_ranks_on_half_batches_equal_one_rank_on_the_batch():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_equiv_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_equiv_worker, args=(r, 2, port, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -295,7 +322,7 @@ def test_two_ranks_on_half_batches_equal_one_rank_on_the_batch():
         assert res[r][1] is None, res[r][1]
     for p in procs:
         assert p.exitcode == 0
-    for sparse in (True, False):
+    for sparse in ((True, False) if mode == "reducer" else (True,)):
         r0, r1 = res[0][0][sparse], res[1][0][sparse]
         worst_g, worst_u = [], []
         for step in range(2):
@@ -341,3 +368,93 @@ def _init_params():
             if shp.numel() <= (1 << 22):
                 _INIT[n] = a.flat[o:o + shp.numel()].view(shp).cpu().clone()
     return _INIT
+
+
+# ---------------------------------------------------------------- RCCL, one rank
+def _rccl_worker(port, q):
+    """One process, one GPU, a 1-rank "nccl" (RCCL) group: 2 training steps through the
+    streamed exchange forced on at world 1 (GradReducer(force=True): bucketed async
+    all-reduces issued from the two stacks' backward streams, the row-sparse stack tables
+    with the static-cap id list, per-bucket Adam waiting on each bucket's work) against the
+    same 2 steps with no reducer. At world 1 every collective is an identity, so the updates
+    must agree to fp32 rounding (the split-K weight gradients add in nondeterministic atomic
+    order, so the two runs are not bit-identical by construction)."""
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        from savqa_amd.data import model_args
+        from savqa_amd.ddp import GradReducer
+        from savqa_amd.loss import smoothed_loss
+        from savqa_amd.optim import Adam
+        out = {}
+        for forced in (False, True):
+            m = _equiv_model()
+            batch = _equiv_batch()
+            red = None
+            if forced:
+                red = GradReducer(m._arena, bucket_mb=1.0, force=True)
+                assert dist.get_backend() == "nccl" and red.world == 1 and red.active
+                m.attach_reducer(red, batch_size=8)
+                assert m._engine.vis_gate() is not None   # the gated multi-rank schedule
+            opt = Adam(m, lr=1e-4)
+            a = m._arena
+            rec, nworks = [], []
+            init = a.flat[:a.n_live].cpu().clone()
+            for _ in range(2):
+                if red:
+                    red.begin()
+                lc, lv, ls, mil, _ = m(*model_args(batch), decMask=True, mcb=False)
+                loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil)
+                opt.zero_grad()
+                loss.backward()
+                if red:
+                    nworks.append((len(red.works) + len(red.pending), red.rows_exchanged))
+                opt.step(reducer=red)
+                torch.cuda.synchronize()
+                rec.append((a.grad[:a.n_live].cpu().clone(), a.flat[:a.n_live].cpu().clone()))
+            out[forced] = (rec, nworks, init)
+        q.put((_to_numpy(out), None))
+    except Exception:
+        import traceback
+        q.put((None, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_rccl_single_rank_streamed_exchange_matches_local():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(port, q))
+    p.start()
+    try:
+        out, exc = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert exc is None, exc
+    assert p.exitcode == 0
+    out = _to_torch(out)
+    (loc, _, init), (frc, nworks, _) = out[False], out[True]
+    for works, rows in nworks:
+        assert works > 8 and rows == 2, nworks     # streamed buckets + both tables by rows
+    for step in range(2):
+        (g0, w0), (g1, w1) = loc[step], frc[step]
+        assert float((g1 - g0).norm() / g0.norm()) < 1e-5, step
+        start = init if step == 0 else loc[step - 1][1]
+        du, dr = w1 - start, w0 - start
+        # Adam's update normalises each entry: compare the update vectors
+        assert float((du - dr).norm() / dr.norm()) < 1e-3, step

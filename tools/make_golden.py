@@ -159,13 +159,14 @@ def full_model_cases(modules_mod, att_mod):
 # super-node graph of T_syb = 14 + 3 + 14*13 + 12 = 211 > 128 positions, so the key-tiled
 # attention (csrc/attn_flash.hip) runs inside the semantic stack of the parity case.
 # full_rel_big is the reference's own relation configuration (submit.py:87 maxlen 1600,
-# :101 hidden_size_mil 64) at the benched super-node size: 36 objects -> T_syb = 36 + 3 +
+# :101 hidden_size_mil 64) at the benched super-node size: B = 2 (the reference squeezes a
+# B = 1 batch away at AttModel_x3.py:540), 36 objects -> T_syb = 36 + 3 +
 # 36*35 + 14 = 1313 positions, 311 relation categories, up to 8 listed relations per object
 # pair (~5.7k positive entries), 6 encoder/decoder blocks (the reference hard-codes 6 in its
 # forwards, AttModel_x3.py:127-139; its per-entry Python loop :421-436 dominates the CPU time).
 RELATION_RUNS = {"full_rel_b2": ([5, 4], [7, 5], {}),
                  "full_rel_sn": ([14, 11], [12, 9], {}),
-                 "full_rel_big": ([36], [14], dict(hidden_mil=64, num_blocks=6, nrel=311,
+                 "full_rel_big": ([36, 9], [14, 10], dict(hidden_mil=64, num_blocks=6, nrel=311,
                                                    max_rel_per_pair=8, maxlen=1600))}
 
 
