@@ -101,11 +101,11 @@ def param_value(name: str, shape) -> np.ndarray:
 class HashParams(dict):
     """Lazy name -> fp32 torch tensor map of hash-filled reference parameters."""
 
-    def __init__(self, requires_grad=False, num_relations=4):
+    def __init__(self, requires_grad=False, num_relations=4, **geometry):
         super().__init__()
         self.requires_grad = requires_grad
         from .savqa_oracle import model_param_shapes
-        self.shapes = dict(model_param_shapes(num_relations=num_relations))
+        self.shapes = dict(model_param_shapes(num_relations=num_relations, **geometry))
 
     def __missing__(self, name):
         import torch

@@ -21,6 +21,10 @@
 
 #include <type_traits>
 
+#ifndef SAVQA_ATT_BWD2
+#define SAVQA_ATT_BWD2 1
+#endif
+
 namespace savqa {
 
 // ---------------------------------------------------------------------------------------
@@ -414,6 +418,190 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgsT<T> a) {
   }
 }
 
+// fp32 backward, second structure (SAVQA_ATT_BWD2; the bf16 twin gattn_bwd_mfma_bf2_kernel
+// below explains the restructuring): dQ = dS K in phase 1 from the wave's own dS^T columns and
+// the staged K, then dV^T = dO^T P and dK^T = Q^T dS as 16x16 tiles whose B operand is one b128
+// read of a P^T / dS^T row and whose 4 outputs per lane are one 16-B store. LDS: K stays
+// staged through the kernel (dQ's B operand, dK's ReLU mask); P^T takes V's place once every
+// wave has its dP; dS^T has its own region: 75 KB at T = 73 (2 workgroups per CU, as before).
+template <int NJT, typename T>
+__global__ __launch_bounds__(512) void gattn_bwd_mfma2_kernel(AttnArgsT<T> a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bh / a.H, h = bh % a.H;
+  const int nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = w * 16;
+  constexpr int TK = NJT * 16;
+  const int PLD = 16 * nw + 4;
+  const int VREG = TK * ATT_KLD > TK * PLD ? TK * ATT_KLD : TK * PLD;
+  float* Ks = sm;                   // [TK][ATT_KLD] K_h (whole kernel)
+  float* Vs = sm + TK * ATT_KLD;    // [TK][ATT_KLD] V_h (phase 1a), then
+  float* Pt = Vs;                   // [TK][PLD]     P^T
+  float* dSt = Vs + VREG;           // [TK][PLD]     dS^T (scaled by 1/8, masked)
+  const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
+  const int hd = h * ATT_DK;
+  {
+    f4v qa[4], oa[4];
+    const int iq = min(i0 + col, a.Tq - 1);
+    const T* qr = a.q + (qb + iq) * a.ldq + hd + 4 * g;
+    const float* orr = a.dout + (qb + iq) * a.lddo + hd + 4 * g;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      qa[c] = ldx4(qr + 16 * c);
+      oa[c] = ld4(orr + 16 * c);
+    }
+    float gp[4][NJT];
+    preload_graph<NJT>(a, b, i0, g, col, gp);
+    float kf[NJT];
+#pragma unroll
+    for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[kb + min(jt * 16 + col, a.Tk - 1)];
+    stage_kv_tiles<TK>(a, b, h, Ks, Vs);
+    __syncthreads();  // K/V staged
+    f4v s[NJT], dp[NJT];
+    strip_dots_lds<NJT>(qa, Ks, col, g, s);
+    strip_dots_lds<NJT>(oa, Vs, col, g, dp);
+    __syncthreads();  // every wave is done with V: its region becomes P^T
+    f4v pv[NJT], dsv[NJT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * g + r;
+      const int ic = min(i, a.Tq - 1);
+      float aa[NJT], gg[NJT], bm[NJT];
+      const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
+      const float sden = fmaxf(nrm, 1e-12f);
+      const float rsd = 1.f / sden;
+      const float qf = a.qflag[qb + ic];
+      float dn[NJT], t1 = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        dn[jt] = dp[jt][r] * qf;
+        t1 += dn[jt] * bm[jt];
+      }
+      t1 = row16_sum(t1);
+      const float dnrm = nrm >= 1e-12f ? -t1 * (rsd * rsd) : 0.f;
+      float da[NJT], t2 = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        const float sg = bm[jt] > 0.f ? 1.f : (bm[jt] < 0.f ? -1.f : 0.f);
+        const float dbm = dn[jt] * rsd + dnrm * sg;
+        da[jt] = dbm * gg[jt];
+        t2 += da[jt] * aa[jt];
+      }
+      t2 = row16_sum(t2);
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        const int j = jt * 16 + col;
+        const bool ok = i < a.Tq && j < a.Tk;
+        float ds = aa[jt] * (da[jt] - t2);
+        if (kf[jt] == 0.f) ds = 0.f;
+        dsv[jt][r] = ok ? ds * 0.125f : 0.f;
+        pv[jt][r] = ok ? bm[jt] * rsd * qf : 0.f;
+      }
+    }
+#pragma unroll
+    for (int jt = 0; jt < NJT; ++jt) {
+      *reinterpret_cast<f4v*>(&Pt[(jt * 16 + col) * PLD + i0 + 4 * g]) = pv[jt];
+      *reinterpret_cast<f4v*>(&dSt[(jt * 16 + col) * PLD + i0 + 4 * g]) = dsv[jt];
+    }
+  }
+  {
+    // dQ ReLU masks (rows i0 + 4g + r, columns 16 dt + col), under the dQ products
+    float qm[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const T* qrow = a.q + (qb + min(i0 + 4 * g + r, a.Tq - 1)) * a.ldq + hd + col;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) qm[r][dt] = ldx1(qrow + dt * 16);
+    }
+    __builtin_amdgcn_wave_barrier();  // this wave's dS^T columns are written (in-order LDS)
+    // dQ strip = dS K: A[m = i][k = j] = dS^T[j][i0 + i], B[k = j][n = d] = K[j][16 dt + d]
+    f4v dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < NJT; ++kc) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = kc * 16 + 4 * g + t;
+        const float av = dSt[j * PLD + i0 + col];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(av, Ks[j * ATT_KLD + dt * 16 + col], dq[dt]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * g + r;
+      if (i < a.Tq) {
+        T* drow = a.dq + (qb + i) * a.lddq + hd + col;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) stx1(drow + dt * 16, qm[r][dt] > 0.f ? dq[dt][r] : 0.f);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: dV^T = dO^T P, dK^T = Q^T dS (item = grp * NJT + jt, grp < 4 dV, >= 4 dK);
+  //   A[m = d][k = i] = X[i][16 dt + d] (preloaded per group), B[k = i][n = j] = Y^T[j][i]
+  //   (one b128 per 16 queries: lane group g feeds k = 16 kc + 4g + t at MFMA step t),
+  //   D[m = 4g + r][n = col] = out[j = 16 jt + col][d = 16 dt + 4g + r]: one 16-B store
+  const int nitems = 8 * NJT;
+  const int it0 = nitems * w / nw, it1 = nitems * (w + 1) / nw;
+  constexpr int MAXG = 3;
+  const int g0 = it0 / NJT;
+  float acol[MAXG][NJT][4];  // (query tiles: nw == NJT, host check)
+#pragma unroll
+  for (int u = 0; u < MAXG; ++u) {
+    const int grp = g0 + u;
+    if (grp * NJT < it1 && grp < 8) {  // wave-uniform
+      const int dcol = hd + (grp & 3) * 16 + col;
+#pragma unroll
+      for (int kc = 0; kc < NJT; ++kc)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int64_t row = qb + min(kc * 16 + 4 * g + t, a.Tq - 1);
+          acol[u][kc][t] = grp < 4 ? a.dout[row * a.lddo + dcol] : ldx1(a.q + row * a.ldq + dcol);
+        }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < MAXG; ++u) {
+    const int grp = g0 + u;
+    const int lo = max(it0, grp * NJT), hi = min(it1, (grp + 1) * NJT);
+    if (grp >= 8 || lo >= hi) continue;  // wave-uniform
+    const bool isv = grp < 4;
+    const int dt = grp & 3;
+    const float* Yt = isv ? Pt : dSt;
+    T* dst = isv ? a.dv : a.dk;
+    const int64_t dld = isv ? a.lddv : a.lddk;
+    for (int it = lo; it < hi; ++it) {
+      const int jt = it - grp * NJT;
+      const int j = jt * 16 + col;
+      const int jc = min(j, a.Tk - 1);
+      // ReLU mask: V from global (its LDS image is now P^T), K from its staged image
+      const f4v mk = isv ? ldx4(a.v + (kb + jc) * a.ldv + hd + dt * 16 + 4 * g)
+                         : ld4(Ks + j * ATT_KLD + dt * 16 + 4 * g);
+      f4v acc = {0.f, 0.f, 0.f, 0.f};
+      const float* yrow = Yt + j * PLD + 4 * g;
+#pragma unroll
+      for (int kc = 0; kc < NJT; ++kc) {
+        const f4v yv = ld4(yrow + kc * 16);
+        acc = mfma16(acol[u][kc][0], yv.x, acc);
+        acc = mfma16(acol[u][kc][1], yv.y, acc);
+        acc = mfma16(acol[u][kc][2], yv.z, acc);
+        acc = mfma16(acol[u][kc][3], yv.w, acc);
+      }
+      if (j < a.Tk) {
+        f4v o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = mk[r] > 0.f ? acc[r] : 0.f;
+        stx4(dst + (kb + j) * dld + hd + dt * 16 + 4 * g, o, vec_rows(dst, dld));
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // bf16 MFMA strip kernels (bf16 training modes, cfg 3 / cfg 5). Same workgroup / wave /
 // strip structure and the same fp32 softmax -> graph -> L1 chain (and adjoint) as the fp32
@@ -755,6 +943,194 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf_kernel(AttnArgsT<__bf16
   }
 }
 
+// Backward, second structure (SAVQA_ATT_BWD2): the round-2 kernel above spends its phase 2 on
+// 8 NJT + 4 nw 16x16 tiles per workgroup whose B operands come from global memory per
+// (tensor, column block) and whose 4 mask loads per tile are issued after the previous
+// tile's stores (vmcnt counts stores: each tile waits for a store round trip), writing
+// scalar bf16 elements. Here
+//   * dQ = dS K moves into phase 1: each wave multiplies its own dS strip (read back from the
+//     block dS^T image it just wrote, no barrier needed) by the staged K; the dQ masks
+//     (Q > 0) are loaded before any store;
+//   * phase 2 computes dV and dK TRANSPOSED, dV^T = dO^T P and dK^T = Q^T dS: the B operand is
+//     then a contiguous 4-query run of a P^T / dS^T row (one 8-B LDS read), the ReLU mask a
+//     4-column run of the staged V / K row (8-B LDS read), and each lane's 4 outputs are 4
+//     consecutive d of one key row: one 8-B store instead of four 2-B ones;
+//   * the A operands (dO / Q columns, k = query) of every (tensor, column block) group a wave
+//     touches are loaded at the start of phase 2, before its first store.
+template <int NJT>
+__global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf16> a) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);  // heads of a sample on one XCD
+  const int b = bh / a.H, h = bh % a.H;
+  const int nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = w * 16;
+  constexpr int TK = NJT * 16;
+  const int PLB = 16 * nw + 8;
+  __bf16* Ks = smb;                // [TK][ATT_KLB]
+  __bf16* Vs = smb + TK * ATT_KLB;
+  __bf16* Pt = Vs + TK * ATT_KLB;  // [TK][PLB]  P^T
+  __bf16* dSt = Pt + TK * PLB;     // [TK][PLB]  dS^T (scaled by 1/8, masked)
+  const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
+  const int hd = h * ATT_DK;
+
+  // ---- phase 1: strips, then dQ of the strip
+  {
+    att_bf16x8 qa[2], oa[2];
+    const int iq = min(i0 + col, a.Tq - 1);
+    const __bf16* qr = a.q + (qb + iq) * a.ldq + hd + 8 * g;
+    const float* orr = a.dout + (qb + iq) * a.lddo + hd + 8 * g;
+    qa[0] = strip8(qr);
+    qa[1] = strip8(qr + 32);
+    oa[0] = strip8(orr);
+    oa[1] = strip8(orr + 32);
+    float gp[4][NJT];
+    preload_graph<NJT>(a, b, i0, g, col, gp);
+    float kf[NJT];
+#pragma unroll
+    for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[kb + min(jt * 16 + col, a.Tk - 1)];
+    stage_kv_bf<TK>(a, b, h, Ks, Vs);
+    __syncthreads();  // K/V staged
+    f4v s[NJT], dp[NJT];
+    strip_dots_bf<NJT>(qa, Ks, col, g, s);
+    strip_dots_bf<NJT>(oa, Vs, col, g, dp);
+    f4v pv[NJT], dsv[NJT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * g + r;
+      const int ic = min(i, a.Tq - 1);
+      float aa[NJT], gg[NJT], bm[NJT];
+      const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
+      const float sden = fmaxf(nrm, 1e-12f);
+      const float rsd = 1.f / sden;
+      const float qf = a.qflag[qb + ic];
+      float dn[NJT], t1 = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        dn[jt] = dp[jt][r] * qf;
+        t1 += dn[jt] * bm[jt];
+      }
+      t1 = row16_sum(t1);
+      const float dnrm = nrm >= 1e-12f ? -t1 * (rsd * rsd) : 0.f;
+      float da[NJT], t2 = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        const float sg = bm[jt] > 0.f ? 1.f : (bm[jt] < 0.f ? -1.f : 0.f);
+        const float dbm = dn[jt] * rsd + dnrm * sg;
+        da[jt] = dbm * gg[jt];
+        t2 += da[jt] * aa[jt];
+      }
+      t2 = row16_sum(t2);
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        const int j = jt * 16 + col;
+        const bool ok = i < a.Tq && j < a.Tk;
+        float ds = aa[jt] * (da[jt] - t2);
+        if (kf[jt] == 0.f) ds = 0.f;
+        dsv[jt][r] = ok ? ds * 0.125f : 0.f;
+        pv[jt][r] = ok ? bm[jt] * rsd * qf : 0.f;
+      }
+    }
+#pragma unroll
+    for (int jt = 0; jt < NJT; ++jt) {
+      *reinterpret_cast<att_bf16x4*>(&Pt[(jt * 16 + col) * PLB + i0 + 4 * g]) = pack4(pv[jt]);
+      *reinterpret_cast<att_bf16x4*>(&dSt[(jt * 16 + col) * PLB + i0 + 4 * g]) = pack4(dsv[jt]);
+    }
+    // dQ ReLU masks of this lane's outputs (rows i0 + 4g + r, columns 16 dt + col): loaded
+    // here, where the strip registers are dead, under the dQ products below
+    __bf16 qm[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const __bf16* qrow = a.q + (qb + min(i0 + 4 * g + r, a.Tq - 1)) * a.ldq + hd + col;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) qm[r][dt] = qrow[dt * 16];
+    }
+    __builtin_amdgcn_wave_barrier();  // this wave's dS^T columns are written (in-order LDS)
+    // dQ strip = dS K: A[m = i][k = j] = dS^T[j][i0 + i], B[k = j][n = d] = K[j][16 dt + d]
+    f4v dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < NJT; ++kc) {
+      const __bf16* ac = dSt + (kc * 16 + 4 * g) * PLB + i0 + col;
+      const att_bf16x4 av = {ac[0], ac[PLB], ac[2 * PLB], ac[3 * PLB]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const __bf16* kcp = Ks + (kc * 16 + 4 * g) * ATT_KLB + dt * 16 + col;
+        const att_bf16x4 kv = {kcp[0], kcp[ATT_KLB], kcp[2 * ATT_KLB], kcp[3 * ATT_KLB]};
+        dq[dt] = mfma_bf16(av, kv, dq[dt]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * g + r;
+      if (i < a.Tq) {
+        __bf16* drow = a.dq + (qb + i) * a.lddq + hd + col;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) drow[dt * 16] = (__bf16)((float)qm[r][dt] > 0.f ? dq[dt][r] : 0.f);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: dV^T = dO^T P and dK^T = Q^T dS, 16x16 tiles (key tile jt, column block dt),
+  // grouped (tensor, dt): item = grp * NJT + jt, grp < 4 dV, grp >= 4 dK; k = query.
+  //   A[m = d][k = i] = X[i][16 dt + d]   (X = dO rounded to bf16, or Q): preloaded per group
+  //   B[k = i][n = j] = Y^T[j][i]          (Y^T = P^T or dS^T): one 8-B LDS read per 16 k
+  //   D[m = 4g + r][n = col] = out[j = 16 jt + col][d = 16 dt + 4g + r]
+  const int nitems = 8 * NJT;
+  const int it0 = nitems * w / nw, it1 = nitems * (w + 1) / nw;
+  constexpr int MAXG = 3;  // groups a wave's item run can touch (checked on the host)
+  const int g0 = it0 / NJT;
+  att_bf16x4 acol[MAXG][NJT];  // (query tiles: nw == NJT, host check)
+#pragma unroll
+  for (int u = 0; u < MAXG; ++u) {
+    const int grp = g0 + u;
+    if (grp * NJT < it1 && grp < 8) {  // wave-uniform
+      const int dt = grp & 3;
+      const int dcol = hd + dt * 16 + col;
+#pragma unroll
+      for (int kc = 0; kc < NJT; ++kc) {
+        float t4[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int64_t row = qb + min(kc * 16 + 4 * g + t, a.Tq - 1);
+          t4[t] = grp < 4 ? a.dout[row * a.lddo + dcol] : (float)a.q[row * a.ldq + dcol];
+        }
+        acol[u][kc] = pack4(f4v{t4[0], t4[1], t4[2], t4[3]});
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < MAXG; ++u) {
+    const int grp = g0 + u;
+    const int lo = max(it0, grp * NJT), hi = min(it1, (grp + 1) * NJT);
+    if (grp >= 8 || lo >= hi) continue;  // wave-uniform
+    const bool isv = grp < 4;
+    const int dt = grp & 3;
+    const __bf16* Yt = isv ? Pt : dSt;
+    const __bf16* Ms = isv ? Vs : Ks;
+    __bf16* dst = isv ? a.dv : a.dk;
+    const int64_t dld = isv ? a.lddv : a.lddk;
+    for (int it = lo; it < hi; ++it) {
+      const int jt = it - grp * NJT;
+      const int j = jt * 16 + col;
+      const att_bf16x4 mk = ldb4(Ms + j * ATT_KLB + dt * 16 + 4 * g);
+      f4v acc = {0.f, 0.f, 0.f, 0.f};
+      const __bf16* yrow = Yt + j * PLB + 4 * g;
+#pragma unroll
+      for (int kc = 0; kc < NJT; ++kc) acc = mfma_bf16(acol[u][kc], ldb4(yrow + kc * 16), acc);
+      if (j < a.Tk) {
+        f4v o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (float)mk[r] > 0.f ? acc[r] : 0.f;
+        stx4(dst + (kb + j) * dld + hd + dt * 16 + 4 * g, o, vec_rows(dst, dld));
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Single-query path (T_q = 1: the decoder cross-attention, one query token per sample).
 // One wave per (b, h); 16 lanes per key row (lane = (key slot kk = lane>>4, float4 chunk
@@ -818,28 +1194,6 @@ __device__ __forceinline__ void q1_forward(const A& a, int b, int hd, int kk, in
   nrm = rows4_sum(nr);
 }
 
-// 4 consecutive outputs of one lane: one 16-B (fp32) / 8-B (bf16) store when the row is
-// vector-aligned (vec: wave-uniform), else 4 element stores (4 / 8 x the store instructions)
-__device__ __forceinline__ void stx4(float* p, f4v v, bool vec) {
-  if (vec) {
-    *reinterpret_cast<f4v*>(p) = v;
-  } else {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) p[e] = v[e];
-  }
-}
-__device__ __forceinline__ void stx4(__bf16* p, f4v v, bool vec) {
-  if (vec) {
-    *reinterpret_cast<att_bf16x4*>(p) = __builtin_convertvector(v, att_bf16x4);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) p[e] = (__bf16)v[e];
-  }
-}
-template <typename T>
-__device__ __forceinline__ bool vec_rows(const T* p, int64_t ld) {
-  return (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & (4 * sizeof(T) - 1)) == 0;
-}
 
 template <int NIT, typename TQ, typename TKV>
 __global__ __launch_bounds__(256) void gattn_fwd_q1_kernel(AttnArgsT<TQ, TKV> a) {
@@ -1044,10 +1398,15 @@ static int launch_bwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const ch
     if constexpr (sizeof(T) == 2) {
       // bf16 MFMA kernels: bf16 K/V images kept next to the bf16 P^T / dS^T images
       const size_t ldsb = 2 * 2 * (size_t)njt * 16 * (size_t)(16 * nw + 8 + ATT_KLB);
+      // second structure (transposed dV / dK, dQ in phase 1): as many query as key tiles (the
+      // self-attention shape), and a wave's phase-2 item run (8 NJT / nw items) must touch at
+      // most 3 (tensor, column block) groups
+      const bool v2 = SAVQA_ATT_BWD2 && nw == njt && (8 * njt + nw - 1) / nw <= 2 * njt;
       switch (njt) {
 #define SAVQA_BWD_CASE(N)                                                                       \
   case N:                                                                                       \
-    hipLaunchKernelGGL((gattn_bwd_mfma_bf_kernel<N>), dim3(B * H), dim3(64 * nw), ldsb, s, a);  \
+    if (v2) hipLaunchKernelGGL((gattn_bwd_mfma_bf2_kernel<N>), dim3(B * H), dim3(64 * nw), ldsb, s, a); \
+    else hipLaunchKernelGGL((gattn_bwd_mfma_bf_kernel<N>), dim3(B * H), dim3(64 * nw), ldsb, s, a); \
     break;
         SAVQA_BWD_CASE(1) SAVQA_BWD_CASE(2) SAVQA_BWD_CASE(3) SAVQA_BWD_CASE(4)
         SAVQA_BWD_CASE(5) SAVQA_BWD_CASE(6) SAVQA_BWD_CASE(7) SAVQA_BWD_CASE(8)
@@ -1055,10 +1414,17 @@ static int launch_bwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const ch
       }
     } else {
     const size_t lds = sizeof(float) * 2 * (size_t)njt * 16 * (size_t)std::max(16 * nw + 4, ATT_KLD);
+    // v2: K [TK][ATT_KLD] + max(V, P^T) + dS^T [TK][16 nw + 4] (over the 160 KB of a CU at
+    // TK = 128: the round-2 structure then)
+    const size_t lds2 = sizeof(float) * (size_t)njt * 16 *
+                        ((size_t)ATT_KLD + std::max(16 * nw + 4, ATT_KLD) + (size_t)(16 * nw + 4));
+    const bool v2 = SAVQA_ATT_BWD2 && nw == njt && (8 * njt + nw - 1) / nw <= 2 * njt &&
+                    lds2 <= 160 * 1024;
     switch (njt) {
 #define SAVQA_BWD_CASE(N)                                                                      \
   case N:                                                                                      \
-    hipLaunchKernelGGL((gattn_bwd_mfma_kernel<N, T>), dim3(B * H), dim3(64 * nw), lds, s, a);  \
+    if (v2) hipLaunchKernelGGL((gattn_bwd_mfma2_kernel<N, T>), dim3(B * H), dim3(64 * nw), lds2, s, a); \
+    else hipLaunchKernelGGL((gattn_bwd_mfma_kernel<N, T>), dim3(B * H), dim3(64 * nw), lds, s, a);  \
     break;
       SAVQA_BWD_CASE(1) SAVQA_BWD_CASE(2) SAVQA_BWD_CASE(3) SAVQA_BWD_CASE(4)
       SAVQA_BWD_CASE(5) SAVQA_BWD_CASE(6) SAVQA_BWD_CASE(7) SAVQA_BWD_CASE(8)

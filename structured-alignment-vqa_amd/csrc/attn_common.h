@@ -69,6 +69,29 @@ __device__ __forceinline__ float ldx1(const __bf16* p) { return (float)*p; }
 __device__ __forceinline__ void stx1(float* p, float v) { *p = v; }
 __device__ __forceinline__ void stx1(__bf16* p, float v) { *p = (__bf16)v; }
 
+// 4 consecutive outputs of one lane: one 16-B (fp32) / 8-B (bf16) store when the row is
+// vector-aligned (vec: wave-uniform), else 4 element stores (4 / 8 x the store instructions)
+__device__ __forceinline__ void stx4(float* p, f4v v, bool vec) {
+  if (vec) {
+    *reinterpret_cast<f4v*>(p) = v;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p[e] = v[e];
+  }
+}
+__device__ __forceinline__ void stx4(__bf16* p, f4v v, bool vec) {
+  if (vec) {
+    *reinterpret_cast<att_bf16x4*>(p) = __builtin_convertvector(v, att_bf16x4);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p[e] = (__bf16)v[e];
+  }
+}
+template <typename T>
+__device__ __forceinline__ bool vec_rows(const T* p, int64_t ld) {
+  return (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & (4 * sizeof(T) - 1)) == 0;
+}
+
 // Same with Y staged in LDS ([TK][ATT_KLD], rows >= Tk zero): b128 reads, lanes 0-15 of a
 // read phase hit 16 disjoint bank quads (row stride 68 floats).
 template <int NJT>

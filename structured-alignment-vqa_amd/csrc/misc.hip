@@ -431,6 +431,9 @@ __global__ void scatter_rows_kernel(const float* __restrict__ g, const int64_t* 
 typedef float adam_f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void adam4(adam_f4& pp, adam_f4 gg, adam_f4& mm, adam_f4& vv, float b1,
                                       float b2, float eps, float step_size, float sbc2, float gs) {
+  // no FMA contraction: every launch site (grid-stride body, its tail, the row kernel) must round
+  // identically, so a row-tracked step is bit-identical to the dense one
+#pragma clang fp contract(off)
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const float gx = gg[e] * gs;
@@ -471,13 +474,15 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     adam4(p0, Gv[i], m0, v0, b1, b2, eps, step_size, sbc2, gs);
     P[i] = p0; M[i] = m0; V[i] = v0;
   }
-  // scalar tail
-  for (int64_t k = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
-    const float gx = g[k] * gs;
-    m[k] = m[k] + (1.f - b1) * (gx - m[k]);
-    v[k] = b2 * v[k] + (1.f - b2) * gx * gx;
-    const float den = sqrtf(v[k]) / sbc2 + eps;
-    p[k] = p[k] - step_size * (m[k] / den);
+  {  // scalar tail (same roundings as adam4)
+#pragma clang fp contract(off)
+    for (int64_t k = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+      const float gx = g[k] * gs;
+      m[k] = m[k] + (1.f - b1) * (gx - m[k]);
+      v[k] = b2 * v[k] + (1.f - b2) * gx * gx;
+      const float den = sqrtf(v[k]) / sbc2 + eps;
+      p[k] = p[k] - step_size * (m[k] / den);
+    }
   }
 }
 

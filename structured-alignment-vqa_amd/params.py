@@ -195,10 +195,12 @@ class ParamArena:
                 self.mark_rows(n, ids)
 
     def mark_all_rows(self, name: str):
-        """Every row of `name` has (or may have) Adam state: after a dense update."""
+        """After a dense update of `name` (its gradient came from an exchange the flags do not
+        see): every row may hold Adam state AND a non-zero gradient, so the next zero_grad
+        clears the whole table and a later row-tracked step reads every row's gradient."""
         f = self.row_flags.get(name)
         if f is not None:
-            f.fill_(1)
+            f.fill_(3)
 
     def _clear_touched(self):
         # the whole gradient was just zeroed densely: clear the touched bits with it

@@ -93,7 +93,16 @@ def test_untracked_tables_under_foreign_data_parallel_exchange_update_densely(mo
     monkeypatch.setattr(dist, "is_initialized", lambda: True)
     monkeypatch.setattr(dist, "get_world_size", lambda *a, **k: 2)
     assert opt._row_tables(None) == ()
+    a = m._arena
+    # a row only another rank touched: the exchanged gradient is non-zero there
+    for n in a.row_flags:
+        o, shp = a.offsets[n]
+        a.gview(n)[shp[0] - 1].fill_(0.25)
     opt.step()
     torch.cuda.synchronize()
-    for f in m._arena.row_flags.values():
+    for f in a.row_flags.values():
         assert bool((f & 1).ne(0).all())
+    # ... so the next zero_grad clears the whole table, not just the locally touched rows
+    opt.zero_grad()
+    torch.cuda.synchronize()
+    assert int(torch.count_nonzero(a.grad)) == 0

@@ -154,13 +154,16 @@ REL_INPUTS = ("vis_fea", "vis_mask", "q_ipt", "q_mask", "q_graph", "macro_ipt", 
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("case", ["full_rel_b2", "full_rel_sn"])
+@pytest.mark.parametrize("case", ["full_rel_b2", "full_rel_sn", "full_rel_big"])
 def test_relation_branch_full_model(case):
     """MIL-NCE relation branch (only_obj=False, AttModel_x3.py:382-437) end to end: logits,
     mil_nce_obj, mil_nce_rel, loss and every trained gradient (R included) against the
-    reference run on super-node batches (tests/golden/full_rel_{b2,sn}.npz; sn: T_syb=211)."""
+    reference run on super-node batches (tests/golden/full_rel_{b2,sn,big}.npz; sn: T_syb=211;
+    big: the reference's relation configuration, hidden_size_mil 64 / maxlen 1600 / 311
+    categories, T_syb=1313, ~6k listed relations)."""
     g = np.load(os.path.join(GOLD, f"{case}.npz"))
-    P = hashfill.HashParams(requires_grad=True, num_relations=int(g["num_relations"]))
+    geo = {k: int(g[k]) for k in ("hidden_mil", "maxlen") if k in g}
+    P = hashfill.HashParams(requires_grad=True, num_relations=int(g["num_relations"]), **geo)
     inp = {k: torch.from_numpy(g[k]) for k in REL_INPUTS}
     lc, lv, ls, mil, mil_rel = O.attmodel_forward(P, inp, decMask=True, only_obj=False)
     assert rel_err(lc.detach(), g["logits_concat"]) < 1e-5
