@@ -184,8 +184,10 @@ def _digest(arena, t):
 
 def _equiv_run(world, rank, steps=2, sparse=True, mode="reducer"):
     """`steps` full training steps on this rank's contiguous shard of the 8-sample batch;
-    returns per step the gradient the optimizer consumed (averaged over ranks) and the
-    parameters after the step.
+    returns per step the gradient the optimizer consumed (averaged over ranks), the
+    parameters after the step and -- on rank 0 of a multi-rank run -- the per-tensor
+    Frobenius-relative error of that gradient against the 1-rank full-batch gradient
+    recomputed at the SAME pre-step parameters (a second model on the device).
       mode "reducer": forward, loss, backward, streamed GradReducer, per-bucket savqa Adam;
       mode "ddp": the reference's own wrapping (main:203/:206/:363-366) --
         DistributedDataParallel(model, find_unused_parameters=True), torch.optim.Adam over
@@ -212,10 +214,12 @@ def _equiv_run(world, rank, steps=2, sparse=True, mode="reducer"):
                 red.sparse = []
         opt = Adam(m, lr=1e-4)
     a = m._arena
+    rm = _equiv_model() if world > 1 and rank == 0 else None
     rec = []
     for _ in range(steps):
         if red:
             red.begin()
+        pre = a.flat.clone() if rm is not None else None
         lc, lv, ls, mil, _ = net(*model_args(batch), decMask=True, mcb=False)
         loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil)
         opt.zero_grad()
@@ -228,7 +232,25 @@ def _equiv_run(world, rank, steps=2, sparse=True, mode="reducer"):
             scale = world      # the reducer sums; Adam folds in 1/world
         torch.cuda.synchronize()
         g = a.grad[:a.n_live] / scale
-        rec.append((_digest(a, g), _digest(a, a.flat[:a.n_live])))
+        gerr = None
+        if rm is not None:
+            ra = rm._arena
+            with torch.no_grad():
+                ra.flat.copy_(pre)
+            del pre
+            rlc, rlv, rls, rmil, _ = rm(*model_args(full), decMask=True, mcb=False)
+            rloss, _ = smoothed_loss(rlc, rlv, rls, full["answer"], rmil)
+            ra.ensure_grads()
+            ra.zero_grad()
+            rloss.backward()
+            torch.cuda.synchronize()
+            gerr = {}
+            for name in a.live_names:
+                o, shp = a.offsets[name]
+                x, y = g[o:o + shp.numel()].double(), ra.grad[o:o + shp.numel()].double()
+                gerr[name] = (float((x - y).norm() / y.norm().clamp_min(1e-30)),
+                              float(y.abs().max()), float(x.abs().max()))
+        rec.append((_digest(a, g), _digest(a, a.flat[:a.n_live]), gerr))
     return rec
 
 
@@ -283,15 +305,21 @@ def _cmp(a, b):
 @pytest.mark.parametrize("mode", ["reducer", "ddp"])
 def test_two_ranks_on_half_batches_equal_one_rank_on_the_batch(mode):
     """SURVEY 4 / main:203,363 (DistributedDataParallel): the same global batch gives the same
-    update on 1 rank and on 2 ranks with B/2 each -- 2 training steps through the full path
-    (forward, loss, backward with the gated enc4 schedule, streamed bucketed all-reduce,
-    per-bucket Adam), with the stack tables exchanged by rows and densely. The two replicas
-    are bit-identical; against the 1-rank run, the gradient Adam consumes agrees per tensor
-    to 1e-4 (Frobenius-relative: only the fp32 summation order differs) and the parameters'
-    2-step updates to 1e-3 (Adam divides by sqrt(v), so near-zero gradient entries amplify
+    training on 1 rank and on 2 ranks with B/2 each -- 2 steps through the full path (forward,
+    loss, backward with the gated enc4 schedule, streamed bucketed all-reduce, per-bucket
+    Adam), with the stack tables exchanged by rows and densely. The two replicas are
+    bit-identical at every step. At every step the gradient Adam consumes agrees per tensor to
+    1e-4 (Frobenius-relative: only the fp32 summation order differs) with the full-batch
+    gradient of ONE rank recomputed at the same parameters, and the first update agrees with
+    the 1-rank run's to 1e-3 (Adam divides by sqrt(v), so near-zero gradient entries amplify
     rounding; the key-projection biases have an exactly-zero true gradient -- softmax shift
     invariance -- and their Adam update is rounding noise in every implementation, so they
-    are left out).
+    are left out). Later steps are not compared against a separate 1-rank RUN: the model is
+    ill-conditioned around these parameters (tools/dbg/sens_dbg.py: a 1e-6 relative
+    perturbation of the init moves the logits by O(1); the layer norm divides by std + 1e-8,
+    modules.py layer_normalization, and near-constant rows amplify), so the 6e-7 parameter
+    differences of the two runs after step 0 become ~7% gradient differences at step 1 --
+    measured as such, with the exchanged gradient equal to the local-gradient sum to 3e-8.
     mode "ddp": the same with the model wrapped exactly as the reference wraps it --
     DistributedDataParallel(model, find_unused_parameters=True) and torch.optim.Adam
     (main:203/:206) -- instead of GradReducer + the fused Adam: the gradients reach DDP's
@@ -300,7 +328,7 @@ def test_two_ranks_on_half_batches_equal_one_rank_on_the_batch(mode):
         pytest.skip("no HIP device")
     import socket
     import torch.multiprocessing as mp
-    ref = _equiv_run(1, 0)
+    ref = _equiv_run(1, 0, steps=1)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -326,8 +354,8 @@ def test_two_ranks_on_half_batches_equal_one_rank_on_the_batch(mode):
         r0, r1 = res[0][0][sparse], res[1][0][sparse]
         worst_g, worst_u = [], []
         for step in range(2):
-            (g0, w0), (g1, w1) = r0[step], r1[step]
-            gref, wref = ref[step]
+            (g0, w0, gerr), (g1, w1, _) = r0[step], r1[step]
+            gref, wref, _ = ref[0]     # the 1-rank run's first step
             for n in wref:
                 x0, x1 = w0[n], w1[n]
                 if isinstance(x0, tuple):
@@ -335,12 +363,18 @@ def test_two_ranks_on_half_batches_equal_one_rank_on_the_batch(mode):
                 assert torch.equal(x0, x1), ("replicas diverged", sparse, step, n)
                 if n.endswith("K_proj.0.bias"):
                     continue
-                if not isinstance(gref[n], tuple) and float(gref[n].abs().max()) == 0.0:
-                    assert float(g0[n].abs().max()) == 0.0, n
+                # the exchanged gradient vs the full-batch one at the same parameters
+                err, ymax, xmax = gerr[n]
+                if ymax == 0.0:
+                    assert xmax == 0.0, n
+                else:
+                    worst_g.append((err, step, n))
+                if step > 0 or isinstance(wref[n], tuple):  # tables: gradient rows compared above
                     continue
-                worst_g.append((_cmp(g0[n], gref[n]), step, n))
-                if isinstance(wref[n], tuple):   # tables: gradient rows compared above
-                    continue
+                # the first update against the 1-rank run (same start, same gradient to 1e-7)
+                gr = gref[n][1] if isinstance(gref[n], tuple) else gref[n]
+                if float(gr.abs().max()) > 0.0:
+                    assert _cmp(g0[n], gref[n]) < 1e-4, (sparse, n)
                 du = w0[n] - _start(n, step, ref)
                 dr = wref[n] - _start(n, step, ref)
                 worst_u.append((_cmp(du, dr), step, n))

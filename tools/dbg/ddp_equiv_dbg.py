@@ -11,6 +11,8 @@ import torch.multiprocessing as mp
 
 import tests.test_ddp_gpu as T
 
+SYNC = os.environ.get("DBG_SYNC", "")
+
 
 def _patch_reducer():
     import savqa_amd.ddp as D
@@ -30,6 +32,16 @@ def _patch_reducer():
             super()._dense(lo, hi)
     D.GradReducer = Rec
     return Rec
+
+
+def _dead(a):
+    out = {}
+    for n in a.order:
+        o, shp = a.offsets[n]
+        if o >= a.n_live:
+            v = a.flat[o:o + shp.numel()].double()
+            out[n] = (float(v.sum()), float(v.abs().sum()))
+    return out
 
 
 def worker(rank, world, port, q):
@@ -55,15 +67,35 @@ def worker(rank, world, port, q):
         out = []
         for step in range(2):
             red.begin()
+            pre = a.flat.clone()
             lc, lv, ls, mil, _ = m(*model_args(batch), decMask=True, mcb=False)
             loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil)
             opt.zero_grad()
+            if "zg" in SYNC:
+                torch.cuda.synchronize()
             loss.backward()
+            if "bw" in SYNC:
+                torch.cuda.synchronize()
             opt.step(reducer=red)
             torch.cuda.synchronize()
+            if "late" in SYNC:
+                fm = T._equiv_model()
+                with torch.no_grad():
+                    fm._arena.flat.copy_(pre)
+                flc, flv, fls, fmil, _ = fm(*model_args(batch), decMask=True, mcb=False)
+                floss, _ = smoothed_loss(flc, flv, fls, batch["answer"], fmil)
+                fm._arena.ensure_grads()
+                floss.backward()
+                torch.cuda.synchronize()
+                d = (red.local[:a.n_live] - fm._arena.grad[:a.n_live]).abs()
+                print(f"rank {rank} step {step} loss {float(loss):.6f} fresh {float(floss):.6f} "
+                      f"logits {float((lc - flc).abs().max()):.3e} local-vs-fresh {float(d.max()):.3e}",
+                      flush=True)
+                del fm
             out.append((red.local[:a.n_live].cpu().clone(), a.grad[:a.n_live].cpu().clone(),
-                        list(red.issued)))
-        q.put((rank, out, None))
+                        list(red.issued), a.flat[:a.n_live].cpu().clone(), _dead(a),
+                        {k: v.cpu().clone() for k, v in batch.items()}))
+        q.put((rank, T._to_numpy(out), None))
     except Exception:
         import traceback
         q.put((rank, None, traceback.format_exc()))
@@ -80,6 +112,7 @@ def ref_run():
     opt = Adam(m, lr=1e-4)
     a = m._arena
     out = []
+    flats = []
     for step in range(2):
         lc, lv, ls, mil, _ = m(*model_args(batch), decMask=True, mcb=False)
         loss, _ = smoothed_loss(lc, lv, ls, batch["answer"], mil)
@@ -88,11 +121,13 @@ def ref_run():
         torch.cuda.synchronize()
         out.append(a.grad[:a.n_live].cpu().clone())
         opt.step()
-    return m, out
+        torch.cuda.synchronize()
+        flats.append((a.flat[:a.n_live].cpu().clone(), _dead(a)))
+    return m, out, flats
 
 
 def main():
-    m, ref = ref_run()
+    m, ref, rflats = ref_run()
     a = m._arena
     ctx = mp.get_context("spawn")
     s = socket.socket()
@@ -103,16 +138,36 @@ def main():
     procs = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (o, e)) for r, o, e in (q.get(timeout=240) for _ in procs))
+    res = dict((r, (T._to_torch(o), e)) for r, o, e in (q.get(timeout=240) for _ in procs))
     for p in procs:
         p.join(timeout=60)
     for r in (0, 1):
         if res[r][1]:
             print(res[r][1])
             return
+    print("sync", SYNC)
+    f0 = res[0][0][0][3]
+    worst = []
+    for n in a.live_names:
+        o, shp = a.offsets[n]
+        d = (f0[o:o + shp.numel()] - rflats[0][0][o:o + shp.numel()]).abs()
+        worst.append((float(d.max()), int((d > 1e-5).sum()), n))
+    worst.sort(reverse=True)
+    print("params after step 0 (max diff, #>1e-5):", worst[:8])
+    for n, v in res[0][0][0][4].items():
+        if v != rflats[0][1][n]:
+            print("dead param differs", n, v, rflats[0][1][n])
+    orig = T._equiv_batch()
+    for r in (0, 1):
+        for st in (0, 1):
+            b = res[r][0][st][5]
+            for k, v in b.items():
+                o = orig[k][r * 4:(r + 1) * 4].cpu()
+                if not torch.equal(v, o):
+                    print("batch changed", r, st, k)
     for step in range(2):
-        l0, x0, iss = res[0][0][step]
-        l1, x1, _ = res[1][0][step]
+        l0, x0, iss, _, _, _ = res[0][0][step]
+        l1, x1, _, _, _, _ = res[1][0][step]
         gref = ref[step]
         print(f"== step {step}: {len(iss)} dense all-reduces, nan local {int(l0.isnan().sum())}")
         for lo, hi, st in iss:
@@ -123,6 +178,10 @@ def main():
             e_loc = float(((l0[sl].double() + l1[sl].double()) / 2 - gref[sl].double()).norm()) / den
             e_sum = float((x0[sl].double() - l0[sl].double() - l1[sl].double()).norm()) / (2 * den)
             if max(e_ex, e_loc, e_sum) <= 1e-4:
+                continue
+            nbad = getattr(main, "nbad", 0) + 1
+            main.nbad = nbad
+            if nbad > 4:
                 continue
             dd = ((l0[sl].double() + l1[sl].double()) / 2 - gref[sl].double()).abs()
             k = lo + int(dd.argmax())
