@@ -13,7 +13,8 @@
 //
 // Backward (per row i, with c_i = [W_i >= 1e-12 Z_i], n = e g / D, P = e / Z):
 //   delta_i = sum_j n_ij dN_ij,  dN_ij = qflag_i dO_i . V_j   (= dO_i . O_i analytically;
-//             computed from the dN values themselves so sum_j dS_ij = 0 holds to rounding)
+//             computed from the dN values themselves, and n from W, Z re-summed over the
+//             backward's own e values, so sum_j dS_ij = 0 holds to rounding)
 //   dS_ij = n_ij (dN_ij - c_i sgn(g_ij) delta_i) - (1 - c_i) P_ij delta_i   (0 on masked keys)
 // i.e. the softmax / L1-normalise adjoints collapse to per-row scalars, so the backward
 // is two tiled kernels: dQ (workgroup per query tile, two sweeps over the key tiles:
@@ -341,11 +342,20 @@ __global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
   f4v dq[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dq[dt] = f4v{0.f, 0.f, 0.f, 0.f};
-  float dpart[4] = {0.f, 0.f, 0.f, 0.f};
+  double sa[4] = {0., 0., 0., 0.}, sw[4] = {0., 0., 0., 0.}, sz[4] = {0., 0., 0., 0.};
+  double dx[4] = {0., 0., 0., 0.};
   const int nkt = (a.Tk + FL_KT - 1) / FL_KT;
-  // pass 0: delta_i = sum_j n_ij dN_ij from the SAME dN values pass 1 uses, so the
-  // analytic identity sum_j dS_ij = 0 holds to rounding (dQ_i = sum_j dS_ij K_j cancels
-  // the common part of the keys); pass 1: dS and dQ.
+  // dQ_i = sum_j dS_ij K_j / 8 with sum_j dS_ij = 0 analytically: the keys' common part
+  // cancels, so any residual of that sum comes back as (residual) x (mean key) -- with
+  // near-parallel V rows (dN_ij ~ delta_i) it is larger than dQ itself. The residual of
+  // the direct form n (dN - delta) is ~1 ulp of delta (its rounding, and sum_j |n_j| != 1
+  // by rounding), which measured 15x torch-fp32's dQ error at T = 1313
+  // (tools/dbg/flash_prec.py). So, per row, with a_j = e g qf dp and w_j = e |g| (normal)
+  // or e (clamped), both the exact fp32 values pass 1 recomputes:
+  //   pass 0: A = sum_j a_j, W' = sum_j e|g|, Z' = sum_j e in fp64;  dx = A / sum_j w_j
+  //   pass 1: dS_j = rD (a_j - dx w_j), the bracket in fp64 (sum_j dS_j = 0 to fp64 rounding)
+  // i.e. the softmax / L1-normalise adjoint with its common term removed exactly, as torch's
+  // softmax backward (x (g - sum x g)) removes it. (W', Z', delta) go to stats for dK / dV.
   for (int it = 0; it < 2 * nkt; ++it) {
     const int pass = it >= nkt;
     const int kt = it - pass * nkt;
@@ -353,10 +363,29 @@ __global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
     if (it == nkt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float dl = row16_sum(dpart[r]);
-        coef_delta(rc[r], dl);
         const int i = i0 + 4 * g + r;
-        if (col == 0 && i < a.Tq) stats[(((int64_t)b * a.H + h) * a.Tq + i) * 4 + 3] = dl;
+        double A = sa[r], Wd = sw[r], Zd = sz[r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          A += __shfl_xor(A, o, 16);
+          Wd += __shfl_xor(Wd, o, 16);
+          Zd += __shfl_xor(Zd, o, 16);
+        }
+        if (i < a.Tq) {
+          RowCoef& c = rc[r];
+          const float w = (float)Wd, z = (float)Zd;
+          c.normal = w >= 1e-12f * z;
+          const float D = c.normal ? w : 1e-12f * z;
+          c.rD = 1.f / D;
+          const double den = c.normal ? Wd : Zd;
+          dx[r] = den > 0. ? A / den : 0.;
+          if (col == 0) {
+            float* st = stats + (((int64_t)b * a.H + h) * a.Tq + i) * 4;
+            st[1] = z;
+            st[2] = w;
+            st[3] = c.normal ? (float)dx[r] : (float)(dx[r] * (double)c.rD * Zd);
+          }
+        }
       }
     }
     __syncthreads();
@@ -381,7 +410,10 @@ __global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
           const int j = k0 + jt * 16 + col;
           const float x = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * 0.125f;
           const float e = j < a.Tk ? expf(x - rc[r].m) : 0.f;
-          dpart[r] += e * gv[r][jt] * rc[r].rD * rc[r].qf * dp[jt][r];
+          const float gg = gv[r][jt];
+          sa[r] += (double)(e * gg * rc[r].qf * dp[jt][r]);
+          sw[r] += (double)(e * fabsf(gg));
+          sz[r] += (double)e;
         }
       }
       continue;
@@ -396,7 +428,9 @@ __global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
         const float x = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * 0.125f;
         const float e = j < a.Tk ? expf(x - c.m) : 0.f;
         const float gg = gv[r][jt];
-        const float ds = e * gg * c.rD * c.qf * dp[jt][r] - c.cd * e * fabsf(gg) - c.pd * e;
+        const float av = e * gg * c.qf * dp[jt][r];
+        const float wv = c.normal ? e * fabsf(gg) : e;
+        const float ds = (float)((double)av - dx[r] * (double)wv) * c.rD;
         dsv[jt][r] = (kf[jt] == 0.f || j >= a.Tk) ? 0.f : ds;
       }
     }

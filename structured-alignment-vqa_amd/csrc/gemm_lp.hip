@@ -650,21 +650,31 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
     if (nt == 0 && !tail) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
   }
 
-  // fp8 block scales of this lane's rows: A rows (m), B rows (n), block k/32 + g
+  // fp8 block scales of this lane's rows: A rows (m), B rows (n), block k/32 + g. The row
+  // pointers (a_rows gather included) are resolved once: a gather inside the k-loop made every
+  // k-tile wait for two dependent global round trips before its barrier.
   int sca[4], scb[4];
-  const int g = lane >> 4;
+  const uint8_t* scp_a[4];
+  const uint8_t* scp_b[4];
+  if constexpr (FP8) {
+    const int g = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int64_t m = m0 + wm * 64 + 16 * i + (lane & 15);
+      m = m < d.M ? m : d.M - 1;
+      const int64_t rr = d.a_rows ? d.a_rows[m] : m;
+      scp_a[i] = d.a_scale + rr * d.lds_a + (kbeg >> 5) + g;
+      int64_t n = n0 + wn * 64 + 16 * i + (lane & 15);
+      n = n < d.N ? n : d.N - 1;
+      scp_b[i] = d.b_scale + n * d.lds_b + (kbeg >> 5) + g;
+    }
+  }
   auto load_scales = [&](int64_t kt) {
     if constexpr (FP8) {
-      const int64_t blk = (kbeg >> 5) + kt * 4 + g;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        int64_t m = m0 + wm * 64 + 16 * i + (lane & 15);
-        m = m < d.M ? m : d.M - 1;
-        const int64_t rr = d.a_rows ? d.a_rows[m] : m;
-        sca[i] = d.a_scale[rr * d.lds_a + blk];
-        int64_t n = n0 + wn * 64 + 16 * i + (lane & 15);
-        n = n < d.N ? n : d.N - 1;
-        scb[i] = d.b_scale[n * d.lds_b + blk];
+        sca[i] = scp_a[i][kt * 4];
+        scb[i] = scp_b[i][kt * 4];
       }
     }
   };

@@ -61,6 +61,15 @@ def main():
             f = lambda: ops.gemm(A, X, C, m, n, k, lda=m, ldb=n, ldc=n, a_trans=True, atomic=True,
                                  split_k=sk, prec=prec)
             g = lambda: torch.mm(A.t(), X, out=C)
+        C.zero_()
+        f()
+        if lay == "NT":
+            ref = A.double() @ W.double().t()
+        elif lay == "NN":
+            ref = A.double() @ W.double()
+        else:
+            ref = A.double().t() @ X.double()
+        err = float((C.double() - ref).abs().max() / ref.abs().max())
         t1 = timeit(f)
         if prec:  # yardstick: torch's bf16 GEMM on bf16 copies
             A16 = A.bfloat16()
@@ -74,7 +83,7 @@ def main():
                 g = lambda: torch.mm(A16.t(), B16, out=C16)
         t2 = timeit(g)
         print(f"{name:10s} {lay} {m:6d}x{n:5d}x{k:6d}  savqa {t1*1e6:8.1f}us {fl/t1/1e12:6.1f} TF   "
-              f"torch {t2*1e6:8.1f}us {fl/t2/1e12:6.1f} TF", flush=True)
+              f"torch {t2*1e6:8.1f}us {fl/t2/1e12:6.1f} TF  err {err:.1e}", flush=True)
 
 
 if __name__ == "__main__":
