@@ -46,13 +46,14 @@ def bwd(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout, lddo, stats
     Gm = G.reshape(B, Tq, Tk)
     res = {}
     for nm, dt in (("f64", torch.float64), ("f32", torch.float32)):
-        Qr = Q.to(dt).clone().requires_grad_(True)
-        Kr = K.to(dt).clone().requires_grad_(True)
-        Vr = V.to(dt).clone().requires_grad_(True)
+      with torch.enable_grad():
+        Qr = Q.detach().to(dt).clone().requires_grad_(True)
+        Kr = K.detach().to(dt).clone().requires_grad_(True)
+        Vr = V.detach().to(dt).clone().requires_grad_(True)
         o, _ = _attn_ref(Qr, Kr, Vr, Gm.to(dt), kflag.reshape(B, Tk).to(dt),
                          qflag.reshape(B, Tq).to(dt), h=H)
-        (o * dO.to(dt)).sum().backward()
-        res[nm] = (Qr.grad * (Qr > 0), Kr.grad * (Kr > 0), Vr.grad * (Vr > 0))
+        gq, gk, gv = torch.autograd.grad((o * dO.detach().to(dt)).sum(), (Qr, Kr, Vr))
+        res[nm] = (gq * (Qr > 0), gk * (Kr > 0), gv * (Vr > 0))
     ours = (view(dq, B * Tq, lddq, D).reshape(B, Tq, D), view(dk_, B * Tk, lddk, D).reshape(B, Tk, D),
             view(dv, B * Tk, lddv, D).reshape(B, Tk, D))
     line = f"bwd Tq={Tq} Tk={Tk} H={H}:"
