@@ -92,7 +92,7 @@ int savqa_gemm_plan(const savqa_gemm_desc* d, int32_t* out);
  *   B(k,n) = b_trans ? B[n*ldb + k] : B[k*ldb + n]
  *   a_type / b_type: SAVQA_DT_BF16 or SAVQA_DT_FP8 (OCP e4m3fn). fp8 needs both operands
  *   fp8, a_trans = 0, b_trans = 1, K % 128 == 0, and e8m0 block scales a_scale[m][k/32]
- *   (row stride lds_a bytes) / b_scale[n][k/32]: value = e4m3 * 2^(scale - 127)
+ *   (row stride lds_a bytes, 4-byte aligned rows) / b_scale[n][k/32]: value = e4m3 * 2^(scale - 127)
  *   (v_mfma_scale_f32_16x16x128_f8f6f4). bf16 needs K % 8 == 0 (unless both operands are
  *   k-major: a_trans = 1, b_trans = 0), 16-B aligned operands with ld % 8 == 0, and M % 8 == 0
  *   (a_trans) / N % 8 == 0 (b_trans = 0).

@@ -607,7 +607,8 @@ __device__ __forceinline__ void lp_epilogue_pre(const savqa_gemm_lp_desc& d, f4 
 template <bool AT, bool BT, bool FP8, int PRE>
 __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   const savqa_gemm_lp_desc& d = args.d;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * LP_IMG];
+  // fp8: + two 1-KB e8m0 scale images [A rows 0..127 | B rows 0..127][4 blocks of 32 k]
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * LP_IMG + (FP8 ? 2048 : 0)];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -650,31 +651,40 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
     if (nt == 0 && !tail) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
   }
 
-  // fp8 block scales of this lane's rows: A rows (m), B rows (n), block k/32 + g. The row
-  // pointers (a_rows gather included) are resolved once: a gather inside the k-loop made every
-  // k-tile wait for two dependent global round trips before its barrier.
-  int sca[4], scb[4];
-  const uint8_t* scp_a[4];
-  const uint8_t* scp_b[4];
+  // fp8 block scales: staged by LDS-DMA with the operand tiles (one 4-byte granule per lane:
+  // the 4 blocks of 32 k of one row in a k-tile; wave w stages A rows (w < 2) or B rows
+  // 64 (w & 1) + lane), so the k-loop carries no ordinary global loads. Scales loaded into
+  // VGPRs per k-tile (8 byte loads per lane, the a_rows gather resolved inside the loop) left
+  // the fp8 kernel slower per FLOP than the bf16 one (profiles/r02_lp_diag.txt).
+  const uint8_t* scp = nullptr;
   if constexpr (FP8) {
-    const int g = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int64_t m = m0 + wm * 64 + 16 * i + (lane & 15);
+    const int r = 64 * (wave & 1) + lane;
+    if (wave < 2) {
+      int64_t m = m0 + r;
       m = m < d.M ? m : d.M - 1;
       const int64_t rr = d.a_rows ? d.a_rows[m] : m;
-      scp_a[i] = d.a_scale + rr * d.lds_a + (kbeg >> 5) + g;
-      int64_t n = n0 + wn * 64 + 16 * i + (lane & 15);
+      scp = d.a_scale + rr * d.lds_a + (kbeg >> 5);
+    } else {
+      int64_t n = n0 + r;
       n = n < d.N ? n : d.N - 1;
-      scp_b[i] = d.b_scale + n * d.lds_b + (kbeg >> 5) + g;
+      scp = d.b_scale + n * d.lds_b + (kbeg >> 5);
     }
   }
-  auto load_scales = [&](int64_t kt) {
+  char* const sc_img = smem + 2 * 2 * LP_IMG;  // fp8 only: [buffer][A 512 B | B 512 B]
+  auto stage_scales = [&](int buf, int64_t kt) {
+    if constexpr (FP8)
+      __builtin_amdgcn_global_load_lds(scp + kt * 4, (lds_void*)(sc_img + buf * 1024 + wave * 256),
+                                       4, 0, 0);
+  };
+  int sca[4], scb[4];
+  auto read_scales = [&](int buf) {
     if constexpr (FP8) {
+      const int g = lane >> 4;
+      const uint8_t* si = reinterpret_cast<const uint8_t*>(sc_img + buf * 1024);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        sca[i] = scp_a[i][kt * 4];
-        scb[i] = scp_b[i][kt * 4];
+        sca[i] = si[(wm * 64 + 16 * i + (lane & 15)) * 4 + g];
+        scb[i] = si[512 + (wn * 64 + 16 * i + (lane & 15)) * 4 + g];
       }
     }
   };
@@ -690,19 +700,15 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   };
   if (nt > 0) {
     stage(smem, 0);
-    load_scales(0);
+    stage_scales(0, 0);
     __syncthreads();  // vmcnt(0) + barrier: stage 0 landed for every wave
     for (int kt = 0; kt < nt; ++kt) {
       const char* ia = smem + (kt & 1) * 2 * LP_IMG;
       const char* ib = ia + LP_IMG;
-      int sca_c[4], scb_c[4];
-      if constexpr (FP8) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { sca_c[i] = sca[i]; scb_c[i] = scb[i]; }
-      }
+      read_scales(kt & 1);
       if (kt + 1 < nt) {  // next k-tile into the other buffer (read one barrier ago)
         stage(smem + ((kt + 1) & 1) * 2 * LP_IMG, kt + 1);
-        load_scales(kt + 1);
+        stage_scales((kt + 1) & 1, kt + 1);
       } else if constexpr (PRE != 0) {  // last k-tile: epilogue operands under its MFMAs
         if (!tail) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
       }
@@ -717,7 +723,7 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                b[j], a[i], acc[i][j], 0, 0, 0, scb_c[j], 0, sca_c[i]);
+                b[j], a[i], acc[i][j], 0, 0, 0, scb[j], 0, sca[i]);
       } else {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
@@ -1133,6 +1139,8 @@ static bool lp_ok(const savqa_gemm_lp_desc& d, const char** msg) {
     if (d.K % 128) return no("fp8 needs K % 128 == 0");
     if (d.lda % 16 || d.ldb % 16) return no("fp8 needs ld % 16 == 0");
     if (!d.a_scale || !d.b_scale) return no("fp8 needs block scales");
+    if ((d.lds_a % 4) || (d.lds_b % 4) || ((uintptr_t)d.a_scale & 3) || ((uintptr_t)d.b_scale & 3))
+      return no("fp8 needs 4-byte aligned scale rows (lds % 4 == 0)");
   } else {
     // 16-B granules run along k only in k-contiguous (R image) operands
     if (d.K % 8 && (!d.a_trans || d.b_trans)) return no("bf16 needs K % 8 == 0");

@@ -103,6 +103,8 @@ def main():
     elif "--dbg" in sys.argv:  # v5 as is / without MFMAs / without k-loop DMAs / no epilogue
         hints = [5, 5 + 256, 5 + 512, 5 + 1024, 5 + 256 + 1024]
         cases = cases[1:4] + cases[6:7] + cases[10:11]
+    if "--fp8" in sys.argv:  # only the cfg-5 fp8 region-feature GEMMs
+        cases = []
     tot_f = 0.0
     tot_t = {h: 0.0 for h in hints}
     for name, lay, m, n, k, out in cases:
@@ -120,7 +122,7 @@ def main():
             tot_t[h] += t1
             line += f" v{h} {t1*1e6:7.1f}us {fl/t1/1e12:6.1f}TF"
         print(line + f" | torch bf16 {t2*1e6:7.1f}us {fl/t2/1e12:6.1f}TF", flush=True)
-    for h in hints:
+    for h in (hints if cases else []):
         print(f"bf16 total v{h}: {tot_f/tot_t[h]/1e12:.1f} TF over the cfg-3 encoder shapes",
               flush=True)
     for name, m, n, k in (() if "--square" in sys.argv else
