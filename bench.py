@@ -167,8 +167,7 @@ WORKLOADS = {
 
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 # committed PMC passes of each workload's bench command (tools/profile_round.sh)
-ROOFLINE_JSON = {"cfg2": "r02_cfg2_roofline.json", "cfg3": "r02_cfg3_roofline.json",
-                 "cfg5": "r02_cfg5_roofline.json"}
+ROOFLINE_JSON = {w: f"r03_{w}_roofline.json" for w in ("cfg2", "cfg3", "cfg4", "cfg5", "rel")}
 
 
 def committed_traffic(variant, workload="cfg2"):
