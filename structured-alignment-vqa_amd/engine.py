@@ -48,6 +48,29 @@ def _rows_index(B: int, T: int, start: int, count: int, dev) -> torch.Tensor:
             + start + torch.arange(count, device=dev, dtype=torch.int64).unsqueeze(0)).reshape(-1)
 
 
+_QV_WROWS = {}
+
+
+def _qv_wrows(d: int, dev) -> torch.Tensor:
+    """Row ids [0, d) + [2d, 3d) of a fused [Wq; Wk; Wv] matrix: its Q and V blocks."""
+    key = (d, str(dev))
+    t = _QV_WROWS.get(key)
+    if t is None:
+        t = torch.cat((torch.arange(d, dtype=torch.int64),
+                       torch.arange(2 * d, 3 * d, dtype=torch.int64))).to(dev)
+        _QV_WROWS[key] = t
+    return t
+
+
+# Layers 0-1 attend with graph_diag (AttModel_x3.py:113-116 / :238-241), whose only non-zero
+# block is question x question: a node query row's normalised weights are exactly 0 (it returns
+# LN(x)), and a node key is never a neighbour, so its V is multiplied by 0 and its Q and V get
+# exactly zero gradient. Its K still enters every question row's softmax denominator (the
+# F.normalize clamp decision reads it) and gets gradient in the clamped case, so K stays
+# computed for every row; Q and V only for the question rows (node rows zero).
+PRUNE_L01 = True
+
+
 # ----------------------------------------------------------------------------- weights
 def _views(arena, grad=False, buf=None):
     """(view, span) accessors over the parameters, their gradients, or a shadow buffer laid
@@ -132,6 +155,7 @@ class StackSaved:
     graph: torch.Tensor = None
     dmask: torch.Tensor = None
     q_flat: torch.Tensor = None
+    qrows: torch.Tensor = None     # row ids of the question tokens in the [B*T] stack buffers
     enc: List[dict] = field(default_factory=list)
     x6: torch.Tensor = None
     f6: torch.Tensor = None
@@ -211,11 +235,29 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
     ops.graph_build(node_mask, q_mask, q_graph, node_graph, B, Nn, Lq, decMask, s.gdiag, s.graph,
                     s.dmask)
     x = s.x0
+    s.qrows = _rows_index(B, T, Nn, Lq, dev)
     for i, L in enumerate(W.enc):
         G = s.gdiag if i < 2 else s.graph
         e = dict(x=x, flag=flag)
         o = _empty(M, d, dev=dev)
-        if lp is not None:
+        if lp is None and i < 2 and Nn > 0 and PRUNE_L01:
+            kb = _empty(M, d, dev=dev)
+            ops.linear(x, L["Wqkv"][d:2 * d], L["bqkv"][d:2 * d], kb, relu=True)
+            qv = torch.zeros(M, 2 * d, device=dev)
+            bqv = torch.cat((L["bqkv"][:d], L["bqkv"][2 * d:]))
+            ops.gemm(x, L["Wqkv"], qv, B * Lq, 2 * d, d, lda=d, ldb=d, ldc=2 * d, b_trans=True,
+                     a_rows=s.qrows, b_rows=_qv_wrows(d, dev), bias=bqv, relu=True, c_group=Lq,
+                     c_stride=T, c_offset=Nn)
+            if ops.use_flash(T, T):
+                ast = _empty(B * H * T * 4, dev=dev)
+                ops.gattn_fwd_flash(qv, 2 * d, kb, d, qv[:, d:], 2 * d, G, flag, flag, B, T, T, H,
+                                    o, d, ast)
+                e.update(ast=ast)
+            else:
+                ops.gattn_fwd(qv, 2 * d, kb, d, qv[:, d:], 2 * d, G, flag, flag, B, T, T, H, o, d)
+            qkv = None
+            e.update(qv=qv, kb=kb)
+        elif lp is not None:
             Lb = lp.W.enc[i]
             qkv = _bf(M, 3 * d, dev=dev)
             ops.linear_lp(xb, Lb["Wqkv"], L["bqkv"], None, qkv, relu=True)
@@ -417,6 +459,31 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         del dh
         dz1 = _empty(M, d, dev=dev)
         ops.ln_bwd(dy1, e["z1"], *e["st1"], L["g1"], dz1, Lg["g1"], Lg["b1"])
+        if e.get("qv") is not None:  # layers 0-1: K of every row, Q / V of the question rows
+            qv, kb = e["qv"], e["kb"]
+            dqv, dk = _empty(M, 2 * d, dev=dev), _empty(M, d, dev=dev)
+            if "ast" in e:
+                ops.gattn_bwd_flash(qv, 2 * d, kb, d, qv[:, d:], 2 * d, Gm, e["flag"], e["flag"],
+                                    B, T, T, H, dz1, d, e["ast"], dqv, 2 * d, dk, d, dqv[:, d:],
+                                    2 * d)
+            else:
+                ops.gattn_bwd(qv, 2 * d, kb, d, qv[:, d:], 2 * d, Gm, e["flag"], e["flag"], B, T,
+                              T, H, dz1, d, dqv, 2 * d, dk, d, dqv[:, d:], 2 * d)
+            dxn = _empty(M, d, dev=dev)
+            ops.linear_dw(dk, e["x"], Lg["Wqkv"][d:2 * d], Lg["bqkv"][d:2 * d], rows=M)
+            ops.linear_dx(dk, L["Wqkv"][d:2 * d], dxn, rows=M, resid=dz1)
+            for off in (0, 2 * d):  # dW_q, dW_v over the question rows (k-row gathers)
+                ops.gemm(dqv[:, off // 2:], e["x"], Lg["Wqkv"][off:off + d], d, d, B * Lq,
+                         lda=2 * d, ldb=d, ldc=d, a_trans=True, a_rows=s.qrows, b_rows=s.qrows,
+                         atomic=True, split_k=-1, colsum_a=Lg["bqkv"][off:off + d])
+            ops.gemm(dqv, L["Wqkv"], dxn, B * Lq, d, 2 * d, lda=2 * d, ldb=d, ldc=d,
+                     a_rows=s.qrows, b_rows=_qv_wrows(d, dev), c_group=Lq, c_stride=T,
+                     c_offset=Nn, beta=1.0)
+            del dqv, dk
+            dx = dxn
+            if i > 0:
+                mark(f"enc_feed_forward_{i - 1}.normalization.gamma")
+            continue
         qkv = e["qkv"]
         dqkv = (_bf if lp is not None else _empty)(M, 3 * d, dev=dev)
         if "ast" in e:
