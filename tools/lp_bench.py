@@ -51,9 +51,10 @@ def bf16_case(lay, m, n, k, out, hint=0):
     elif out == "bf16":
         Cb = torch.empty(m, n, device=dev, dtype=BF)
         f = lambda: ops.gemm_lp(A, B, m, n, k, Cb=Cb, ldcb=n, relu=True, tile_hint=hint, **kw)
-    elif out == "atomic":
+    elif out.startswith("atomic"):  # "atomic" (library split) or "atomicS" (split_k = S)
         C = torch.zeros(m, n, device=dev)
-        f = lambda: ops.gemm_lp(A, B, m, n, k, C=C, ldc=n, atomic=True, split_k=-1,
+        sk = int(out[6:]) if len(out) > 6 else -1
+        f = lambda: ops.gemm_lp(A, B, m, n, k, C=C, ldc=n, atomic=True, split_k=sk,
                                 tile_hint=hint, **kw)
     else:
         C = torch.empty(m, n, device=dev)
@@ -105,6 +106,18 @@ def main():
         cases = cases[1:4] + cases[6:7] + cases[10:11]
     if "--fp8" in sys.argv:  # only the cfg-5 fp8 region-feature GEMMs
         cases = []
+    custom = [a for a in sys.argv[1:] if a.count(":") == 4]  # LAYOUT:M:N:K:OUT
+    if custom:
+        cases = [(a, a.split(":")[0], int(a.split(":")[1]), int(a.split(":")[2]),
+                  int(a.split(":")[3]), a.split(":")[4]) for a in custom]
+    if "--dwvar" in sys.argv:  # the weight-gradient shapes on every kernel variant
+        hints = [1, 3, 4, 5]
+        cases = [c for c in cases if c[0].startswith("dw")]
+    if "--splits" in sys.argv:  # split-K factor sweep of the weight-gradient shapes
+        cases = [(f"{nm} s{sk}", "TN", m, n, k, "atomic" + (str(sk) if sk > 0 else ""))
+                 for nm, m, n, k in (("dw ffn1", 2048, 512, Ms), ("dw qkv", 1536, 512, Ms),
+                                     ("dw ffn2", 512, 2048, Ms))
+                 for sk in (-1, 2, 3, 4, 6, 8, 12)]
     tot_f = 0.0
     tot_t = {h: 0.0 for h in hints}
     for name, lay, m, n, k, out in cases:
