@@ -1054,9 +1054,55 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X
 }
 }  // namespace savqa
 
+// Wide form (cols % 4 == 0, 16-B aligned rows): each lane sums 4 consecutive columns with
+// 16-B loads (a wave covers 256 columns of a row, four rows in flight per lane), the 4 waves
+// of a block take interleaved rows of its row chunk and fold through LDS before one atomicAdd
+// per column and block (the 4-B-per-lane form above: 25.7 us for the 37376 x 512 bias
+// gradients of cfg 3, ~3 TB/s).
+namespace savqa {
+__global__ __launch_bounds__(256) void colsum_wide_kernel(const float* __restrict__ X, int64_t rows,
+                                                          int64_t cols, int64_t ldx, int64_t rchunk,
+                                                          float* __restrict__ out) {
+  __shared__ f4 part[4][64];
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 256 + 4 * lane;
+  const int64_t r0 = (int64_t)blockIdx.y * rchunk;
+  const int64_t r1 = min(rows, r0 + rchunk);
+  f4 s = {0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    int64_t r = r0 + sl;
+    for (; r + 12 < r1; r += 16) {
+      f4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f4*>(X + (r + 4 * u) * ldx + c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; r < r1; r += 4) s += *reinterpret_cast<const f4*>(X + r * ldx + c);
+  }
+  part[sl][lane] = s;
+  __syncthreads();
+  if (sl == 0 && c < cols) {
+    const f4 t = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) atomicAdd(&out[c + q], t[q]);
+  }
+}
+}  // namespace savqa
+
 extern "C" int savqa_colsum_acc(void* stream, const float* X, int64_t rows, int64_t cols,
                                 int64_t ldx, float* out) {
   if (rows <= 0 || cols <= 0) return 0;
+  if (cols % 4 == 0 && ldx % 4 == 0 && aligned16(X)) {
+    const int64_t cb = (cols + 255) / 256;
+    int64_t chunks = (2048 + cb - 1) / cb;
+    int64_t rchunk = (rows + chunks - 1) / chunks;
+    if (rchunk < 64) rchunk = 64;
+    chunks = (rows + rchunk - 1) / rchunk;
+    hipLaunchKernelGGL(colsum_wide_kernel, dim3((unsigned)cb, (unsigned)chunks), dim3(256), 0,
+                       as_stream(stream), X, rows, cols, ldx, rchunk, out);
+    return check_launch("savqa_colsum_acc");
+  }
   const int64_t cb = (cols + 63) / 64;
   int64_t chunks = (2048 + cb - 1) / cb;
   int64_t rchunk = (rows + chunks - 1) / chunks;

@@ -221,6 +221,19 @@ def test_colsum_bf16_shapes(rows, cols, ld):
     assert rel(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("rows,cols,ld", [(37376, 512, 512), (1000, 300, 304), (77, 2048, 2052),
+                                           (5, 12, 12), (4096, 1536, 1536)])
+def test_colsum_fp32_shapes(rows, cols, ld):
+    """savqa_colsum_acc (fp32 bias-gradient column sums, 16-B-per-lane form where the rows
+    allow, the 4-B form otherwise) accumulates into an existing vector."""
+    O = ops()
+    g = torch.Generator(device=dev).manual_seed(rows + cols)
+    X = torch.randn(rows, ld, generator=g, device=dev)
+    out = torch.ones(cols, device=dev)
+    O.colsum_acc(X, rows, cols, ld, out)
+    assert rel(out - 1, X[:, :cols].double().sum(0)) < 1e-5
+
+
 def test_gather_rows_bf16_zero_padded():
     """GloVe rows of a token list into a 304-column bf16 matrix (the K = 300 embedding GEMMs
     of the low-precision modes): bf16 of the rows, pad columns zero."""
