@@ -38,6 +38,9 @@ namespace savqa {
 #ifndef SAVQA_GEMM_PLAN_OCC
 #define SAVQA_GEMM_PLAN_OCC 3
 #endif
+#ifndef SAVQA_GEMM_CU_TAIL
+#define SAVQA_GEMM_CU_TAIL 1
+#endif
 constexpr int GEMM_OCC = SAVQA_GEMM_OCC;
 constexpr int GEMM_PLAN_OCC = SAVQA_GEMM_PLAN_OCC;
 constexpr int GEMM_BK = 16;   // k-tile; 16 beats 32 on the K=512 step shapes (shorter prologue)
@@ -944,12 +947,20 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
     const char* r1 = (const char*)(d.resid + (d.M - 1) * d.ldr + d.N);
     if (r0 < c1 && c0 < r1) tail_ok = false;
   }
-  if (tail_ok && T > slots) {
+  // Underfilled single round (SAVQA_GEMM_CU_TAIL): T tiles over `cus` CUs put
+  // ceil(T / cus) tiles on some CUs while the average is T / cus (the N = 512 step shapes:
+  // 584 tiles = 2.28 per CU, so 3 tile-times per launch). Whole tiles for k = floor(T / cus)
+  // per CU, the r left over split into f <= cus / r k-slices dispatched after them: at most
+  // k tiles + one slice per CU.
+  const int cus = slots / GEMM_PLAN_OCC;
+  const bool cu_tail = SAVQA_GEMM_CU_TAIL && tail_ok && T <= slots && T > cus;
+  if (tail_ok && (T > slots || cu_tail)) {
     const int64_t nch = (d.K + BK - 1) / BK;
-    int r = T % slots;
+    const int cap = cu_tail ? cus : slots;
+    int r = cu_tail ? T - (T / cus) * cus : T % slots;
     r = (r + tn - 1) / tn * tn;  // whole rows of tiles: one contiguous zero-fill
     if (r > 0 && r < T) {
-      int f = slots / r;
+      int f = cap / r;
       if (f > nch / 4) f = (int)(nch / 4);
       if (f >= 2) {
         p.gg.full = T - r;
