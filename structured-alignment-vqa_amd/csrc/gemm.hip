@@ -961,6 +961,19 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
     r = (r + tn - 1) / tn * tn;  // whole rows of tiles: one contiguous zero-fill
     if (r > 0 && r < T) {
       int f = cap / r;
+      if (cu_tail) {
+        // slices per left-over tile minimising the per-CU time k + ceil(r f / cus) / f
+        // (in whole-tile times) within one round of slots, e.g. 400 tiles = 256 + 144 x 3
+        // slices: 1.67 instead of 2 tile-times
+        const int k = T / cus;
+        double best = k + 1.0;
+        f = 1;
+        for (int g = 2; g <= 8 && g <= nch / 4; ++g) {
+          if ((int64_t)k * cus + (int64_t)r * g > slots) break;
+          const double t = k + (double)((r * g + cus - 1) / cus) / g;
+          if (t < best - 1e-9) { best = t; f = g; }
+        }
+      }
       if (f > nch / 4) f = (int)(nch / 4);
       if (f >= 2) {
         p.gg.full = T - r;
