@@ -25,7 +25,22 @@
 namespace savqa {
 
 constexpr int FL_KT = 64;   // keys (or queries) per staged tile
-constexpr int FL_WLD = 20;  // per-wave transposed image, [64][16 + 4] floats
+constexpr int FL_WLD = 16;  // per-wave transposed image, [64][16] floats, rows placed by fl_img
+constexpr int FL_WLDP = 20;  // padded [64][16 + 4] image of the dQ kernel (fl_imgp)
+
+// Float offset of element (r, f) of a per-wave [64][16] image. Unpadded (64 B rows), so the
+// 4-wave forward workgroup takes 51200 B of LDS and three fit a CU (55296 B with 20-float
+// padded rows: two). Rows are placed so that the 16-B column-group writes (lanes: 16
+// consecutive rows r, one group f = 4g) and the row reads of fl_accum (lanes: 16 columns of
+// the 4 rows j, j+4, j+8, j+12) both fall on distinct banks: the row's 64-B window is
+// (r + r/4) mod 4 of its 4-row block, and the column group is XORed with (r/4) mod 4.
+__device__ __forceinline__ int fl_img(int r, int f) {
+  const int h = (r >> 2) & 3;
+  return (((r & ~3) | ((r + h) & 3)) << 4) + (f ^ (h << 2));
+}
+// The dQ kernel keeps the padded image: it is register-bound at two workgroups per CU either
+// way, and fl_img's address arithmetic took it from 254 to 268 registers (one wave per SIMD).
+__device__ __forceinline__ int fl_imgp(int r, int f) { return r * FL_WLDP + f; }
 
 // Cooperative stage of rows [r0, r0 + 64) of X and Y (head slice hd) into LDS, zero past lim.
 __device__ __forceinline__ void fl_stage2(const float* X, int64_t ldx, const float* Y, int64_t ldy,
@@ -52,6 +67,7 @@ __device__ __forceinline__ void fl_load_strip(const float* X, int64_t ldx, int64
 }
 
 // acc[dt] += sum over the 64 rows j of the tile: img[j][col] (A: m = col, k = j) * Ys[j][16dt+col]
+template <bool PAD = false>
 __device__ __forceinline__ void fl_accum(const float* img, const float* Ys, int col, int g,
                                          f4v (&acc)[4]) {
 #pragma unroll
@@ -59,7 +75,7 @@ __device__ __forceinline__ void fl_accum(const float* img, const float* Ys, int 
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = jc * 16 + 4 * g + t;
-      const float av = img[j * FL_WLD + col];
+      const float av = img[PAD ? fl_imgp(j, col) : fl_img(j, col)];
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma16(av, Ys[j * ATT_KLD + dt * 16 + col], acc[dt]);
     }
@@ -150,7 +166,7 @@ __global__ __launch_bounds__(256) void gattn_fwd_flash_kernel(AttnArgs a, float*
     }
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt)
-      *reinterpret_cast<f4v*>(&Pw[(jt * 16 + col) * FL_WLD + 4 * g]) = pv[jt];
+      *reinterpret_cast<f4v*>(&Pw[fl_img(jt * 16 + col, 4 * g)]) = pv[jt];
     __builtin_amdgcn_wave_barrier();
     fl_accum(Pw, Vs, col, g, o);
   }
@@ -219,7 +235,7 @@ __global__ __launch_bounds__(256) void gattn_bwd_kv_flash_kernel(AttnArgs a,
   float* Qs = sm;                                  // [64][KLD]
   float* dOs = Qs + FL_KT * ATT_KLD;               // [64][KLD]
   float* cf = dOs + FL_KT * ATT_KLD;               // [64][8] per-query coefficients
-  float* Nimg = cf + FL_KT * 8 + w * 2 * FL_KT * FL_WLD;  // [64 queries][20] (keys 4g+r)
+  float* Nimg = cf + FL_KT * 8 + w * 2 * FL_KT * FL_WLD;  // [64 queries][16] (keys 4g+r)
   float* Simg = Nimg + FL_KT * FL_WLD;
   const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
   const int hd = h * ATT_DK;
@@ -284,8 +300,8 @@ __global__ __launch_bounds__(256) void gattn_bwd_kv_flash_kernel(AttnArgs a,
         const float ds = n * c0.z * dp[jt][r] - c0.w * e * fabsf(gg) - pd * e;
         dsv[jt][r] = kf[r] == 0.f ? 0.f : ds;
       }
-      *reinterpret_cast<f4v*>(&Nimg[(jt * 16 + col) * FL_WLD + 4 * g]) = nv[jt];
-      *reinterpret_cast<f4v*>(&Simg[(jt * 16 + col) * FL_WLD + 4 * g]) = dsv[jt];
+      *reinterpret_cast<f4v*>(&Nimg[fl_img(jt * 16 + col, 4 * g)]) = nv[jt];
+      *reinterpret_cast<f4v*>(&Simg[fl_img(jt * 16 + col, 4 * g)]) = dsv[jt];
     }
     __builtin_amdgcn_wave_barrier();
     fl_accum(Nimg, dOs, col, g, dv);  // dV_j += sum_i nq_ij dO_i
@@ -322,7 +338,7 @@ __global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
   const int i0 = qt * 16 * nw + w * 16;
   float* Ks = sm;
   float* Vs = Ks + FL_KT * ATT_KLD;
-  float* Simg = Vs + FL_KT * ATT_KLD + w * FL_KT * FL_WLD;  // [64 keys][20] (queries 4g+r)
+  float* Simg = Vs + FL_KT * ATT_KLD + w * FL_KT * FL_WLDP;  // [64 keys][20] (queries 4g+r)
   const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
   const int hd = h * ATT_DK;
   const float* sth = stats + ((int64_t)b * a.H + h) * a.Tq * 4;
@@ -436,9 +452,9 @@ __global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
     }
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt)
-      *reinterpret_cast<f4v*>(&Simg[(jt * 16 + col) * FL_WLD + 4 * g]) = dsv[jt];
+      *reinterpret_cast<f4v*>(&Simg[fl_imgp(jt * 16 + col, 4 * g)]) = dsv[jt];
     __builtin_amdgcn_wave_barrier();
-    fl_accum(Simg, Ks, col, g, dq);  // dQ_i += sum_j dS_ij K_j   (x 1/8 at the end)
+    fl_accum<true>(Simg, Ks, col, g, dq);  // dQ_i += sum_j dS_ij K_j   (x 1/8 at the end)
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -509,7 +525,7 @@ extern "C" int savqa_gattn_bwd_flash(void* stream, const float* q, int64_t ldq, 
   {  // dQ first: it also writes delta (stats[..][3]) for the dK/dV pass
     const int nw = waves_for((int)Tq);
     const int nqt = (int)((Tq + 16 * nw - 1) / (16 * nw));
-    const size_t lds = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + (size_t)nw * FL_KT * FL_WLD);
+    const size_t lds = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + (size_t)nw * FL_KT * FL_WLDP);
     hipLaunchKernelGGL(gattn_bwd_q_flash_kernel, dim3((unsigned)(B * H * nqt)), dim3(64 * nw), lds,
                        s, a, stats, nqt);
     if (int rc = check_launch("savqa_gattn_bwd_flash(dq)")) return rc;

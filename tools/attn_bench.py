@@ -29,17 +29,21 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--bf16", action="store_true", help="bf16 Q/K/V storage (cfg-3 mode)")
-    ap.add_argument("--B", type=int, default=256)
+    ap.add_argument("--B", type=int, nargs="*", default=[256])
     ap.add_argument("--T", type=int, nargs="*", default=[73, 50])
     ap.add_argument("--q1", action="store_true",
                     help="decoder cross-attention: one fp32 query per sample, K/V of T rows")
+    ap.add_argument("--flash", action="store_true",
+                    help="key-tiled kernels (T > 128: cfg 4, super-node relation graphs), fp32")
     args = ap.parse_args()
     if args.q1:
         return q1_main(args)
+    if args.flash:
+        return flash_main(args)
     H, dk = 8, 64
     d = H * dk
     dt = torch.bfloat16 if args.bf16 else torch.float32
-    for B, T in ((args.B, t) for t in args.T):
+    for B, T in ((args.B[0], t) for t in args.T):
         qkv = torch.randn(B * T, 3 * d, device=dev).relu_().to(dt)
         G = (torch.rand(B, T, T, device=dev) < 0.3).float()
         flag = torch.ones(B * T, device=dev)
@@ -61,13 +65,40 @@ def main():
               f"bwd {tb*1e6:7.1f} us {bb/tb/1e9:6.0f} GB/s {bfl/tb/1e12:5.1f} TF", flush=True)
 
 
+def flash_main(args):
+    """gattn_{fwd,bwd}_flash at B x T (e.g. --B 4 --T 1314: the relation workload's stack);
+    the backward is reported as its two launches together (dQ, then dK / dV)."""
+    H, dk = 8, 64
+    d = H * dk
+    pairs = zip(args.B, args.T) if len(args.B) == len(args.T) else ((args.B[0], t) for t in args.T)
+    for B, T in pairs:
+        qkv = torch.randn(B * T, 3 * d, device=dev).relu_()
+        G = (torch.rand(B, T, T, device=dev) < 0.3).float()
+        flag = torch.ones(B * T, device=dev)
+        o = torch.empty(B * T, d, device=dev)
+        st = torch.empty(B * H * T, 4, device=dev)
+        dout = torch.randn(B * T, d, device=dev)
+        dqkv = torch.zeros(B * T, 3 * d, device=dev)
+        f = lambda: ops.gattn_fwd_flash(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G,
+                                        flag, flag, B, T, T, H, o, d, st)
+        g = lambda: ops.gattn_bwd_flash(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G,
+                                        flag, flag, B, T, T, H, dout, d, st, dqkv, 3 * d,
+                                        dqkv[:, d:], 3 * d, dqkv[:, 2 * d:], 3 * d)
+        tf = timeit(f)
+        tb = timeit(g)
+        ffl = B * H * 4 * T * T * dk
+        bfl = B * H * 14 * T * T * dk  # dQ: S, dN twice + dS K; dK/dV: S, dN, dV, dK
+        print(f"flash B={B} T={T}: fwd {tf*1e6:7.1f} us {ffl/tf/1e12:5.1f} TF | "
+              f"bwd {tb*1e6:7.1f} us {bfl/tb/1e12:5.1f} TF", flush=True)
+
+
 def q1_main(args):
     """T_q = 1 kernels (gattn_{fwd,bwd}_q1): bytes = K, V read + dK, dV written (+ q, o)."""
     H, dk = 8, 64
     d = H * dk
     dt = torch.bfloat16 if args.bf16 else torch.float32
     es = 2 if args.bf16 else 4
-    for B, T in ((args.B, t) for t in args.T):
+    for B, T in ((args.B[0], t) for t in args.T):
         q = torch.randn(B, d, device=dev).relu_()
         kv = torch.randn(B * T, 2 * d, device=dev).relu_().to(dt)
         G = (torch.rand(B, 1, T, device=dev) < 0.3).float()
