@@ -220,7 +220,7 @@ __device__ __forceinline__ void coef_delta(RowCoef& c, float dl) {
 
 // ------------------------------------------------------------------------- dK / dV
 // grid = B*H*nkt2 (key tiles of 16*nw keys; wave w owns keys j0 = tile*16nw + 16w)
-__global__ __launch_bounds__(256) void gattn_bwd_kv_flash_kernel(AttnArgs a,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gattn_bwd_kv_flash_kernel(AttnArgs a,
                                                                 const float* __restrict__ stats,
                                                                 int nkt2) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -235,8 +235,7 @@ __global__ __launch_bounds__(256) void gattn_bwd_kv_flash_kernel(AttnArgs a,
   float* Qs = sm;                                  // [64][KLD]
   float* dOs = Qs + FL_KT * ATT_KLD;               // [64][KLD]
   float* cf = dOs + FL_KT * ATT_KLD;               // [64][8] per-query coefficients
-  float* Nimg = cf + FL_KT * 8 + w * 2 * FL_KT * FL_WLD;  // [64 queries][16] (keys 4g+r)
-  float* Simg = Nimg + FL_KT * FL_WLD;
+  float* img = cf + FL_KT * 8 + w * FL_KT * FL_WLD;  // [64 queries][16] (keys 4g+r): N, then dS
   const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
   const int hd = h * ATT_DK;
   const float* sth = stats + ((int64_t)b * a.H + h) * a.Tq * 4;
@@ -300,12 +299,16 @@ __global__ __launch_bounds__(256) void gattn_bwd_kv_flash_kernel(AttnArgs a,
         const float ds = n * c0.z * dp[jt][r] - c0.w * e * fabsf(gg) - pd * e;
         dsv[jt][r] = kf[r] == 0.f ? 0.f : ds;
       }
-      *reinterpret_cast<f4v*>(&Nimg[fl_img(jt * 16 + col, 4 * g)]) = nv[jt];
-      *reinterpret_cast<f4v*>(&Simg[fl_img(jt * 16 + col, 4 * g)]) = dsv[jt];
+      *reinterpret_cast<f4v*>(&img[fl_img(jt * 16 + col, 4 * g)]) = nv[jt];
     }
     __builtin_amdgcn_wave_barrier();
-    fl_accum(Nimg, dOs, col, g, dv);  // dV_j += sum_i nq_ij dO_i
-    fl_accum(Simg, Qs, col, g, dk);   // dK_j += sum_i dS_ij Q_i   (x 1/8 at the end)
+    fl_accum(img, dOs, col, g, dv);  // dV_j += sum_i nq_ij dO_i
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+      *reinterpret_cast<f4v*>(&img[fl_img(jt * 16 + col, 4 * g)]) = dsv[jt];
+    __builtin_amdgcn_wave_barrier();
+    fl_accum(img, Qs, col, g, dk);   // dK_j += sum_i dS_ij Q_i   (x 1/8 at the end)
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -534,7 +537,7 @@ extern "C" int savqa_gattn_bwd_flash(void* stream, const float* q, int64_t ldq, 
     const int nw = waves_for((int)Tk);
     const int nkt2 = (int)((Tk + 16 * nw - 1) / (16 * nw));
     const size_t lds = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + FL_KT * 8 +
-                                        (size_t)nw * 2 * FL_KT * FL_WLD);
+                                        (size_t)nw * FL_KT * FL_WLD);
     hipLaunchKernelGGL(gattn_bwd_kv_flash_kernel, dim3((unsigned)(B * H * nkt2)), dim3(64 * nw),
                        lds, s, a, stats, nkt2);
   }
