@@ -17,16 +17,17 @@
 //             backward's own e values, so sum_j dS_ij = 0 holds to rounding)
 //   dS_ij = n_ij (dN_ij - c_i sgn(g_ij) delta_i) - (1 - c_i) P_ij delta_i   (0 on masked keys)
 // i.e. the softmax / L1-normalise adjoints collapse to per-row scalars, so the backward
-// is two tiled kernels: dQ (workgroup per query tile, two sweeps over the key tiles:
-// delta, then dS and dQ) and dK, dV (workgroup per key tile, loop over query tiles), both
-// recomputing S from the saved (m, Z, W). stats = [B*H*Tq][4] floats: m, Z, W, delta.
+// is three tiled kernels: delta (workgroup per query tile, one sweep over the key tiles),
+// dQ (the same tiles, a second sweep: dS and dQ) and dK, dV (workgroup per key tile, loop
+// over query tiles), all recomputing S from the saved (m, Z, W). stats = [B*H*Tq][4]
+// floats: m, Z, W, delta. The delta sweep is its own kernel so that neither sweep holds
+// the other's registers (three and four workgroups per CU instead of two for the fused one).
 #include "attn_common.h"
 
 namespace savqa {
 
 constexpr int FL_KT = 64;   // keys (or queries) per staged tile
 constexpr int FL_WLD = 16;  // per-wave transposed image, [64][16] floats, rows placed by fl_img
-constexpr int FL_WLDP = 20;  // padded [64][16 + 4] image of the dQ kernel (fl_imgp)
 
 // Float offset of element (r, f) of a per-wave [64][16] image. Unpadded (64 B rows), so the
 // 4-wave forward workgroup takes 51200 B of LDS and three fit a CU (55296 B with 20-float
@@ -38,9 +39,6 @@ __device__ __forceinline__ int fl_img(int r, int f) {
   const int h = (r >> 2) & 3;
   return (((r & ~3) | ((r + h) & 3)) << 4) + (f ^ (h << 2));
 }
-// The dQ kernel keeps the padded image: it is register-bound at two workgroups per CU either
-// way, and fl_img's address arithmetic took it from 254 to 268 registers (one wave per SIMD).
-__device__ __forceinline__ int fl_imgp(int r, int f) { return r * FL_WLDP + f; }
 
 // Cooperative stage of rows [r0, r0 + 64) of X and Y (head slice hd) into LDS, zero past lim.
 __device__ __forceinline__ void fl_stage2(const float* X, int64_t ldx, const float* Y, int64_t ldy,
@@ -67,7 +65,6 @@ __device__ __forceinline__ void fl_load_strip(const float* X, int64_t ldx, int64
 }
 
 // acc[dt] += sum over the 64 rows j of the tile: img[j][col] (A: m = col, k = j) * Ys[j][16dt+col]
-template <bool PAD = false>
 __device__ __forceinline__ void fl_accum(const float* img, const float* Ys, int col, int g,
                                          f4v (&acc)[4]) {
 #pragma unroll
@@ -75,7 +72,7 @@ __device__ __forceinline__ void fl_accum(const float* img, const float* Ys, int 
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = jc * 16 + 4 * g + t;
-      const float av = img[PAD ? fl_imgp(j, col) : fl_img(j, col)];
+      const float av = img[fl_img(j, col)];
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma16(av, Ys[j * ATT_KLD + dt * 16 + col], acc[dt]);
     }
@@ -325,14 +322,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   }
 }
 
-// ------------------------------------------------------------------------------ dQ
-// grid = B*H*nqt (query tiles of 16*nw rows), loop over key tiles
-__global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
-                                                               float* __restrict__ stats,
-                                                               int nqt) {
+// --------------------------------------------------------------------------- delta
+// grid = B*H*nqt (query tiles of 16*nw rows), one sweep over the key tiles.
+// dQ_i = sum_j dS_ij K_j / 8 with sum_j dS_ij = 0 analytically: the keys' common part
+// cancels, so any residual of that sum comes back as (residual) x (mean key) -- with
+// near-parallel V rows (dN_ij ~ delta_i) it is larger than dQ itself. The residual of
+// the direct form n (dN - delta) is ~1 ulp of delta (its rounding, and sum_j |n_j| != 1
+// by rounding), which measured 15x torch-fp32's dQ error at T = 1313
+// (tools/dbg/flash_prec.py). So, per row, with a_j = e g qf dp and w_j = e |g| (normal)
+// or e (clamped), both the exact fp32 values the dQ sweep recomputes:
+//   delta sweep: A = sum_j a_j, W' = sum_j e|g|, Z' = sum_j e in fp64;  dx = A / sum_j w_j
+//   dQ sweep:    dS_j = rD (a_j - dx w_j), the bracket in fp64 (sum_j dS_j = 0 to fp64 rounding)
+// i.e. the softmax / L1-normalise adjoint with its common term removed exactly, as torch's
+// softmax backward (x (g - sum x g)) removes it. (W', Z', delta) go to stats for dK / dV;
+// dx travels to the dQ kernel as a float pair (hi, lo) in columns 0-1 of the row's own dQ
+// head slice, which only that kernel's same wave overwrites, after reading it.
+__global__ __launch_bounds__(256) void gattn_bwd_delta_flash_kernel(AttnArgs a,
+                                                                   float* __restrict__ stats,
+                                                                   int nqt) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int nw = blockDim.x >> 6;
-  // XCD-aware: the tiles of a (sample, head) and the heads of a sample share an XCD's L2
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qt = bid % nqt, bh = bid / nqt;
   const int b = bh / a.H, h = bh % a.H;
@@ -341,7 +350,6 @@ __global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
   const int i0 = qt * 16 * nw + w * 16;
   float* Ks = sm;
   float* Vs = Ks + FL_KT * ATT_KLD;
-  float* Simg = Vs + FL_KT * ATT_KLD + w * FL_KT * FL_WLDP;  // [64 keys][20] (queries 4g+r)
   const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
   const int hd = h * ATT_DK;
   const float* sth = stats + ((int64_t)b * a.H + h) * a.Tq * 4;
@@ -349,64 +357,21 @@ __global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
   f4v qa[4], oa[4];
   fl_load_strip(a.q, a.ldq, qb + min(i0 + col, a.Tq - 1), hd, g, qa);
   fl_load_strip(a.dout, a.lddo, qb + min(i0 + col, a.Tq - 1), hd, g, oa);
-  RowCoef rc[4];
+  float rm[4], rq[4];
   const float* grow[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = i0 + 4 * g + r;
     const int ic = min(i, a.Tq - 1);
-    rc[r] = row_coef(sth + (int64_t)ic * 4, a.qflag[qb + ic], i < a.Tq);
+    const RowCoef c = row_coef(sth + (int64_t)ic * 4, a.qflag[qb + ic], i < a.Tq);
+    rm[r] = c.m;
+    rq[r] = c.qf;
     grow[r] = a.G + (qb + ic) * a.Tk;
   }
-  f4v dq[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dq[dt] = f4v{0.f, 0.f, 0.f, 0.f};
   double sa[4] = {0., 0., 0., 0.}, sw[4] = {0., 0., 0., 0.}, sz[4] = {0., 0., 0., 0.};
-  double dx[4] = {0., 0., 0., 0.};
   const int nkt = (a.Tk + FL_KT - 1) / FL_KT;
-  // dQ_i = sum_j dS_ij K_j / 8 with sum_j dS_ij = 0 analytically: the keys' common part
-  // cancels, so any residual of that sum comes back as (residual) x (mean key) -- with
-  // near-parallel V rows (dN_ij ~ delta_i) it is larger than dQ itself. The residual of
-  // the direct form n (dN - delta) is ~1 ulp of delta (its rounding, and sum_j |n_j| != 1
-  // by rounding), which measured 15x torch-fp32's dQ error at T = 1313
-  // (tools/dbg/flash_prec.py). So, per row, with a_j = e g qf dp and w_j = e |g| (normal)
-  // or e (clamped), both the exact fp32 values pass 1 recomputes:
-  //   pass 0: A = sum_j a_j, W' = sum_j e|g|, Z' = sum_j e in fp64;  dx = A / sum_j w_j
-  //   pass 1: dS_j = rD (a_j - dx w_j), the bracket in fp64 (sum_j dS_j = 0 to fp64 rounding)
-  // i.e. the softmax / L1-normalise adjoint with its common term removed exactly, as torch's
-  // softmax backward (x (g - sum x g)) removes it. (W', Z', delta) go to stats for dK / dV.
-  for (int it = 0; it < 2 * nkt; ++it) {
-    const int pass = it >= nkt;
-    const int kt = it - pass * nkt;
+  for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * FL_KT;
-    if (it == nkt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = i0 + 4 * g + r;
-        double A = sa[r], Wd = sw[r], Zd = sz[r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          A += __shfl_xor(A, o, 16);
-          Wd += __shfl_xor(Wd, o, 16);
-          Zd += __shfl_xor(Zd, o, 16);
-        }
-        if (i < a.Tq) {
-          RowCoef& c = rc[r];
-          const float w = (float)Wd, z = (float)Zd;
-          c.normal = w >= 1e-12f * z;
-          const float D = c.normal ? w : 1e-12f * z;
-          c.rD = 1.f / D;
-          const double den = c.normal ? Wd : Zd;
-          dx[r] = den > 0. ? A / den : 0.;
-          if (col == 0) {
-            float* st = stats + (((int64_t)b * a.H + h) * a.Tq + i) * 4;
-            st[1] = z;
-            st[2] = w;
-            st[3] = c.normal ? (float)dx[r] : (float)(dx[r] * (double)c.rD * Zd);
-          }
-        }
-      }
-    }
     __syncthreads();
     fl_stage2(a.k, a.ldk, a.v, a.ldv, kb, k0, a.Tk, hd, Ks, Vs);
     float kf[4], gv[4][4];
@@ -421,22 +386,105 @@ __global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
     f4v s[4], dp[4];
     strip_dots_lds<4>(qa, Ks, col, g, s);   // [query 4g+r][key 16jt+col]
     strip_dots_lds<4>(oa, Vs, col, g, dp);
-    if (!pass) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 4; ++r) {
 #pragma unroll
-        for (int jt = 0; jt < 4; ++jt) {
-          const int j = k0 + jt * 16 + col;
-          const float x = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * 0.125f;
-          const float e = j < a.Tk ? expf(x - rc[r].m) : 0.f;
-          const float gg = gv[r][jt];
-          sa[r] += (double)(e * gg * rc[r].qf * dp[jt][r]);
-          sw[r] += (double)(e * fabsf(gg));
-          sz[r] += (double)e;
-        }
+      for (int jt = 0; jt < 4; ++jt) {
+        const int j = k0 + jt * 16 + col;
+        const float x = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * 0.125f;
+        const float e = j < a.Tk ? expf(x - rm[r]) : 0.f;
+        const float gg = gv[r][jt];
+        sa[r] += (double)(e * gg * rq[r] * dp[jt][r]);
+        sw[r] += (double)(e * fabsf(gg));
+        sz[r] += (double)e;
       }
-      continue;
     }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 4 * g + r;
+    double A = sa[r], Wd = sw[r], Zd = sz[r];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      A += __shfl_xor(A, o, 16);
+      Wd += __shfl_xor(Wd, o, 16);
+      Zd += __shfl_xor(Zd, o, 16);
+    }
+    if (i < a.Tq && col == 0) {
+      const float wf = (float)Wd, zf = (float)Zd;
+      const bool normal = wf >= 1e-12f * zf;
+      const float rD = 1.f / (normal ? wf : 1e-12f * zf);
+      const double den = normal ? Wd : Zd;
+      const double dx = den > 0. ? A / den : 0.;
+      float* st = stats + (((int64_t)b * a.H + h) * a.Tq + i) * 4;
+      st[1] = zf;
+      st[2] = wf;
+      st[3] = normal ? (float)dx : (float)(dx * (double)rD * Zd);
+      const float hi = (float)dx;
+      float* dxs = a.dq + (qb + i) * a.lddq + hd;
+      dxs[0] = hi;
+      dxs[1] = (float)(dx - (double)hi);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ dQ
+// grid = B*H*nqt (query tiles of 16*nw rows), loop over key tiles; reads (m, Z', W') from
+// stats and dx from the delta kernel (see above)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gattn_bwd_q_flash_kernel(AttnArgs a,
+                                                               const float* __restrict__ stats,
+                                                               int nqt) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int nw = blockDim.x >> 6;
+  // XCD-aware: the tiles of a (sample, head) and the heads of a sample share an XCD's L2
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = bid % nqt, bh = bid / nqt;
+  const int b = bh / a.H, h = bh % a.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = qt * 16 * nw + w * 16;
+  float* Ks = sm;
+  float* Vs = Ks + FL_KT * ATT_KLD;
+  float* Simg = Vs + FL_KT * ATT_KLD + w * FL_KT * FL_WLD;  // [64 keys][16] (queries 4g+r)
+  const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
+  const int hd = h * ATT_DK;
+  const float* sth = stats + ((int64_t)b * a.H + h) * a.Tq * 4;
+
+  f4v qa[4], oa[4];
+  fl_load_strip(a.q, a.ldq, qb + min(i0 + col, a.Tq - 1), hd, g, qa);
+  fl_load_strip(a.dout, a.lddo, qb + min(i0 + col, a.Tq - 1), hd, g, oa);
+  RowCoef rc[4];
+  const float* grow[4];
+  double dx[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 4 * g + r;
+    const int ic = min(i, a.Tq - 1);
+    rc[r] = row_coef(sth + (int64_t)ic * 4, a.qflag[qb + ic], i < a.Tq);
+    grow[r] = a.G + (qb + ic) * a.Tk;
+    const float* dxs = a.dq + (qb + ic) * a.lddq + hd;
+    dx[r] = i < a.Tq ? (double)dxs[0] + (double)dxs[1] : 0.;
+  }
+  f4v dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dq[dt] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int nkt = (a.Tk + FL_KT - 1) / FL_KT;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * FL_KT;
+    __syncthreads();
+    fl_stage2(a.k, a.ldk, a.v, a.ldv, kb, k0, a.Tk, hd, Ks, Vs);
+    float kf[4], gv[4][4];
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) {
+      const int jc = min(k0 + jt * 16 + col, a.Tk - 1);
+      kf[jt] = a.kflag[kb + jc];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gv[r][jt] = grow[r][jc];
+    }
+    __syncthreads();
+    f4v s[4], dp[4];
+    strip_dots_lds<4>(qa, Ks, col, g, s);   // [query 4g+r][key 16jt+col]
+    strip_dots_lds<4>(oa, Vs, col, g, dp);
     f4v dsv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -455,9 +503,9 @@ __global__ __launch_bounds__(256) void gattn_bwd_q_flash_kernel(AttnArgs a,
     }
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt)
-      *reinterpret_cast<f4v*>(&Simg[fl_imgp(jt * 16 + col, 4 * g)]) = dsv[jt];
+      *reinterpret_cast<f4v*>(&Simg[fl_img(jt * 16 + col, 4 * g)]) = dsv[jt];
     __builtin_amdgcn_wave_barrier();
-    fl_accum<true>(Simg, Ks, col, g, dq);  // dQ_i += sum_j dS_ij K_j   (x 1/8 at the end)
+    fl_accum(Simg, Ks, col, g, dq);  // dQ_i += sum_j dS_ij K_j   (x 1/8 at the end)
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -525,10 +573,13 @@ extern "C" int savqa_gattn_bwd_flash(void* stream, const float* q, int64_t ldq, 
   if ((((uintptr_t)dout) & 15) || (lddo & 3))
     return fail(SAVQA_EINVAL, "savqa_gattn_bwd_flash: dO must be 16-B aligned, ld % 4 == 0");
   hipStream_t s = as_stream(stream);
-  {  // dQ first: it also writes delta (stats[..][3]) for the dK/dV pass
+  {  // delta (stats[..][3]) for the dK/dV pass and dx for the dQ pass, then dQ
     const int nw = waves_for((int)Tq);
     const int nqt = (int)((Tq + 16 * nw - 1) / (16 * nw));
-    const size_t lds = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + (size_t)nw * FL_KT * FL_WLDP);
+    hipLaunchKernelGGL(gattn_bwd_delta_flash_kernel, dim3((unsigned)(B * H * nqt)), dim3(64 * nw),
+                       sizeof(float) * (size_t)2 * FL_KT * ATT_KLD, s, a, stats, nqt);
+    if (int rc = check_launch("savqa_gattn_bwd_flash(delta)")) return rc;
+    const size_t lds = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + (size_t)nw * FL_KT * FL_WLD);
     hipLaunchKernelGGL(gattn_bwd_q_flash_kernel, dim3((unsigned)(B * H * nqt)), dim3(64 * nw), lds,
                        s, a, stats, nqt);
     if (int rc = check_launch("savqa_gattn_bwd_flash(dq)")) return rc;
