@@ -250,8 +250,10 @@ int savqa_gattn_fwd_flash(void* stream, const float* q, int64_t ldq, const float
                           const float* qflag, int64_t B, int64_t Tq, int64_t Tk, int64_t H,
                           int64_t dk, float* o, int64_t ldo, float* stats);
 
-/* Backward of savqa_gattn_fwd_flash: dQ (workgroup per query tile; its first sweep also
- * writes delta), then dK/dV (workgroup per key tile), ReLU-masked like savqa_gattn_bwd. */
+/* Backward of savqa_gattn_fwd_flash: delta (workgroup per query tile, one key sweep; writes
+ * stats' Z, W, delta and parks a per-row fp64 term in dq, which must therefore not alias any
+ * input), dQ (second key sweep), then dK/dV (workgroup per key tile); ReLU-masked like
+ * savqa_gattn_bwd. */
 int savqa_gattn_bwd_flash(void* stream, const float* q, int64_t ldq, const float* k, int64_t ldk,
                           const float* v, int64_t ldv, const float* G, const float* kflag,
                           const float* qflag, int64_t B, int64_t Tq, int64_t Tk, int64_t H,
