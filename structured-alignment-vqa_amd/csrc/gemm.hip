@@ -951,15 +951,18 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   // ceil(T / cus) tiles on some CUs while the average is T / cus (the N = 512 step shapes:
   // 584 tiles = 2.28 per CU, so 3 tile-times per launch). Whole tiles for k = floor(T / cus)
   // per CU, the r left over split into f <= cus / r k-slices dispatched after them: at most
-  // k tiles + one slice per CU.
+  // k tiles + one slice per CU. With T <= cus (k = 0: the relation workload's 5256-row
+  // stack, 168 tiles) every tile is split, for K >= 64 k-tiles only: 5256x512x2048 175 ->
+  // 130 us, x1536 129 -> 101 us, but x512 53 -> 56 us (the zero fill and atomics dominate).
   const int cus = slots / GEMM_PLAN_OCC;
-  const bool cu_tail = SAVQA_GEMM_CU_TAIL && tail_ok && T <= slots && T > cus;
+  const bool cu_tail = SAVQA_GEMM_CU_TAIL && tail_ok && T <= slots &&
+                       (T > cus || (d.K + BK - 1) / BK >= 64);
   if (tail_ok && (T > slots || cu_tail)) {
     const int64_t nch = (d.K + BK - 1) / BK;
     const int cap = cu_tail ? cus : slots;
     int r = cu_tail ? T - (T / cus) * cus : T % slots;
     r = (r + tn - 1) / tn * tn;  // whole rows of tiles: one contiguous zero-fill
-    if (r > 0 && r < T) {
+    if (r > 0 && (r < T || cu_tail)) {
       int f = cap / r;
       if (cu_tail) {
         // slices per left-over tile minimising the per-CU time k + ceil(r f / cus) / f

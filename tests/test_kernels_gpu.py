@@ -93,10 +93,13 @@ def test_gemm_dx_dw(M, N, K):
     assert rel(dW2, dY.t() @ table[idx]) < 1e-5
 
 
-@pytest.mark.parametrize("M,N,K", [(16640, 512, 512), (16600, 512, 2048), (18688, 512, 1536)])
+@pytest.mark.parametrize("M,N,K", [(16640, 512, 512), (16600, 512, 2048), (18688, 512, 1536),
+                                   (5256, 512, 2048), (5256, 512, 512)])
 def test_gemm_tail_split(M, N, K):
     """More 128x128 tiles than one wave of workgroups: the partial last wave is split
-    over K (zero-fill + atomics) when the epilogue is linear; relu/beta keep one pass."""
+    over K (zero-fill + atomics) when the epilogue is linear; relu/beta keep one pass.
+    (5256 rows x 512: 168 tiles, fewer than the chip's CUs -- the relation workload's
+    B = 4 x T_syb = 1314 stack.)"""
     O = ops()
     X, W, b = g(M, K, seed=30), g(N, K, seed=31), g(N, seed=32)
     res = g(M, N, seed=33)
