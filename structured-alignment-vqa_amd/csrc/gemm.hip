@@ -433,76 +433,8 @@ __global__ __launch_bounds__(GEMM_NT, GEMM_OCC) __attribute__((amdgpu_waves_per_
   }
 
   // ---------------------------------------------------------------- epilogue
-  const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
-  // Operands of the epilogue are fetched before a fragment's first store: vmcnt also
-  // counts stores, so a load issued after a store waits for it, and one load per element
-  // (bias, ReLU-backward mask, residual) serialised a memory round trip per element.
-  //   bias: FN values per lane and the mask bits (rows indexed by m) for the whole tile,
-  //   the residual per 32-row fragment (a whole tile's would spill).
-  const bool mask_pre = d.mask && !d.mask_arows;
-  const bool res_pre = first_split && d.resid != nullptr;
-  float bv[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int64_t n = min(n0 + wn * WN + j * MI::FR + MI::col(lane), (int64_t)d.N - 1);
-    bv[j] = (first_split && d.bias) ? d.bias[n] : 0.f;
-  }
-  uint32_t keep[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    keep[i] = 0xffffffffu;
-    if (mask_pre) {  // this fragment's mask bits (a whole tile's up front spilled)
-      float mv[MI::NACC][FN];
-#pragma unroll
-      for (int r = 0; r < MI::NACC; ++r) {
-        const int64_t m = min(m0 + wm * WM + i * MI::FR + MI::row(r, lane), (int64_t)d.M - 1);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int64_t n = min(n0 + wn * WN + j * MI::FR + MI::col(lane), (int64_t)d.N - 1);
-          mv[r][j] = d.mask[m * d.ldmask + n];
-        }
-      }
-      keep[i] = 0;
-#pragma unroll
-      for (int r = 0; r < MI::NACC; ++r)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) keep[i] |= (mv[r][j] > 0.f ? 1u : 0u) << (r * FN + j);
-    }
-    float rv[MI::NACC][FN];  // this fragment's residual values (32 registers)
-#pragma unroll
-    for (int r = 0; r < MI::NACC; ++r) {
-      const int64_t m = min(m0 + wm * WM + i * MI::FR + MI::row(r, lane), (int64_t)d.M - 1);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int64_t n = min(n0 + wn * WN + j * MI::FR + MI::col(lane), (int64_t)d.N - 1);
-        rv[r][j] = res_pre ? d.resid[m * d.ldr + n] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < MI::NACC; ++r) {
-      const int64_t m = m0 + wm * WM + i * MI::FR + MI::row(r, lane);
-      if (m >= d.M) continue;
-      const EpiRow er = epi_row(d, m, ident);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int64_t n = n0 + wn * WN + j * MI::FR + MI::col(lane);
-        if (n >= d.N) continue;
-        // savqa_gemm epilogue (include/savqa.h), operands prefetched above
-        float v = acc[i][j][r] * d.alpha + bv[j];
-        if (first_split && d.rowvec) v += d.rowvec[er.pr * d.ldrv + n];
-        if (d.relu) v = fmaxf(v, 0.f);
-        v *= er.rs;
-        if (d.mask && (mask_pre ? !((keep[i] >> (r * FN + j)) & 1u)
-                                : !(d.mask[er.mr * d.ldmask + n] > 0.f)))
-          v = 0.f;
-        v += rv[r][j];
-        float* cp = er.crow + n;
-        if (atomic) atomicAdd(cp, v);
-        else if (d.beta != 0.f) *cp = v + d.beta * *cp;
-        else *cp = v;
-      }
-    }
-  }
+  static_assert(MI::FR == 16 && MI::NACC == 4, "16x16 accumulator layout");
+  gemm_epilogue16<FM, FN, WM, WN>(d, acc, m0, n0, wm, wn, lane, first_split, atomic);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -841,16 +773,16 @@ __global__ __launch_bounds__(64 * NW) void gemm_skinny16_kernel(savqa_gemm_desc 
     else hipLaunchKernelGGL((K_<AT_, BT_, SK_WAVES, false, false>), g, b, 0, s, d, tn, avec, bvec);               \
   } while (0)
 
-static int slots_per_launch() {
-  // 2 workgroups per CU (launch bounds / LDS); the CU count of the current device
+static int cu_count() {
+  // the CU count of the current device
   static int cached[64] = {0};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 512;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
   if (!cached[dev]) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
-    cached[dev] = GEMM_PLAN_OCC * cus;
+    cached[dev] = cus;
   }
   return cached[dev];
 }
@@ -897,11 +829,12 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.rowvec && d.rowvec_period <= 0) return fail(SAVQA_EINVAL, "savqa_gemm: rowvec_period");
   if (d.split_k < 0 && !d.atomic) return fail(SAVQA_EINVAL, "savqa_gemm: auto split-K needs atomic=1");
   if (d.colsum_a && !d.a_trans) return fail(SAVQA_EINVAL, "savqa_gemm: colsum_a needs a_trans=1");
-  if (d.prec != 0 && d.prec != 3)
-    return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32) or 3 (3xbf16)");
-  // gemm_bf16_kernel k-tile: 32
+  if (d.prec != 0 && d.prec != 3 && d.prec != 6)
+    return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32), 3 (3xbf16) or 6 (fp32 x6)");
+  // gemm_bf16_kernel / gemm_x6_kernel k-tile: 32; workgroups per CU the planner counts
   const int BK = d.prec ? 32 : (d.a_trans ? GEMM_BK_DW : GEMM_BK);
-  const int slots = slots_per_launch();
+  const int occ = d.prec == 6 ? 2 : GEMM_PLAN_OCC;
+  const int slots = occ * cu_count();
   const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
   int split = d.split_k > 1 ? d.split_k : 1;
   if (d.split_k < 0) split = auto_split(tiles128, d.K, BK, slots);
@@ -954,7 +887,7 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   // k tiles + one slice per CU. With T <= cus (k = 0: the relation workload's 5256-row
   // stack, 168 tiles) every tile is split, for K >= 64 k-tiles only: 5256x512x2048 175 ->
   // 130 us, x1536 129 -> 101 us, but x512 53 -> 56 us (the zero fill and atomics dominate).
-  const int cus = slots / GEMM_PLAN_OCC;
+  const int cus = slots / occ;
   const bool cu_tail = SAVQA_GEMM_CU_TAIL && tail_ok && T <= slots &&
                        (T > cus || (d.K + BK - 1) / BK >= 64);
   if (tail_ok && (T > slots || cu_tail)) {
@@ -1031,11 +964,20 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   const int avec = (d.lda % 4 == 0) && aligned16(d.A);
   const int bvec = (d.ldb % 4 == 0) && aligned16(d.B);
   hipStream_t s = as_stream(stream);
+  if (p.tile == 128 && d.prec == 6 &&
+      (!avec || !bvec || (d.a_trans && d.a_rows) || (!d.b_trans && d.b_rows))) {
+    // unaligned operands and k-row gathers (guarded loads only in the x6 kernel) take the
+    // fp32 kernel
+    d.prec = 0;
+    if (int rc = plan_gemm(d, p)) return rc;
+  }
   if (p.zero_row0 >= 0 &&
       hipMemset2DAsync(d.C + p.zero_row0 * d.ldc, d.ldc * sizeof(float), 0, d.N * sizeof(float),
                        d.M - p.zero_row0, s) != hipSuccess)
     return fail(SAVQA_EUNSUP, "savqa_gemm: tail zero-fill failed");
-  if (p.tile == 128 && d.prec != 0) {
+  if (p.tile == 128 && d.prec == 6) {
+    savqa_launch_gemm_x6(d, p.gg, p.grid_x, p.nsplit, s);
+  } else if (p.tile == 128 && d.prec != 0) {
     savqa_launch_gemm_bf16(d, p.gg, p.grid_x, p.nsplit, s, avec, bvec);
   } else if (p.tile == 128) {
     dispatch_layout<128, 128, GEMM_BK>(d, p, s, avec, bvec);

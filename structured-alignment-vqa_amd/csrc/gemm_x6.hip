@@ -1,0 +1,324 @@
+// fp32 GEMM on the bf16 matrix cores of gfx950 (savqa_gemm_desc.prec = 6).
+//
+// Same operator, operand layouts, epilogues and launch plan as gemm_f32_kernel (gemm.hip);
+// only the products move from v_mfma_f32_16x16x4_f32 (64 FLOP/clk/SIMD) to
+// v_mfma_f32_16x16x32_bf16 (1024 FLOP/clk/SIMD). Every fp32 operand value is split EXACTLY
+// into three bf16 terms while its tile is staged,
+//   a = a0 + a1 + a2,  a0 = bf16(a), a1 = bf16(a - a0), a2 = a - a0 - a1
+// (round to nearest even; a - a0 and a - a0 - a1 are exact fp32 differences, and the last
+// remainder has at most 8 significant bits, so a2 is a bf16 value: the split loses nothing),
+// and each product is the sum of the six terms of order <= 2:
+//   a*b = a0 b0 + (a0 b1 + a1 b0) + (a0 b2 + a1 b1 + a2 b0)      [+ a1 b2 + a2 b1 + a2 b2]
+// The dropped bracket is below 2^-23 |a b| in the worst case (|a1| <= 2^-8 |a|, |a2| <= 2^-16
+// |a|; typically 2^-26), bf16 x bf16 products are exact in the fp32 accumulator, and the
+// accumulation is fp32 -- the accuracy of an fp32 GEMM (tests/test_kernels_gpu.py holds it to
+// the native fp32 kernel's error against fp64 on every cfg-2 step shape) at 6/16 of the fp32
+// MFMA's cycles per product.
+//
+// Tiling: 256 threads = 4 waves (2x2), 128x128 outputs, k-tile 32; each wave owns 64x64 =
+// 4x4 fragments of 16x16. Operand tiles are register-staged (float4 global loads issued one
+// k-tile ahead, a whole k-tile of MFMAs -- 96 per wave -- to land), split in registers and
+// written as three bf16 planes per operand into ONE LDS stage (48 KB: two workgroups per
+// CU), two barriers per k-tile. Plane images are k-major for both operands: [128 rows][32 k]
+// bf16 (64-B rows), 16-B chunk c of row r at chunk c ^ S[(r >> 2) & 3], S = {0, 2, 3, 1}, so
+// a fragment (16 rows x 8 k per lane group) is one conflict-free ds_read_b128 over every
+// lane group of gfx950. k-contiguous operands (X, W of the forward; dY of dX) store their
+// float4s as they are; m-contiguous ones (W of dX; dY^T and X of dW) are loaded as 4k x 4m
+// blocks and transposed in registers before their ds_write_b64s.
+#include "gemm_common.h"
+
+namespace savqa {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int X6_TILE = 128;
+constexpr int X6_BK = 32;
+constexpr int X6_ROWB = X6_BK * 2;           // bytes per plane row
+constexpr int X6_PLANE = X6_TILE * X6_ROWB;  // bytes per plane (8 KB)
+constexpr int X6_OCC = 2;                    // workgroups per CU (VGPR-limited)
+
+// chunk XOR of plane row r: S[(r >> 2) & 3], S = {0, 2, 3, 1}
+__device__ __forceinline__ int x6_swz(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }
+
+__device__ __forceinline__ int x6_off(int r, int k) {  // byte offset of (row, k) in a plane
+  return r * X6_ROWB + ((((k >> 3) ^ x6_swz(r))) << 4) + (k & 7) * 2;
+}
+
+// exact three-term split of four fp32 values
+__device__ __forceinline__ void split3(f4 v, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
+  p0 = __builtin_convertvector(v, bf16x4);
+  const f4 r1 = v - __builtin_convertvector(p0, f4);
+  p1 = __builtin_convertvector(r1, bf16x4);
+  const f4 r2 = r1 - __builtin_convertvector(p1, f4);
+  p2 = __builtin_convertvector(r2, bf16x4);
+}
+
+__device__ __forceinline__ void put3(char* img, int off, f4 v) {
+  bf16x4 p0, p1, p2;
+  split3(v, p0, p1, p2);
+  *reinterpret_cast<bf16x4*>(img + off) = p0;
+  *reinterpret_cast<bf16x4*>(img + X6_PLANE + off) = p1;
+  *reinterpret_cast<bf16x4*>(img + 2 * X6_PLANE + off) = p2;
+}
+
+// One operand's share of a 128 x 32 tile: 4 float4 per thread.
+//   ROW (k contiguous in memory): float4 u = tid + 256 it covers tile row u / 8, k 4 (u % 8).
+//   COL (m contiguous): thread (g = tid / 8, kg = tid % 8) owns tile rows 4g .. 4g+3 and
+//        k 4kg .. 4kg+3; float4 it = k row 4kg + it (16 B at column 4g), transposed at store
+//        time. (Each 16-lane store group then covers two rows of opposite parity in full:
+//        conflict-free ds_write_b64.)
+template <bool ROW>
+struct X6Operand {
+  f4 r[4];
+  const float* rp[4];
+
+  // FAST path pointers, resolved once per block. Edge tiles clamp: a ROW operand's rows past
+  // mlim re-read row mlim-1, a COL operand's float4 groups past mlim re-read the last group
+  // (mlim % 4 == 0); those plane rows only reach outputs the epilogue never stores.
+  __device__ __forceinline__ void setup_fast(const float* __restrict__ base, int64_t ld,
+                                             const int64_t* __restrict__ rows, int64_t m0,
+                                             int64_t mlim, int tid) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      if constexpr (ROW) {
+        const int u = tid + 256 * it;
+        const int64_t m = min(m0 + (u >> 3), mlim - 1);
+        const int64_t rr = rows ? rows[m] : m;
+        rp[it] = base + rr * ld + 4 * (u & 7);
+      } else {
+        rp[it] = base + (int64_t)(4 * (tid & 7) + it) * ld + min(m0 + 4 * (tid >> 3), mlim - 4);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load_fast(int64_t ld, int64_t k0) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+      r[it] = *reinterpret_cast<const f4*>(ROW ? rp[it] + k0 : rp[it] + k0 * ld);
+  }
+
+  // guarded: clamped addresses, out-of-range elements selected to 0 (branch-free); rows
+  // gathers the m index (ROW) or the k index (COL)
+  __device__ __forceinline__ void load_slow(const float* __restrict__ base, int64_t ld,
+                                            const int64_t* __restrict__ rows, int64_t mlim,
+                                            int64_t m0, int64_t k0, int64_t kend, int tid) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      int64_t row, col, rlim, clim;
+      if constexpr (ROW) {
+        const int u = tid + 256 * it;
+        row = m0 + (u >> 3);
+        col = k0 + 4 * (u & 7);
+        rlim = mlim;
+        clim = kend;
+      } else {
+        row = k0 + 4 * (tid & 7) + it;
+        col = m0 + 4 * (tid >> 3);
+        rlim = kend;
+        clim = mlim;
+      }
+      const bool rok = row < rlim;
+      const int64_t rc = rok ? row : 0;
+      const int64_t rr = rows ? rows[rc] : rc;
+      const float* p = base + rr * ld;
+      float e[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = rok && (col + q < clim);
+        const float val = p[ok ? col + q : 0];
+        e[q] = ok ? val : 0.f;
+      }
+      r[it] = f4{e[0], e[1], e[2], e[3]};
+    }
+  }
+
+  // colsum_a (dW bias gradient, COL operand): cs[q] += sum over this thread's 4 k of
+  // A(m = 4g + q, k)
+  __device__ __forceinline__ void accum(f4& cs) const { cs += (r[0] + r[1]) + (r[2] + r[3]); }
+
+  // split and store the staged values into the three planes at img
+  __device__ __forceinline__ void store(char* img, int tid) const {
+    if constexpr (ROW) {
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int u = tid + 256 * it;
+        put3(img, x6_off(u >> 3, 4 * (u & 7)), r[it]);
+      }
+    } else {
+      const int g = tid >> 3, kg = tid & 7;
+      const bool odd = g & 1;  // odd groups take the rows in the order 1, 0, 3, 2
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        f4 v;  // k = 4kg .. 4kg+3 of tile row 4g + (s ^ odd)
+#pragma unroll
+        for (int it = 0; it < 4; ++it) v[it] = odd ? r[it][s ^ 1] : r[it][s];
+        put3(img, x6_off(4 * g + (s ^ (int)odd), 4 * kg), v);
+      }
+    }
+  }
+};
+
+// fragment of plane img: 16 rows from base, lane (i = lane % 16, c = lane / 16) holds row
+// base + i, k 8c .. 8c+7
+__device__ __forceinline__ bf16x8 x6_frag(const char* img, int base, int lane) {
+  const int r = base + (lane & 15);
+  return *reinterpret_cast<const bf16x8*>(img + r * X6_ROWB + (((lane >> 4) ^ x6_swz(r)) << 4));
+}
+
+__device__ __forceinline__ f4 mma(bf16x8 a, bf16x8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// one k-tile: acc[i][j] += A_i B_j^T over 32 k, six products per term pair, smallest first
+__device__ __forceinline__ void x6_compute(const char* As, const char* Bs, int wm, int wn,
+                                           int lane, f4 (&acc)[4][4]) {
+  bf16x8 b[4][3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) b[j][p] = x6_frag(Bs + p * X6_PLANE, wn * 64 + 16 * j, lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    bf16x8 a[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[p] = x6_frag(As + p * X6_PLANE, wm * 64 + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[2], b[j][0], acc[i][j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[1], b[j][1], acc[i][j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[0], b[j][2], acc[i][j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[1], b[j][0], acc[i][j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[0], b[j][1], acc[i][j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[0], b[j][0], acc[i][j]);
+  }
+}
+
+// k-loop load mode (block-uniform): 0 = guarded loads everywhere (edge widths that are not
+// whole float4 groups, k-row gathers), 1 = branch-free loads on every k-tile, 2 = branch-free
+// except a guarded last k-tile (K not a multiple of 32)
+template <bool AT, bool BT>
+__device__ __forceinline__ int x6_mode(const savqa_gemm_desc& d, int64_t m0, int64_t n0,
+                                       int64_t kbeg, int64_t kend) {
+  if ((AT && d.a_rows) || (!BT && d.b_rows)) return 0;
+  if (m0 + X6_TILE > d.M && AT && (d.M & 3)) return 0;
+  if (n0 + X6_TILE > d.N && !BT && (d.N & 3)) return 0;
+  return ((kend - kbeg) % X6_BK == 0) ? 1 : 2;
+}
+
+template <bool AT, bool BT, int MODE>
+__device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem, int64_t m0,
+                                            int64_t n0, int64_t kbeg, int64_t kend, int ntiles,
+                                            f4 (&acc)[4][4], bool do_cs, f4& cs) {
+  X6Operand<!AT> la;
+  X6Operand<BT> lb;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  if constexpr (MODE != 0) {
+    la.setup_fast(d.A, d.lda, AT ? nullptr : d.a_rows, m0, d.M, tid);
+    lb.setup_fast(d.B, d.ldb, BT ? d.b_rows : nullptr, n0, d.N, tid);
+  }
+  auto load = [&](int64_t k0) {
+    if (MODE == 1 || (MODE == 2 && k0 + X6_BK <= kend)) {
+      la.load_fast(d.lda, k0);
+      lb.load_fast(d.ldb, k0);
+    } else {
+      la.load_slow(d.A, d.lda, d.a_rows, d.M, m0, k0, kend, tid);
+      lb.load_slow(d.B, d.ldb, d.b_rows, d.N, n0, k0, kend, tid);
+    }
+  };
+  load(kbeg);
+  for (int tt = 0; tt < ntiles; ++tt) {
+    if (do_cs) la.accum(cs);
+    if (tt > 0) __syncthreads();  // every wave has read k-tile tt-1's planes
+    la.store(smem, tid);
+    lb.store(smem + 3 * X6_PLANE, tid);
+    if (tt + 1 < ntiles) load(kbeg + (int64_t)(tt + 1) * X6_BK);  // lands under compute tt
+    __syncthreads();
+    x6_compute(smem, smem + 3 * X6_PLANE, wm, wn, lane, acc);
+  }
+  __syncthreads();  // LDS is reused by the colsum fold
+}
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(GEMM_NT, X6_OCC) void gemm_x6_kernel(savqa_gemm_desc d, GemmGrid gg) {
+  __shared__ __attribute__((aligned(16))) char smem[6 * X6_PLANE];  // A planes 0-2, B planes 0-2
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int bid = blockIdx.x;
+  int t;
+  int64_t kbeg, kend;
+  bool first_split, atomic;
+  if (bid < gg.full) {
+    int slice;  // (split launches have no tail: grid.x == gg.full)
+    split_remap(gg.full, t, slice);
+    kbeg = (int64_t)slice * gg.kchunk;
+    kend = min(d.K, kbeg + gg.kchunk);
+    first_split = slice == 0;
+    atomic = d.atomic || gridDim.y > 1;
+  } else {
+    const int u = bid - gg.full;
+    const int part = u % gg.tail_f;
+    t = gg.tail_t0 + u / gg.tail_f;
+    kbeg = (int64_t)part * gg.tail_kchunk;
+    kend = min(d.K, kbeg + gg.tail_kchunk);
+    first_split = part == 0;
+    atomic = true;
+  }
+  const int tn = t % gg.tiles_n, tm = t / gg.tiles_n;
+  const int64_t m0 = (int64_t)tm * X6_TILE, n0 = (int64_t)tn * X6_TILE;
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const int ntiles = kend > kbeg ? (int)((kend - kbeg + X6_BK - 1) / X6_BK) : 0;
+  // colsum_a (a_trans only): column tile 0 also sums its A tiles over k (bias gradient)
+  const bool do_cs = AT && d.colsum_a != nullptr && tn == 0;
+  f4 cs = {0.f, 0.f, 0.f, 0.f};
+  if (ntiles > 0) {
+    const int mode = x6_mode<AT, BT>(d, m0, n0, kbeg, kend);
+    if (mode == 1)
+      x6_mainloop<AT, BT, 1>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+    else if (mode == 2)
+      x6_mainloop<AT, BT, 2>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+    else
+      x6_mainloop<AT, BT, 0>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+  }
+  if constexpr (AT) {
+    if (do_cs) {  // block-uniform; LDS is free after the main loop's last barrier
+      // thread (g, kg) holds partials of columns 4g .. 4g+3: plain LDS rows per kg, then one
+      // thread per column (no LDS float atomics)
+      float* red = reinterpret_cast<float*>(smem);
+      *reinterpret_cast<f4*>(&red[(threadIdx.x & 7) * X6_TILE + 4 * (threadIdx.x >> 3)]) = cs;
+      __syncthreads();
+      for (int i = threadIdx.x; i < X6_TILE; i += GEMM_NT) {
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v += red[r * X6_TILE + i];
+        if (m0 + i < d.M) atomicAdd(&d.colsum_a[m0 + i], v);
+      }
+    }
+  }
+  gemm_epilogue16<4, 4, 64, 64>(d, acc, m0, n0, wm, wn, lane, first_split, atomic);
+}
+
+}  // namespace savqa
+
+// Launch of the x6 kernels on a plan made by savqa_gemm (gemm.hip): grid (grid_x, nsplit).
+int savqa_launch_gemm_x6(const savqa_gemm_desc& d, const savqa::GemmGrid& gg, int grid_x,
+                         int nsplit, hipStream_t s) {
+  using namespace savqa;
+  const dim3 g(grid_x, nsplit), b(GEMM_NT);
+  if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, true>), g, b, 0, s, d, gg);
+  else if (!d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, false>), g, b, 0, s, d, gg);
+  else if (d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<true, false>), g, b, 0, s, d, gg);
+  else hipLaunchKernelGGL((gemm_x6_kernel<true, true>), g, b, 0, s, d, gg);
+  return 0;
+}

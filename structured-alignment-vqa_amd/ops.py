@@ -62,6 +62,8 @@ class GemmProbe:
             return f"gemm_skinny_kernel<{lay}>"
         if plan[0] == 16:
             return f"gemm_skinny16_kernel<{lay}>"
+        if d.prec == 6:
+            return f"gemm_x6_kernel<{lay}>"
         if d.prec:
             return f"gemm_bf16_kernel<{lay},{d.prec}>"
         return f"gemm_f32_kernel<{plan[0]},{plan[0]},{lay}>"
@@ -83,7 +85,7 @@ _probe = None
 # Product precision of the fp32-storage 128x128-tile GEMMs (savqa_gemm_desc.prec): 0 = fp32
 # MFMA (exact fp32, the default), 3 = 3xbf16 split products. Set per model (AttModel(...,
 # gemm_precision="bf16x3")) via gemm_precision(); the bf16 / fp8 modes use gemm_lp instead.
-PREC = {"fp32": 0, "bf16x3": 3}
+PREC = {"fp32": 0, "bf16x3": 3, "fp32x6": 6}
 _prec = 0
 
 

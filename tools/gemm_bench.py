@@ -71,7 +71,7 @@ def main():
             ref = A.double().t() @ X.double()
         err = float((C.double() - ref).abs().max() / ref.abs().max())
         t1 = timeit(f)
-        if prec:  # yardstick: torch's bf16 GEMM on bf16 copies
+        if prec == 3:  # yardstick: torch's bf16 GEMM on bf16 copies
             A16 = A.bfloat16()
             B16 = (W if lay != "TN" else X).bfloat16()
             C16 = C.bfloat16()
