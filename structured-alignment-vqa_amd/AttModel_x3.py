@@ -272,7 +272,8 @@ class AttModel(nn.Module):
         self.label_smoothing = label_smoothing()
         # flatten every parameter into the arena (state_dict keys unchanged)
         object.__setattr__(self, "_arena", ParamArena(self, num_blocks, device=device))
-        # gemm_precision (engine.ModelEngine): "fp32" (default, exact fp32 products),
+        # gemm_precision (engine.ModelEngine): "fp32" (default, fp32 GEMMs; "fp32_native" forces
+        # the v_mfma_f32_16x16x4_f32 kernel),
         # "bf16x3" (three bf16 MFMAs per product, ~2^-16 relative), "bf16" (BASELINE cfg 3:
         # bf16-resident GEMM / attention operands, fp32 accumulation, residual stream, LN,
         # softmax, loss and master weights) or "fp8" (cfg 5: "bf16" + fp8-e4m3 region

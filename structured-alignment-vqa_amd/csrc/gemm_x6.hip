@@ -45,13 +45,32 @@ __device__ __forceinline__ int x6_off(int r, int k) {  // byte offset of (row, k
   return r * X6_ROWB + ((((k >> 3) ^ x6_swz(r))) << 4) + (k & 7) * 2;
 }
 
-// exact three-term split of four fp32 values
+// exact three-term split of four fp32 values, packed as bf16 pairs: per pair one
+// v_cvt_pk_bf16_f32 per term, the rounded term read back by a shift / mask of the packed word
+// (22 VALU per float4; letting the compiler widen bf16x4 back to float cost 30)
+__device__ __forceinline__ uint32_t pk_bf16(float x, float y) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{x, y}, bf16x2));
+}
+__device__ __forceinline__ float pk_lo(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float pk_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
+
 __device__ __forceinline__ void split3(f4 v, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
-  p0 = __builtin_convertvector(v, bf16x4);
-  const f4 r1 = v - __builtin_convertvector(p0, f4);
-  p1 = __builtin_convertvector(r1, bf16x4);
-  const f4 r2 = r1 - __builtin_convertvector(p1, f4);
-  p2 = __builtin_convertvector(r2, bf16x4);
+  uint32_t t0[2], t1[2], t2[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float x = v[2 * h], y = v[2 * h + 1];
+    t0[h] = pk_bf16(x, y);
+    const float rx = x - pk_lo(t0[h]), ry = y - pk_hi(t0[h]);
+    t1[h] = pk_bf16(rx, ry);
+    const float sx = rx - pk_lo(t1[h]), sy = ry - pk_hi(t1[h]);
+    t2[h] = pk_bf16(sx, sy);
+  }
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  p0 = __builtin_bit_cast(bf16x4, u2{t0[0], t0[1]});
+  p1 = __builtin_bit_cast(bf16x4, u2{t1[0], t1[1]});
+  p2 = __builtin_bit_cast(bf16x4, u2{t2[0], t2[1]});
 }
 
 __device__ __forceinline__ void put3(char* img, int off, f4 v) {
@@ -66,8 +85,8 @@ __device__ __forceinline__ void put3(char* img, int off, f4 v) {
 //   ROW (k contiguous in memory): float4 u = tid + 256 it covers tile row u / 8, k 4 (u % 8).
 //   COL (m contiguous): thread (g = tid / 8, kg = tid % 8) owns tile rows 4g .. 4g+3 and
 //        k 4kg .. 4kg+3; float4 it = k row 4kg + it (16 B at column 4g), transposed at store
-//        time. (Each 16-lane store group then covers two rows of opposite parity in full:
-//        conflict-free ds_write_b64.)
+//        time. (Each 16-lane store group covers two rows of one parity: a 2-way conflict that
+//        costs a ds_write_b64 2 of its 6 cycles; staggering the rows per lane took 62 VALU.)
 template <bool ROW>
 struct X6Operand {
   f4 r[4];
@@ -147,14 +166,9 @@ struct X6Operand {
       }
     } else {
       const int g = tid >> 3, kg = tid & 7;
-      const bool odd = g & 1;  // odd groups take the rows in the order 1, 0, 3, 2
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        f4 v;  // k = 4kg .. 4kg+3 of tile row 4g + (s ^ odd)
-#pragma unroll
-        for (int it = 0; it < 4; ++it) v[it] = odd ? r[it][s ^ 1] : r[it][s];
-        put3(img, x6_off(4 * g + (s ^ (int)odd), 4 * kg), v);
-      }
+      for (int s = 0; s < 4; ++s)  // k = 4kg .. 4kg+3 of tile row 4g + s
+        put3(img, x6_off(4 * g + s, 4 * kg), f4{r[0][s], r[1][s], r[2][s], r[3][s]});
     }
   }
 };

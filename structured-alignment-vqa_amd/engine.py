@@ -798,7 +798,12 @@ def heads_backward(Wh: HeadWeights, Gh: HeadWeights, saved, dlc, dlv, dls, d: in
 
 # ----------------------------------------------------------------------------- precision
 LP_MODES = ("bf16", "fp8")
-PRECISIONS = ("fp32", "bf16x3") + LP_MODES
+PRECISIONS = ("fp32", "fp32_native", "bf16x3") + LP_MODES
+# Kernel of the fp32 mode's 128x128-tile GEMMs: "x6" (default: fp32 products from exact
+# three-term bf16 splits on the bf16 matrix cores, gemm_x6.hip) or "native" (v_mfma_f32_16x16x4_f32,
+# gemm.hip); SAVQA_FP32_GEMM overrides it for A/B runs. Both are fp32 GEMMs: the x6 error
+# against fp64 is at or below the native kernel's on every step shape (tests/test_kernels_gpu.py).
+FP32_GEMM = os.environ.get("SAVQA_FP32_GEMM", "x6")
 
 
 @dataclass
@@ -893,7 +898,8 @@ class LpShadow:
 class ModelEngine:
     """Binds arena views once; runs the whole-model forward / backward.
 
-    gemm_precision: "fp32" (exact fp32 MFMA everywhere, the north-star tolerance), "bf16x3"
+    gemm_precision: "fp32" (fp32 GEMMs everywhere, the north-star tolerance; the big Linears on
+    the x6 kernel, FP32_GEMM), "fp32_native" (the same on v_mfma_f32_16x16x4_f32), "bf16x3"
     (fp32 storage, three bf16 MFMAs per product), "bf16" (BASELINE cfg 3: bf16-resident GEMM
     operands and bf16 attention storage, fp32 accumulation / residual stream / LN / softmax
     / loss / Adam), "fp8" (BASELINE cfg 5: "bf16" plus fp8-e4m3 region features, block-scaled,
@@ -914,8 +920,13 @@ class ModelEngine:
 
     def _fp32_kernel_precision(self):
         """Product precision of the fp32-storage GEMMs (ops.PREC): bf16x3 in that mode,
-        exact fp32 otherwise (incl. the GEMMs the low-precision modes keep in fp32)."""
-        return "bf16x3" if self.gemm_precision == "bf16x3" else "fp32"
+        fp32 otherwise (incl. the GEMMs the low-precision modes keep in fp32): the x6 kernel
+        unless the mode or FP32_GEMM asks for the native one."""
+        if self.gemm_precision == "bf16x3":
+            return "bf16x3"
+        if self.gemm_precision == "fp32_native" or FP32_GEMM == "native":
+            return "fp32_native"
+        return "fp32x6"
 
     def rebind(self):
         a = self.arena

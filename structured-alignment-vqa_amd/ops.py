@@ -62,8 +62,12 @@ class GemmProbe:
             return f"gemm_skinny_kernel<{lay}>"
         if plan[0] == 16:
             return f"gemm_skinny16_kernel<{lay}>"
-        if d.prec == 6:
-            return f"gemm_x6_kernel<{lay}>"
+        if d.prec == 6:  # (savqa_gemm's fallback: unaligned operands, k-row gathers)
+            al = all(p % 16 == 0 and ld % 4 == 0 for p, ld in ((d.A, d.lda), (d.B, d.ldb)))
+            kg = (d.a_trans and d.a_rows) or (not d.b_trans and d.b_rows)
+            if al and not kg:
+                return f"gemm_x6_kernel<{lay}>"
+            return f"gemm_f32_kernel<{plan[0]},{plan[0]},{lay}>"
         if d.prec:
             return f"gemm_bf16_kernel<{lay},{d.prec}>"
         return f"gemm_f32_kernel<{plan[0]},{plan[0]},{lay}>"
@@ -83,9 +87,10 @@ class GemmProbe:
 _probe = None
 
 # Product precision of the fp32-storage 128x128-tile GEMMs (savqa_gemm_desc.prec): 0 = fp32
-# MFMA (exact fp32, the default), 3 = 3xbf16 split products. Set per model (AttModel(...,
+# MFMA (exact fp32, the ops-level default), 3 = 3xbf16 split products (~2^-16), 6 = fp32 from
+# exact three-term bf16 splits, six products per pair (gemm_x6.hip; the engine's fp32 mode). Set per model (AttModel(...,
 # gemm_precision="bf16x3")) via gemm_precision(); the bf16 / fp8 modes use gemm_lp instead.
-PREC = {"fp32": 0, "bf16x3": 3, "fp32x6": 6}
+PREC = {"fp32": 0, "fp32_native": 0, "bf16x3": 3, "fp32x6": 6}
 _prec = 0
 
 
@@ -117,8 +122,10 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
          ldc: int, a_trans=False, b_trans=False, a_rows=None, b_rows=None, c_rows=None,
          c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None, ldrv=0, rowvec_period=0,
          resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False, rowscale=None, relu=False,
-         alpha=1.0, beta=0.0, atomic=False, split_k=1, colsum_a=None, prec=None):
-    """Generic MFMA GEMM with fused epilogue (see savqa_gemm in include/savqa.h)."""
+         alpha=1.0, beta=0.0, atomic=False, split_k=1, colsum_a=None, prec=None,
+         plan_only=False):
+    """Generic MFMA GEMM with fused epilogue (see savqa_gemm in include/savqa.h).
+    plan_only: no launch, return savqa_gemm_plan's [tile, split, tail slices, workgroups]."""
     d = GemmDesc()
     d.prec = _prec if prec is None else int(prec)
     d.M, d.N, d.K = int(M), int(N), int(K)
@@ -137,6 +144,10 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
     d.alpha, d.beta = float(alpha), float(beta)
     d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
     d.colsum_a = _p(colsum_a)
+    if plan_only:
+        plan = (C.c_int32 * 4)()
+        call("savqa_gemm_plan", C.byref(d), C.cast(plan, C.c_void_p))
+        return list(plan)
     if _probe is None:
         call("savqa_gemm", _stream(), C.byref(d))
         return

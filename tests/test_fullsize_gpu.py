@@ -106,9 +106,14 @@ def test_cfg2_against_cpu_oracle(model):
     tests/golden/) on the same weights and inputs: logits at the north-star 1e-3 max-relative
     with exact answer argmax, loss 1e-4, and the gradients of the heads (max-relative 1e-3)
     and of the first layers under the 6-layer stacks and the MIL-NCE front end (Frobenius-
-    relative 2e-3: fp32 sums over B*T = 18688 rows in different orders, see
-    test_gradient_linearity_cfg2). Only the compared parameters require grad on the CPU side
-    (the backward still runs through every layer above them)."""
+    relative 5e-3, the bar of test_gradient_linearity_cfg2). Why not tighter: at this size the
+    exact gradient of those layers moves by up to 2.2e-3 when every weight moves by <= 1 ulp
+    (ReLU pre-activations within fp32 rounding of 0 flip), so any fp32 summation order lands
+    0.2-3e-3 from the fp64 oracle by chance -- the CPU fp32 oracle, the native and the x6 GEMM
+    kernels alike (profiles/r04_cfg2_conditioning.txt, tools/cfg2_fp64_check.py over 10
+    seeds; per launch the two kernels' errors against fp64 are statistically equal,
+    tools/x6_audit.py). Only the compared parameters require grad on the CPU side (the
+    backward still runs through every layer above them)."""
     import time
 
     from oracle import savqa_oracle as O
@@ -152,7 +157,7 @@ def test_cfg2_against_cpu_oracle(model):
     for n in heads:
         assert errs[n] < 1e-3, (n, errs)
     for n in deep:
-        assert errs[n] < 2e-3, (n, errs)
+        assert errs[n] < 5e-3, (n, errs)
 
 
 # ------------------------------------------------------------------ benched low-precision sizes
