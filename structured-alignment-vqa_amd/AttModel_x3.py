@@ -189,8 +189,10 @@ class _AttModelFn(torch.autograd.Function):
     the Parameters as inputs puts their AccumulateGrad nodes into the graph, so everything
     that hooks gradient accumulation sees each parameter become ready after the backward:
     torch's DistributedDataParallel (main:203, find_unused_parameters=True) then averages
-    the arena's gradients in place (its bucket copies read and write .grad), and
-    register_post_accumulate_grad_hook users run as usual."""
+    the arena's gradients in place (its bucket copies read and write .grad): DDP hooks the
+    AccumulateGrad NODES, whose hooks the engine runs after each. Per-tensor
+    register_post_accumulate_grad_hook hooks do NOT fire: AccumulateGrad returns before
+    them for an undefined incoming gradient -- read .grad after backward() instead."""
 
     @staticmethod
     def forward(ctx, model, decMask, drop, ntensors, *args):

@@ -16,13 +16,15 @@ ROCm) over xGMI:
     extra pass over 1.8 GB of gradients;
   * row tables whose gradient rows are known from the inputs (the two stacks' 407000x300
     syb_emb tables: only the question-token rows, AttModel_x3.py:96-99 / :216-219, get a
-    gradient) are exchanged as the union of the touched rows instead of densely
-    (SURVEY 8(e) "exchange only the touched rows"): the token ids are all-gathered in
-    the forward, and at the table's turn in the backward every rank gathers the rows
-    of the sorted id list (first occurrence of each id; duplicates zero) into a compact
-    [world*B*Lq, 300] buffer that is all-reduced, then written back before Adam. Rows
-    nobody touched are zero on every rank, so the result equals the dense all-reduce;
-    at cfg 2 / N=8 the two tables shrink from 976 MB to 2 x 34 MB on the wire.
+    gradient) are exchanged by rows instead of densely (SURVEY 8(e) "exchange only the
+    touched rows"): the token ids are all-gathered in the forward (padded to a static cap
+    with a filler row, so no host exchange); at the table's turn in the backward every rank
+    sends ITS OWN rows once -- its id list sorted, duplicates zeroed -- by an all-gather of
+    [cap, 300], and every rank then sums the rows of each id over the ranks in rank order
+    (an index_add per rank: at most one non-zero row per id and rank, so the sums are the
+    same bits on every rank) into the table before Adam. Rows nobody touched stay zero, so
+    the result equals the dense all-reduce; an all-gather of cap rows moves half the bytes of
+    an all-reduce of the world*cap-row union (ring: (N-1)*cap vs 2(N-1)*cap rows per rank).
 Works with any torch.distributed backend (gloo on CPU tensors for the host tests).
 """
 from __future__ import annotations
@@ -34,16 +36,18 @@ import torch.distributed as dist
 
 
 class _RowsWork:
-    """Work handle of a row-sparse table exchange: wait() makes the current stream wait
-    for the all-reduce, then writes the summed rows back (every duplicate of an id
-    carries its first occurrence's sum, so the write-back is order-independent)."""
+    """Work handle of a row-sparse table exchange: wait() makes the current stream wait for
+    the all-gather of every rank's compact rows, then writes their per-id sums into the table
+    (zero the union's rows, then one index_add per rank in rank order)."""
 
-    def __init__(self, work, table, ids, src, buf):
-        self.work, self.table, self.ids, self.src, self.buf = work, table, ids, src, buf
+    def __init__(self, work, table, union, ids, outs):
+        self.work, self.table, self.union, self.ids, self.outs = work, table, union, ids, outs
 
     def wait(self):
         self.work.wait()
-        self.table.index_copy_(0, self.ids, self.buf.index_select(0, self.src))
+        self.table.index_fill_(0, self.union, 0.0)
+        for r, rows in enumerate(self.outs):
+            self.table.index_add_(0, self.ids[r], rows)
         return True
 
 
@@ -82,7 +86,11 @@ class GradReducer:
         self.pending = {}
         self.sparse: List = []      # [(lo, hi, width)] arena ranges exchanged by rows
         self._ids = None            # (all_gather work, [world] id tensors) of this step
-        self._rows = None           # (sorted ids, first-occurrence mask, source position)
+        self._rows = None           # (union ids, per-rank sorted ids, this rank's first mask)
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # every collective this reducer issued since begin(), in issue order: (kind, lo, hi)
+        # -- RCCL needs the same sequence on every rank (tests compare it across ranks)
+        self.trace: List = []
         self._rows_done = set()     # arena offsets of the tables exchanged by rows this step
         self.rows_exchanged = 0     # tables exchanged by rows in the current step
 
@@ -105,6 +113,7 @@ class GradReducer:
         self._ids = None
         self._rows = None
         self.rows_exchanged = 0
+        self.trace = []
 
     def set_rows(self, ids: torch.Tensor, cap: Optional[int] = None):
         """This step's touched rows of the sparse tables (any integer tensor): all-gathered
@@ -139,6 +148,7 @@ class GradReducer:
             ids = torch.cat([ids, fill.expand(cap - n)])
         outs = [torch.empty_like(ids) for _ in range(self.world)]
         w = dist.all_gather(outs, ids, group=self.group, async_op=True)
+        self.trace.append(("ids", 0, cap))
         if self._ids is None or self._rows is not None:
             self._ids = []
         self._ids.append((w, outs))
@@ -146,19 +156,22 @@ class GradReducer:
 
     def prepare_rows(self):
         """Sort the gathered ids (on the current stream; call at the start of the
-        backward, when the all-gather has long landed)."""
+        backward, when the all-gather has long landed): every rank's own list sorted (the
+        order its rows travel in; the same computation on every rank), this rank's
+        first-occurrence mask (duplicates send zero rows), and the union for the write-back
+        and the Adam row flags."""
         if self._ids is None or self._rows is not None:
             return
-        outs = []
+        per = [[] for _ in range(self.world)]
         for w, o in self._ids:
             w.wait()
-            outs.extend(o)
-        ids, _ = torch.sort(torch.cat(outs))
-        first = torch.ones_like(ids, dtype=torch.bool)
-        first[1:] = ids[1:] != ids[:-1]
-        pos = torch.arange(ids.numel(), device=ids.device)
-        src = torch.cummax(torch.where(first, pos, torch.zeros_like(pos)), 0).values
-        self._rows = (ids, first, src)
+            for r in range(self.world):
+                per[r].append(o[r])
+        ids = [torch.sort(torch.cat(p)).values for p in per]
+        mine = ids[self.rank]
+        first = torch.ones_like(mine, dtype=torch.bool)
+        first[1:] = mine[1:] != mine[:-1]
+        self._rows = (torch.cat(ids), ids, first)
 
     @staticmethod
     def _stream_key():
@@ -168,6 +181,7 @@ class GradReducer:
         g = self.arena.grad
         w = dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.works.append((w, lo, hi))
+        self.trace.append(("dense", lo, hi))
 
     def _issue(self, lo: int, hi: int):
         # final range [lo, hi): dense pieces around the sparse tables; a table goes out
@@ -189,16 +203,18 @@ class GradReducer:
         if self._rows is None:       # no set_rows() this step: dense exchange
             self._dense(t0, t1)
             return
-        ids, first, src = self._rows
+        union, ids, first = self._rows
         table = self.arena.grad[t0:t1].view(-1, width)
         mark = getattr(self.arena, "mark_table_rows", None)
         if mark is not None:  # rows other ranks touched get a gradient here too
-            mark(t0, ids)
+            mark(t0, union)
         self._rows_done.add(t0)
-        buf = table.index_select(0, ids)
+        buf = table.index_select(0, ids[self.rank])
         buf.mul_(first.unsqueeze(1).to(buf.dtype))
-        w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        self.works.append((_RowsWork(w, table, ids, src, buf), t0, t1))
+        outs = [torch.empty_like(buf) for _ in range(self.world)]
+        w = dist.all_gather(outs, buf, group=self.group, async_op=True)
+        self.works.append((_RowsWork(w, table, union, ids, outs), t0, t1))
+        self.trace.append(("rows", t0, t1))
         self.rows_exchanged += 1
 
     def reduce_range(self, start: int, end: int, flush: bool = False):

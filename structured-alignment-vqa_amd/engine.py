@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import math
 import os
+import sys
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -175,6 +176,24 @@ SYB_SITES = (-1, 4, 5)  # (none -- plain position table :178, enc_dropout :227, 
 HEAD_SITES = {"cls": 6, "cls_vis": 7, "cls_syb": 8}  # Dropout(inplace) in the heads :482-500
 
 
+# Persistent Q|V buffers of the pruned encoder layers 0-1 (PRUNE_L01): the gathered GEMM
+# writes the question rows only, the node rows must read as zeros (finite Q / V: their weights
+# are exactly 0 and 0 * NaN would not be), and they stay zero across steps -- so the buffer is
+# zero-filled once instead of a 38-76 MB torch.zeros per layer per step. A buffer still held
+# by an earlier forward's saved state (no backward yet: two forwards in flight) is not reused.
+_QV_BUFS: Dict[tuple, torch.Tensor] = {}
+
+
+def _zeroed_qv(key, M: int, width: int, dev) -> torch.Tensor:
+    k = key + (M, width, str(dev))
+    buf = _QV_BUFS.get(k)
+    # references when free: the dict, `buf`, getrefcount's argument
+    if buf is None or sys.getrefcount(buf) > 3:
+        buf = torch.zeros(M, width, device=dev)
+        _QV_BUFS[k] = buf
+    return buf
+
+
 def _ln_stats(rows, dev):
     return _empty(rows, dev=dev), _empty(rows, dev=dev), _empty(rows, dev=dev)
 
@@ -243,7 +262,7 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
         if lp is None and i < 2 and Nn > 0 and PRUNE_L01:
             kb = _empty(M, d, dev=dev)
             ops.linear(x, L["Wqkv"][d:2 * d], L["bqkv"][d:2 * d], kb, relu=True)
-            qv = torch.zeros(M, 2 * d, device=dev)
+            qv = _zeroed_qv((L["Wqkv"].data_ptr(),), M, 2 * d, dev)
             bqv = torch.cat((L["bqkv"][:d], L["bqkv"][2 * d:]))
             ops.gemm(x, L["Wqkv"], qv, B * Lq, 2 * d, d, lda=d, ldb=d, ldc=2 * d, b_trans=True,
                      a_rows=s.qrows, b_rows=_qv_wrows(d, dev), bias=bqv, relu=True, c_group=Lq,

@@ -105,7 +105,8 @@ def _sparse_worker(rank, world, port, q):
     spans = sorted((lo, hi) for _, lo, hi in works)
     for w, _, _ in works:
         w.wait()
-    q.put((rank, float((arena.grad - dense).abs().max()), spans, scale, n, (u0, u1)))
+    q.put((rank, float((arena.grad - dense).abs().max()), spans, scale, n, (u0, u1),
+           list(red.trace)))
     dist.destroy_process_group()
 
 
@@ -122,7 +123,10 @@ def test_sparse_table_rows_exchange_equals_dense_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, err, spans, scale, n, tab2 in res:
+    # RCCL needs every rank to issue the same collectives in the same order
+    assert res[0][6] == res[1][6] and len(res[0][6]) > 3, (res[0][6], res[1][6])
+    assert [k for k, _, _ in res[0][6]].count("rows") == 2
+    for rank, err, spans, scale, n, tab2, _ in res:
         assert err < 1e-6
         assert scale == 0.5
         assert (1000, 1350) in spans and tab2 in spans
@@ -178,7 +182,7 @@ def _ragged_worker(rank, world, port, q, static_cap=False):
     for w, _, _ in works:
         w.wait()
     q.put((rank, float((arena.grad - dense).abs().max()),
-           sorted((lo, hi) for _, lo, hi in works)))
+           sorted((lo, hi) for _, lo, hi in works), list(red.trace)))
     dist.destroy_process_group()
 
 
@@ -199,7 +203,8 @@ def test_ragged_rows_accumulated_forwards_and_coverage_gap_gloo_world2(static_ca
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, err, spans in res:
+    assert res[0][3] == res[1][3], (res[0][3], res[1][3])  # same collective sequence
+    for rank, err, spans, _ in res:
         assert err < 1e-6, (rank, err)
         assert (100, 250) in spans
         pos = 0

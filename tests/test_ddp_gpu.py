@@ -208,7 +208,9 @@ def _equiv_run(world, rank, steps=2, sparse=True, mode="reducer"):
     else:
         if world > 1:
             red = GradReducer(m._arena, bucket_mb=1.0)
-            m.attach_reducer(red)      # multi_rank: the gated enc4 backward schedule is on
+            # multi_rank: the gated enc4 backward schedule is on; the static id cap of the
+            # row exchange (batch_size * maxlen_q) pads every rank's ids with the filler row
+            m.attach_reducer(red, batch_size=n)
             assert m._engine.vis_gate() is not None
             if not sparse:
                 red.sparse = []
@@ -250,7 +252,8 @@ def _equiv_run(world, rank, steps=2, sparse=True, mode="reducer"):
                 x, y = g[o:o + shp.numel()].double(), ra.grad[o:o + shp.numel()].double()
                 gerr[name] = (float((x - y).norm() / y.norm().clamp_min(1e-30)),
                               float(y.abs().max()), float(x.abs().max()))
-        rec.append((_digest(a, g), _digest(a, a.flat[:a.n_live]), gerr))
+        rec.append((_digest(a, g), _digest(a, a.flat[:a.n_live]), gerr,
+                    list(red.trace) if red else []))
     return rec
 
 
@@ -354,8 +357,13 @@ def test_two_ranks_on_half_batches_equal_one_rank_on_the_batch(mode):
         r0, r1 = res[0][0][sparse], res[1][0][sparse]
         worst_g, worst_u = [], []
         for step in range(2):
-            (g0, w0, gerr), (g1, w1, _) = r0[step], r1[step]
-            gref, wref, _ = ref[0]     # the 1-rank run's first step
+            (g0, w0, gerr, t0), (g1, w1, _, t1) = r0[step], r1[step]
+            gref, wref, _, _ = ref[0]  # the 1-rank run's first step
+            # RCCL's requirement: both ranks issued the same collectives in the same order
+            # (buckets come from two backward streams; the row exchange from the gated one)
+            assert t0 == t1, ("collective sequences differ", sparse, step)
+            if mode == "reducer":
+                assert len(t0) > 10 and ("rows" in [k for k, _, _ in t0]) == sparse, t0
             for n in wref:
                 x0, x1 = w0[n], w1[n]
                 if isinstance(x0, tuple):
