@@ -54,20 +54,45 @@ def _cpu_model():
     return "unknown"
 
 
+def _cgroup_cpus():
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max / v1 cfs quota),
+    or None when unlimited / unknown."""
+    import math
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            return max(1, math.ceil(int(q) / int(p)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return max(1, math.ceil(q / p)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(seconds=24.0, rate=0.5):
     """Time the CPU oracle (oracle/savqa_oracle.py, the parity checker) on the host, per
     SURVEY.md 8(d): forward+loss AND the full train step (fwd+loss+bwd+Adam), at the cfg-1
     shape B=4 and at the reference's per-GPU batch B=32, with torch.set_num_threads(every CPU
-    of the process's affinity mask) as the survey specifies; the train step at B=32 is also
-    timed at OMP_NUM_THREADS threads when that is set (the box exports 16) as an extra leg.
-    Bounded: ~seconds/4 per leg. The headline `value` is the train step at B=32 on all CPUs."""
+    the process may run on): the affinity mask (the survey's os.cpu_count()) capped by the
+    cgroup's CPU quota -- the GPU box shows 256 CPUs but grants one GPU's job a 16-CPU share,
+    and 256 threads on 16 CPUs' time made the oracle stall for minutes (a bench run was killed
+    for silence). Both counts are reported. Bounded: ~seconds/4 per leg, progress on stderr.
+    The headline `value` is the train step at B=32."""
     from oracle import hashfill
     from oracle import savqa_oracle as O
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    threads = avail
+    quota = _cgroup_cpus()
+    threads = min(avail, quota) if quota else avail
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     torch.set_num_threads(threads)
     Nv, Lq, Ns, K = 36, 14, 59, 5
@@ -125,6 +150,8 @@ def cpu_baseline(seconds=24.0, rate=0.5):
             dt = time.perf_counter() - t0
             legs[f"{name}_b{B}"] = {"samples_per_s": round(B * n / dt, 3), "iters": n,
                                     "seconds": round(dt, 2), "threads": threads}
+            print(f"cpu_baseline {name} B={B}: {B * n / dt:.2f} samples/s ({threads} threads)",
+                  file=sys.stderr, flush=True)
     if omp and omp != threads:  # the same leg at the job's OMP_NUM_THREADS
         torch.set_num_threads(omp)
         inp, answer = inputs(32)
@@ -142,10 +169,12 @@ def cpu_baseline(seconds=24.0, rate=0.5):
     head = legs["train_step_b32"]
     return {"value": head["samples_per_s"], "unit": "QA-samples/s", "cores": threads,
             "kind": "port",
-            "host_cpus": os.cpu_count(), "affinity_cpus": avail, "cpu_model": _cpu_model(),
+            "host_cpus": os.cpu_count(), "affinity_cpus": avail, "cgroup_cpus": quota,
+            "cpu_model": _cpu_model(),
             "legs": legs,
             "sample": f"oracle/savqa_oracle.py on torch CPU ({threads} threads = the affinity "
-                      f"mask; extra leg at OMP_NUM_THREADS={omp or 'unset'}): train step "
+                      f"mask capped by the cgroup CPU quota; extra leg at OMP_NUM_THREADS="
+                      f"{omp or 'unset'} when different): train step "
                       f"(fwd+loss+bwd+Adam, dropout {rate}) and fwd+loss at the cfg-1 shape, "
                       f"B=4 and B=32 (value = train step, B=32), ~{seconds / 4:.0f}s per leg"}
 

@@ -1,5 +1,12 @@
-set -eo pipefail
-for s in 0 3 7 9 1 2; do
-WPERTURB=1 NO_CPU32=1 SEED=$s timeout -k 10 600 python -u tools/cfg2_fp64_check.py > gpurun_out/fp64w_s$s.txt 2>&1 || { tail -30 gpurun_out/fp64w_s$s.txt; exit 1; }
-echo "== seed $s"; grep -v "amdgpu.ids\|oracle torch\|logits max" gpurun_out/fp64w_s$s.txt
+set -o pipefail
+cat /sys/fs/cgroup/cpu.max 2>&1; cat /sys/fs/cgroup/cpu.weight 2>&1; nproc; python3 -c "import os;print(len(os.sched_getaffinity(0)), os.cpu_count())"
+for t in 16 64 256; do
+timeout -k 5 60 python3 -c "
+import torch,time
+torch.set_num_threads($t)
+a=torch.randn(2048,2048)
+t0=time.perf_counter()
+for _ in range(5): a@a
+print($t, 'threads', (time.perf_counter()-t0)/5, 's per 2048^3 matmul')
+" || echo "$t threads: timed out"
 done
