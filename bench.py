@@ -54,6 +54,35 @@ def _cpu_model():
     return "unknown"
 
 
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def hbm_report(records, lp):
+    """Per kernel family (LayerNorm, Adam, graph attention): launches per step, mean launch
+    time (HIP events on the launch stream, stacks serialised), ALGORITHMIC bytes per launch and
+    the rate they imply against the 8 TB/s HBM peak; attention also its MFMA rate."""
+    torch.cuda.synchronize()
+    agg = {}
+    for tag, nb, fl, e0, e1 in records:
+        a = agg.setdefault(tag, [0, 0.0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += nb
+        a[2] += fl
+        a[3] += e0.elapsed_time(e1)
+    out = {}
+    for tag, (n, nb, fl, ms) in sorted(agg.items(), key=lambda kv: -kv[1][3]):
+        gbs = nb / (ms * 1e-3) / 1e9
+        r = {"launches_per_step": n // 2, "avg_us": round(ms / n * 1e3, 2),
+             "bytes_per_launch": round(nb / n), "GB/s": round(gbs, 1),
+             "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+        if fl:
+            tf = fl / (ms * 1e-3) / 1e12
+            pk = BF16_MFMA_PEAK_TFLOPS if "bf16" in tag else FP32_MFMA_PEAK_TFLOPS
+            r.update({"TFLOP/s": round(tf, 2), "mfma_frac": round(tf / pk, 4)})
+        out[tag] = r
+    return out
+
+
 def _cgroup_cpus():
     """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max / v1 cfs quota),
     or None when unlimited / unknown."""
@@ -347,18 +376,28 @@ def main():
         # per-kernel timing needs kernels that do not share the GPU: run the probe steps
         # with both stacks on one stream (the timed region above overlaps them)
         probe = ops.GemmProbe()
+        kprobe = []
         model._engine.concurrent = False
         ops.set_gemm_probe(probe)
+        ops.set_kernel_probe(kprobe)
         for _ in range(2):
             step()
         ops.set_gemm_probe(None)
+        ops.set_kernel_probe(None)
         model._engine.concurrent = not args.serial
         agg = probe.summary()
         var, (n, flops, ms) = max(agg.items(), key=lambda kv: kv[1][2])
         achieved = (flops / n) / (ms / n * 1e-3) / 1e12
         kpeak = peak
+        basis = None
         if var.startswith("gemm_lp"):  # bf16 operands, or fp8 (gemm_lp_kernel<...,true>)
             kpeak = FP8_MFMA_PEAK_TFLOPS if var.endswith(",true>") else BF16_MFMA_PEAK_TFLOPS
+        elif var.startswith("gemm_x6"):
+            # fp32 products as six bf16 MFMA products each: the ceiling is the dense bf16 MFMA
+            # peak / 6 (416.7 TF of fp32 work), above the 157.3 TF fp32 MFMA peak
+            kpeak = round(BF16_MFMA_PEAK_TFLOPS / 6, 1)
+            basis = ("2.5 PF dense bf16 MFMA / 6 bf16 products per fp32 product "
+                     "(gemm_x6.hip); fp32 MFMA peak 157.3 TF")
         allfl = sum(v[1] for v in agg.values())
         allms = sum(v[2] for v in agg.values())
         roof = {"bound": "mfma", "kernel": var, "launches_per_step": n // 2,
@@ -368,6 +407,9 @@ def main():
                 "traffic": committed_traffic(var, args.workload),
                 "all_gemm_tflops": round(allfl / (allms * 1e-3) / 1e12, 2),
                 "gemm_ms_per_step": round(allms / 2, 2)}
+        if basis:
+            roof["peak_basis"] = basis
+        roof["hbm_kernels"] = hbm_report(kprobe, lp)
 
     if rank == 0:
         cpu = None

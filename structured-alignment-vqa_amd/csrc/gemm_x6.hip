@@ -27,6 +27,8 @@
 // blocks and transposed in registers before their ds_write_b64s.
 #include "gemm_common.h"
 
+#include <type_traits>
+
 namespace savqa {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -37,6 +39,10 @@ constexpr int X6_BK = 32;
 constexpr int X6_ROWB = X6_BK * 2;           // bytes per plane row
 constexpr int X6_PLANE = X6_TILE * X6_ROWB;  // bytes per plane (8 KB)
 constexpr int X6_OCC = 2;                    // workgroups per CU (VGPR-limited)
+#ifndef SAVQA_X6_DEPTH
+#define SAVQA_X6_DEPTH 1
+#endif
+constexpr int X6_DEPTH = SAVQA_X6_DEPTH;     // k-tiles of operand loads in flight (1 or 2)
 
 // chunk XOR of plane row r: S[(r >> 2) & 3], S = {0, 2, 3, 1}
 __device__ __forceinline__ int x6_swz(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }
@@ -89,7 +95,7 @@ __device__ __forceinline__ void put3(char* img, int off, f4 v) {
 //        costs a ds_write_b64 2 of its 6 cycles; staggering the rows per lane took 62 VALU.)
 template <bool ROW>
 struct X6Operand {
-  f4 r[4];
+  f4 r[X6_DEPTH][4];  // X6_DEPTH register sets: k-tiles in flight
   const float* rp[4];
 
   // FAST path pointers, resolved once per block. Edge tiles clamp: a ROW operand's rows past
@@ -111,14 +117,16 @@ struct X6Operand {
     }
   }
 
+  template <int S>
   __device__ __forceinline__ void load_fast(int64_t ld, int64_t k0) {
 #pragma unroll
     for (int it = 0; it < 4; ++it)
-      r[it] = *reinterpret_cast<const f4*>(ROW ? rp[it] + k0 : rp[it] + k0 * ld);
+      r[S][it] = *reinterpret_cast<const f4*>(ROW ? rp[it] + k0 : rp[it] + k0 * ld);
   }
 
   // guarded: clamped addresses, out-of-range elements selected to 0 (branch-free); rows
   // gathers the m index (ROW) or the k index (COL)
+  template <int S>
   __device__ __forceinline__ void load_slow(const float* __restrict__ base, int64_t ld,
                                             const int64_t* __restrict__ rows, int64_t mlim,
                                             int64_t m0, int64_t k0, int64_t kend, int tid) {
@@ -148,27 +156,32 @@ struct X6Operand {
         const float val = p[ok ? col + q : 0];
         e[q] = ok ? val : 0.f;
       }
-      r[it] = f4{e[0], e[1], e[2], e[3]};
+      r[S][it] = f4{e[0], e[1], e[2], e[3]};
     }
   }
 
   // colsum_a (dW bias gradient, COL operand): cs[q] += sum over this thread's 4 k of
   // A(m = 4g + q, k)
-  __device__ __forceinline__ void accum(f4& cs) const { cs += (r[0] + r[1]) + (r[2] + r[3]); }
+  template <int S>
+  __device__ __forceinline__ void accum(f4& cs) const {
+    cs += (r[S][0] + r[S][1]) + (r[S][2] + r[S][3]);
+  }
 
-  // split and store the staged values into the three planes at img
+  // split and store the staged values of set S into the three planes at img
+  template <int S>
   __device__ __forceinline__ void store(char* img, int tid) const {
     if constexpr (ROW) {
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
         const int u = tid + 256 * it;
-        put3(img, x6_off(u >> 3, 4 * (u & 7)), r[it]);
+        put3(img, x6_off(u >> 3, 4 * (u & 7)), r[S][it]);
       }
     } else {
       const int g = tid >> 3, kg = tid & 7;
 #pragma unroll
       for (int s = 0; s < 4; ++s)  // k = 4kg .. 4kg+3 of tile row 4g + s
-        put3(img, x6_off(4 * g + s, 4 * kg), f4{r[0][s], r[1][s], r[2][s], r[3][s]});
+        put3(img, x6_off(4 * g + s, 4 * kg),
+             f4{r[S][0][s], r[S][1][s], r[S][2][s], r[S][3][s]});
     }
   }
 };
@@ -237,24 +250,35 @@ __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem
     la.setup_fast(d.A, d.lda, AT ? nullptr : d.a_rows, m0, d.M, tid);
     lb.setup_fast(d.B, d.ldb, BT ? d.b_rows : nullptr, n0, d.N, tid);
   }
-  auto load = [&](int64_t k0) {
+  auto load = [&](auto set, int64_t k0) {
+    constexpr int S = decltype(set)::value;
     if (MODE == 1 || (MODE == 2 && k0 + X6_BK <= kend)) {
-      la.load_fast(d.lda, k0);
-      lb.load_fast(d.ldb, k0);
+      la.template load_fast<S>(d.lda, k0);
+      lb.template load_fast<S>(d.ldb, k0);
     } else {
-      la.load_slow(d.A, d.lda, d.a_rows, d.M, m0, k0, kend, tid);
-      lb.load_slow(d.B, d.ldb, d.b_rows, d.N, n0, k0, kend, tid);
+      la.template load_slow<S>(d.A, d.lda, d.a_rows, d.M, m0, k0, kend, tid);
+      lb.template load_slow<S>(d.B, d.ldb, d.b_rows, d.N, n0, k0, kend, tid);
     }
   };
-  load(kbeg);
-  for (int tt = 0; tt < ntiles; ++tt) {
-    if (do_cs) la.accum(cs);
+  // k-tile tt from register set S: split into the planes, refill S with k-tile tt + DEPTH
+  // (DEPTH k-tiles of loads in flight), then the MFMAs
+  auto step = [&](auto set, int tt) {
+    constexpr int S = decltype(set)::value;
+    if (do_cs) la.template accum<S>(cs);
     if (tt > 0) __syncthreads();  // every wave has read k-tile tt-1's planes
-    la.store(smem, tid);
-    lb.store(smem + 3 * X6_PLANE, tid);
-    if (tt + 1 < ntiles) load(kbeg + (int64_t)(tt + 1) * X6_BK);  // lands under compute tt
+    la.template store<S>(smem, tid);
+    lb.template store<S>(smem + 3 * X6_PLANE, tid);
+    if (tt + X6_DEPTH < ntiles) load(set, kbeg + (int64_t)(tt + X6_DEPTH) * X6_BK);
     __syncthreads();
     x6_compute(smem, smem + 3 * X6_PLANE, wm, wn, lane, acc);
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, X6_DEPTH - 1>;
+  load(S0{}, kbeg);
+  if (X6_DEPTH > 1 && ntiles > 1) load(S1{}, kbeg + X6_BK);
+  for (int tt = 0; tt < ntiles; tt += X6_DEPTH) {
+    step(S0{}, tt);
+    if (X6_DEPTH > 1 && tt + 1 < ntiles) step(S1{}, tt + 1);
   }
   __syncthreads();  // LDS is reused by the colsum fold
 }

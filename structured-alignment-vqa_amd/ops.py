@@ -113,6 +113,37 @@ class gemm_precision:
         return False
 
 
+# Optional per-launch timing of the HBM-bound kernels (LayerNorm, Adam, graph attention) with
+# HIP events on the launch stream, keyed by kernel family, with each launch's ALGORITHMIC bytes
+# and FLOPs (bench.py's "hbm_kernels" report). Off unless a recorder list is installed.
+_kprobe = None
+
+
+def set_kernel_probe(probe):
+    global _kprobe
+    _kprobe = probe
+
+
+def _kcall(tag: str, nbytes: float, flops: float, name: str, *args):
+    if _kprobe is None:
+        call(name, *args)
+        return
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    call(name, *args)
+    e1.record()
+    _kprobe.append((tag, float(nbytes), float(flops), e0, e1))
+
+
+def _attn_bytes(q, B, Tq, Tk, H, dk, n_in, n_out):
+    """Algorithmic bytes of one graph-attention launch: n_in (Tq or Tk) x dk operands per
+    (sample, head) read, n_out written, the fp32 (B, Tq, Tk) graph read ONCE per sample."""
+    es = q.element_size()
+    rows = B * H * dk * es
+    return rows * (n_in + n_out) + B * Tq * Tk * 4
+
+
 def set_gemm_probe(probe):
     global _probe
     _probe = probe
@@ -349,8 +380,11 @@ def ln_fwd(x: Tensor, gamma: Tensor, beta: Tensor, y: Tensor, mean: Tensor, rden
     """yb: optional bf16 copy of y (operand of the next low-precision GEMM)."""
     cols = gamma.numel()
     rows = x.numel() // cols
-    call("savqa_ln_fwd", _stream(), _p(x), _p(xscale), _p(r), rows, cols, _p(gamma), _p(beta),
-         float(eps), _p(z_out), _p(y), _p(mean), _p(rden), _p(std), _p(flag), _p(yb))
+    nb = rows * cols * (4 * (2 + (r is not None) + (z_out is not None)) + 2 * (yb is not None)) \
+        + rows * 12
+    _kcall("ln_fwd", nb, 0, "savqa_ln_fwd", _stream(), _p(x), _p(xscale), _p(r), rows, cols,
+           _p(gamma), _p(beta), float(eps), _p(z_out), _p(y), _p(mean), _p(rden), _p(std),
+           _p(flag), _p(yb))
 
 
 _ln_ws = {}
@@ -375,8 +409,10 @@ def ln_bwd(dy: Tensor, z: Tensor, mean: Tensor, rden: Tensor, std: Tensor, gamma
     cols = gamma.numel()
     rows = z.numel() // cols
     ws = ln_workspace(cols, z.device)
-    call("savqa_ln_bwd", _stream(), _p(dy), _p(z), _p(mean), _p(rden), _p(std), _p(gamma), rows,
-         cols, _p(dz_add), _p(dz), _p(dgamma), _p(dbeta), _p(ws), ws.numel() * 4, _p(dzb))
+    nb = rows * cols * (4 * (3 + (dz_add is not None)) + 2 * (dzb is not None)) + rows * 12
+    _kcall("ln_bwd", nb, 0, "savqa_ln_bwd", _stream(), _p(dy), _p(z), _p(mean), _p(rden), _p(std),
+           _p(gamma), rows, cols, _p(dz_add), _p(dz), _p(dgamma), _p(dbeta), _p(ws),
+           ws.numel() * 4, _p(dzb))
 
 
 def rowflag(X: Tensor, rows: int, cols: int, ldx: int, flag: Tensor):
@@ -386,35 +422,46 @@ def rowflag(X: Tensor, rows: int, cols: int, ldx: int, flag: Tensor):
 # ------------------------------------------------------------------------------ attention
 def gattn_fwd(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, o, ldo, att=None, dk=64):
     """Graph-attention forward; bf16 Q/K/V select the bf16-storage kernels (fp32 math)."""
+    fl = 4.0 * B * H * Tq * Tk * dk
     if k.dtype == torch.bfloat16:
-        call("savqa_gattn_fwd_bf16", _stream(), int(q.dtype == torch.bfloat16), _p(q), ldq, _p(k),
-             ldk, _p(v), ldv, _p(G), _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(att))
+        nb = _attn_bytes(k, B, Tq, Tk, H, dk, Tq + 2 * Tk, 0) + B * H * Tq * dk * o.element_size()
+        _kcall(f"gattn_fwd_bf16 T{Tq}x{Tk}", nb, fl, "savqa_gattn_fwd_bf16", _stream(),
+               int(q.dtype == torch.bfloat16), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G),
+               _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(att))
         return
-    call("savqa_gattn_fwd", _stream(), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G), _p(kflag),
-         _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(att))
+    _kcall(f"gattn_fwd T{Tq}x{Tk}", _attn_bytes(q, B, Tq, Tk, H, dk, Tq + 2 * Tk, Tq), fl,
+           "savqa_gattn_fwd", _stream(), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G), _p(kflag),
+           _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(att))
 
 
 def gattn_bwd(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout, lddo, dq, lddq, dk_,
               lddk, dv, lddv, dk=64):
+    fl = 10.0 * B * H * Tq * Tk * dk
+    nb = _attn_bytes(k, B, Tq, Tk, H, dk, 2 * Tq + 2 * Tk, Tq + 2 * Tk)
     if k.dtype == torch.bfloat16:
-        call("savqa_gattn_bwd_bf16", _stream(), int(q.dtype == torch.bfloat16), _p(q), ldq, _p(k),
-             ldk, _p(v), ldv, _p(G), _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo,
-             _p(dq), lddq, _p(dk_), lddk, _p(dv), lddv)
+        _kcall(f"gattn_bwd_bf16 T{Tq}x{Tk}", nb, fl, "savqa_gattn_bwd_bf16", _stream(),
+               int(q.dtype == torch.bfloat16), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G),
+               _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo, _p(dq), lddq, _p(dk_),
+               lddk, _p(dv), lddv)
         return
-    call("savqa_gattn_bwd", _stream(), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G), _p(kflag),
-         _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo, _p(dq), lddq, _p(dk_), lddk, _p(dv), lddv)
+    _kcall(f"gattn_bwd T{Tq}x{Tk}", nb, fl, "savqa_gattn_bwd", _stream(), _p(q), ldq, _p(k), ldk,
+           _p(v), ldv, _p(G), _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo, _p(dq), lddq,
+           _p(dk_), lddk, _p(dv), lddv)
 
 
 def gattn_fwd_flash(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, o, ldo, stats, dk=64):
-    call("savqa_gattn_fwd_flash", _stream(), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G), _p(kflag),
-         _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(stats))
+    _kcall(f"gattn_fwd_flash T{Tq}x{Tk}", _attn_bytes(q, B, Tq, Tk, H, dk, Tq + 2 * Tk, Tq),
+           4.0 * B * H * Tq * Tk * dk, "savqa_gattn_fwd_flash", _stream(), _p(q), ldq, _p(k), ldk,
+           _p(v), ldv, _p(G), _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(stats))
 
 
 def gattn_bwd_flash(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout, lddo,
                     stats, dq, lddq, dk_, lddk, dv, lddv, dk=64):
-    call("savqa_gattn_bwd_flash", _stream(), _p(q), ldq, _p(k), ldk, _p(v), ldv, _p(G), _p(kflag),
-         _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo, _p(stats), _p(dq), lddq, _p(dk_), lddk,
-         _p(dv), lddv)
+    _kcall(f"gattn_bwd_flash T{Tq}x{Tk}",
+           _attn_bytes(q, B, Tq, Tk, H, dk, 2 * Tq + 2 * Tk, Tq + 2 * Tk),
+           10.0 * B * H * Tq * Tk * dk, "savqa_gattn_bwd_flash", _stream(), _p(q), ldq, _p(k), ldk,
+           _p(v), ldv, _p(G), _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo, _p(stats),
+           _p(dq), lddq, _p(dk_), lddk, _p(dv), lddv)
 
 
 FULL_ROW_MAX_T = 128  # attn.hip's full-row kernels; longer sequences use the key-tiled path
@@ -576,5 +623,7 @@ def adam_rows(p, g, m, v, width, nrows, flags, lr, beta1, beta2, eps, bc1, bc2, 
 
 
 def adam(p, g, m, v, n, lr, beta1, beta2, eps, bc1, bc2, grad_scale=1.0):
-    call("savqa_adam", _stream(), _p(p), _p(g), _p(m), _p(v), int(n), float(lr), float(beta1),
-         float(beta2), float(eps), float(bc1), float(bc2), float(grad_scale))
+    # 28 B per parameter: p, m, v read and written, g read
+    _kcall("adam", 28 * int(n), 0, "savqa_adam", _stream(), _p(p), _p(g), _p(m), _p(v), int(n),
+           float(lr), float(beta1), float(beta2), float(eps), float(bc1), float(bc2),
+           float(grad_scale))

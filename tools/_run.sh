@@ -1,12 +1,7 @@
-set -o pipefail
-cat /sys/fs/cgroup/cpu.max 2>&1; cat /sys/fs/cgroup/cpu.weight 2>&1; nproc; python3 -c "import os;print(len(os.sched_getaffinity(0)), os.cpu_count())"
-for t in 16 64 256; do
-timeout -k 5 60 python3 -c "
-import torch,time
-torch.set_num_threads($t)
-a=torch.randn(2048,2048)
-t0=time.perf_counter()
-for _ in range(5): a@a
-print($t, 'threads', (time.perf_counter()-t0)/5, 's per 2048^3 matmul')
-" || echo "$t threads: timed out"
-done
+set -eo pipefail
+export SAVQA_BENCH_PREC=fp32x6
+TO=600 bash tools/gpu.sh tests tests/test_kernels_gpu.py -k "gemm" > gpurun_out/t_gemm.txt 2>&1 || { tail -40 gpurun_out/t_gemm.txt; exit 1; }
+tail -2 gpurun_out/t_gemm.txt
+TO=600 bash tools/gpu.sh tests tests/test_cfg4_gpu.py > gpurun_out/t_cfg4.txt 2>&1 || { tail -60 gpurun_out/t_cfg4.txt; exit 1; }
+tail -8 gpurun_out/t_cfg4.txt
+TO=300 bash tools/gpu.sh ab d2 2>&1 | grep -v "amdgpu.ids\|UserWarning\|detach\|final_loss"
