@@ -59,9 +59,11 @@ const char* savqa_last_error(void);
 typedef struct savqa_gemm_desc {
     int64_t M, N, K;
     const float* A; int64_t lda; int32_t a_trans;
-    int32_t prec;      /* products: 0 fp32 MFMA (exact), 3 3xbf16 split */
+    int32_t prec;      /* products: 0 fp32 MFMA (exact), 3 3xbf16 split, 6 fp32 from exact
+                          three-term bf16 splits (six bf16 MFMA products, gemm_x6.hip) */
     const int64_t* a_rows;
-    const float* B; int64_t ldb; int32_t b_trans; int32_t _pad1;
+    const float* B; int64_t ldb; int32_t b_trans;
+    int32_t tile_hint; /* prec 6: 0 = library's choice, 1 = 128x128 kernel, 2 = 256x128 kernel */
     const int64_t* b_rows;
     float* C; int64_t ldc;
     int64_t c_group, c_stride, c_offset;
@@ -128,6 +130,11 @@ typedef struct savqa_gemm_lp_desc {
     const int64_t* c_rows;  /* atomic only: output row of m is c_rows[m] (scatter-add) */
     int64_t n_store;        /* atomic only, > 0: columns >= n_store are not stored (an operand
                                zero-padded to a multiple of 8 columns, C rows n_store wide) */
+    float* ws; int64_t ws_elems;  /* optional split-K workspace (fp32 elements): a split-K
+                               launch into fp32 C with a linear epilogue (no relu / mask / Cb /
+                               c_rows / n_store / row map) and ws_elems >= slices*M*N stores
+                               each K slice's partial tile with plain stores and then adds the
+                               slices into C in one pass (C += sum), instead of fp32 atomics */
 } savqa_gemm_lp_desc;
 
 int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* d);

@@ -65,6 +65,7 @@ struct LpArgs {
   // tail_t0 on, in tail_f k-slices of tail_kchunk each, accumulated atomically into C
   int full, tail_t0, tail_f;
   int64_t tail_kchunk;
+  float* slab;            // split-K partial slabs [slice][M][N] (savqa_gemm_lp_desc.ws), or null
   int dbg;                // diagnostic builds only (SAVQA_LP_DIAG=1, tools/lp_bench.py --dbg):
                           // 1 = skip the MFMAs, 2 = skip the k-loop DMAs, 4 = skip the
                           // epilogue; production builds compile every test of it away
@@ -514,6 +515,69 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
   }
 }
 
+// Split-K slab epilogue (128 x 128 kernel): the slice's partial tile goes to its own slab
+// [slice][M][N] with plain 16-B stores straight from the swapped-MFMA accumulators (lane:
+// row 16i + lane % 16, columns 16j + 4 (lane / 16) .. +3); lp_slab_reduce_kernel then adds the
+// slices into C. Replaces the fp32 atomics (~1.3 TB/s chip-wide: ~30 % of a cfg-3 dW launch,
+// all of it after the last k-tile) with full-rate stores and one pass over the slabs, and
+// makes the sum deterministic. Linear epilogue only (host-checked): alpha, and bias / row
+// vector / residual on slice 0; N % 4 == 0.
+__device__ __forceinline__ void lp_epilogue_slab(const savqa_gemm_lp_desc& d, const f4 (&acc)[4][4],
+                                                 int64_t row0, int64_t col0, bool first_split,
+                                                 int lane, float* __restrict__ slab) {
+  const int ri = lane & 15, g = lane >> 4;
+  f4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t n = col0 + 16 * j + 4 * g;
+    bv[j] = f4{0.f, 0.f, 0.f, 0.f};
+    if (first_split && d.bias && n < d.N) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[j][r] = d.bias[n + r];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t m = row0 + 16 * i + ri;
+    if (m >= d.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = col0 + 16 * j + 4 * g;
+      if (n >= d.N) continue;
+      f4 v = acc[i][j] * d.alpha + bv[j];
+      if (first_split && (d.rowvec || d.resid)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (d.rowvec) v[r] += d.rowvec[(m % d.rowvec_period) * d.ldrv + n + r];
+          if (d.resid) v[r] += d.resid[m * d.ldr + n + r];
+        }
+      }
+      *reinterpret_cast<f4*>(slab + m * d.N + n) = v;
+    }
+  }
+}
+
+// C[m][n] += sum over the ns slabs (fixed order), four columns per thread
+__global__ __launch_bounds__(256) void lp_slab_reduce_kernel(const float* __restrict__ slab, int ns,
+                                                             int64_t M, int64_t N,
+                                                             float* __restrict__ C, int64_t ldc,
+                                                             int vec) {
+  const int64_t n4 = N / 4;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= M * n4) return;
+  const int64_t m = t / n4, n = 4 * (t - m * n4);
+  const int64_t plane = M * N;
+  f4 acc = *reinterpret_cast<const f4*>(slab + m * N + n);
+  for (int k = 1; k < ns; ++k) acc += *reinterpret_cast<const f4*>(slab + k * plane + m * N + n);
+  float* cp = C + m * ldc + n;
+  if (vec) {
+    *reinterpret_cast<f4*>(cp) += acc;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cp[r] += acc[r];
+  }
+}
+
 // Epilogue operands prefetched under the last k-tile's MFMAs (128 x 128 kernel, one 64-row
 // pass per wave): PRE = 1 the fp32 residual (the 16 rows x 4 columns each lane stores,
 // lp_rows' map), PRE = 2 the bf16 ReLU-backward mask of a bf16-only output (optionally through
@@ -745,7 +809,10 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
 
   // ---------------------------------------------------------------- epilogue
   __syncthreads();  // every wave's last k-tile reads are done: LDS is free
-  if (tail)
+  if (PRE == 0 && !FP8 && args.slab && !tail)
+    lp_epilogue_slab(d, acc, m0 + wm * 64, n0 + wn * 64, first_split, lane,
+                     args.slab + (int64_t)slice * d.M * d.N);
+  else if (tail)
     lp_epilogue<4, 4>(d, acc, smem + wave * 16384, m0 + wm * 64, n0 + wn * 64, first_split, lane,
                       64, -1, true);
   else if constexpr (PRE != 0)
@@ -1295,6 +1362,12 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   a.tail_f = p.tail_f;
   a.tail_kchunk = p.tail_per * bk;
   if (d.K == 0) a.kchunk = 0;
+  // split-K slabs instead of atomics (savqa_gemm_lp_desc.ws): 128 x 128 kernel, plain
+  // accumulation into fp32 C with a linear epilogue
+  const bool slabs = d.ws && var == 1 && !fp8 && p.nsplit > 1 && d.C && !d.Cb && !d.relu &&
+                     !d.mask && !d.c_rows && d.n_store == 0 && d.c_group <= 0 && d.N % 4 == 0 &&
+                     ((uintptr_t)d.ws & 15) == 0 && d.ws_elems >= (int64_t)p.nsplit * d.M * d.N;
+  a.slab = slabs ? d.ws : nullptr;
   hipStream_t s = as_stream(stream);
   if (p.zero_row0 >= 0 &&
       hipMemset2DAsync(d.C + p.zero_row0 * d.ldc, d.ldc * sizeof(float), 0, d.N * sizeof(float),
@@ -1343,6 +1416,12 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
     else if (d.a_trans && !d.b_trans) SAVQA_LP1(true, false);
     else SAVQA_LP1(true, true);
 #undef SAVQA_LP1
+  }
+  if (slabs) {
+    const int vec = (d.ldc % 4 == 0) && (((uintptr_t)d.C & 15) == 0);
+    const int64_t n = d.M * (d.N / 4);
+    hipLaunchKernelGGL(lp_slab_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       d.ws, p.nsplit, d.M, d.N, d.C, d.ldc, vec);
   }
   return check_launch("savqa_gemm_lp");
 }

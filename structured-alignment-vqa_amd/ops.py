@@ -8,6 +8,7 @@ missing library or a CPU tensor raises.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional
 
 import torch
@@ -66,7 +67,7 @@ class GemmProbe:
             al = all(p % 16 == 0 and ld % 4 == 0 for p, ld in ((d.A, d.lda), (d.B, d.ldb)))
             kg = (d.a_trans and d.a_rows) or (not d.b_trans and d.b_rows)
             if al and not kg:
-                return f"gemm_x6_kernel<{lay}>"
+                return f"gemm_x6w_kernel<{lay}>" if plan[0] == 256 else f"gemm_x6_kernel<{lay}>"
             return f"gemm_f32_kernel<{plan[0]},{plan[0]},{lay}>"
         if d.prec:
             return f"gemm_bf16_kernel<{lay},{d.prec}>"
@@ -92,6 +93,24 @@ _probe = None
 # gemm_precision="bf16x3")) via gemm_precision(); the bf16 / fp8 modes use gemm_lp instead.
 PREC = {"fp32": 0, "fp32_native": 0, "bf16x3": 3, "fp32x6": 6}
 _prec = 0
+_tile_hint = 0  # x6 kernel variant (savqa_gemm_desc.tile_hint): 0 library, 1 128x128, 2 256x128
+
+
+class x6_tiles:
+    """Context manager: x6 GEMMs launched inside use the given kernel variant (tests / A/B)."""
+
+    def __init__(self, hint: int):
+        self.h = int(hint)
+
+    def __enter__(self):
+        global _tile_hint
+        self.old, _tile_hint = _tile_hint, self.h
+        return self
+
+    def __exit__(self, *exc):
+        global _tile_hint
+        _tile_hint = self.old
+        return False
 
 
 class gemm_precision:
@@ -154,7 +173,7 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
          c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None, ldrv=0, rowvec_period=0,
          resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False, rowscale=None, relu=False,
          alpha=1.0, beta=0.0, atomic=False, split_k=1, colsum_a=None, prec=None,
-         plan_only=False):
+         plan_only=False, tile_hint=None):
     """Generic MFMA GEMM with fused epilogue (see savqa_gemm in include/savqa.h).
     plan_only: no launch, return savqa_gemm_plan's [tile, split, tail slices, workgroups]."""
     d = GemmDesc()
@@ -175,6 +194,7 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
     d.alpha, d.beta = float(alpha), float(beta)
     d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
     d.colsum_a = _p(colsum_a)
+    d.tile_hint = _tile_hint if tile_hint is None else int(tile_hint)
     if plan_only:
         plan = (C.c_int32 * 4)()
         call("savqa_gemm_plan", C.byref(d), C.cast(plan, C.c_void_p))
@@ -202,8 +222,9 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
             ldc=0, Cb=None, ldcb=0, c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None,
             ldrv=0, rowvec_period=0, resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False,
             alpha=1.0, relu=False, atomic=False, split_k=1, tile_hint=0, c_rows=None,
-            n_store=0):
-    """savqa_gemm_lp_desc for bf16 / fp8 operands (include/savqa.h)."""
+            n_store=0, ws=None):
+    """savqa_gemm_lp_desc for bf16 / fp8 operands (include/savqa.h). ws: split-K partial-slab
+    workspace (fp32 tensor), see lp_workspace."""
     d = _lib.GemmLpDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
     d.A, d.lda, d.a_trans, d.a_type = _p(A), int(lda), int(bool(a_trans)), DT[A.dtype]
@@ -220,7 +241,29 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
     d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
     d.tile_hint = int(tile_hint)
     d.c_rows, d.n_store = _p(c_rows), int(n_store)
+    if ws is not None:
+        d.ws, d.ws_elems = _p(ws), int(ws.numel())
     return d
+
+
+_lp_ws = {}
+LP_SLABS = os.environ.get("SAVQA_LP_SLABS", "0") != "0"  # default on once measured
+
+
+def lp_workspace(d, dev) -> Optional[Tensor]:
+    """The split-K slab workspace a savqa_gemm_lp launch of d needs (slices x M x N fp32), one
+    per (device, stream), grown as needed (None when d does not split K)."""
+    plan = (C.c_int32 * 4)()
+    call("savqa_gemm_lp_plan", C.byref(d), C.cast(plan, C.c_void_p))
+    if plan[1] <= 1:
+        return None
+    need = int(plan[1]) * int(d.M) * int(d.N)
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), _stream())
+    ws = _lp_ws.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.float32, device=dev)
+        _lp_ws[key] = ws
+    return ws
 
 
 def lp_variant(d) -> str:
@@ -242,9 +285,14 @@ def lp_supported(d) -> bool:
     return bool(_lib.load().savqa_gemm_lp_supported(C.byref(d)))
 
 
-def gemm_lp(*args, **kw):
-    """Low-precision-operand MFMA GEMM (savqa_gemm_lp): same arguments as lp_desc."""
+def gemm_lp(*args, slabs=False, **kw):
+    """Low-precision-operand MFMA GEMM (savqa_gemm_lp): same arguments as lp_desc; slabs: give a
+    split-K launch its partial-slab workspace (no fp32 atomics)."""
     d = lp_desc(*args, **kw)
+    if slabs and LP_SLABS:
+        ws = lp_workspace(d, args[0].device)
+        if ws is not None:
+            d.ws, d.ws_elems = _p(ws), int(ws.numel())
     if _probe is None:
         call("savqa_gemm_lp", _stream(), C.byref(d))
         return
@@ -326,7 +374,8 @@ def linear_dw_lp(dY: Tensor, X: Tensor, dW: Tensor, db: Optional[Tensor], *, row
     """dW += dY^T X on bf16 operands (split-K, atomics); db += colsum(dY) from the fp32 dY
     when the caller has it (dy32), else from the bf16 one."""
     N, K = dW.shape
-    gemm_lp(dY, X, N, K, rows, lda=N, ldb=K, a_trans=True, C=dW, ldc=K, atomic=True, split_k=-1)
+    gemm_lp(dY, X, N, K, rows, lda=N, ldb=K, a_trans=True, C=dW, ldc=K, atomic=True, split_k=-1,
+            slabs=True)
     if db is not None:
         if dy32 is not None:
             colsum_acc(dy32, rows, N, N, db)

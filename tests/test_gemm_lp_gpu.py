@@ -7,6 +7,8 @@ so what is checked is the kernel's indexing, transposed LDS reads, swizzles, sca
 epilogue; products of bf16 or fp8 values are exact in fp32 and only the fp32 summation
 order differs (bar 2e-5 of sum|a*b| scale).
 """
+import ctypes
+
 import pytest
 import torch
 
@@ -72,6 +74,36 @@ def test_bf16_kernel_variants(hint, lay, M, N, K):
     ref = Ar @ Br + resid.double()
     assert rel(C, ref) < 2e-5
     assert torch.equal(Cb.cpu(), C.to(torch.bfloat16).cpu())
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 1536, 18688), (520, 1300, 37376), (2048, 512, 25600),
+                                   (512, 2048, 2440)])
+def test_bf16_dw_split_k_slabs(M, N, K):
+    """Split-K dW through per-slice slabs (savqa_gemm_lp_desc.ws: plain stores + one reduce
+    pass) instead of fp32 atomics: accumulates into the existing gradient like the atomic path,
+    within fp32 rounding of it and of fp64, bit-identical from run to run (fixed order), with
+    bias on slice 0 and edge tiles (M, N not multiples of 128)."""
+    O = ops()
+    O.LP_SLABS = True  # (the library default is decided by measurement)
+    dY = bf((K, N), 5)
+    X = bf((K, M), 6)
+    b = torch.randn(M, device=dev)
+    W0 = torch.randn(N, M, device=dev)
+    outs = []
+    for slabs in (False, True, True):
+        dW = W0.clone()
+        O.gemm_lp(dY, X, N, M, K, lda=N, ldb=M, a_trans=True, C=dW, ldc=M, atomic=True,
+                  split_k=-1, bias=b, slabs=slabs)
+        outs.append(dW)
+    plan = (ctypes.c_int32 * 4)()
+    d = O.lp_desc(dY, X, N, M, K, lda=N, ldb=M, a_trans=True, C=outs[0], ldc=M, atomic=True,
+                  split_k=-1)
+    O.call("savqa_gemm_lp_plan", ctypes.byref(d), ctypes.cast(plan, ctypes.c_void_p))
+    assert plan[1] > 1, "the shape must split K"
+    ref = W0.double() + dY.double().t() @ X.double() + b.double()
+    assert rel(outs[1] - W0, ref - W0.double()) < 2e-5
+    assert rel(outs[1] - W0, outs[0] - W0) < 2e-5
+    assert torch.equal(outs[1], outs[2])  # no atomics: the same bits every run
 
 
 @pytest.mark.parametrize("hint", [0, 5])

@@ -54,8 +54,9 @@ def bf16_case(lay, m, n, k, out, hint=0):
     elif out.startswith("atomic"):  # "atomic" (library split) or "atomicS" (split_k = S)
         C = torch.zeros(m, n, device=dev)
         sk = int(out[6:]) if len(out) > 6 else -1
+        slabs = os.environ.get("SAVQA_LP_SLABS", "1") != "0"  # split-K slabs (ops.linear_dw_lp)
         f = lambda: ops.gemm_lp(A, B, m, n, k, C=C, ldc=n, atomic=True, split_k=sk,
-                                tile_hint=hint, **kw)
+                                tile_hint=hint, slabs=slabs, **kw)
     else:
         C = torch.empty(m, n, device=dev)
         f = lambda: ops.gemm_lp(A, B, m, n, k, C=C, ldc=n, tile_hint=hint, **kw)
