@@ -78,13 +78,13 @@ def test_bf16_kernel_variants(hint, lay, M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(512, 1536, 18688), (520, 1300, 37376), (2048, 512, 25600),
                                    (512, 2048, 2440)])
-def test_bf16_dw_split_k_slabs(M, N, K):
+def test_bf16_dw_split_k_slabs(M, N, K, monkeypatch):
     """Split-K dW through per-slice slabs (savqa_gemm_lp_desc.ws: plain stores + one reduce
     pass) instead of fp32 atomics: accumulates into the existing gradient like the atomic path,
     within fp32 rounding of it and of fp64, bit-identical from run to run (fixed order), with
     bias on slice 0 and edge tiles (M, N not multiples of 128)."""
     O = ops()
-    O.LP_SLABS = True  # (the library default is decided by measurement)
+    monkeypatch.setattr(O, "LP_SLABS", True)  # (the default is decided by measurement)
     dY = bf((K, N), 5)
     X = bf((K, M), 6)
     b = torch.randn(M, device=dev)
