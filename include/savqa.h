@@ -62,8 +62,7 @@ typedef struct savqa_gemm_desc {
     int32_t prec;      /* products: 0 fp32 MFMA (exact), 3 3xbf16 split, 6 fp32 from exact
                           three-term bf16 splits (six bf16 MFMA products, gemm_x6.hip) */
     const int64_t* a_rows;
-    const float* B; int64_t ldb; int32_t b_trans;
-    int32_t tile_hint; /* prec 6: 0 = library's choice, 1 = 128x128 kernel, 2 = 256x128 kernel */
+    const float* B; int64_t ldb; int32_t b_trans; int32_t _pad1;
     const int64_t* b_rows;
     float* C; int64_t ldc;
     int64_t c_group, c_stride, c_offset;

@@ -24,7 +24,7 @@ class GemmDesc(C.Structure):
         ("M", c_i64), ("N", c_i64), ("K", c_i64),
         ("A", c_p), ("lda", c_i64), ("a_trans", c_i32), ("prec", c_i32),
         ("a_rows", c_p),
-        ("B", c_p), ("ldb", c_i64), ("b_trans", c_i32), ("tile_hint", c_i32),
+        ("B", c_p), ("ldb", c_i64), ("b_trans", c_i32), ("_pad1", c_i32),
         ("b_rows", c_p),
         ("C", c_p), ("ldc", c_i64),
         ("c_group", c_i64), ("c_stride", c_i64), ("c_offset", c_i64),

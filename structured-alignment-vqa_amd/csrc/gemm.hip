@@ -773,19 +773,6 @@ __global__ __launch_bounds__(64 * NW) void gemm_skinny16_kernel(savqa_gemm_desc 
     else hipLaunchKernelGGL((K_<AT_, BT_, SK_WAVES, false, false>), g, b, 0, s, d, tn, avec, bvec);               \
   } while (0)
 
-#ifndef SAVQA_X6_WIDE_DEFAULT
-#define SAVQA_X6_WIDE_DEFAULT 0
-#endif
-// the x6 kernel variant: SAVQA_X6_WIDE=1 the 256 x 128 kernel, 0 the 128 x 128 one
-static bool x6_wide() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SAVQA_X6_WIDE");
-    v = e ? (atoi(e) != 0) : SAVQA_X6_WIDE_DEFAULT;
-  }
-  return v != 0;
-}
-
 static int cu_count() {
   // the CU count of the current device
   static int cached[64] = {0};
@@ -816,7 +803,6 @@ static int auto_split(int64_t tiles, int64_t K, int BK, int slots) {
 // Launch plan: tile size, split-K, tail split (shared by savqa_gemm / savqa_gemm_plan).
 struct GemmPlan {
   int tile, split;
-  int bm, bn;  // 128-class tiles: rows / columns per workgroup (x6 wide kernel: 256 x 128)
   GemmGrid gg;
   int grid_x, nsplit;
   int64_t zero_row0;  // >= 0: rows [zero_row0, M) of C are zero-filled before the launch
@@ -847,22 +833,17 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
     return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32), 3 (3xbf16) or 6 (fp32 x6)");
   // gemm_bf16_kernel / gemm_x6_kernel k-tile: 32; workgroups per CU the planner counts
   const int BK = d.prec ? 32 : (d.a_trans ? GEMM_BK_DW : GEMM_BK);
-  // x6 wide variant (gemm_x6w_kernel, 256 x 128, one workgroup per CU): SAVQA_X6_WIDE=0/1
-  const bool wide = d.prec == 6 && (d.tile_hint == 2 || (d.tile_hint != 1 && x6_wide()));
-  const int bm = wide ? 256 : 128, bn = 128;
-  const int occ = d.prec == 6 ? (wide ? 1 : 2) : GEMM_PLAN_OCC;
+  const int occ = d.prec == 6 ? 2 : GEMM_PLAN_OCC;
   const int slots = occ * cu_count();
   const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
-  const int64_t tilesb = ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn);
   int split = d.split_k > 1 ? d.split_k : 1;
-  if (d.split_k < 0) split = auto_split(tilesb, d.K, BK, slots);
+  if (d.split_k < 0) split = auto_split(tiles128, d.K, BK, slots);
   // 128x128 tiles once there is enough parallelism (split-K counts), else the skinny
   // kernel (32x32 tiles, K split over the 8 waves of a workgroup; no split-K launch),
   // 16x16 tiles while 32x32 ones would leave CUs idle (< SK16_MAX_TILES tiles)
   if (tiles128 * split < 160) {
     const int64_t tiles32 = ((d.M + 31) / 32) * ((d.N + 31) / 32);
     p.tile = tiles32 < SK16_MAX_TILES ? 16 : 32;
-    p.bm = p.bn = p.tile;
     p.split = 1;
     p.nsplit = 1;
     p.gg.tiles_n = (int)((d.N + p.tile - 1) / p.tile);
@@ -872,10 +853,8 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
     return 0;
   }
   p.tile = 128;
-  p.bm = bm;
-  p.bn = bn;
-  const int tm = (int)((d.M + bm - 1) / bm);
-  const int tn = (int)((d.N + bn - 1) / bn);
+  const int tm = (int)((d.M + p.tile - 1) / p.tile);
+  const int tn = (int)((d.N + p.tile - 1) / p.tile);
   const int T = tm * tn;
   int64_t kchunk = (d.K + split - 1) / split;
   kchunk = (kchunk + BK - 1) / BK * BK;
@@ -939,7 +918,7 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
         const int64_t tk = (d.K + f - 1) / f;
         p.gg.tail_kchunk = (tk + BK - 1) / BK * BK;
         p.grid_x = p.gg.full + r * f;
-        p.zero_row0 = (int64_t)(p.gg.tail_t0 / tn) * bm;
+        p.zero_row0 = (int64_t)(p.gg.tail_t0 / tn) * p.tile;
       }
     }
   }
@@ -968,7 +947,7 @@ extern "C" int savqa_gemm_plan(const savqa_gemm_desc* dp, int32_t* out) {
   savqa_gemm_desc d = *dp;
   GemmPlan p{};
   if (int rc = plan_gemm(d, p)) return rc;
-  out[0] = p.tile == 128 ? p.bm : p.tile;  // 256: the x6 wide kernel (256 x 128 tiles)
+  out[0] = p.tile;
   out[1] = p.split;
   out[2] = p.gg.tail_f > 1 ? p.gg.tail_f : 0;
   out[3] = p.grid_x * p.nsplit;
@@ -997,7 +976,7 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
                        d.M - p.zero_row0, s) != hipSuccess)
     return fail(SAVQA_EUNSUP, "savqa_gemm: tail zero-fill failed");
   if (p.tile == 128 && d.prec == 6) {
-    savqa_launch_gemm_x6(d, p.gg, p.grid_x, p.nsplit, s, p.bm == 256);
+    savqa_launch_gemm_x6(d, p.gg, p.grid_x, p.nsplit, s);
   } else if (p.tile == 128 && d.prec != 0) {
     savqa_launch_gemm_bf16(d, p.gg, p.grid_x, p.nsplit, s, avec, bvec);
   } else if (p.tile == 128) {

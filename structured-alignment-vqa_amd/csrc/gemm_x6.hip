@@ -347,304 +347,13 @@ __global__ __launch_bounds__(GEMM_NT, X6_OCC) void gemm_x6_kernel(savqa_gemm_des
   gemm_epilogue16<4, 4, 64, 64>(d, acc, m0, n0, wm, wn, lane, first_split, atomic);
 }
 
-// ---------------------------------------------------------------------------------------
-// Wide variant (gemm_x6w_kernel): 256 x 128 tile, 512 threads = 8 waves (4 x 2) of 64 x 64,
-// ONE workgroup per CU with two LDS stages (2 x 72 KB) and one barrier per k-tile; operand
-// loads two k-tiles ahead in two register sets. In iteration t every wave runs k-tile t's
-// MFMAs from one stage and, fragment row by fragment row beside them, splits the staged
-// k-tile t+1 into the other stage, then refills the freed register set with k-tile t+3 -- so
-// the split VALU overlaps the MFMAs of the same wave and a load has a whole iteration to land.
-// Per k-tile a workgroup splits (256 + 128) x 32 values for 768 MFMAs (the 128 x 128 kernel:
-// 256 x 32 for 384), and fetches 0.75x the operand bytes per FLOP.
-//   ROW operand of R rows: float4 u = tid + 512 it (it < R / 64) covers row u / 8, k 4 (u % 8).
-//   COL operand of R columns: one 4k x 4m block per thread (g = tid / 8, kg = tid % 8): R = 256
-//     every thread, R = 128 threads < 256 (waves 0-3: one of them on each SIMD).
-constexpr int X6W_NT = 512;
-constexpr int X6W_BM = 256, X6W_BN = 128;
-constexpr int X6W_APL = X6W_BM * X6_ROWB;           // bytes of one A plane (16 KB)
-constexpr int X6W_BPL = X6W_BN * X6_ROWB;           // bytes of one B plane (8 KB)
-constexpr int X6W_STAGE = 3 * (X6W_APL + X6W_BPL);  // 72 KB: A planes, then B planes
-
-template <bool ROW, int R>
-struct X6WOp {
-  static constexpr int IT = ROW ? R / 64 : 4;       // float4 per thread
-  static constexpr int NTH = ROW ? X6W_NT : R * 2;  // threads holding data
-  f4 r[2][IT];
-  const float* rp[ROW ? IT : 1];
-  int64_t ld;
-
-  static __device__ __forceinline__ bool active(int tid) { return ROW || tid < NTH; }
-
-  // FAST path pointers (edge tiles clamp as X6Operand)
-  __device__ __forceinline__ void setup_fast(const float* __restrict__ base, int64_t ld_,
-                                             const int64_t* __restrict__ rows, int64_t m0,
-                                             int64_t mlim, int tid) {
-    ld = ld_;
-    if constexpr (ROW) {
-#pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int u = tid + X6W_NT * it;
-        const int64_t m = min(m0 + (u >> 3), mlim - 1);
-        const int64_t rr = rows ? rows[m] : m;
-        rp[it] = base + rr * ld + 4 * (u & 7);
-      }
-    } else {
-      const int t = active(tid) ? tid : 0;
-      rp[0] = base + (int64_t)(4 * (t & 7)) * ld + min(m0 + 4 * (t >> 3), mlim - 4);
-    }
-  }
-
-  template <int S>
-  __device__ __forceinline__ void load_fast(int64_t k0, int tid) {
-    if (!active(tid)) return;
-#pragma unroll
-    for (int it = 0; it < IT; ++it)
-      r[S][it] = *reinterpret_cast<const f4*>(ROW ? rp[it] + k0 : rp[0] + (k0 + it) * ld);
-  }
-
-  // guarded (k tail, edge widths, k-row gathers): clamped addresses, zeros outside
-  template <int S>
-  __device__ __forceinline__ void load_slow(const float* __restrict__ base, int64_t ldb,
-                                            const int64_t* __restrict__ rows, int64_t mlim,
-                                            int64_t m0, int64_t k0, int64_t kend, int tid) {
-    if (!active(tid)) return;
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      int64_t row, col, rlim, clim;
-      if constexpr (ROW) {
-        const int u = tid + X6W_NT * it;
-        row = m0 + (u >> 3);
-        col = k0 + 4 * (u & 7);
-        rlim = mlim;
-        clim = kend;
-      } else {
-        row = k0 + 4 * (tid & 7) + it;
-        col = m0 + 4 * (tid >> 3);
-        rlim = kend;
-        clim = mlim;
-      }
-      const bool rok = row < rlim;
-      const int64_t rc = rok ? row : 0;
-      const int64_t rr = rows ? rows[rc] : rc;
-      const float* p = base + rr * ldb;
-      float e[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool ok = rok && (col + q < clim);
-        const float val = p[ok ? col + q : 0];
-        e[q] = ok ? val : 0.f;
-      }
-      r[S][it] = f4{e[0], e[1], e[2], e[3]};
-    }
-  }
-
-  // colsum_a (COL operand): cs[q] += sum over this thread's 4 k of A(m = 4g + q, k)
-  template <int S>
-  __device__ __forceinline__ void accum(f4& cs) const {
-    cs += (r[S][0] + r[S][1]) + (r[S][2] + r[S][3]);
-  }
-
-  // part q (of 4) of the split-and-store of set S into the planes at img: ROW float4 it with
-  // it % 4 == q (R = 128: parts 0-1 only), COL block row q
-  template <int S>
-  __device__ __forceinline__ void store_part(char* img, int pstride, int tid, int q) const {
-    if (!active(tid)) return;
-    if constexpr (ROW) {
-#pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        if (it % 4 != q) continue;
-        const int u = tid + X6W_NT * it;
-        put3s(img, pstride, x6_off(u >> 3, 4 * (u & 7)), r[S][it]);
-      }
-    } else {
-      const int g = tid >> 3, kg = tid & 7;
-      put3s(img, pstride, x6_off(4 * g + q, 4 * kg), f4{r[S][0][q], r[S][1][q], r[S][2][q], r[S][3][q]});
-    }
-  }
-
-  // three bf16 planes at img, img + pstride, img + 2 pstride
-  static __device__ __forceinline__ void put3s(char* img, int pstride, int off, f4 v) {
-    bf16x4 p0, p1, p2;
-    split3(v, p0, p1, p2);
-    *reinterpret_cast<bf16x4*>(img + off) = p0;
-    *reinterpret_cast<bf16x4*>(img + pstride + off) = p1;
-    *reinterpret_cast<bf16x4*>(img + 2 * pstride + off) = p2;
-  }
-};
-
-// one k-tile of MFMAs from a stage, between(i) run after fragment row i's 24 MFMAs
-template <class F>
-__device__ __forceinline__ void x6w_compute(const char* st, int wm, int wn, int lane,
-                                            f4 (&acc)[4][4], F&& between) {
-  const char* Bs = st + 3 * X6W_APL;
-  bf16x8 b[4][3];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int p = 0; p < 3; ++p) b[j][p] = x6_frag(Bs + p * X6W_BPL, wn * 64 + 16 * j, lane);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    bf16x8 a[3];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) a[p] = x6_frag(st + p * X6W_APL, wm * 64 + 16 * i, lane);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[2], b[j][0], acc[i][j]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[1], b[j][1], acc[i][j]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[0], b[j][2], acc[i][j]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[1], b[j][0], acc[i][j]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[0], b[j][1], acc[i][j]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[0], b[j][0], acc[i][j]);
-    between(i);
-  }
-}
-
-template <bool AT, bool BT, int MODE>
-__device__ __forceinline__ void x6w_mainloop(const savqa_gemm_desc& d, char* smem, int64_t m0,
-                                             int64_t n0, int64_t kbeg, int64_t kend, int nt,
-                                             f4 (&acc)[4][4], bool do_cs, f4& cs) {
-  X6WOp<!AT, X6W_BM> la;
-  X6WOp<BT, X6W_BN> lb;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  if constexpr (MODE != 0) {
-    la.setup_fast(d.A, d.lda, AT ? nullptr : d.a_rows, m0, d.M, tid);
-    lb.setup_fast(d.B, d.ldb, BT ? d.b_rows : nullptr, n0, d.N, tid);
-  }
-  auto load = [&](auto set, int t) {  // k-tile t into register set S
-    constexpr int S = decltype(set)::value;
-    const int64_t k0 = kbeg + (int64_t)t * X6_BK;
-    if (MODE == 1 || (MODE == 2 && k0 + X6_BK <= kend)) {
-      la.template load_fast<S>(k0, tid);
-      lb.template load_fast<S>(k0, tid);
-    } else {
-      la.template load_slow<S>(d.A, d.lda, d.a_rows, d.M, m0, k0, kend, tid);
-      lb.template load_slow<S>(d.B, d.ldb, d.b_rows, d.N, n0, k0, kend, tid);
-    }
-  };
-  auto store = [&](auto set, int t, int q) {  // part q of register set S into k-tile t's stage
-    constexpr int S = decltype(set)::value;
-    char* st = smem + (t & 1) * X6W_STAGE;
-    la.template store_part<S>(st, X6W_APL, tid, q);
-    lb.template store_part<S>(st + 3 * X6W_APL, X6W_BPL, tid, q);
-  };
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
-  load(S0{}, 0);
-  if (nt > 1) load(S1{}, 1);
-  if (do_cs) la.template accum<0>(cs);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) store(S0{}, 0, q);
-  if (nt > 2) load(S0{}, 2);
-  __syncthreads();
-  // iteration t: k-tile t+1 waits in set (t+1) % 2, k-tile t+2 in the other
-  auto iter = [&](auto nxt, int t) {
-    const bool more = t + 1 < nt;
-    if (more && do_cs) la.template accum<decltype(nxt)::value>(cs);
-    x6w_compute(smem + (t & 1) * X6W_STAGE, wm, wn, lane, acc, [&](int i) {
-      if (more) store(nxt, t + 1, i);
-    });
-    if (t + 3 < nt) load(nxt, t + 3);
-    __syncthreads();  // stage t free for k-tile t+2; stage t+1 complete
-  };
-  for (int t = 0; t < nt; t += 2) {
-    iter(S1{}, t);
-    if (t + 1 < nt) iter(S0{}, t + 1);
-  }
-}
-
-template <bool AT, bool BT>
-__device__ __forceinline__ int x6w_mode(const savqa_gemm_desc& d, int64_t m0, int64_t n0,
-                                        int64_t kbeg, int64_t kend) {
-  if ((AT && d.a_rows) || (!BT && d.b_rows)) return 0;
-  if (m0 + X6W_BM > d.M && AT && (d.M & 3)) return 0;
-  if (n0 + X6W_BN > d.N && !BT && (d.N & 3)) return 0;
-  return ((kend - kbeg) % X6_BK == 0) ? 1 : 2;
-}
-
-template <bool AT, bool BT>
-__global__ __launch_bounds__(X6W_NT, 1) void gemm_x6w_kernel(savqa_gemm_desc d, GemmGrid gg) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * X6W_STAGE];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int bid = blockIdx.x;
-  int t;
-  int64_t kbeg, kend;
-  bool first_split, atomic;
-  if (bid < gg.full) {
-    int slice;
-    split_remap(gg.full, t, slice);
-    kbeg = (int64_t)slice * gg.kchunk;
-    kend = min(d.K, kbeg + gg.kchunk);
-    first_split = slice == 0;
-    atomic = d.atomic || gridDim.y > 1;
-  } else {
-    const int u = bid - gg.full;
-    const int part = u % gg.tail_f;
-    t = gg.tail_t0 + u / gg.tail_f;
-    kbeg = (int64_t)part * gg.tail_kchunk;
-    kend = min(d.K, kbeg + gg.tail_kchunk);
-    first_split = part == 0;
-    atomic = true;
-  }
-  const int tn = t % gg.tiles_n, tm = t / gg.tiles_n;
-  const int64_t m0 = (int64_t)tm * X6W_BM, n0 = (int64_t)tn * X6W_BN;
-  f4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  const int nt = kend > kbeg ? (int)((kend - kbeg + X6_BK - 1) / X6_BK) : 0;
-  const bool do_cs = AT && d.colsum_a != nullptr && tn == 0;
-  f4 cs = {0.f, 0.f, 0.f, 0.f};
-  if (nt > 0) {
-    const int mode = x6w_mode<AT, BT>(d, m0, n0, kbeg, kend);
-    if (mode == 1)
-      x6w_mainloop<AT, BT, 1>(d, smem, m0, n0, kbeg, kend, nt, acc, do_cs, cs);
-    else if (mode == 2)
-      x6w_mainloop<AT, BT, 2>(d, smem, m0, n0, kbeg, kend, nt, acc, do_cs, cs);
-    else
-      x6w_mainloop<AT, BT, 0>(d, smem, m0, n0, kbeg, kend, nt, acc, do_cs, cs);
-  }
-  if constexpr (AT) {
-    if (do_cs) {  // block-uniform; the main loop ended with a barrier
-      float* red = reinterpret_cast<float*>(smem);
-      *reinterpret_cast<f4*>(&red[(threadIdx.x & 7) * X6W_BM + 4 * (threadIdx.x >> 3)]) = cs;
-      __syncthreads();
-      for (int i = threadIdx.x; i < X6W_BM; i += X6W_NT) {
-        float v = 0.f;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) v += red[r * X6W_BM + i];
-        if (m0 + i < d.M) atomicAdd(&d.colsum_a[m0 + i], v);
-      }
-    }
-  }
-  gemm_epilogue16<4, 4, 64, 64>(d, acc, m0, n0, wm, wn, lane, first_split, atomic);
-}
-
 }  // namespace savqa
 
-// Launch of the x6 kernels on a plan made by savqa_gemm (gemm.hip): grid (grid_x, nsplit);
-// wide: the 256 x 128 one-workgroup-per-CU kernel (the plan was made for its tile).
+// Launch of the x6 kernels on a plan made by savqa_gemm (gemm.hip): grid (grid_x, nsplit).
 int savqa_launch_gemm_x6(const savqa_gemm_desc& d, const savqa::GemmGrid& gg, int grid_x,
-                         int nsplit, hipStream_t s, bool wide) {
+                         int nsplit, hipStream_t s) {
   using namespace savqa;
-  const dim3 g(grid_x, nsplit);
-  if (wide) {
-    const dim3 b(X6W_NT);
-    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_x6w_kernel<false, true>), g, b, 0, s, d, gg);
-    else if (!d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6w_kernel<false, false>), g, b, 0, s, d, gg);
-    else if (d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6w_kernel<true, false>), g, b, 0, s, d, gg);
-    else hipLaunchKernelGGL((gemm_x6w_kernel<true, true>), g, b, 0, s, d, gg);
-    return 0;
-  }
-  const dim3 b(GEMM_NT);
+  const dim3 g(grid_x, nsplit), b(GEMM_NT);
   if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, true>), g, b, 0, s, d, gg);
   else if (!d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, false>), g, b, 0, s, d, gg);
   else if (d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<true, false>), g, b, 0, s, d, gg);

@@ -67,7 +67,7 @@ class GemmProbe:
             al = all(p % 16 == 0 and ld % 4 == 0 for p, ld in ((d.A, d.lda), (d.B, d.ldb)))
             kg = (d.a_trans and d.a_rows) or (not d.b_trans and d.b_rows)
             if al and not kg:
-                return f"gemm_x6w_kernel<{lay}>" if plan[0] == 256 else f"gemm_x6_kernel<{lay}>"
+                return f"gemm_x6_kernel<{lay}>"
             return f"gemm_f32_kernel<{plan[0]},{plan[0]},{lay}>"
         if d.prec:
             return f"gemm_bf16_kernel<{lay},{d.prec}>"
@@ -93,26 +93,6 @@ _probe = None
 # gemm_precision="bf16x3")) via gemm_precision(); the bf16 / fp8 modes use gemm_lp instead.
 PREC = {"fp32": 0, "fp32_native": 0, "bf16x3": 3, "fp32x6": 6}
 _prec = 0
-_tile_hint = 0  # x6 kernel variant (savqa_gemm_desc.tile_hint): 0 library, 1 128x128, 2 256x128
-
-
-class x6_tiles:
-    """Context manager: x6 GEMMs launched inside use the given kernel variant (tests / A/B)."""
-
-    def __init__(self, hint: int):
-        self.h = int(hint)
-
-    def __enter__(self):
-        global _tile_hint
-        self.old, _tile_hint = _tile_hint, self.h
-        return self
-
-    def __exit__(self, *exc):
-        global _tile_hint
-        _tile_hint = self.old
-        return False
-
-
 class gemm_precision:
     """Context manager: GEMMs launched inside use the given product precision."""
 
@@ -173,7 +153,7 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
          c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None, ldrv=0, rowvec_period=0,
          resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False, rowscale=None, relu=False,
          alpha=1.0, beta=0.0, atomic=False, split_k=1, colsum_a=None, prec=None,
-         plan_only=False, tile_hint=None):
+         plan_only=False):
     """Generic MFMA GEMM with fused epilogue (see savqa_gemm in include/savqa.h).
     plan_only: no launch, return savqa_gemm_plan's [tile, split, tail slices, workgroups]."""
     d = GemmDesc()
@@ -194,7 +174,6 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
     d.alpha, d.beta = float(alpha), float(beta)
     d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
     d.colsum_a = _p(colsum_a)
-    d.tile_hint = _tile_hint if tile_hint is None else int(tile_hint)
     if plan_only:
         plan = (C.c_int32 * 4)()
         call("savqa_gemm_plan", C.byref(d), C.cast(plan, C.c_void_p))

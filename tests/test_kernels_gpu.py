@@ -24,15 +24,13 @@ def ops():
     return O
 
 
-@pytest.fixture(params=["fp32_native", "fp32x6", "fp32x6w"])
+@pytest.fixture(params=["fp32_native", "fp32x6"])
 def fp32k(request):
-    """The fp32 GEMM kernels of the 128x128-class shapes: v_mfma_f32_16x16x4_f32 (gemm.hip)
-    and exact three-term bf16 splits on the bf16 matrix cores (gemm_x6.hip: the 128x128 kernel
-    and the 256x128 one-workgroup-per-CU kernel, "w"); the skinny kernels are the same."""
-    O = ops()
-    name = request.param
-    with O.gemm_precision(name.rstrip("w")), O.x6_tiles(2 if name.endswith("w") else 1):
-        yield name
+    """The two fp32 GEMM kernels of the 128x128-tile shapes: v_mfma_f32_16x16x4_f32
+    (gemm.hip) and exact three-term bf16 splits on the bf16 matrix cores (gemm_x6.hip, the
+    engine's default); the skinny kernels are the same under both."""
+    with ops().gemm_precision(request.param):
+        yield request.param
 
 
 def rel(a, b):
@@ -524,16 +522,15 @@ def test_gemm_x6_error_at_most_native(lay, M, N, K):
         kw = dict(lda=M, ldb=N, ldc=N, a_trans=True, atomic=True, split_k=-1)
         ref = A.double().t() @ B.double()
     errs = {}
-    for prec, hint in ((0, 0), (6, 1), (6, 2)):
+    for prec in (0, 6):
         out = torch.zeros(M, N, device=dev)
         cs = torch.zeros(M, device=dev) if lay == "TN" else None
-        O.gemm(A, B, out, M, N, K, colsum_a=cs, prec=prec, tile_hint=hint, **kw)
-        errs[(prec, hint)] = float((out.double() - ref).abs().max() / ref.abs().max())
+        O.gemm(A, B, out, M, N, K, colsum_a=cs, prec=prec, **kw)
+        errs[prec] = float((out.double() - ref).abs().max() / ref.abs().max())
         if cs is not None:
             assert rel(cs, A.double().sum(0)) < 1e-5
-    for h in (1, 2):
-        assert errs[(6, h)] <= 1.25 * errs[(0, 0)] + 1e-8, errs
-        assert errs[(6, h)] < 5e-6, errs
+    assert errs[6] <= 1.25 * errs[0] + 1e-8, errs
+    assert errs[6] < 5e-6, errs
 
 
 @pytest.mark.parametrize("gather", ["b", "a", "ab"])
