@@ -226,7 +226,7 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
 
 
 _lp_ws = {}
-LP_SLABS = os.environ.get("SAVQA_LP_SLABS", "0") != "0"  # default on once measured
+LP_SLABS = os.environ.get("SAVQA_LP_SLABS", "1") != "0"  # cfg 3: 17.86k -> 18.32k QA-samples/s
 
 
 def lp_workspace(d, dev) -> Optional[Tensor]:
