@@ -72,29 +72,30 @@ __device__ __forceinline__ void strip_dots(const f4v (&x)[4], const float* y, in
   }
 }
 
-// Cooperative stage of K_h and V_h rows [0, TK) into LDS (zero rows past Tk). Batches of
-// SKV_BATCH loads per thread are issued back to back from clamped (always valid) rows and
-// only then stored, so a batch costs one memory latency (a guarded load in a rolled loop
-// waited for every iteration's loads in turn: 4 round trips per workgroup at T = 73).
+// Cooperative stage of K_h and V_h rows [0, TK) into LDS (zero rows past Tk) through the
+// (sample, head) views: thread t moves 16-B chunk t % 16 of rows t / 16 + 4 nw u' (one 32-bit
+// lane offset; the row block of each load is its soffset). Batches of SKV_BATCH loads per
+// thread are issued back to back and only then stored, so a batch costs one memory latency.
 constexpr int SKV_BATCH = 4;
-template <int TK, class A>
-__device__ __forceinline__ void stage_kv_tiles(const A& a, int b, int h, float* Ks, float* Vs) {
-  for (int base = threadIdx.x; base < TK * 16; base += SKV_BATCH * blockDim.x) {
+template <int TK>
+__device__ __forceinline__ void stage_kv_tiles(const BView& K, const BView& V, int Tk, float* Ks,
+                                               float* Vs) {
+  const int t = threadIdx.x, rstep = blockDim.x >> 4;
+  const uint32_t kvo = (uint32_t)(t >> 4) * K.ld + 16u * (t & 15);
+  const uint32_t vvo = (uint32_t)(t >> 4) * V.ld + 16u * (t & 15);
+  for (int r0 = 0; r0 < TK; r0 += SKV_BATCH * rstep) {
     f4v kv[SKV_BATCH], vv[SKV_BATCH];
 #pragma unroll
     for (int u = 0; u < SKV_BATCH; ++u) {
-      const int idx = base + u * blockDim.x;
-      const int j = min(idx >> 4, a.Tk - 1), c4 = (idx & 15) * 4;
-      const int64_t row = (int64_t)b * a.Tk + j;
-      kv[u] = ldx4(a.k + row * a.ldk + h * ATT_DK + c4);
-      vv[u] = ldx4(a.v + row * a.ldv + h * ATT_DK + c4);
+      const uint32_t row = (uint32_t)(r0 + u * rstep);
+      kv[u] = bld16b<f4v>(K, kvo, row * K.ld);
+      vv[u] = bld16b<f4v>(V, vvo, row * V.ld);
     }
 #pragma unroll
     for (int u = 0; u < SKV_BATCH; ++u) {
-      const int idx = base + u * blockDim.x;
-      if (idx < TK * 16) {
-        const int j = idx >> 4, c4 = (idx & 15) * 4;
-        const bool ok = j < a.Tk;
+      const int j = r0 + u * rstep + (t >> 4), c4 = (t & 15) * 4;
+      if (j < TK) {
+        const bool ok = j < Tk;
         const f4v z = {0.f, 0.f, 0.f, 0.f};
         *reinterpret_cast<f4v*>(&Ks[j * ATT_KLD + c4]) = ok ? kv[u] : z;
         *reinterpret_cast<f4v*>(&Vs[j * ATT_KLD + c4]) = ok ? vv[u] : z;
@@ -104,7 +105,8 @@ __device__ __forceinline__ void stage_kv_tiles(const A& a, int b, int h, float* 
 }
 
 // Forward row chain for accumulator row r of this lane (query i, keys 16 jt + col):
-// a = softmax, gg = graph, bm = a*gg, nrm = sum|bm| (all keys < Tk).
+// a = softmax, gg = graph, bm = a*gg, nrm = sum|bm| (all keys < Tk). The exponent runs in
+// base 2 (attn_common.h ATT_SCALE2: one v_exp_f32 per element).
 template <int NJT>
 __device__ __forceinline__ float strip_row_forward(const f4v (&s)[NJT], int r, const float (&kf)[NJT],
                                                    const float (&gpre)[NJT], int Tk, int col,
@@ -116,7 +118,7 @@ __device__ __forceinline__ float strip_row_forward(const f4v (&s)[NJT], int r, c
   for (int jt = 0; jt < NJT; ++jt) {
     const int j = jt * 16 + col;
     float v = -INFINITY;
-    if (j < Tk) v = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * 0.125f;
+    if (j < Tk) v = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * ATT_SCALE2;
     x[jt] = v;
     mx = fmaxf(mx, v);
   }
@@ -125,12 +127,12 @@ __device__ __forceinline__ float strip_row_forward(const f4v (&s)[NJT], int r, c
 #pragma unroll
   for (int jt = 0; jt < NJT; ++jt) {
     const int j = jt * 16 + col;
-    const float e = j < Tk ? expf(x[jt] - mx) : 0.f;
+    const float e = j < Tk ? att_exp2(x[jt] - mx) : 0.f;
     x[jt] = e;
     sum += e;
   }
   sum = row16_sum(sum);
-  const float rsum = 1.f / sum;  // one division per row (the elements multiply)
+  const float rsum = __builtin_amdgcn_rcpf(sum);  // one reciprocal per row (the elements multiply)
   float nrm = 0.f;
 #pragma unroll
   for (int jt = 0; jt < NJT; ++jt) {
@@ -143,19 +145,42 @@ __device__ __forceinline__ float strip_row_forward(const f4v (&s)[NJT], int r, c
   return row16_sum(nrm);
 }
 
-// graph values of this lane's 4 accumulator rows (queries i0+4g+r) x keys 16 jt + col,
-// loaded up front with clamped (branch-free) addresses so their latency overlaps the
-// MFMA strip products instead of serialising inside the row chain
-template <int NJT, class A>
-__device__ __forceinline__ void preload_graph(const A& a, int b, int i0, int g, int col,
+// graph values of this lane's 4 accumulator rows (queries i0+4g+r) x keys 16 jt + col, and the
+// key / query flags of the strip, loaded up front (their latency overlaps the MFMA strip
+// products instead of serialising inside the row chain): one lane offset, the (r, jt) parts in
+// soffset. Rows / columns past T read neighbouring (or zero) values that the chain masks.
+template <int NJT>
+__device__ __forceinline__ void preload_graph(const BView& G, int Tk, int i0, int g, int col,
                                               float (&gp)[4][NJT]) {
+  const uint32_t vo = (uint32_t)((i0 + 4 * g) * Tk + col) * 4u;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float* grow = a.G + ((int64_t)b * a.Tq + min(i0 + 4 * g + r, a.Tq - 1)) * a.Tk;
+  for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int jt = 0; jt < NJT; ++jt) gp[r][jt] = grow[min(jt * 16 + col, a.Tk - 1)];
-  }
+    for (int jt = 0; jt < NJT; ++jt) gp[r][jt] = bld1(G, vo, (uint32_t)(r * Tk + jt * 16) * 4u);
 }
+template <int NJT>
+__device__ __forceinline__ void preload_flags(const BView& KF, const BView& QF, int i0, int g,
+                                              int col, float (&kf)[NJT], float (&qf)[4]) {
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt) kf[jt] = bld1(KF, 4u * col, 64u * jt);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) qf[r] = bld1(QF, 4u * (i0 + 4 * g), 4u * r);
+}
+
+// the views every strip kernel of (sample b, head h) reads
+template <class A>
+struct StripViews {
+  BView q, k, v, g, kf, qf;
+  __device__ __forceinline__ StripViews(const A& a, int b, int h) {
+    const int64_t nq = (int64_t)a.B * a.Tq, nk = (int64_t)a.B * a.Tk;
+    q = head_view(a.q, a.ldq, nq, (int64_t)b * a.Tq, h * ATT_DK);
+    k = head_view(a.k, a.ldk, nk, (int64_t)b * a.Tk, h * ATT_DK);
+    v = head_view(a.v, a.ldv, nk, (int64_t)b * a.Tk, h * ATT_DK);
+    g = graph_view(a, b);
+    kf = flag_view(a.kflag, a.Tk, a.B, b);
+    qf = flag_view(a.qflag, a.Tq, a.B, b);
+  }
+};
 
 template <int NJT, typename T>
 __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgsT<T> a) {
@@ -164,32 +189,31 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgsT<T> a) {
   // rows come from HBM once per L2 instead of once per head
   const int bh = xcd_remap(blockIdx.x, gridDim.x);
   const int b = bh / a.H, h = bh % a.H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g = lane >> 4;
   const int i0 = w * 16;
   constexpr int TK = NJT * 16;
   constexpr int WLD = 20;                   // per-wave P^T image [TK][16 + 4]
+  constexpr uint32_t ES = sizeof(T);
   // V first, then K; the per-wave P^T images reuse K's space once S is computed (one
   // block barrier), so the block needs V + max(K, P) instead of V + K + P (T=73: 54 KB,
   // 3 workgroups per CU instead of 2)
   float* Vs = sm;                           // [TK][ATT_KLD]
   float* Ks = Vs + TK * ATT_KLD;            // [TK][ATT_KLD]
   float* Pw = Ks + w * TK * WLD;
+  const StripViews<AttnArgsT<T>> sv(a, b, h);
   // strip operands, graph and flags first, then the K/V staging: every load of the
-  // workgroup's first phase is in flight together
+  // workgroup's first phase is in flight together (rows past Tq: masked outputs)
   f4v qa[4];
   {
-    const int iq = min(i0 + col, a.Tq - 1);
-    const T* qr = a.q + ((int64_t)b * a.Tq + iq) * a.ldq + h * ATT_DK + 4 * g;
+    const uint32_t vo = (uint32_t)(i0 + col) * sv.q.ld + 4 * ES * g;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) qa[c] = ldx4(qr + 16 * c);
+    for (int c = 0; c < 4; ++c) qa[c] = bldx4<T>(sv.q, vo, 16 * ES * c);
   }
-  float gp[4][NJT];
-  preload_graph<NJT>(a, b, i0, g, col, gp);
-  float kf[NJT];
-#pragma unroll
-  for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[(int64_t)b * a.Tk + min(jt * 16 + col, a.Tk - 1)];
-  stage_kv_tiles<TK>(a, b, h, Ks, Vs);
+  float gp[4][NJT], kf[NJT], qf[4];
+  preload_graph<NJT>(sv.g, a.Tk, i0, g, col, gp);
+  preload_flags<NJT>(sv.kf, sv.qf, i0, g, col, kf, qf);
+  stage_kv_tiles<TK>(sv.k, sv.v, a.Tk, Ks, Vs);
   __syncthreads();  // K/V staged
   f4v s[NJT];
   strip_dots_lds<NJT>(qa, Ks, col, g, s);
@@ -199,18 +223,16 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgsT<T> a) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = i0 + 4 * g + r;
-    const int ic = min(i, a.Tq - 1);
     float aa[NJT], gg[NJT], bm[NJT];
     const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
-    const float rsd = 1.f / fmaxf(nrm, 1e-12f);
-    const float qf = a.qflag[(int64_t)b * a.Tq + ic];
+    const float rsd = __builtin_amdgcn_rcpf(fmaxf(nrm, 1e-12f));
 #pragma unroll
     for (int jt = 0; jt < NJT; ++jt) {
       const int j = jt * 16 + col;
       const float n = bm[jt] * rsd;
       const bool ok = i < a.Tq && j < a.Tk;
       if (a.att && ok) a.att[(((int64_t)h * a.B + b) * a.Tq + i) * a.Tk + j] = n;
-      pv[jt][r] = ok ? n * qf : 0.f;
+      pv[jt][r] = ok ? n * qf[r] : 0.f;
     }
   }
 #pragma unroll
@@ -231,13 +253,13 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgsT<T> a) {
       for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(pa, Vs[j * ATT_KLD + dt * 16 + col], o[dt]);
     }
   }
+  const BView O = head_view(a.o, a.ldo, (int64_t)a.B * a.Tq, (int64_t)b * a.Tq, h * ATT_DK);
+  const uint32_t ovo = (uint32_t)(i0 + 4 * g) * O.ld + 4u * col;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int i = i0 + 4 * g + r;
-    if (i < a.Tq) {
-      float* orow = a.o + ((int64_t)b * a.Tq + i) * a.ldo + h * ATT_DK + col;
+    if (i0 + 4 * g + r < a.Tq) {
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) orow[dt * 16] = o[dt][r];
+      for (int dt = 0; dt < 4; ++dt) bst32(O, o[dt][r], ovo, r * O.ld + 64u * dt);
     }
   }
 }
@@ -275,11 +297,12 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_kernel(AttnArgsT<T> a) {
       oa[c] = ld4(orr + 16 * c);
     }
     float gp[4][NJT];
-    preload_graph<NJT>(a, b, i0, g, col, gp);
+    const StripViews<std::remove_reference_t<decltype(a)>> sv(a, b, h);
+    preload_graph<NJT>(sv.g, a.Tk, i0, g, col, gp);
     float kf[NJT];
 #pragma unroll
     for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[kb + min(jt * 16 + col, a.Tk - 1)];
-    stage_kv_tiles<TK>(a, b, h, Ks, Vs);
+    stage_kv_tiles<TK>(sv.k, sv.v, a.Tk, Ks, Vs);
     __syncthreads();  // K/V staged
     f4v s[NJT], dp[NJT];
     strip_dots_lds<NJT>(qa, Ks, col, g, s);
@@ -430,34 +453,34 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma2_kernel(AttnArgsT<T> a) {
   const int bh = xcd_remap(blockIdx.x, gridDim.x);
   const int b = bh / a.H, h = bh % a.H;
   const int nw = blockDim.x >> 6;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g = lane >> 4;
   const int i0 = w * 16;
   constexpr int TK = NJT * 16;
+  constexpr uint32_t ES = sizeof(T);
   const int PLD = 16 * nw + 4;
   const int VREG = TK * ATT_KLD > TK * PLD ? TK * ATT_KLD : TK * PLD;
   float* Ks = sm;                   // [TK][ATT_KLD] K_h (whole kernel)
   float* Vs = sm + TK * ATT_KLD;    // [TK][ATT_KLD] V_h (phase 1a), then
   float* Pt = Vs;                   // [TK][PLD]     P^T
   float* dSt = Vs + VREG;           // [TK][PLD]     dS^T (scaled by 1/8, masked)
+  const StripViews<AttnArgsT<T>> sv(a, b, h);
+  const int64_t nq = (int64_t)a.B * a.Tq, nk = (int64_t)a.B * a.Tk;
   const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
-  const int hd = h * ATT_DK;
+  const BView DO = head_view(a.dout, a.lddo, nq, qb, h * ATT_DK);
   {
     f4v qa[4], oa[4];
-    const int iq = min(i0 + col, a.Tq - 1);
-    const T* qr = a.q + (qb + iq) * a.ldq + hd + 4 * g;
-    const float* orr = a.dout + (qb + iq) * a.lddo + hd + 4 * g;
+    const uint32_t qvo = (uint32_t)(i0 + col) * sv.q.ld + 4 * ES * g;
+    const uint32_t ovo = (uint32_t)(i0 + col) * DO.ld + 16u * g;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      qa[c] = ldx4(qr + 16 * c);
-      oa[c] = ld4(orr + 16 * c);
+      qa[c] = bldx4<T>(sv.q, qvo, 16 * ES * c);
+      oa[c] = bld16b<f4v>(DO, ovo, 64u * c);
     }
-    float gp[4][NJT];
-    preload_graph<NJT>(a, b, i0, g, col, gp);
-    float kf[NJT];
-#pragma unroll
-    for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[kb + min(jt * 16 + col, a.Tk - 1)];
-    stage_kv_tiles<TK>(a, b, h, Ks, Vs);
+    float gp[4][NJT], kf[NJT], qf[4];
+    preload_graph<NJT>(sv.g, a.Tk, i0, g, col, gp);
+    preload_flags<NJT>(sv.kf, sv.qf, i0, g, col, kf, qf);
+    stage_kv_tiles<TK>(sv.k, sv.v, a.Tk, Ks, Vs);
     __syncthreads();  // K/V staged
     f4v s[NJT], dp[NJT];
     strip_dots_lds<NJT>(qa, Ks, col, g, s);
@@ -467,16 +490,13 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma2_kernel(AttnArgsT<T> a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + 4 * g + r;
-      const int ic = min(i, a.Tq - 1);
       float aa[NJT], gg[NJT], bm[NJT];
       const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
-      const float sden = fmaxf(nrm, 1e-12f);
-      const float rsd = 1.f / sden;
-      const float qf = a.qflag[qb + ic];
+      const float rsd = __builtin_amdgcn_rcpf(fmaxf(nrm, 1e-12f));
       float dn[NJT], t1 = 0.f;
 #pragma unroll
       for (int jt = 0; jt < NJT; ++jt) {
-        dn[jt] = dp[jt][r] * qf;
+        dn[jt] = dp[jt][r] * qf[r];
         t1 += dn[jt] * bm[jt];
       }
       t1 = row16_sum(t1);
@@ -497,7 +517,7 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma2_kernel(AttnArgsT<T> a) {
         float ds = aa[jt] * (da[jt] - t2);
         if (kf[jt] == 0.f) ds = 0.f;
         dsv[jt][r] = ok ? ds * 0.125f : 0.f;
-        pv[jt][r] = ok ? bm[jt] * rsd * qf : 0.f;
+        pv[jt][r] = ok ? bm[jt] * rsd * qf[r] : 0.f;
       }
     }
 #pragma unroll
@@ -508,13 +528,12 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma2_kernel(AttnArgsT<T> a) {
   }
   {
     // dQ ReLU masks (rows i0 + 4g + r, columns 16 dt + col), under the dQ products
+    const uint32_t mvo = (uint32_t)(i0 + 4 * g) * sv.q.ld + ES * col;
     float qm[4][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const T* qrow = a.q + (qb + min(i0 + 4 * g + r, a.Tq - 1)) * a.ldq + hd + col;
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) qm[r][dt] = ldx1(qrow + dt * 16);
-    }
+      for (int dt = 0; dt < 4; ++dt) qm[r][dt] = bldx1<T>(sv.q, mvo, r * sv.q.ld + 16 * ES * dt);
     __builtin_amdgcn_wave_barrier();  // this wave's dS^T columns are written (in-order LDS)
     // dQ strip = dS K: A[m = i][k = j] = dS^T[j][i0 + i], B[k = j][n = d] = K[j][16 dt + d]
     f4v dq[4];
@@ -530,41 +549,50 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma2_kernel(AttnArgsT<T> a) {
         for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(av, Ks[j * ATT_KLD + dt * 16 + col], dq[dt]);
       }
     }
+    const BView DQ = head_view(a.dq, a.lddq, nq, qb, h * ATT_DK);
+    const uint32_t dvo = (uint32_t)(i0 + 4 * g) * DQ.ld + ES * col;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = i0 + 4 * g + r;
-      if (i < a.Tq) {
-        T* drow = a.dq + (qb + i) * a.lddq + hd + col;
+      if (i0 + 4 * g + r < a.Tq) {
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) stx1(drow + dt * 16, qm[r][dt] > 0.f ? dq[dt][r] : 0.f);
+        for (int dt = 0; dt < 4; ++dt)
+          bstx1<T>(DQ, qm[r][dt] > 0.f ? dq[dt][r] : 0.f, dvo, r * DQ.ld + 16 * ES * dt);
       }
     }
   }
   __syncthreads();
 
   // ---- phase 2: dV^T = dO^T P, dK^T = Q^T dS (item = grp * NJT + jt, grp < 4 dV, >= 4 dK);
-  //   A[m = d][k = i] = X[i][16 dt + d] (preloaded per group), B[k = i][n = j] = Y^T[j][i]
-  //   (one b128 per 16 queries: lane group g feeds k = 16 kc + 4g + t at MFMA step t),
-  //   D[m = 4g + r][n = col] = out[j = 16 jt + col][d = 16 dt + 4g + r]: one 16-B store
+  //   A[m = d][k = i] = X[i][16 dt + d] (preloaded per group; query rows past Tq read as 0),
+  //   B[k = i][n = j] = Y^T[j][i] (one b128 per 16 queries: lane group g feeds k = 16 kc + 4g + t
+  //   at MFMA step t), D[m = 4g + r][n = col] = out[j = 16 jt + col][d = 16 dt + 4g + r]: one
+  //   16-B store
   const int nitems = 8 * NJT;
   const int it0 = nitems * w / nw, it1 = nitems * (w + 1) / nw;
   constexpr int MAXG = 3;
   const int g0 = it0 / NJT;
+  const uint32_t avo_o = (uint32_t)(4 * g) * DO.ld + 4u * col;
+  const uint32_t avo_q = (uint32_t)(4 * g) * sv.q.ld + ES * col;
   float acol[MAXG][NJT][4];  // (query tiles: nw == NJT, host check)
 #pragma unroll
   for (int u = 0; u < MAXG; ++u) {
     const int grp = g0 + u;
     if (grp * NJT < it1 && grp < 8) {  // wave-uniform
-      const int dcol = hd + (grp & 3) * 16 + col;
+      const int dt = grp & 3;
 #pragma unroll
       for (int kc = 0; kc < NJT; ++kc)
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const int64_t row = qb + min(kc * 16 + 4 * g + t, a.Tq - 1);
-          acol[u][kc][t] = grp < 4 ? a.dout[row * a.lddo + dcol] : ldx1(a.q + row * a.ldq + dcol);
+          const uint32_t row = (uint32_t)(kc * 16 + t);
+          const float x = grp < 4 ? bld1(DO, avo_o, row * DO.ld + 64u * dt)
+                                  : bldx1<T>(sv.q, avo_q, row * sv.q.ld + 16 * ES * dt);
+          acol[u][kc][t] = kc * 16 + 4 * g + t < a.Tq ? x : 0.f;
         }
     }
   }
+  const BView DK = head_view(a.dk, a.lddk, nk, kb, h * ATT_DK);
+  const BView DV = head_view(a.dv, a.lddv, nk, kb, h * ATT_DK);
+  const bool vk = vec_rows(a.dk, a.lddk), vv = vec_rows(a.dv, a.lddv);
 #pragma unroll
   for (int u = 0; u < MAXG; ++u) {
     const int grp = g0 + u;
@@ -573,14 +601,14 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma2_kernel(AttnArgsT<T> a) {
     const bool isv = grp < 4;
     const int dt = grp & 3;
     const float* Yt = isv ? Pt : dSt;
-    T* dst = isv ? a.dv : a.dk;
-    const int64_t dld = isv ? a.lddv : a.lddk;
+    const BView& D = isv ? DV : DK;
+    const uint32_t svo = (uint32_t)col * D.ld + 4 * ES * g;
+    const uint32_t vvo = (uint32_t)col * sv.v.ld + 4 * ES * g;
     for (int it = lo; it < hi; ++it) {
       const int jt = it - grp * NJT;
       const int j = jt * 16 + col;
-      const int jc = min(j, a.Tk - 1);
       // ReLU mask: V from global (its LDS image is now P^T), K from its staged image
-      const f4v mk = isv ? ldx4(a.v + (kb + jc) * a.ldv + hd + dt * 16 + 4 * g)
+      const f4v mk = isv ? bldx4<T>(sv.v, vvo, (uint32_t)(jt * 16) * sv.v.ld + 16 * ES * dt)
                          : ld4(Ks + j * ATT_KLD + dt * 16 + 4 * g);
       f4v acc = {0.f, 0.f, 0.f, 0.f};
       const float* yrow = Yt + j * PLD + 4 * g;
@@ -596,7 +624,7 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma2_kernel(AttnArgsT<T> a) {
         f4v o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = mk[r] > 0.f ? acc[r] : 0.f;
-        stx4(dst + (kb + j) * dld + hd + dt * 16 + 4 * g, o, vec_rows(dst, dld));
+        bstx4<T>(D, o, svo, (uint32_t)(jt * 16) * D.ld + 16 * ES * dt, isv ? vv : vk);
       }
     }
   }
@@ -642,30 +670,31 @@ __device__ __forceinline__ att_bf16x8 strip8(const float* p) {
   return cat8(__builtin_convertvector(ld4(p), att_bf16x4), __builtin_convertvector(ld4(p + 4), att_bf16x4));
 }
 
-// K_h, V_h rows [0, TK) of sample b into bf16 LDS images [TK][ATT_KLB] (zero rows past Tk);
-// batched like stage_kv_tiles (all loads of a batch issued before any store)
+// K_h, V_h rows [0, TK) of sample b into bf16 LDS images [TK][ATT_KLB] (zero rows past Tk):
+// thread t moves 16-B chunk t % 8 of rows t / 8 + 8 nw u' (one lane offset per view, the row
+// block in soffset); batched like stage_kv_tiles (all loads of a batch issued before any store)
 template <int TK>
-__device__ __forceinline__ void stage_kv_bf(const AttnArgsT<__bf16>& a, int b, int h, __bf16* Ks,
+__device__ __forceinline__ void stage_kv_bf(const BView& K, const BView& V, int Tk, __bf16* Ks,
                                             __bf16* Vs) {
-  for (int base = threadIdx.x; base < TK * 16; base += SKV_BATCH * blockDim.x) {
-    att_bf16x4 kv[SKV_BATCH], vv[SKV_BATCH];
+  const int t = threadIdx.x, rstep = blockDim.x >> 3;
+  const uint32_t kvo = (uint32_t)(t >> 3) * K.ld + 16u * (t & 7);
+  const uint32_t vvo = (uint32_t)(t >> 3) * V.ld + 16u * (t & 7);
+  for (int r0 = 0; r0 < TK; r0 += SKV_BATCH * rstep) {
+    att_bf16x8 kv[SKV_BATCH], vv[SKV_BATCH];
 #pragma unroll
     for (int u = 0; u < SKV_BATCH; ++u) {
-      const int idx = base + u * blockDim.x;
-      const int j = min(idx >> 4, a.Tk - 1), c4 = (idx & 15) * 4;
-      const int64_t row = (int64_t)b * a.Tk + j;
-      kv[u] = ldb4(a.k + row * a.ldk + h * ATT_DK + c4);
-      vv[u] = ldb4(a.v + row * a.ldv + h * ATT_DK + c4);
+      const uint32_t row = (uint32_t)(r0 + u * rstep);
+      kv[u] = bld16b<att_bf16x8>(K, kvo, row * K.ld);
+      vv[u] = bld16b<att_bf16x8>(V, vvo, row * V.ld);
     }
 #pragma unroll
     for (int u = 0; u < SKV_BATCH; ++u) {
-      const int idx = base + u * blockDim.x;
-      if (idx < TK * 16) {
-        const int j = idx >> 4, c4 = (idx & 15) * 4;
-        const bool ok = j < a.Tk;
-        const att_bf16x4 z = {};
-        *reinterpret_cast<att_bf16x4*>(&Ks[j * ATT_KLB + c4]) = ok ? kv[u] : z;
-        *reinterpret_cast<att_bf16x4*>(&Vs[j * ATT_KLB + c4]) = ok ? vv[u] : z;
+      const int j = r0 + u * rstep + (t >> 3), c8 = (t & 7) * 8;
+      if (j < TK) {
+        const bool ok = j < Tk;
+        const att_bf16x8 z = {};
+        *reinterpret_cast<att_bf16x8*>(&Ks[j * ATT_KLB + c8]) = ok ? kv[u] : z;
+        *reinterpret_cast<att_bf16x8*>(&Vs[j * ATT_KLB + c8]) = ok ? vv[u] : z;
       }
     }
   }
@@ -692,7 +721,7 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_bf_kernel(AttnArgsT<__bf16
   extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
   const int bh = xcd_remap(blockIdx.x, gridDim.x);  // heads of a sample on one XCD
   const int b = bh / a.H, h = bh % a.H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g = lane >> 4;
   const int i0 = w * 16;
   constexpr int TK = NJT * 16;
@@ -700,19 +729,17 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_bf_kernel(AttnArgsT<__bf16
   __bf16* Ks = smb;                        // [TK][ATT_KLB]
   __bf16* Vs = Ks + TK * ATT_KLB;          // [TK][ATT_KLB]
   __bf16* Pw = Vs + TK * ATT_KLB + w * TK * WLB;
+  const StripViews<AttnArgsT<__bf16>> sv(a, b, h);
   att_bf16x8 qa[2];
   {
-    const int iq = min(i0 + col, a.Tq - 1);
-    const __bf16* qr = a.q + ((int64_t)b * a.Tq + iq) * a.ldq + h * ATT_DK + 8 * g;
-    qa[0] = strip8(qr);
-    qa[1] = strip8(qr + 32);
+    const uint32_t vo = (uint32_t)(i0 + col) * sv.q.ld + 16u * g;
+    qa[0] = bld16b<att_bf16x8>(sv.q, vo, 0);
+    qa[1] = bld16b<att_bf16x8>(sv.q, vo, 64);
   }
-  float gp[4][NJT];
-  preload_graph<NJT>(a, b, i0, g, col, gp);
-  float kf[NJT];
-#pragma unroll
-  for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[(int64_t)b * a.Tk + min(jt * 16 + col, a.Tk - 1)];
-  stage_kv_bf<TK>(a, b, h, Ks, Vs);
+  float gp[4][NJT], kf[NJT], qf[4];
+  preload_graph<NJT>(sv.g, a.Tk, i0, g, col, gp);
+  preload_flags<NJT>(sv.kf, sv.qf, i0, g, col, kf, qf);
+  stage_kv_bf<TK>(sv.k, sv.v, a.Tk, Ks, Vs);
   __syncthreads();  // K/V staged
   f4v s[NJT];
   strip_dots_bf<NJT>(qa, Ks, col, g, s);
@@ -720,18 +747,16 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_bf_kernel(AttnArgsT<__bf16
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = i0 + 4 * g + r;
-    const int ic = min(i, a.Tq - 1);
     float aa[NJT], gg[NJT], bm[NJT];
     const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
-    const float rsd = 1.f / fmaxf(nrm, 1e-12f);
-    const float qf = a.qflag[(int64_t)b * a.Tq + ic];
+    const float rsd = __builtin_amdgcn_rcpf(fmaxf(nrm, 1e-12f));
 #pragma unroll
     for (int jt = 0; jt < NJT; ++jt) {
       const int j = jt * 16 + col;
       const float n = bm[jt] * rsd;
       const bool ok = i < a.Tq && j < a.Tk;
       if (a.att && ok) a.att[(((int64_t)h * a.B + b) * a.Tq + i) * a.Tk + j] = n;
-      pv[jt][r] = ok ? n * qf : 0.f;
+      pv[jt][r] = ok ? n * qf[r] : 0.f;
     }
   }
 #pragma unroll
@@ -754,13 +779,13 @@ __global__ __launch_bounds__(512) void gattn_fwd_mfma_bf_kernel(AttnArgsT<__bf16
       o[dt] = mfma_bf16(pa, vb, o[dt]);
     }
   }
+  const BView O = head_view(a.o, a.ldo, (int64_t)a.B * a.Tq, (int64_t)b * a.Tq, h * ATT_DK);
+  const uint32_t ovo = (uint32_t)(i0 + 4 * g) * O.ld + 4u * col;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int i = i0 + 4 * g + r;
-    if (i < a.Tq) {
-      float* orow = a.o + ((int64_t)b * a.Tq + i) * a.ldo + h * ATT_DK + col;
+    if (i0 + 4 * g + r < a.Tq) {
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) orow[dt * 16] = o[dt][r];
+      for (int dt = 0; dt < 4; ++dt) bst32(O, o[dt][r], ovo, r * O.ld + 64u * dt);
     }
   }
 }
@@ -799,11 +824,12 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf_kernel(AttnArgsT<__bf16
     oa[0] = strip8(orr);
     oa[1] = strip8(orr + 32);
     float gp[4][NJT];
-    preload_graph<NJT>(a, b, i0, g, col, gp);
+    const StripViews<std::remove_reference_t<decltype(a)>> sv(a, b, h);
+    preload_graph<NJT>(sv.g, a.Tk, i0, g, col, gp);
     float kf[NJT];
 #pragma unroll
     for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[kb + min(jt * 16 + col, a.Tk - 1)];
-    stage_kv_bf<TK>(a, b, h, Ks, Vs);
+    stage_kv_bf<TK>(sv.k, sv.v, a.Tk, Ks, Vs);
     __syncthreads();  // K/V staged
     f4v s[NJT], dp[NJT];
     strip_dots_bf<NJT>(qa, Ks, col, g, s);
@@ -963,7 +989,7 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
   const int bh = xcd_remap(blockIdx.x, gridDim.x);  // heads of a sample on one XCD
   const int b = bh / a.H, h = bh % a.H;
   const int nw = blockDim.x >> 6;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g = lane >> 4;
   const int i0 = w * 16;
   constexpr int TK = NJT * 16;
@@ -972,25 +998,29 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
   __bf16* Vs = smb + TK * ATT_KLB;
   __bf16* Pt = Vs + TK * ATT_KLB;  // [TK][PLB]  P^T
   __bf16* dSt = Pt + TK * PLB;     // [TK][PLB]  dS^T (scaled by 1/8, masked)
+  const StripViews<AttnArgsT<__bf16>> sv(a, b, h);
+  const int64_t nq = (int64_t)a.B * a.Tq, nk = (int64_t)a.B * a.Tk;
   const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
-  const int hd = h * ATT_DK;
+  const BView DO = head_view(a.dout, a.lddo, nq, qb, h * ATT_DK);
 
   // ---- phase 1: strips, then dQ of the strip
   {
     att_bf16x8 qa[2], oa[2];
-    const int iq = min(i0 + col, a.Tq - 1);
-    const __bf16* qr = a.q + (qb + iq) * a.ldq + hd + 8 * g;
-    const float* orr = a.dout + (qb + iq) * a.lddo + hd + 8 * g;
-    qa[0] = strip8(qr);
-    qa[1] = strip8(qr + 32);
-    oa[0] = strip8(orr);
-    oa[1] = strip8(orr + 32);
-    float gp[4][NJT];
-    preload_graph<NJT>(a, b, i0, g, col, gp);
-    float kf[NJT];
+    {
+      const uint32_t qvo = (uint32_t)(i0 + col) * sv.q.ld + 16u * g;
+      const uint32_t ovo = (uint32_t)(i0 + col) * DO.ld + 32u * g;
+      qa[0] = bld16b<att_bf16x8>(sv.q, qvo, 0);
+      qa[1] = bld16b<att_bf16x8>(sv.q, qvo, 64);
+      f4v o4[4];
 #pragma unroll
-    for (int jt = 0; jt < NJT; ++jt) kf[jt] = a.kflag[kb + min(jt * 16 + col, a.Tk - 1)];
-    stage_kv_bf<TK>(a, b, h, Ks, Vs);
+      for (int c = 0; c < 4; ++c) o4[c] = bld16b<f4v>(DO, ovo, (c >> 1) * 128u + (c & 1) * 16u);
+      oa[0] = cat8(pack4(o4[0]), pack4(o4[1]));
+      oa[1] = cat8(pack4(o4[2]), pack4(o4[3]));
+    }
+    float gp[4][NJT], kf[NJT], qf[4];
+    preload_graph<NJT>(sv.g, a.Tk, i0, g, col, gp);
+    preload_flags<NJT>(sv.kf, sv.qf, i0, g, col, kf, qf);
+    stage_kv_bf<TK>(sv.k, sv.v, a.Tk, Ks, Vs);
     __syncthreads();  // K/V staged
     f4v s[NJT], dp[NJT];
     strip_dots_bf<NJT>(qa, Ks, col, g, s);
@@ -999,16 +1029,13 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + 4 * g + r;
-      const int ic = min(i, a.Tq - 1);
       float aa[NJT], gg[NJT], bm[NJT];
       const float nrm = strip_row_forward<NJT>(s, r, kf, gp[r], a.Tk, col, aa, gg, bm);
-      const float sden = fmaxf(nrm, 1e-12f);
-      const float rsd = 1.f / sden;
-      const float qf = a.qflag[qb + ic];
+      const float rsd = __builtin_amdgcn_rcpf(fmaxf(nrm, 1e-12f));
       float dn[NJT], t1 = 0.f;
 #pragma unroll
       for (int jt = 0; jt < NJT; ++jt) {
-        dn[jt] = dp[jt][r] * qf;
+        dn[jt] = dp[jt][r] * qf[r];
         t1 += dn[jt] * bm[jt];
       }
       t1 = row16_sum(t1);
@@ -1029,7 +1056,7 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
         float ds = aa[jt] * (da[jt] - t2);
         if (kf[jt] == 0.f) ds = 0.f;
         dsv[jt][r] = ok ? ds * 0.125f : 0.f;
-        pv[jt][r] = ok ? bm[jt] * rsd * qf : 0.f;
+        pv[jt][r] = ok ? bm[jt] * rsd * qf[r] : 0.f;
       }
     }
 #pragma unroll
@@ -1039,13 +1066,12 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
     }
     // dQ ReLU masks of this lane's outputs (rows i0 + 4g + r, columns 16 dt + col): loaded
     // here, where the strip registers are dead, under the dQ products below
-    __bf16 qm[4][4];
+    const uint32_t mvo = (uint32_t)(i0 + 4 * g) * sv.q.ld + 2u * col;
+    unsigned short qm[4][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const __bf16* qrow = a.q + (qb + min(i0 + 4 * g + r, a.Tq - 1)) * a.ldq + hd + col;
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) qm[r][dt] = qrow[dt * 16];
-    }
+      for (int dt = 0; dt < 4; ++dt) qm[r][dt] = bld16(sv.q, mvo, r * sv.q.ld + 32u * dt);
     __builtin_amdgcn_wave_barrier();  // this wave's dS^T columns are written (in-order LDS)
     // dQ strip = dS K: A[m = i][k = j] = dS^T[j][i0 + i], B[k = j][n = d] = K[j][16 dt + d]
     f4v dq[4];
@@ -1062,13 +1088,16 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
         dq[dt] = mfma_bf16(av, kv, dq[dt]);
       }
     }
+    const BView DQ = head_view(a.dq, a.lddq, nq, qb, h * ATT_DK);
+    const uint32_t dvo = (uint32_t)(i0 + 4 * g) * DQ.ld + 2u * col;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = i0 + 4 * g + r;
-      if (i < a.Tq) {
-        __bf16* drow = a.dq + (qb + i) * a.lddq + hd + col;
+      if (i0 + 4 * g + r < a.Tq) {
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) drow[dt * 16] = (__bf16)((float)qm[r][dt] > 0.f ? dq[dt][r] : 0.f);
+        for (int dt = 0; dt < 4; ++dt) {
+          const float m = (float)__builtin_bit_cast(__bf16, qm[r][dt]);
+          bstx1<__bf16>(DQ, m > 0.f ? dq[dt][r] : 0.f, dvo, r * DQ.ld + 32u * dt);
+        }
       }
     }
   }
@@ -1076,32 +1105,40 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
 
   // ---- phase 2: dV^T = dO^T P and dK^T = Q^T dS, 16x16 tiles (key tile jt, column block dt),
   // grouped (tensor, dt): item = grp * NJT + jt, grp < 4 dV, grp >= 4 dK; k = query.
-  //   A[m = d][k = i] = X[i][16 dt + d]   (X = dO rounded to bf16, or Q): preloaded per group
+  //   A[m = d][k = i] = X[i][16 dt + d]   (X = dO rounded to bf16, or Q): preloaded per group,
+  //                                        query rows past Tq read as 0
   //   B[k = i][n = j] = Y^T[j][i]          (Y^T = P^T or dS^T): one 8-B LDS read per 16 k
   //   D[m = 4g + r][n = col] = out[j = 16 jt + col][d = 16 dt + 4g + r]
   const int nitems = 8 * NJT;
   const int it0 = nitems * w / nw, it1 = nitems * (w + 1) / nw;
   constexpr int MAXG = 3;  // groups a wave's item run can touch (checked on the host)
   const int g0 = it0 / NJT;
+  const uint32_t avo_o = (uint32_t)(4 * g) * DO.ld + 4u * col;
+  const uint32_t avo_q = (uint32_t)(4 * g) * sv.q.ld + 2u * col;
   att_bf16x4 acol[MAXG][NJT];  // (query tiles: nw == NJT, host check)
 #pragma unroll
   for (int u = 0; u < MAXG; ++u) {
     const int grp = g0 + u;
     if (grp * NJT < it1 && grp < 8) {  // wave-uniform
       const int dt = grp & 3;
-      const int dcol = hd + dt * 16 + col;
 #pragma unroll
       for (int kc = 0; kc < NJT; ++kc) {
         float t4[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const int64_t row = qb + min(kc * 16 + 4 * g + t, a.Tq - 1);
-          t4[t] = grp < 4 ? a.dout[row * a.lddo + dcol] : (float)a.q[row * a.ldq + dcol];
+          const uint32_t row = (uint32_t)(kc * 16 + t);
+          const float x = grp < 4 ? bld1(DO, avo_o, row * DO.ld + 64u * dt)
+                                  : (float)__builtin_bit_cast(
+                                        __bf16, bld16(sv.q, avo_q, row * sv.q.ld + 32u * dt));
+          t4[t] = kc * 16 + 4 * g + t < a.Tq ? x : 0.f;
         }
         acol[u][kc] = pack4(f4v{t4[0], t4[1], t4[2], t4[3]});
       }
     }
   }
+  const BView DK = head_view(a.dk, a.lddk, nk, kb, h * ATT_DK);
+  const BView DV = head_view(a.dv, a.lddv, nk, kb, h * ATT_DK);
+  const bool vk = vec_rows(a.dk, a.lddk), vv = vec_rows(a.dv, a.lddv);
 #pragma unroll
   for (int u = 0; u < MAXG; ++u) {
     const int grp = g0 + u;
@@ -1111,8 +1148,8 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
     const int dt = grp & 3;
     const __bf16* Yt = isv ? Pt : dSt;
     const __bf16* Ms = isv ? Vs : Ks;
-    __bf16* dst = isv ? a.dv : a.dk;
-    const int64_t dld = isv ? a.lddv : a.lddk;
+    const BView& D = isv ? DV : DK;
+    const uint32_t svo = (uint32_t)col * D.ld + 8u * g;
     for (int it = lo; it < hi; ++it) {
       const int jt = it - grp * NJT;
       const int j = jt * 16 + col;
@@ -1125,7 +1162,7 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
         f4v o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = (float)mk[r] > 0.f ? acc[r] : 0.f;
-        stx4(dst + (kb + j) * dld + hd + dt * 16 + 4 * g, o, vec_rows(dst, dld));
+        bstx4<__bf16>(D, o, svo, (uint32_t)(jt * 16) * D.ld + 32u * dt, isv ? vv : vk);
       }
     }
   }

@@ -92,6 +92,69 @@ __device__ __forceinline__ bool vec_rows(const T* p, int64_t ld) {
   return (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & (4 * sizeof(T) - 1)) == 0;
 }
 
+// (sample b, head h) views (common.h BView) of the attention operands: a row-major [rows][ld]
+// operand of `rows` rows seen from row r0, column c0; the range ends at the tensor's last
+// (row, 64-column head) element, so reads past it return 0.
+template <typename T>
+__device__ __forceinline__ BView head_view(const T* p, int64_t ld, int64_t rows, int64_t r0,
+                                           int64_t c0) {
+  return bview(p + r0 * ld + c0, ld * (int64_t)sizeof(T),
+               ((rows - 1 - r0) * ld + ATT_DK) * (int64_t)sizeof(T));
+}
+// graph G[b] ([Tq][Tk] fp32) and the key / query flags of sample b
+template <class A>
+__device__ __forceinline__ BView graph_view(const A& a, int b) {
+  const int64_t tt = (int64_t)a.Tq * a.Tk;
+  return bview(a.G + b * tt, (int64_t)a.Tk * 4, (int64_t)(a.B - b) * tt * 4);
+}
+__device__ __forceinline__ BView flag_view(const float* f, int64_t T, int64_t B, int b) {
+  return bview(f + b * T, 4, (B - b) * T * 4);
+}
+
+// 4 consecutive Q/K/V values (fp32 or bf16 storage) as fp32 through a view; one value
+template <typename T>
+__device__ __forceinline__ f4v bldx4(const BView& v, uint32_t vo, uint32_t so) {
+  if constexpr (sizeof(T) == 4) {
+    return bld16b<f4v>(v, vo, so);
+  } else {
+    return __builtin_convertvector(bld8b<att_bf16x4>(v, vo, so), f4v);
+  }
+}
+template <typename T>
+__device__ __forceinline__ float bldx1(const BView& v, uint32_t vo, uint32_t so) {
+  if constexpr (sizeof(T) == 4) {
+    return bld1(v, vo, so);
+  } else {
+    return (float)__builtin_bit_cast(__bf16, bld16(v, vo, so));
+  }
+}
+template <typename T>
+__device__ __forceinline__ void bstx1(const BView& v, float x, uint32_t vo, uint32_t so) {
+  if constexpr (sizeof(T) == 4) {
+    bst32(v, x, vo, so);
+  } else {
+    bst16(v, __builtin_bit_cast(unsigned short, (__bf16)x), vo, so);
+  }
+}
+// 4 consecutive outputs of one lane through a view: one 16-B (fp32) / 8-B (bf16) store when
+// the rows are vector-aligned (vec: wave-uniform), else 4 element stores
+template <typename T>
+__device__ __forceinline__ void bstx4(const BView& v, f4v x, uint32_t vo, uint32_t so, bool vec) {
+  if (vec) {
+    if constexpr (sizeof(T) == 4) bst16b(v, x, vo, so);
+    else bst8b(v, __builtin_convertvector(x, att_bf16x4), vo, so);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bstx1<T>(v, x[e], vo + e * (uint32_t)sizeof(T), so);
+  }
+}
+
+// softmax exponent in base 2: x2 = s * (log2(e) / 8), e = 2^(x2 - max x2) on v_exp_f32 (the
+// masked score keeps the reference's "all keys masked -> uniform" behaviour: every masked key
+// gets the same value, and any unmasked key's 2^(x2 - max) underflows it to 0)
+constexpr float ATT_SCALE2 = 0.18033688011112042f;  // log2(e) / sqrt(64)
+__device__ __forceinline__ float att_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // Same with Y staged in LDS ([TK][ATT_KLD], rows >= Tk zero): b128 reads, lanes 0-15 of a
 // read phase hit 16 disjoint bank quads (row stride 68 floats).
 template <int NJT>

@@ -107,4 +107,55 @@ __device__ __forceinline__ float drop_mul(const DropParam& d, uint32_t site, uin
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Buffer-resource view of one operand from a wave-uniform origin (cdna_hip_programming.md T8 /
+// T20): every lane address is a 32-bit byte offset from the origin, wave-uniform parts go to
+// the instruction's SGPR soffset, and the hardware range check returns 0 for reads at or past
+// `n_bytes` (writes there are dropped) -- so a (sample, head) origin turns the 64-bit
+// row * ld address arithmetic of each load into one 32-bit lane offset per access pattern,
+// and rows past the end of the tensor need no clamped addresses.
+struct BView {
+  __amdgpu_buffer_rsrc_t r;
+  uint32_t ld;  // bytes per row
+};
+
+__device__ __forceinline__ BView bview(const void* origin, int64_t ld_bytes, int64_t n_bytes) {
+  BView v;
+  const int64_t nb = n_bytes < 0 ? 0 : (n_bytes > 0xFFFFFFFFll ? 0xFFFFFFFFll : n_bytes);
+  v.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(origin), (short)0, (int)(uint32_t)nb,
+                                          0x00020000);
+  v.ld = (uint32_t)ld_bytes;
+  return v;
+}
+
+__device__ __forceinline__ float bld1(const BView& v, uint32_t vo, uint32_t so) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(v.r, vo, so, 0));
+}
+__device__ __forceinline__ unsigned short bld16(const BView& v, uint32_t vo, uint32_t so) {
+  return __builtin_amdgcn_raw_buffer_load_b16(v.r, vo, so, 0);
+}
+template <class V>  // 8 bytes
+__device__ __forceinline__ V bld8b(const BView& v, uint32_t vo, uint32_t so) {
+  return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(v.r, vo, so, 0));
+}
+template <class V>  // 16 bytes
+__device__ __forceinline__ V bld16b(const BView& v, uint32_t vo, uint32_t so) {
+  return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(v.r, vo, so, 0));
+}
+__device__ __forceinline__ void bst16(const BView& v, unsigned short x, uint32_t vo, uint32_t so) {
+  __builtin_amdgcn_raw_buffer_store_b16(x, v.r, vo, so, 0);
+}
+__device__ __forceinline__ void bst32(const BView& v, float x, uint32_t vo, uint32_t so) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), v.r, vo, so, 0);
+}
+template <class V>
+__device__ __forceinline__ void bst8b(const BView& v, V x, uint32_t vo, uint32_t so) {
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, x), v.r, vo, so, 0);
+}
+template <class V>
+__device__ __forceinline__ void bst16b(const BView& v, V x, uint32_t vo, uint32_t so) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, x), v.r, vo, so, 0);
+}
+
 }  // namespace savqa
