@@ -167,21 +167,6 @@ __device__ __forceinline__ void preload_flags(const BView& KF, const BView& QF, 
   for (int r = 0; r < 4; ++r) qf[r] = bld1(QF, 4u * (i0 + 4 * g), 4u * r);
 }
 
-// the views every strip kernel of (sample b, head h) reads
-template <class A>
-struct StripViews {
-  BView q, k, v, g, kf, qf;
-  __device__ __forceinline__ StripViews(const A& a, int b, int h) {
-    const int64_t nq = (int64_t)a.B * a.Tq, nk = (int64_t)a.B * a.Tk;
-    q = head_view(a.q, a.ldq, nq, (int64_t)b * a.Tq, h * ATT_DK);
-    k = head_view(a.k, a.ldk, nk, (int64_t)b * a.Tk, h * ATT_DK);
-    v = head_view(a.v, a.ldv, nk, (int64_t)b * a.Tk, h * ATT_DK);
-    g = graph_view(a, b);
-    kf = flag_view(a.kflag, a.Tk, a.B, b);
-    qf = flag_view(a.qflag, a.Tq, a.B, b);
-  }
-};
-
 template <int NJT, typename T>
 __global__ __launch_bounds__(512) void gattn_fwd_mfma_kernel(AttnArgsT<T> a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];

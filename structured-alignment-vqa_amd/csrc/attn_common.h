@@ -111,6 +111,21 @@ __device__ __forceinline__ BView flag_view(const float* f, int64_t T, int64_t B,
   return bview(f + b * T, 4, (B - b) * T * 4);
 }
 
+// the views every attention kernel of (sample b, head h) reads
+template <class A>
+struct StripViews {
+  BView q, k, v, g, kf, qf;
+  __device__ __forceinline__ StripViews(const A& a, int b, int h) {
+    const int64_t nq = (int64_t)a.B * a.Tq, nk = (int64_t)a.B * a.Tk;
+    q = head_view(a.q, a.ldq, nq, (int64_t)b * a.Tq, h * ATT_DK);
+    k = head_view(a.k, a.ldk, nk, (int64_t)b * a.Tk, h * ATT_DK);
+    v = head_view(a.v, a.ldv, nk, (int64_t)b * a.Tk, h * ATT_DK);
+    g = graph_view(a, b);
+    kf = flag_view(a.kflag, a.Tk, a.B, b);
+    qf = flag_view(a.qflag, a.Tq, a.B, b);
+  }
+};
+
 // 4 consecutive Q/K/V values (fp32 or bf16 storage) as fp32 through a view; one value
 template <typename T>
 __device__ __forceinline__ f4v bldx4(const BView& v, uint32_t vo, uint32_t so) {

@@ -26,6 +26,10 @@
 
 namespace savqa {
 
+#ifndef SAVQA_FL_DELTA_WPE
+#define SAVQA_FL_DELTA_WPE 3  // delta kernel occupancy (4: 128 VGPRs with 20 dwords spilled, 3-4 % slower)
+#endif
+
 constexpr int FL_KT = 64;   // keys (or queries) per staged tile
 constexpr int FL_WLD = 16;  // per-wave transposed image, [64][16] floats, rows placed by fl_img
 
@@ -40,28 +44,55 @@ __device__ __forceinline__ int fl_img(int r, int f) {
   return (((r & ~3) | ((r + h) & 3)) << 4) + (f ^ (h << 2));
 }
 
-// Cooperative stage of rows [r0, r0 + 64) of X and Y (head slice hd) into LDS, zero past lim.
-__device__ __forceinline__ void fl_stage2(const float* X, int64_t ldx, const float* Y, int64_t ldy,
-                                          int64_t base, int r0, int lim, int hd, float* Xs,
-                                          float* Ys) {
-  for (int idx = threadIdx.x; idx < FL_KT * 16; idx += blockDim.x) {
-    const int j = idx >> 4, c4 = (idx & 15) * 4;
-    f4v xv = {0.f, 0.f, 0.f, 0.f}, yv = xv;
-    if (r0 + j < lim) {
-      const int64_t row = base + r0 + j;
-      xv = ld4(X + row * ldx + hd + c4);
-      yv = ld4(Y + row * ldy + hd + c4);
+// Cooperative stage of rows [r0, r0 + 64) of X and Y ((sample, head) views) into LDS, zero
+// past lim: thread t moves 16-B chunk t % 16 of rows t / 16 + 4 nw p, four passes' loads
+// issued back to back before their stores (one memory latency per batch instead of one per
+// guarded pass); one lane offset per view, the row block in soffset.
+__device__ __forceinline__ void fl_stage2(const BView& X, const BView& Y, int r0, int lim,
+                                          float* Xs, float* Ys) {
+  const int t = threadIdx.x, rstep = blockDim.x >> 4;
+  const uint32_t xvo = (uint32_t)(t >> 4) * X.ld + 16u * (t & 15);
+  const uint32_t yvo = (uint32_t)(t >> 4) * Y.ld + 16u * (t & 15);
+  for (int p0 = 0; p0 < FL_KT; p0 += 4 * rstep) {
+    f4v xv[4], yv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t row = (uint32_t)(r0 + p0 + u * rstep);
+      xv[u] = bld16b<f4v>(X, xvo, row * X.ld);
+      yv[u] = bld16b<f4v>(Y, yvo, row * Y.ld);
     }
-    *reinterpret_cast<f4v*>(&Xs[j * ATT_KLD + c4]) = xv;
-    *reinterpret_cast<f4v*>(&Ys[j * ATT_KLD + c4]) = yv;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = p0 + u * rstep + (t >> 4), c4 = (t & 15) * 4;
+      if (j < FL_KT) {
+        const bool ok = r0 + j < lim;
+        const f4v z = {0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4v*>(&Xs[j * ATT_KLD + c4]) = ok ? xv[u] : z;
+        *reinterpret_cast<f4v*>(&Ys[j * ATT_KLD + c4]) = ok ? yv[u] : z;
+      }
+    }
   }
 }
 
-__device__ __forceinline__ void fl_load_strip(const float* X, int64_t ldx, int64_t row, int hd,
-                                              int g, f4v (&x)[4]) {
-  const float* p = X + row * ldx + hd + 4 * g;
+// strip operand of row `row` (relative to the view): 16 consecutive d per lane group
+__device__ __forceinline__ void fl_load_strip(const BView& X, int row, int g, f4v (&x)[4]) {
+  const uint32_t vo = (uint32_t)row * X.ld + 16u * g;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) x[c] = ld4(p + 16 * c);
+  for (int c = 0; c < 4; ++c) x[c] = bld16b<f4v>(X, vo, 64u * c);
+}
+
+// graph values G[i0 + 4g + r][k0 + 16 jt + col] and key flags of one key tile (rows / columns
+// past T: neighbouring or zero values, masked by the callers)
+__device__ __forceinline__ void fl_graph_tile(const BView& G, const BView& KF, int Tk, int i0,
+                                              int k0, int g, int col, float (&kf)[4],
+                                              float (&gv)[4][4]) {
+  const uint32_t vo = (uint32_t)((i0 + 4 * g) * Tk + col) * 4u;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) {
+    kf[jt] = bld1(KF, 4u * col, 4u * (k0 + 16 * jt));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gv[r][jt] = bld1(G, vo, (uint32_t)(r * Tk + k0 + 16 * jt) * 4u);
+  }
 }
 
 // acc[dt] += sum over the 64 rows j of the tile: img[j][col] (A: m = col, k = j) * Ys[j][16dt+col]
@@ -80,7 +111,8 @@ __device__ __forceinline__ void fl_accum(const float* img, const float* Ys, int 
 }
 
 // ---------------------------------------------------------------------------------- fwd
-// grid = B*H*nqt, block = 64*nw (wave w: query strip qt*16nw + 16w)
+// grid = B*H*nqt, block = 64*nw (wave w: query strip qt*16nw + 16w). Scores run in base 2
+// (attn_common.h ATT_SCALE2): m and every exponent below are log2-scaled, in all four kernels.
 __global__ __launch_bounds__(256) void gattn_fwd_flash_kernel(AttnArgs a, float* __restrict__ stats,
                                                              int nqt) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -89,20 +121,16 @@ __global__ __launch_bounds__(256) void gattn_fwd_flash_kernel(AttnArgs a, float*
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qt = bid % nqt, bh = bid / nqt;
   const int b = bh / a.H, h = bh % a.H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g = lane >> 4;
   const int i0 = qt * 16 * nw + w * 16;
   float* Ks = sm;
   float* Vs = Ks + FL_KT * ATT_KLD;
   float* Pw = Vs + FL_KT * ATT_KLD + w * FL_KT * FL_WLD;
-  const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
-  const int hd = h * ATT_DK;
+  const StripViews<AttnArgs> sv(a, b, h);
 
   f4v qa[4];
-  fl_load_strip(a.q, a.ldq, qb + min(i0 + col, a.Tq - 1), hd, g, qa);
-  const float* grow[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) grow[r] = a.G + (qb + min(i0 + 4 * g + r, a.Tq - 1)) * a.Tk;
+  fl_load_strip(sv.q, i0 + col, g, qa);
   float m[4], Z[4], W[4];
   f4v o[4];
 #pragma unroll
@@ -116,15 +144,9 @@ __global__ __launch_bounds__(256) void gattn_fwd_flash_kernel(AttnArgs a, float*
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * FL_KT;
     __syncthreads();  // every wave is done with the previous tile
-    fl_stage2(a.k, a.ldk, a.v, a.ldv, kb, k0, a.Tk, hd, Ks, Vs);
     float kf[4], gv[4][4];
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      const int jc = min(k0 + jt * 16 + col, a.Tk - 1);
-      kf[jt] = a.kflag[kb + jc];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) gv[r][jt] = grow[r][jc];
-    }
+    fl_graph_tile(sv.g, sv.kf, a.Tk, i0, k0, g, col, kf, gv);
+    fl_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
     __syncthreads();
     f4v s[4];
     strip_dots_lds<4>(qa, Ks, col, g, s);
@@ -136,18 +158,18 @@ __global__ __launch_bounds__(256) void gattn_fwd_flash_kernel(AttnArgs a, float*
       for (int jt = 0; jt < 4; ++jt) {
         const int j = k0 + jt * 16 + col;
         float v = -INFINITY;
-        if (j < a.Tk) v = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * 0.125f;
+        if (j < a.Tk) v = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * ATT_SCALE2;
         x[jt] = v;
         mx = fmaxf(mx, v);
       }
       mx = row16_max(mx);
       const float mn = fmaxf(m[r], mx);  // finite: every tile holds a key < Tk
-      const float alpha = expf(m[r] - mn);
+      const float alpha = att_exp2(m[r] - mn);
       float zs = 0.f, ws = 0.f;
 #pragma unroll
       for (int jt = 0; jt < 4; ++jt) {
         const int j = k0 + jt * 16 + col;
-        const float e = j < a.Tk ? expf(x[jt] - mn) : 0.f;
+        const float e = j < a.Tk ? att_exp2(x[jt] - mn) : 0.f;
         const float gg = j < a.Tk ? gv[r][jt] : 0.f;
         zs += e;
         ws += e * fabsf(gg);
@@ -167,15 +189,17 @@ __global__ __launch_bounds__(256) void gattn_fwd_flash_kernel(AttnArgs a, float*
     __builtin_amdgcn_wave_barrier();
     fl_accum(Pw, Vs, col, g, o);
   }
+  const int64_t qb = (int64_t)b * a.Tq;
+  const BView O = head_view(a.o, a.ldo, (int64_t)a.B * a.Tq, qb, h * ATT_DK);
+  const uint32_t ovo = (uint32_t)(i0 + 4 * g) * O.ld + 4u * col;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = i0 + 4 * g + r;
     if (i < a.Tq) {
       const float D = fmaxf(W[r], 1e-12f * Z[r]);
-      const float sc = a.qflag[qb + i] / D;
-      float* orow = a.o + (qb + i) * a.ldo + hd + col;
+      const float sc = bld1(sv.qf, 4u * (i0 + 4 * g), 4u * r) / D;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) orow[dt * 16] = o[dt][r] * sc;
+      for (int dt = 0; dt < 4; ++dt) bst32(O, o[dt][r] * sc, ovo, r * O.ld + 64u * dt);
       if (col == 0) {
         float* st = stats + (((int64_t)b * a.H + h) * a.Tq + i) * 4;
         st[0] = m[r];
@@ -226,7 +250,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int kt = bid % nkt2, bh = bid / nkt2;
   const int b = bh / a.H, h = bh % a.H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g = lane >> 4;
   const int j0 = kt * 16 * nw + w * 16;
   float* Qs = sm;                                  // [64][KLD]
@@ -234,28 +258,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   float* cf = dOs + FL_KT * ATT_KLD;               // [64][8] per-query coefficients
   float* img = cf + FL_KT * 8 + w * FL_KT * FL_WLD;  // [64 queries][16] (keys 4g+r): N, then dS
   const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
-  const int hd = h * ATT_DK;
   const float* sth = stats + ((int64_t)b * a.H + h) * a.Tq * 4;
+  const StripViews<AttnArgs> sv(a, b, h);
+  const BView DO = head_view(a.dout, a.lddo, (int64_t)a.B * a.Tq, qb, h * ATT_DK);
 
   f4v ka[4], va[4];
-  fl_load_strip(a.k, a.ldk, kb + min(j0 + col, a.Tk - 1), hd, g, ka);
-  fl_load_strip(a.v, a.ldv, kb + min(j0 + col, a.Tk - 1), hd, g, va);
+  fl_load_strip(sv.k, j0 + col, g, ka);
+  fl_load_strip(sv.v, j0 + col, g, va);
   float kf[4];
   bool kval[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int j = j0 + 4 * g + r;
-    kval[r] = j < a.Tk;
-    kf[r] = a.kflag[kb + min(j, a.Tk - 1)];
+    kval[r] = j0 + 4 * g + r < a.Tk;
+    kf[r] = bld1(sv.kf, 4u * (j0 + 4 * g), 4u * r);
   }
   f4v dk[4], dv[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f4v{0.f, 0.f, 0.f, 0.f};
+  const uint32_t gvo = (uint32_t)(col * a.Tk + j0 + 4 * g) * 4u;
   const int nqt = (a.Tq + FL_KT - 1) / FL_KT;
   for (int qt = 0; qt < nqt; ++qt) {
     const int iq0 = qt * FL_KT;
     __syncthreads();
-    fl_stage2(a.q, a.ldq, a.dout, a.lddo, qb, iq0, a.Tq, hd, Qs, dOs);
+    float gv[4][4];  // [jt][r]: G[query iq0 + 16jt + col][key j0 + 4g + r]
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gv[jt][r] = bld1(sv.g, gvo, (uint32_t)((iq0 + 16 * jt) * a.Tk + r) * 4u);
+    fl_stage2(sv.q, DO, iq0, a.Tq, Qs, dOs);
     if (threadIdx.x < FL_KT) {
       const int i = iq0 + threadIdx.x;
       const bool valid = i < a.Tq;
@@ -269,13 +299,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
       cp[3] = c.cd;
       cp[4] = c.pd;
     }
-    float gv[4][4];  // [jt][r]: G[query iq0 + 16jt + col][key j0 + 4g + r]
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      const float* gr = a.G + (qb + min(iq0 + jt * 16 + col, a.Tq - 1)) * a.Tk;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) gv[jt][r] = gr[min(j0 + 4 * g + r, a.Tk - 1)];
-    }
     __syncthreads();
     f4v s[4], dp[4];
     strip_dots_lds<4>(ka, Qs, col, g, s);   // [key 4g+r][query 16jt+col]
@@ -288,8 +311,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
       const float pd = cp[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float x = kf[r] == 0.f ? ATT_MASKED : s[jt][r] * 0.125f;
-        const float e = kval[r] ? expf(x - c0.x) : 0.f;
+        const float x = kf[r] == 0.f ? ATT_MASKED : s[jt][r] * ATT_SCALE2;
+        const float e = kval[r] ? att_exp2(x - c0.x) : 0.f;
         const float gg = gv[jt][r];
         const float n = e * gg * c0.y;
         nv[jt][r] = n * c0.z;
@@ -307,16 +330,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
     __builtin_amdgcn_wave_barrier();
     fl_accum(img, Qs, col, g, dk);   // dK_j += sum_i dS_ij Q_i   (x 1/8 at the end)
   }
+  const int64_t nk = (int64_t)a.B * a.Tk;
+  const BView DK = head_view(a.dk, a.lddk, nk, kb, h * ATT_DK);
+  const BView DV = head_view(a.dv, a.lddv, nk, kb, h * ATT_DK);
+  const uint32_t kvo = (uint32_t)(j0 + 4 * g) * sv.k.ld + 4u * col;
+  const uint32_t vvo = (uint32_t)(j0 + 4 * g) * sv.v.ld + 4u * col;
+  const uint32_t dkvo = (uint32_t)(j0 + 4 * g) * DK.ld + 4u * col;
+  const uint32_t dvvo = (uint32_t)(j0 + 4 * g) * DV.ld + 4u * col;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int j = j0 + 4 * g + r;
-    if (j < a.Tk) {
-      const int64_t row = kb + j;
+    if (j0 + 4 * g + r < a.Tk) {
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const int c = hd + dt * 16 + col;
-        a.dk[row * a.lddk + c] = a.k[row * a.ldk + c] > 0.f ? dk[dt][r] * 0.125f : 0.f;
-        a.dv[row * a.lddv + c] = a.v[row * a.ldv + c] > 0.f ? dv[dt][r] : 0.f;
+        const float kx = bld1(sv.k, kvo, r * sv.k.ld + 64u * dt);
+        const float vx = bld1(sv.v, vvo, r * sv.v.ld + 64u * dt);
+        bst32(DK, kx > 0.f ? dk[dt][r] * 0.125f : 0.f, dkvo, r * DK.ld + 64u * dt);
+        bst32(DV, vx > 0.f ? dv[dt][r] : 0.f, dvvo, r * DV.ld + 64u * dt);
       }
     }
   }
@@ -337,7 +366,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
 // softmax backward (x (g - sum x g)) removes it. (W', Z', delta) go to stats for dK / dV;
 // dx travels to the dQ kernel as a float pair (hi, lo) in columns 0-1 of the row's own dQ
 // head slice, which only that kernel's same wave overwrites, after reading it.
-__global__ __launch_bounds__(256) void gattn_bwd_delta_flash_kernel(AttnArgs a,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAVQA_FL_DELTA_WPE))) void gattn_bwd_delta_flash_kernel(AttnArgs a,
                                                                    float* __restrict__ stats,
                                                                    int nqt) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -345,20 +374,21 @@ __global__ __launch_bounds__(256) void gattn_bwd_delta_flash_kernel(AttnArgs a,
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qt = bid % nqt, bh = bid / nqt;
   const int b = bh / a.H, h = bh % a.H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g = lane >> 4;
   const int i0 = qt * 16 * nw + w * 16;
   float* Ks = sm;
   float* Vs = Ks + FL_KT * ATT_KLD;
-  const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
+  const int64_t qb = (int64_t)b * a.Tq;
   const int hd = h * ATT_DK;
   const float* sth = stats + ((int64_t)b * a.H + h) * a.Tq * 4;
+  const StripViews<AttnArgs> sv(a, b, h);
+  const BView DO = head_view(a.dout, a.lddo, (int64_t)a.B * a.Tq, qb, h * ATT_DK);
 
   f4v qa[4], oa[4];
-  fl_load_strip(a.q, a.ldq, qb + min(i0 + col, a.Tq - 1), hd, g, qa);
-  fl_load_strip(a.dout, a.lddo, qb + min(i0 + col, a.Tq - 1), hd, g, oa);
+  fl_load_strip(sv.q, i0 + col, g, qa);
+  fl_load_strip(DO, i0 + col, g, oa);
   float rm[4], rq[4];
-  const float* grow[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = i0 + 4 * g + r;
@@ -366,22 +396,15 @@ __global__ __launch_bounds__(256) void gattn_bwd_delta_flash_kernel(AttnArgs a,
     const RowCoef c = row_coef(sth + (int64_t)ic * 4, a.qflag[qb + ic], i < a.Tq);
     rm[r] = c.m;
     rq[r] = c.qf;
-    grow[r] = a.G + (qb + ic) * a.Tk;
   }
   double sa[4] = {0., 0., 0., 0.}, sw[4] = {0., 0., 0., 0.}, sz[4] = {0., 0., 0., 0.};
   const int nkt = (a.Tk + FL_KT - 1) / FL_KT;
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * FL_KT;
     __syncthreads();
-    fl_stage2(a.k, a.ldk, a.v, a.ldv, kb, k0, a.Tk, hd, Ks, Vs);
     float kf[4], gv[4][4];
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      const int jc = min(k0 + jt * 16 + col, a.Tk - 1);
-      kf[jt] = a.kflag[kb + jc];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) gv[r][jt] = grow[r][jc];
-    }
+    fl_graph_tile(sv.g, sv.kf, a.Tk, i0, k0, g, col, kf, gv);
+    fl_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
     __syncthreads();
     f4v s[4], dp[4];
     strip_dots_lds<4>(qa, Ks, col, g, s);   // [query 4g+r][key 16jt+col]
@@ -391,9 +414,9 @@ __global__ __launch_bounds__(256) void gattn_bwd_delta_flash_kernel(AttnArgs a,
 #pragma unroll
       for (int jt = 0; jt < 4; ++jt) {
         const int j = k0 + jt * 16 + col;
-        const float x = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * 0.125f;
-        const float e = j < a.Tk ? expf(x - rm[r]) : 0.f;
-        const float gg = gv[r][jt];
+        const float x = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * ATT_SCALE2;
+        const float e = j < a.Tk ? att_exp2(x - rm[r]) : 0.f;
+        const float gg = j < a.Tk ? gv[r][jt] : 0.f;
         sa[r] += (double)(e * gg * rq[r] * dp[jt][r]);
         sw[r] += (double)(e * fabsf(gg));
         sz[r] += (double)e;
@@ -440,28 +463,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qt = bid % nqt, bh = bid / nqt;
   const int b = bh / a.H, h = bh % a.H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g = lane >> 4;
   const int i0 = qt * 16 * nw + w * 16;
   float* Ks = sm;
   float* Vs = Ks + FL_KT * ATT_KLD;
   float* Simg = Vs + FL_KT * ATT_KLD + w * FL_KT * FL_WLD;  // [64 keys][16] (queries 4g+r)
-  const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
+  const int64_t qb = (int64_t)b * a.Tq;
   const int hd = h * ATT_DK;
   const float* sth = stats + ((int64_t)b * a.H + h) * a.Tq * 4;
+  const StripViews<AttnArgs> sv(a, b, h);
+  const BView DO = head_view(a.dout, a.lddo, (int64_t)a.B * a.Tq, qb, h * ATT_DK);
 
   f4v qa[4], oa[4];
-  fl_load_strip(a.q, a.ldq, qb + min(i0 + col, a.Tq - 1), hd, g, qa);
-  fl_load_strip(a.dout, a.lddo, qb + min(i0 + col, a.Tq - 1), hd, g, oa);
+  fl_load_strip(sv.q, i0 + col, g, qa);
+  fl_load_strip(DO, i0 + col, g, oa);
   RowCoef rc[4];
-  const float* grow[4];
   double dx[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = i0 + 4 * g + r;
     const int ic = min(i, a.Tq - 1);
     rc[r] = row_coef(sth + (int64_t)ic * 4, a.qflag[qb + ic], i < a.Tq);
-    grow[r] = a.G + (qb + ic) * a.Tk;
     const float* dxs = a.dq + (qb + ic) * a.lddq + hd;
     dx[r] = i < a.Tq ? (double)dxs[0] + (double)dxs[1] : 0.;
   }
@@ -472,15 +495,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * FL_KT;
     __syncthreads();
-    fl_stage2(a.k, a.ldk, a.v, a.ldv, kb, k0, a.Tk, hd, Ks, Vs);
     float kf[4], gv[4][4];
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      const int jc = min(k0 + jt * 16 + col, a.Tk - 1);
-      kf[jt] = a.kflag[kb + jc];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) gv[r][jt] = grow[r][jc];
-    }
+    fl_graph_tile(sv.g, sv.kf, a.Tk, i0, k0, g, col, kf, gv);
+    fl_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
     __syncthreads();
     f4v s[4], dp[4];
     strip_dots_lds<4>(qa, Ks, col, g, s);   // [query 4g+r][key 16jt+col]
@@ -492,9 +509,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
 #pragma unroll
       for (int jt = 0; jt < 4; ++jt) {
         const int j = k0 + jt * 16 + col;
-        const float x = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * 0.125f;
-        const float e = j < a.Tk ? expf(x - c.m) : 0.f;
-        const float gg = gv[r][jt];
+        const float x = kf[jt] == 0.f ? ATT_MASKED : s[jt][r] * ATT_SCALE2;
+        const float e = j < a.Tk ? att_exp2(x - c.m) : 0.f;
+        const float gg = j < a.Tk ? gv[r][jt] : 0.f;
         const float av = e * gg * c.qf * dp[jt][r];
         const float wv = c.normal ? e * fabsf(gg) : e;
         const float ds = (float)((double)av - dx[r] * (double)wv) * c.rD;
