@@ -964,10 +964,9 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   const int avec = (d.lda % 4 == 0) && aligned16(d.A);
   const int bvec = (d.ldb % 4 == 0) && aligned16(d.B);
   hipStream_t s = as_stream(stream);
-  if (p.tile == 128 && d.prec == 6 &&
-      (!avec || !bvec || (d.a_trans && d.a_rows) || (!d.b_trans && d.b_rows))) {
-    // unaligned operands and k-row gathers (guarded loads only in the x6 kernel) take the
-    // fp32 kernel
+  if (p.tile == 128 && d.prec == 6 && (!avec || !bvec)) {
+    // operands that are not 16-B vectors (guarded loads only in the x6 kernel) take the fp32
+    // kernel
     d.prec = 0;
     if (int rc = plan_gemm(d, p)) return rc;
   }

@@ -97,6 +97,10 @@ template <bool ROW>
 struct X6Operand {
   f4 r[X6_DEPTH][4];  // X6_DEPTH register sets: k-tiles in flight
   const float* rp[4];
+  // COL operands under a k-row gather (rows of the operand are k: dW's X through the GloVe
+  // row map, say): the row of each float4 comes from kr per k-tile, cb = base + column
+  const int64_t* kr = nullptr;
+  const float* cb = nullptr;
 
   // FAST path pointers, resolved once per block. Edge tiles clamp: a ROW operand's rows past
   // mlim re-read row mlim-1, a COL operand's float4 groups past mlim re-read the last group
@@ -115,10 +119,22 @@ struct X6Operand {
         rp[it] = base + (int64_t)(4 * (tid & 7) + it) * ld + min(m0 + 4 * (tid >> 3), mlim - 4);
       }
     }
+    if constexpr (!ROW) cb = base + min(m0 + 4 * (tid >> 3), mlim - 4);
   }
 
   template <int S>
-  __device__ __forceinline__ void load_fast(int64_t ld, int64_t k0) {
+  __device__ __forceinline__ void load_fast(int64_t ld, int64_t k0, int tid) {
+    if constexpr (!ROW) {
+      if (kr) {  // block-uniform
+        const int64_t* kp = kr + k0 + 4 * (tid & 7);
+        int64_t rr[4];
+#pragma unroll
+        for (int it = 0; it < 4; ++it) rr[it] = kp[it];
+#pragma unroll
+        for (int it = 0; it < 4; ++it) r[S][it] = *reinterpret_cast<const f4*>(cb + rr[it] * ld);
+        return;
+      }
+    }
 #pragma unroll
     for (int it = 0; it < 4; ++it)
       r[S][it] = *reinterpret_cast<const f4*>(ROW ? rp[it] + k0 : rp[it] + k0 * ld);
@@ -226,12 +242,11 @@ __device__ __forceinline__ void x6_compute(const char* As, const char* Bs, int w
 }
 
 // k-loop load mode (block-uniform): 0 = guarded loads everywhere (edge widths that are not
-// whole float4 groups, k-row gathers), 1 = branch-free loads on every k-tile, 2 = branch-free
-// except a guarded last k-tile (K not a multiple of 32)
+// whole float4 groups), 1 = branch-free loads on every k-tile, 2 = branch-free except a
+// guarded last k-tile (K not a multiple of 32); k-row gathers take the same modes
 template <bool AT, bool BT>
 __device__ __forceinline__ int x6_mode(const savqa_gemm_desc& d, int64_t m0, int64_t n0,
                                        int64_t kbeg, int64_t kend) {
-  if ((AT && d.a_rows) || (!BT && d.b_rows)) return 0;
   if (m0 + X6_TILE > d.M && AT && (d.M & 3)) return 0;
   if (n0 + X6_TILE > d.N && !BT && (d.N & 3)) return 0;
   return ((kend - kbeg) % X6_BK == 0) ? 1 : 2;
@@ -249,12 +264,14 @@ __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem
   if constexpr (MODE != 0) {
     la.setup_fast(d.A, d.lda, AT ? nullptr : d.a_rows, m0, d.M, tid);
     lb.setup_fast(d.B, d.ldb, BT ? d.b_rows : nullptr, n0, d.N, tid);
+    if constexpr (AT) la.kr = d.a_rows;
+    if constexpr (!BT) lb.kr = d.b_rows;
   }
   auto load = [&](auto set, int64_t k0) {
     constexpr int S = decltype(set)::value;
     if (MODE == 1 || (MODE == 2 && k0 + X6_BK <= kend)) {
-      la.template load_fast<S>(d.lda, k0);
-      lb.template load_fast<S>(d.ldb, k0);
+      la.template load_fast<S>(d.lda, k0, tid);
+      lb.template load_fast<S>(d.ldb, k0, tid);
     } else {
       la.template load_slow<S>(d.A, d.lda, d.a_rows, d.M, m0, k0, kend, tid);
       lb.template load_slow<S>(d.B, d.ldb, d.b_rows, d.N, n0, k0, kend, tid);

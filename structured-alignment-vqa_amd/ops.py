@@ -63,10 +63,9 @@ class GemmProbe:
             return f"gemm_skinny_kernel<{lay}>"
         if plan[0] == 16:
             return f"gemm_skinny16_kernel<{lay}>"
-        if d.prec == 6:  # (savqa_gemm's fallback: unaligned operands, k-row gathers)
+        if d.prec == 6:  # (savqa_gemm's fallback: operands that are not 16-B vectors)
             al = all(p % 16 == 0 and ld % 4 == 0 for p, ld in ((d.A, d.lda), (d.B, d.ldb)))
-            kg = (d.a_trans and d.a_rows) or (not d.b_trans and d.b_rows)
-            if al and not kg:
+            if al:
                 return f"gemm_x6_kernel<{lay}>"
             return f"gemm_f32_kernel<{plan[0]},{plan[0]},{lay}>"
         if d.prec:
