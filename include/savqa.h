@@ -134,6 +134,10 @@ typedef struct savqa_gemm_lp_desc {
                                c_rows / n_store / row map) and ws_elems >= slices*M*N stores
                                each K slice's partial tile with plain stores and then adds the
                                slices into C in one pass (C += sum), instead of fp32 atomics */
+    float* colsum_a;        /* optional, a_trans = 1, bf16: colsum_a[m] += sum_k A(m, k) (the
+                               bias gradient of dW = dY^T X), summed in fp32 from the staged A
+                               tiles by the 128x128 kernel; other kernels add it in a separate
+                               column-sum pass */
 } savqa_gemm_lp_desc;
 
 int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* d);

@@ -61,6 +61,7 @@ class GemmLpDesc(C.Structure):
         ("tile_hint", c_i32),
         ("c_rows", c_p), ("n_store", c_i64),
         ("ws", c_p), ("ws_elems", c_i64),
+        ("colsum_a", c_p),
     ]
 
 

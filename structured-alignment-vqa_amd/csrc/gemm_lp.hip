@@ -714,6 +714,13 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   if constexpr (PRE != 0) {
     if (nt == 0 && !tail) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
   }
+  // fused bias gradient (savqa_gemm_lp_desc.colsum_a, dW launches): the first column tile of
+  // each row block also sums its staged A^T tiles over k, thread (rg, cg) four k rows of 8
+  // columns per k-tile (zero-filled past K), folded across the 16 row groups at the end
+  const bool do_cs = AT && !FP8 && d.colsum_a != nullptr && tn == 0;
+  float cs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
 
   // fp8 block scales: staged by LDS-DMA with the operand tiles (one 4-byte granule per lane:
   // the 4 blocks of 32 k of one row in a k-tile; wave w stages A rows (w < 2) or B rows
@@ -802,6 +809,18 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
             for (int j = 0; j < 4; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
         }
+        if constexpr (AT) {
+          if (do_cs) {  // block-uniform
+            const int cg = threadIdx.x & 15, rg = threadIdx.x >> 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int r = 4 * rg + q;
+              const bf16x8 v = *reinterpret_cast<const bf16x8*>(ia + r * 256 + ((16 * cg) ^ (32 * th(r))));
+#pragma unroll
+              for (int e = 0; e < 8; ++e) cs[e] += (float)v[e];
+            }
+          }
+        }
       }
       __syncthreads();  // k-tile kt+1 landed; buffer kt free for k-tile kt+2
     }
@@ -809,6 +828,22 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
 
   // ---------------------------------------------------------------- epilogue
   __syncthreads();  // every wave's last k-tile reads are done: LDS is free
+  if constexpr (AT && !FP8) {
+    if (do_cs) {  // block-uniform: fold the 16 row groups, one atomic per column
+      float* red = reinterpret_cast<float*>(smem);  // [16 row groups][128 columns]
+      const int cg = threadIdx.x & 15, rg = threadIdx.x >> 4;
+      *reinterpret_cast<f4*>(&red[rg * 128 + 8 * cg]) = f4{cs[0], cs[1], cs[2], cs[3]};
+      *reinterpret_cast<f4*>(&red[rg * 128 + 8 * cg + 4]) = f4{cs[4], cs[5], cs[6], cs[7]};
+      __syncthreads();
+      if (threadIdx.x < 128 && m0 + threadIdx.x < d.M) {
+        float v = 0.f;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) v += red[g * 128 + threadIdx.x];
+        atomicAdd(&d.colsum_a[m0 + threadIdx.x], v);
+      }
+      __syncthreads();  // the epilogue reuses the LDS
+    }
+  }
   if (PRE == 0 && !FP8 && args.slab && !tail)
     lp_epilogue_slab(d, acc, m0 + wm * 64, n0 + wn * 64, first_split, lane,
                      args.slab + (int64_t)slice * d.M * d.N);
@@ -1197,6 +1232,7 @@ static bool lp_ok(const savqa_gemm_lp_desc& d, const char** msg) {
   if ((d.c_rows || d.n_store > 0) && !d.atomic) return no("c_rows / n_store need atomic = 1");
   if ((d.split_k > 1 || d.split_k < 0) && (!d.atomic || !d.C)) return no("split-K needs atomic fp32 C");
   if (d.a_rows && d.a_trans) return no("a_rows needs a_trans = 0");
+  if (d.colsum_a && (!d.a_trans || fp8)) return no("colsum_a needs a_trans = 1 and bf16 operands");
   if (d.mask && d.mask_arows && !d.a_rows) return no("mask_arows needs a_rows");
   if (d.mask && d.mask_type != SAVQA_DT_BF16 && d.mask_type != SAVQA_DT_F32) return no("mask_type");
   if (d.rowvec && d.rowvec_period <= 0) return no("rowvec_period");
@@ -1416,6 +1452,9 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
     else if (d.a_trans && !d.b_trans) SAVQA_LP1(true, false);
     else SAVQA_LP1(true, true);
 #undef SAVQA_LP1
+  }
+  if (d.colsum_a && var != 1) {  // the fused column sum lives in the 128 x 128 kernel only
+    if (int rc = savqa_colsum_bf16(stream, d.A, d.K, d.M, d.lda, d.colsum_a)) return rc;
   }
   if (slabs) {
     const int vec = (d.ldc % 4 == 0) && (((uintptr_t)d.C & 15) == 0);

@@ -462,7 +462,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
             Lb = lp.W.enc[i]
             dz2b = _bf(M, d, dev=dev)
             ops.ln_bwd(dx, e["z2"], *e["st2"], L["g2"], dz2, Lg["g2"], Lg["b2"], dzb=dz2b)
-            ops.linear_dw_lp(dz2b, e["h"], Lg["W2"], Lg["c2"], rows=M, dy32=dz2)
+            ops.linear_dw_lp(dz2b, e["h"], Lg["W2"], Lg["c2"], rows=M)
             dh = _bf(M, 4 * d, dev=dev)
             ops.linear_dx_lp(dz2b, Lb["W2"], None, dh, rows=M, mask=e["h"], ldmask=4 * d)
             del dz2b
@@ -543,7 +543,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         if lp.cat_scale is not None:  # fp8 concat buffer: a bf16 copy for the weight gradient
             catb = _bf(M, D2, dev=dev)
             ops.dequant_fp8_bf16(s.cat, M, D2, D2, lp.cat_scale, D2 // 32, catb, D2)
-        ops.linear_dw_lp(dxb, catb, G.Win, G.bin, rows=M, dy32=dx)
+        ops.linear_dw_lp(dxb, catb, G.Win, G.bin, rows=M)
         dq = _empty(B * Lq, D2, dev=dev)
         ops.linear_dx_lp(dxb, lp.W.Win, dq, rows=B * Lq, a_rows=qrows, mask=catb, ldmask=D2,
                          mask_arows=True)
@@ -693,7 +693,7 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
         dmacro = _empty(B * Ns, Hm, dev=dev)
         if lp is not None:  # (fp32, bf16) node gradient from the low-precision stack
             dnode, dnodeb = dnode
-            ops.linear_dw_lp(dnodeb, s.macrob, G.Wipt, G.bipt, rows=B * Ns, dy32=dnode)
+            ops.linear_dw_lp(dnodeb, s.macrob, G.Wipt, G.bipt, rows=B * Ns)
             ops.linear_dx_lp(dnodeb, lp.Wipt, dmacro, rows=B * Ns)
             del dnodeb
         else:
@@ -761,7 +761,7 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
     if lp is not None:
         dvvb = _bf(B * Nv, Hm, dev=dev)
         ops.cast_bf16(dvv, B * Nv, Hm, Hm, dvvb, Hm)
-        ops.linear_dw_lp(dvvb, lp.vis_bf16(), G.Wv, G.bv, rows=B * Nv, dy32=dvv)
+        ops.linear_dw_lp(dvvb, lp.vis_bf16(), G.Wv, G.bv, rows=B * Nv)
     else:
         ops.linear_dw(dvv, s.vis, G.Wv, G.bv, rows=B * Nv)
 

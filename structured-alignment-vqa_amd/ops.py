@@ -200,7 +200,7 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
             ldc=0, Cb=None, ldcb=0, c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None,
             ldrv=0, rowvec_period=0, resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False,
             alpha=1.0, relu=False, atomic=False, split_k=1, tile_hint=0, c_rows=None,
-            n_store=0, ws=None):
+            n_store=0, ws=None, colsum_a=None):
     """savqa_gemm_lp_desc for bf16 / fp8 operands (include/savqa.h). ws: split-K partial-slab
     workspace (fp32 tensor), see lp_workspace."""
     d = _lib.GemmLpDesc()
@@ -221,6 +221,7 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
     d.c_rows, d.n_store = _p(c_rows), int(n_store)
     if ws is not None:
         d.ws, d.ws_elems = _p(ws), int(ws.numel())
+    d.colsum_a = _p(colsum_a)
     return d
 
 
@@ -347,18 +348,13 @@ def linear_dx_lp(dY: Tensor, W: Tensor, dX: Optional[Tensor] = None,
             mask=mask, ldmask=ldmask, mask_arows=mask_arows, resid=resid, ldr=K)
 
 
-def linear_dw_lp(dY: Tensor, X: Tensor, dW: Tensor, db: Optional[Tensor], *, rows: int,
-                 dy32: Optional[Tensor] = None):
-    """dW += dY^T X on bf16 operands (split-K, atomics); db += colsum(dY) from the fp32 dY
-    when the caller has it (dy32), else from the bf16 one."""
+def linear_dw_lp(dY: Tensor, X: Tensor, dW: Tensor, db: Optional[Tensor], *, rows: int):
+    """dW += dY^T X on bf16 operands (split-K through slabs); db += colsum(dY), summed in fp32
+    from the bf16 dY tiles the GEMM stages (savqa_gemm_lp_desc.colsum_a) -- the bf16 operand,
+    as autocast's bias gradient is."""
     N, K = dW.shape
     gemm_lp(dY, X, N, K, rows, lda=N, ldb=K, a_trans=True, C=dW, ldc=K, atomic=True, split_k=-1,
-            slabs=True)
-    if db is not None:
-        if dy32 is not None:
-            colsum_acc(dy32, rows, N, N, db)
-        else:
-            colsum_bf16(dY, rows, N, N, db)
+            slabs=True, colsum_a=db)
 
 
 def linear(X: Tensor, W: Tensor, b: Optional[Tensor], out: Tensor, *, relu=False,

@@ -127,6 +127,28 @@ def test_bf16_dw_split_k_atomic_and_colsum(K, hint):
     assert rel(cs - 1, dY.double().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("slabs", [False, True])
+@pytest.mark.parametrize("hint", [0, 1, 5])
+@pytest.mark.parametrize("M,N,K", [(512, 1536, 18712), (520, 264, 2400), (2048, 512, 256)])
+def test_bf16_dw_fused_colsum(M, N, K, hint, slabs, monkeypatch):
+    """The bias gradient fused into the dW launch (savqa_gemm_lp_desc.colsum_a): the first
+    column tile of each row block sums its staged dY^T tiles over its k range (every split-K
+    slice, zero-filled past K, edge rows past N dropped); the 256-wide kernels (hint 5) add it
+    in a separate column-sum pass. Accumulates into an existing gradient."""
+    O = ops()
+    monkeypatch.setattr(O, "LP_SLABS", slabs)
+    dY = bf((K, N), 13)
+    X = bf((K, M), 14)
+    W0 = torch.randn(N, M, device=dev)
+    b0 = torch.randn(N, device=dev)
+    dW, db = W0.clone(), b0.clone()
+    O.gemm_lp(dY, X, N, M, K, lda=N, ldb=M, a_trans=True, C=dW, ldc=M, atomic=True,
+              split_k=-1, tile_hint=hint, colsum_a=db, slabs=slabs)
+    ref = dY.double().t() @ X.double()
+    assert rel(dW - W0, ref) < 2e-5
+    assert rel(db - b0, dY.double().sum(0)) < 1e-5
+
+
 def test_bf16_epilogues_rows_mask_resid_rowvec():
     """Row gathers of A (a_rows), the ReLU-backward mask read through them (mask_arows, bf16
     mask), residual, periodic position rows, and the c_group row map of the concat buffer."""
