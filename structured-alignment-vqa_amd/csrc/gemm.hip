@@ -820,6 +820,16 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // 257 / 1100 A/B'd in-step, 192 best)
 constexpr int64_t SK16_MAX_TILES = 192;
 
+// 128x128-tile launches with fewer workgroups than this (tiles x split-K slices) take the
+// skinny kernels; SAVQA_SK_TILES overrides it (tuning runs)
+static int64_t sk_min_tiles() {
+  static int64_t v = [] {
+    const char* e = getenv("SAVQA_SK_TILES");
+    return e ? (int64_t)atoll(e) : (int64_t)160;
+  }();
+  return v;
+}
+
 static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.M < 0 || d.N < 0 || d.K < 0) return fail(SAVQA_EINVAL, "savqa_gemm: negative dims");
   if (d.M >= (1LL << 31) || d.N >= (1LL << 31)) return fail(SAVQA_EUNSUP, "savqa_gemm: M/N >= 2^31");
@@ -841,7 +851,7 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   // 128x128 tiles once there is enough parallelism (split-K counts), else the skinny
   // kernel (32x32 tiles, K split over the 8 waves of a workgroup; no split-K launch),
   // 16x16 tiles while 32x32 ones would leave CUs idle (< SK16_MAX_TILES tiles)
-  if (tiles128 * split < 160) {
+  if (tiles128 * split < sk_min_tiles()) {
     const int64_t tiles32 = ((d.M + 31) / 32) * ((d.N + 31) / 32);
     p.tile = tiles32 < SK16_MAX_TILES ? 16 : 32;
     p.split = 1;

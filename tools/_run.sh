@@ -1,8 +1,10 @@
 set -eo pipefail
-TO=900 bash tools/gpu.sh tests tests/test_gemm_lp_gpu.py tests/test_precision_gpu.py tests/test_fullsize_gpu.py tests/test_lowp_state_gpu.py > gpurun_out/t1.txt 2>&1 || { tail -40 gpurun_out/t1.txt; exit 1; }
-tail -3 gpurun_out/t1.txt
+TO=600 bash tools/gpu.sh tests tests/test_kernels_gpu.py -k "attention or q1" > gpurun_out/t1.txt 2>&1 || { tail -40 gpurun_out/t1.txt; exit 1; }
+tail -2 gpurun_out/t1.txt
 for r in 1 2; do
-for w in cfg3 cfg5; do
-timeout -k 10 300 python -u bench.py --workload $w --no-cpu-baseline 2>/dev/null | python -c "import json,sys;d=json.loads(sys.stdin.read());r=d['roofline'];print('$w', d['value'], r['kernel'], r['frac'])"
+for L in tools/ab/libsavqa_attnold.so structured-alignment-vqa_amd/libsavqa.so; do
+echo "== $L"
+SAVQA_LIB=$L timeout -k 10 200 python -u tools/attn_bench.py --q1 --B 256 --T 73 50 2>&1 | grep -v amdgpu.ids
+SAVQA_LIB=$L timeout -k 10 200 python -u tools/attn_bench.py --q1 --bf16 --B 512 --T 73 50 2>&1 | grep -v amdgpu.ids
 done
 done
