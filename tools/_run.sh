@@ -1,13 +1,4 @@
 set -eo pipefail
-TO=600 bash tools/gpu.sh tests tests/test_kernels_gpu.py tests/test_precision_gpu.py -k "attention or bf16 or precision" > gpurun_out/t1.txt 2>&1 || { tail -40 gpurun_out/t1.txt; exit 1; }
-tail -2 gpurun_out/t1.txt
-for r in 1 2; do
-for L in structured-alignment-vqa_amd/libsavqa.so tools/ab/libsavqa_bf2w4.so; do
-echo "== $L"; SAVQA_LIB=$L timeout -k 10 200 python -u tools/attn_bench.py --bf16 --B 512 2>&1 | grep -v amdgpu.ids
-done
-done
-for r in 1 2; do
-for L in structured-alignment-vqa_amd/libsavqa.so tools/ab/libsavqa_bf2w4.so; do
-SAVQA_LIB=$L timeout -k 10 300 python -u bench.py --workload cfg3 --no-cpu-baseline --no-roofline 2>/dev/null | python -c "import json,sys;d=json.loads(sys.stdin.read());print('$L cfg3', d['value'])"
-done
-done
+S="NT:512:512:512 NT:512:2048:512 NT:512:512:2048 NN:512:512:512 NN:512:2048:512 NN:512:512:2048 TN:512:512:512 TN:2048:512:512 TN:512:2048:512 NT:1024:512:512 NT:1024:2048:512 NN:1024:512:2048"
+echo "== fp32 skinny (x6 mode)"; SAVQA_BENCH_PREC=fp32x6 timeout -k 10 200 python -u tools/gemm_bench.py $S 2>&1 | grep -v amdgpu.ids
+echo "== bf16x3 + torch bf16 yardstick"; SAVQA_BENCH_PREC=bf16x3 timeout -k 10 200 python -u tools/gemm_bench.py $S 2>&1 | grep -v amdgpu.ids
