@@ -73,19 +73,14 @@ def test_relation_branch_against_reference_golden(case):
         asum = float(g[f"g:{n}:abssum"])
         assert abs(flat.sum() - float(g[f"g:{n}:sum"])) <= 1e-3 * max(asum, 1e-12) + 1e-9, n
     worst.sort(reverse=True)
-    if case != "full_rel_big":
-        assert worst[0][0] < 1e-3, worst[:5]
-    else:
-        # At T_syb = 1313 a few ReLU pre-activations sit within ~1e-9 of 0 relative to
-        # |x||w| (oracle in fp64: att_syb.enc_feed_forward_4.conv1 1.5e-9, ...), so ANY fp32
-        # summation order other than the reference's MKL one flips some of them and moves
-        # single gradient elements: torch's own fp32 on this GPU (hipBLASLt, the oracle on
-        # cuda, tools/dbg/rel_big_t32.py) lands 5.4e-3 from the reference on this metric, the
-        # HIP path 2.1e-3, while every kernel call of the step agrees with fp64 on its own
-        # inputs to fp32 rounding (tools/dbg/rel_big_{attn,gemm,ln,graph,macro}.py). Bar: the
-        # conditioning floor for the worst element, and the fp32 bar for the typical one.
-        assert worst[0][0] < 1e-2, worst[:5]
-        assert worst[len(worst) // 2][0] < 1e-4, worst[len(worst) // 2]
+    print(case, "per-gradient worst-element error, top 8 / 1st percentile / median:", worst[:8],
+          worst[len(worst) // 100], worst[len(worst) // 2])
+    # north-star bar for every case: at T_syb = 1313 (full_rel_big) the worst gradient element
+    # lands 2.2e-4 from the reference (round 4: x6 GEMMs, base-2 softmax; 2.1e-3 in round 3,
+    # when this case had a 1e-2 bar), the reference's own fp32 lands <= 2.8e-5 from the fp64
+    # oracle (tests/golden/full_rel_big_fp64dev.json, tools/rel_fp64_check.py)
+    assert worst[0][0] < 1e-3, worst[:5]
+    assert worst[len(worst) // 2][0] < 1e-4, worst[len(worst) // 2]
     used = torch.from_numpy(g["R_used"]).cuda()
     assert rel(params["MIL_NCE.R"].grad[used, :4].cpu().numpy(), g["R_grad_used"]) < 1e-3
     opt.step()
