@@ -20,11 +20,15 @@ import sys
 
 
 def norm(name):
-    """'void savqa::gemm_f32_kernel<128, 128, 16, false, true>(...)' -> 'gemm_f32_kernel<128,128,false,true>'"""
-    m = re.search(r"savqa::(\w+)<([^>]*)>", name)
+    """'void savqa::gemm_f32_kernel<128, 128, 16, false, true>(...)' -> 'gemm_f32_kernel<128,128,false,true>';
+    non-template kernels by their own name ('savqa::gattn_fwd_flash_kernel(savqa::AttnArgsT<...>'
+    -> 'gattn_fwd_flash_kernel', not the argument type's template)."""
+    m = re.match(r"(?:void )?savqa::(\w+)(?:<([^(]*)>)?\(", name)
     if not m:
         m2 = re.search(r"savqa::(\w+)\(", name)
         return m2.group(1) if m2 else name[:60]
+    if m.group(2) is None:
+        return m.group(1)
     args = [a.strip() for a in m.group(2).split(",")]
     if m.group(1) == "gemm_f32_kernel" and len(args) == 5:
         args = args[:2] + args[3:]  # drop BK
