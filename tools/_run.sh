@@ -1,4 +1,6 @@
 set -eo pipefail
-bash tools/gpu.sh suite -s > gpurun_out/suite.txt 2>&1 || { tail -30 gpurun_out/suite.txt; exit 1; }
-tail -4 gpurun_out/suite.txt
-grep "per-gradient worst" gpurun_out/pytest_gpu.log | cut -c1-1500
+export SAVQA_BENCH_PREC=fp32x6
+for p in 0 1; do echo "== pipe $p"; SAVQA_X6_PIPE=$p timeout -k 10 300 python -u tools/gemm_bench.py 2>&1 | grep -v amdgpu.ids; done
+for r in 1 2; do for p in 0 1; do
+SAVQA_X6_PIPE=$p timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-roofline 2>/dev/null | python -c "import json,sys;d=json.loads(sys.stdin.read());print('pipe=$p cfg2', d['value'])"
+done; done
