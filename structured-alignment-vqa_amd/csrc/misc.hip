@@ -52,21 +52,36 @@ __global__ void dec_init_kernel(const float* __restrict__ emb, int64_t idx, floa
   out[t] = v;
 }
 
-// d emb[idx] += scale * sum_b D'(g[b]), d pos[0] += sum_b D'(g[b])
-__global__ void dec_init_bwd_kernel(const float* __restrict__ g, int64_t B, int64_t d,
-                                    int64_t idx, float scale, DropParam dp, int32_t site,
-                                    float* __restrict__ demb, float* __restrict__ dpos) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= d) return;
-  float s = 0.f, ss = 0.f;
-  for (int64_t b = 0; b < B; ++b) {
-    float v = g[b * d + c];
-    if (site >= 0) v *= drop_mul(dp, site, b * d + c);
-    s += v * scale;
-    ss += v;
+// d emb[idx] += scale * sum_b D'(g[b]), d pos[0] += sum_b D'(g[b]). Block: 32 columns x 8
+// row slices (slice r sums rows r, r + 8, ..), folded through LDS in a fixed order -- one
+// thread per column looping over all B rows (two workgroups at d = 512, each element a
+// SplitMix64 mask) took 69-130 us per launch
+constexpr int DIB_COLS = 32, DIB_SLICES = 8;
+__global__ __launch_bounds__(256) void dec_init_bwd_kernel(const float* __restrict__ g, int64_t B,
+                                                           int64_t d, int64_t idx, float scale,
+                                                           DropParam dp, int32_t site,
+                                                           float* __restrict__ demb,
+                                                           float* __restrict__ dpos) {
+  __shared__ float part[DIB_SLICES][DIB_COLS];
+  const int cl = threadIdx.x % DIB_COLS, sl = threadIdx.x / DIB_COLS;
+  const int64_t c = (int64_t)blockIdx.x * DIB_COLS + cl;
+  float ss = 0.f;
+  if (c < d) {
+    for (int64_t b = sl; b < B; b += DIB_SLICES) {
+      float v = g[b * d + c];
+      if (site >= 0) v *= drop_mul(dp, site, b * d + c);
+      ss += v;
+    }
   }
-  if (demb) demb[idx * d + c] += s;
-  if (dpos) dpos[c] += ss;
+  part[sl][cl] = ss;
+  __syncthreads();
+  if (sl == 0 && c < d) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < DIB_SLICES; ++r) t += part[r][cl];
+    if (demb) demb[idx * d + c] += t * scale;
+    if (dpos) dpos[c] += t;
+  }
 }
 
 // out[t][c] += sum_b X[(b*T + t)*ldx + c]  (gradient of a learned position table)
@@ -611,7 +626,8 @@ extern "C" int savqa_dec_init_bwd(void* stream, const float* g, int64_t B, int64
                                   float* dpos) {
   if (B <= 0 || d <= 0) return 0;
   if (p < 0.f || p > 1.f) return fail(SAVQA_EINVAL, "savqa_dec_init_bwd: p outside [0,1]");
-  hipLaunchKernelGGL(dec_init_bwd_kernel, dim3((d + 255) / 256), dim3(256), 0, as_stream(stream), g,
+  hipLaunchKernelGGL(dec_init_bwd_kernel, dim3((unsigned)((d + DIB_COLS - 1) / DIB_COLS)), dim3(256), 0,
+                     as_stream(stream), g,
                      B, d, idx, scale, make_drop(seed, p), p > 0.f ? site : -1, demb, dpos);
   return check_launch("savqa_dec_init_bwd");
 }
