@@ -32,6 +32,9 @@ extern "C" {
 
 int savqa_version(void);
 const char* savqa_last_error(void);
+/* sizeof of the descriptor structs, for bindings to check their layouts: out[0] =
+ * savqa_gemm_desc, out[1] = savqa_gemm_lp_desc, out[2] = savqa_collate_field; n >= 3 */
+int savqa_struct_sizes(int64_t* out, int32_t n);
 
 /* ------------------------------------------------------------------------
  * GEMM:  C[crow(m)][n] (op)= epilogue( sum_k A(m,k) * B(k,n) )

@@ -77,6 +77,7 @@ class CollateField(C.Structure):
 # name -> argtypes (restype is always int except savqa_last_error)
 _SIGS = {
     "savqa_version": [],
+    "savqa_struct_sizes": [c_p, c_i32],
     "savqa_gemm": [c_p, C.POINTER(GemmDesc)],
     "savqa_gemm_plan": [C.POINTER(GemmDesc), c_p],
     "savqa_colsum_acc": [c_p, c_p, c_i64, c_i64, c_i64, c_p],

@@ -27,3 +27,11 @@ int check_launch(const char* what) {
 
 extern "C" int savqa_version(void) { return 1; }
 extern "C" const char* savqa_last_error(void) { return savqa::g_err.c_str(); }
+
+extern "C" int savqa_struct_sizes(int64_t* out, int32_t n) {
+  if (!out || n < 3) return savqa::fail(SAVQA_EINVAL, "savqa_struct_sizes: out needs 3 slots");
+  out[0] = (int64_t)sizeof(savqa_gemm_desc);
+  out[1] = (int64_t)sizeof(savqa_gemm_lp_desc);
+  out[2] = (int64_t)sizeof(savqa_collate_field);
+  return 0;
+}

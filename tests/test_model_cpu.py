@@ -58,6 +58,19 @@ def test_forward_without_device_fails_loudly():
           torch.ones(1, 2, 5, dtype=torch.int32), None, None, None, None)
 
 
+def test_descriptor_layouts_match_the_library():
+    """The ctypes mirrors of the C-ABI descriptors (savqa_amd/_lib.py) have the C structs'
+    sizes (savqa_struct_sizes): a field added on one side only fails here, on CPU."""
+    import ctypes as C
+    from savqa_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libsavqa.so not built")
+    out = (C.c_int64 * 3)()
+    assert _lib.load().savqa_struct_sizes(C.cast(out, C.c_void_p), 3) == 0
+    assert list(out) == [C.sizeof(_lib.GemmDesc), C.sizeof(_lib.GemmLpDesc),
+                         C.sizeof(_lib.CollateField)]
+
+
 def test_library_exports_every_declared_symbol():
     import re
     import ctypes
