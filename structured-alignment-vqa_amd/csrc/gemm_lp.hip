@@ -360,6 +360,22 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
       // one float per lane: row q, column lane (256 contiguous bytes per atomic instruction)
       const int64_t n = ecol(col0, col_hi, lane);
       const float bv = (first_split && d.bias && n < d.N) ? d.bias[n] : 0.f;
+      // the pass's output rows (c_rows scatter) and mask rows, lane q holding row q, loaded
+      // before the first atomic and broadcast per row: loaded inside the loop, each row's
+      // load waited for every atomic before it (vmcnt counts both) -- the GloVe-table
+      // scatter paid one atomic round trip per row
+      int64_t rowv = 0, mrv = 0;
+      {
+        int64_t m = row0 + rstep * pass + lane;
+        m = m < d.M ? m : d.M - 1;
+        if (d.c_rows) rowv = d.c_rows[m];
+        if (d.mask && d.mask_arows) mrv = d.a_rows[m];
+      }
+      auto bcast = [](int64_t v, int q) {
+        const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, q);
+        const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), q);
+        return (int64_t)(((uint64_t)hi << 32) | lo);
+      };
       for (int q = 0; q < 64; ++q) {
         const int64_t m = row0 + rstep * pass + q;
         if (m >= d.M) break;
@@ -370,7 +386,7 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
         if (first_split && d.rowvec) v += d.rowvec[(m % d.rowvec_period) * d.ldrv + n];
         if (d.relu) v = fmaxf(v, 0.f);
         if (d.mask) {
-          const int64_t mr = d.mask_arows ? d.a_rows[m] : m;
+          const int64_t mr = d.mask_arows ? bcast(mrv, q) : m;
           const float mv = d.mask_type == SAVQA_DT_BF16
                                ? bf2f(static_cast<const __bf16*>(d.mask)[mr * d.ldmask + n])
                                : static_cast<const float*>(d.mask)[mr * d.ldmask + n];
@@ -379,7 +395,7 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
         if (first_split && d.resid) v += d.resid[m * d.ldr + n];
         int64_t cr = m;
         if (d.c_rows) {
-          cr = d.c_rows[m];
+          cr = bcast(rowv, q);
         } else if (!ident) {
           const uint32_t mu = (uint32_t)m, cg = (uint32_t)d.c_group;
           cr = (int64_t)(mu / cg) * d.c_stride + (int64_t)(mu % cg) + d.c_offset;
