@@ -386,7 +386,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
 
     Returns d(pre-activation of the node rows of cat) [B*Nn, 2048] when want_node_grad
     (the syb stack feeds it to the MIL-NCE backward), else None; in the low-precision modes
-    a (fp32, bf16) pair.
+    a (None, bf16) pair.
     mark(name) declares every arena gradient before parameter `name` final (the arena is
     in backward-completion order), so the all-reduce streams out layer by layer."""
     mark = mark or (lambda name: None)
@@ -558,12 +558,14 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
     del dq
     if not want_node_grad:
         return None
-    dnode = _empty(B * Nn, D2, dev=dev)
     if lp is not None:
+        # bf16 only: the MIL-NCE input-projection gradients are its only consumers (a fp32
+        # copy was 4 B per element of HBM writes that nothing read)
         dnodeb = _bf(B * Nn, D2, dev=dev)
-        ops.linear_dx_lp(dxb, lp.W.Win, dnode, dnodeb, rows=B * Nn, a_rows=nrows, mask=catb,
+        ops.linear_dx_lp(dxb, lp.W.Win, None, dnodeb, rows=B * Nn, a_rows=nrows, mask=catb,
                          ldmask=D2, mask_arows=True)
-        return dnode, dnodeb
+        return None, dnodeb
+    dnode = _empty(B * Nn, D2, dev=dev)
     ops.linear_dx(dx, W.Win, dnode, rows=B * Nn, a_rows=nrows, mask=s.cat, ldmask=s.cat.shape[1],
                   mask_arows=True)
     return dnode
@@ -691,8 +693,8 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
     dobj = None
     if dnode is not None:
         dmacro = _empty(B * Ns, Hm, dev=dev)
-        if lp is not None:  # (fp32, bf16) node gradient from the low-precision stack
-            dnode, dnodeb = dnode
+        if lp is not None:  # bf16 node gradient from the low-precision stack
+            _, dnodeb = dnode
             ops.linear_dw_lp(dnodeb, s.macrob, G.Wipt, G.bipt, rows=B * Ns)
             ops.linear_dx_lp(dnodeb, lp.Wipt, dmacro, rows=B * Ns)
             del dnodeb

@@ -1,12 +1,8 @@
 set -eo pipefail
+TO=600 bash tools/gpu.sh tests tests/test_precision_gpu.py tests/test_fullsize_gpu.py tests/test_lowp_state_gpu.py tests/test_gemm_lp_gpu.py > gpurun_out/t1.txt 2>&1 || { tail -30 gpurun_out/t1.txt; exit 1; }
+tail -2 gpurun_out/t1.txt
+timeout -k 10 300 python -u tools/gemm_breakdown.py cfg3 > gpurun_out/bd_base.txt 2>&1 || { tail -20 gpurun_out/bd_base.txt; exit 1; }
+grep -E "total|30208x2048x512" gpurun_out/bd_base.txt
 for r in 1 2; do
-for v in base lpold; do
-L=structured-alignment-vqa_amd/libsavqa.so; [ $v = lpold ] && L=tools/ab/libsavqa_lpold.so
-SAVQA_LIB=$L timeout -k 10 300 python -u tools/gemm_breakdown.py cfg3 > gpurun_out/bd_$v.txt 2>&1 || { tail -20 gpurun_out/bd_$v.txt; exit 1; }
-echo "== $v"; grep -E "total|92160x304x1024" gpurun_out/bd_$v.txt
-done; done
-for r in 1 2; do
-for v in base lpold; do
-L=structured-alignment-vqa_amd/libsavqa.so; [ $v = lpold ] && L=tools/ab/libsavqa_lpold.so
-SAVQA_LIB=$L timeout -k 10 300 python -u bench.py --workload cfg3 --no-cpu-baseline --no-roofline 2>/dev/null | python -c "import json,sys;d=json.loads(sys.stdin.read());print('$v cfg3', d['value'])"
-done; done
+timeout -k 10 300 python -u bench.py --workload cfg3 --no-cpu-baseline --no-roofline 2>/dev/null | python -c "import json,sys;d=json.loads(sys.stdin.read());print('cfg3', d['value'])"
+done
