@@ -981,7 +981,8 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
   const int PLB = 16 * nw + 8;
   __bf16* Ks = smb;                // [TK][ATT_KLB]
   __bf16* Vs = smb + TK * ATT_KLB;
-  __bf16* Pt = Vs + TK * ATT_KLB;  // [TK][PLB]  P^T
+  // phase 2 overlays the K / V images with Q^T and dO^T ([64 d][PLB] each)
+  __bf16* Pt = smb + max(2 * TK * ATT_KLB, 2 * ATT_DK * PLB);  // [TK][PLB]  P^T
   __bf16* dSt = Pt + TK * PLB;     // [TK][PLB]  dS^T (scaled by 1/8, masked)
   const StripViews<AttnArgsT<__bf16>> sv(a, b, h);
   const int64_t nq = (int64_t)a.B * a.Tq, nk = (int64_t)a.B * a.Tk;
@@ -989,8 +990,8 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
   const BView DO = head_view(a.dout, a.lddo, nq, qb, h * ATT_DK);
 
   // ---- phase 1: strips, then dQ of the strip
+  att_bf16x8 qa[2], oa[2];  // Q / dO of this lane's strip row (kept for phase 2's images)
   {
-    att_bf16x8 qa[2], oa[2];
     {
       const uint32_t qvo = (uint32_t)(i0 + col) * sv.q.ld + 16u * g;
       const uint32_t ovo = (uint32_t)(i0 + col) * DO.ld + 32u * g;
@@ -1088,67 +1089,66 @@ __global__ __launch_bounds__(512) void gattn_bwd_mfma_bf2_kernel(AttnArgsT<__bf1
   }
   __syncthreads();
 
+  // ---- Q^T and dO^T of every query over the K / V images (phase 2 reads K / V only for its
+  // ReLU masks, which it loads from memory): each phase-2 A operand is then one 8-B LDS read
+  // instead of four scattered global loads (the per-lane loads were ~20 % of the kernel)
+  __bf16* Qt = smb;
+  __bf16* Ot = smb + ATT_DK * PLB;
+  {
+    const int i = i0 + col;
+    const bool ok = i < a.Tq;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int dd = 32 * hf + 8 * g + e;
+        Qt[dd * PLB + i] = ok ? qa[hf][e] : (__bf16)0.f;
+        Ot[dd * PLB + i] = ok ? oa[hf][e] : (__bf16)0.f;
+      }
+  }
   // ---- phase 2: dV^T = dO^T P and dK^T = Q^T dS, 16x16 tiles (key tile jt, column block dt),
   // grouped (tensor, dt): item = grp * NJT + jt, grp < 4 dV, grp >= 4 dK; k = query.
-  //   A[m = d][k = i] = X[i][16 dt + d]   (X = dO rounded to bf16, or Q): preloaded per group,
-  //                                        query rows past Tq read as 0
-  //   B[k = i][n = j] = Y^T[j][i]          (Y^T = P^T or dS^T): one 8-B LDS read per 16 k
+  //   A[m = d][k = i] = X^T[16 dt + d][i]   (X = dO rounded to bf16, or Q; rows i >= Tq zero)
+  //   B[k = i][n = j] = Y^T[j][i]           (Y^T = P^T or dS^T)
   //   D[m = 4g + r][n = col] = out[j = 16 jt + col][d = 16 dt + 4g + r]
   const int nitems = 8 * NJT;
   const int it0 = nitems * w / nw, it1 = nitems * (w + 1) / nw;
-  constexpr int MAXG = 3;  // groups a wave's item run can touch (checked on the host)
-  const int g0 = it0 / NJT;
-  const uint32_t avo_o = (uint32_t)(4 * g) * DO.ld + 4u * col;
-  const uint32_t avo_q = (uint32_t)(4 * g) * sv.q.ld + 2u * col;
-  att_bf16x4 acol[MAXG][NJT];  // (query tiles: nw == NJT, host check)
+  constexpr int MAXI = 8;  // items per wave (nw == NJT: checked on the host)
+  // this wave's ReLU masks (K / V > 0 at its outputs), all loaded before its first store
+  att_bf16x4 mkv[MAXI];
 #pragma unroll
-  for (int u = 0; u < MAXG; ++u) {
-    const int grp = g0 + u;
-    if (grp * NJT < it1 && grp < 8) {  // wave-uniform
-      const int dt = grp & 3;
-#pragma unroll
-      for (int kc = 0; kc < NJT; ++kc) {
-        float t4[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const uint32_t row = (uint32_t)(kc * 16 + t);
-          const float x = grp < 4 ? bld1(DO, avo_o, row * DO.ld + 64u * dt)
-                                  : (float)__builtin_bit_cast(
-                                        __bf16, bld16(sv.q, avo_q, row * sv.q.ld + 32u * dt));
-          t4[t] = kc * 16 + 4 * g + t < a.Tq ? x : 0.f;
-        }
-        acol[u][kc] = pack4(f4v{t4[0], t4[1], t4[2], t4[3]});
-      }
+  for (int q = 0; q < MAXI; ++q) {
+    const int it = it0 + q;
+    mkv[q] = att_bf16x4{(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+    if (it < it1) {  // wave-uniform
+      const int grp = it / NJT, jt = it - grp * NJT;
+      const BView& M = grp < 4 ? sv.v : sv.k;
+      mkv[q] = bld8b<att_bf16x4>(M, (uint32_t)(jt * 16 + col) * M.ld + 8u * g, 32u * (grp & 3));
     }
   }
+  __syncthreads();  // Q^T / dO^T written
   const BView DK = head_view(a.dk, a.lddk, nk, kb, h * ATT_DK);
   const BView DV = head_view(a.dv, a.lddv, nk, kb, h * ATT_DK);
   const bool vk = vec_rows(a.dk, a.lddk), vv = vec_rows(a.dv, a.lddv);
 #pragma unroll
-  for (int u = 0; u < MAXG; ++u) {
-    const int grp = g0 + u;
-    const int lo = max(it0, grp * NJT), hi = min(it1, (grp + 1) * NJT);
-    if (grp >= 8 || lo >= hi) continue;  // wave-uniform
+  for (int q = 0; q < MAXI; ++q) {
+    const int it = it0 + q;
+    if (it >= it1) break;  // wave-uniform
+    const int grp = it / NJT, jt = it - grp * NJT, dt = grp & 3;
     const bool isv = grp < 4;
-    const int dt = grp & 3;
-    const __bf16* Yt = isv ? Pt : dSt;
-    const __bf16* Ms = isv ? Vs : Ks;
-    const BView& D = isv ? DV : DK;
-    const uint32_t svo = (uint32_t)col * D.ld + 8u * g;
-    for (int it = lo; it < hi; ++it) {
-      const int jt = it - grp * NJT;
-      const int j = jt * 16 + col;
-      const att_bf16x4 mk = ldb4(Ms + j * ATT_KLB + dt * 16 + 4 * g);
-      f4v acc = {0.f, 0.f, 0.f, 0.f};
-      const __bf16* yrow = Yt + j * PLB + 4 * g;
+    const __bf16* xcol = (isv ? Ot : Qt) + (16 * dt + col) * PLB + 4 * g;
+    const int j = jt * 16 + col;
+    const __bf16* yrow = (isv ? Pt : dSt) + j * PLB + 4 * g;
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kc = 0; kc < NJT; ++kc) acc = mfma_bf16(acol[u][kc], ldb4(yrow + kc * 16), acc);
-      if (j < a.Tk) {
-        f4v o;
+    for (int kc = 0; kc < NJT; ++kc) acc = mfma_bf16(ldb4(xcol + kc * 16), ldb4(yrow + kc * 16), acc);
+    if (j < a.Tk) {
+      f4v o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (float)mk[r] > 0.f ? acc[r] : 0.f;
-        bstx4<__bf16>(D, o, svo, (uint32_t)(jt * 16) * D.ld + 32u * dt, isv ? vv : vk);
-      }
+      for (int r = 0; r < 4; ++r) o[r] = (float)mkv[q][r] > 0.f ? acc[r] : 0.f;
+      const BView& D = isv ? DV : DK;
+      bstx4<__bf16>(D, o, (uint32_t)col * D.ld + 8u * g, (uint32_t)(jt * 16) * D.ld + 32u * dt,
+                    isv ? vv : vk);
     }
   }
 }
@@ -1420,14 +1420,16 @@ static int launch_bwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const ch
     if constexpr (sizeof(T) == 2) {
       // bf16 MFMA kernels: bf16 K/V images kept next to the bf16 P^T / dS^T images
       const size_t ldsb = 2 * 2 * (size_t)njt * 16 * (size_t)(16 * nw + 8 + ATT_KLB);
+      // second structure: phase 2 overlays the K / V images with Q^T / dO^T [64][16 nw + 8]
+      const size_t ldsb2 = 2 * (std::max(2 * (size_t)njt * 16 * ATT_KLB, 2 * (size_t)ATT_DK * (16 * nw + 8)) +
+                                2 * (size_t)njt * 16 * (size_t)(16 * nw + 8));
       // second structure (transposed dV / dK, dQ in phase 1): as many query as key tiles (the
-      // self-attention shape), and a wave's phase-2 item run (8 NJT / nw items) must touch at
-      // most 3 (tensor, column block) groups
-      const bool v2 = SAVQA_ATT_BWD2 && nw == njt && (8 * njt + nw - 1) / nw <= 2 * njt;
+      // self-attention shape), so a wave's phase-2 item run is 8 NJT / nw = 8 items
+      const bool v2 = SAVQA_ATT_BWD2 && nw == njt;
       switch (njt) {
 #define SAVQA_BWD_CASE(N)                                                                       \
   case N:                                                                                       \
-    if (v2) hipLaunchKernelGGL((gattn_bwd_mfma_bf2_kernel<N>), dim3(B * H), dim3(64 * nw), ldsb, s, a); \
+    if (v2) hipLaunchKernelGGL((gattn_bwd_mfma_bf2_kernel<N>), dim3(B * H), dim3(64 * nw), ldsb2, s, a); \
     else hipLaunchKernelGGL((gattn_bwd_mfma_bf_kernel<N>), dim3(B * H), dim3(64 * nw), ldsb, s, a); \
     break;
         SAVQA_BWD_CASE(1) SAVQA_BWD_CASE(2) SAVQA_BWD_CASE(3) SAVQA_BWD_CASE(4)
