@@ -1,3 +1,3 @@
 set -eo pipefail
-timeout -k 10 900 bash tools/profile_round.sh r04 cfg3
-ls gpurun_out/prof_r04_cfg3/
+timeout -k 10 900 bash tools/profile_round.sh r04 cfg5
+ls gpurun_out/prof_r04_cfg5/
