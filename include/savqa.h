@@ -439,6 +439,12 @@ int savqa_scale_by(void* stream, const float* in, const float* scale, int64_t n,
 int savqa_adam(void* stream, float* p, const float* g, float* m, float* v, int64_t n,
                float lr, float beta1, float beta2, float eps, float bc1, float bc2,
                float grad_scale);
+/* The same update, also writing the updated p rounded to bf16 (round to nearest even) into
+ * shadow[0, n) (8-B aligned): the bf16 weight image of the low-precision modes, refreshed in
+ * the optimizer's pass instead of a cast that re-reads p. shadow may be NULL (= savqa_adam). */
+int savqa_adam_shadow(void* stream, float* p, const float* g, float* m, float* v, int64_t n,
+                      float lr, float beta1, float beta2, float eps, float bc1, float bc2,
+                      float grad_scale, void* shadow);
 
 /* Row-tracked tables (the three 407000 x 300 GloVe tables, AttModel_x3.py:36-41, :168-171,
  * :295): flags[r] bit 0 = row r has Adam state (touched at some step), bit 1 = row

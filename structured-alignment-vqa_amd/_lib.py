@@ -149,6 +149,7 @@ _SIGS = {
     "savqa_gather_rows": [c_p, c_p, c_p, c_i64, c_i64, c_f, c_p],
     "savqa_scatter_rows": [c_p, c_p, c_p, c_i64, c_i64, c_f, c_i64, c_p],
     "savqa_adam": [c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_f, c_f],
+    "savqa_adam_shadow": [c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_f, c_f, c_p],
 }
 
 _I64_RET = {"savqa_ln_bwd_workspace_bytes"}

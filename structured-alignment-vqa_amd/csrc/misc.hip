@@ -459,11 +459,20 @@ __device__ __forceinline__ void adam4(adam_f4& pp, adam_f4 gg, adam_f4& mm, adam
   }
 }
 
+__device__ __forceinline__ void adam_sh4(__bf16* q, adam_f4 x) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  typedef float f4_ __attribute__((ext_vector_type(4)));
+  const f4_ y = {x[0], x[1], x[2], x[3]};
+  *reinterpret_cast<bf16x4*>(q) = __builtin_convertvector(y, bf16x4);
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    int64_t n, float lr, float b1, float b2,
                                                    float eps, float step_size, float sbc2,
-                                                   float gs) {
+                                                   float gs, __bf16* __restrict__ sh) {
+  // sh (optional): the bf16 image of p (the low-precision modes' weight shadow), written from
+  // the updated values in the same pass instead of a separate cast that re-reads p
   (void)lr;
   const int64_t n4 = n / 4;
   adam_f4* P = reinterpret_cast<adam_f4*>(p);
@@ -483,11 +492,16 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     __builtin_nontemporal_store(p0, P + i); __builtin_nontemporal_store(p1, P + j);
     __builtin_nontemporal_store(m0, M + i); __builtin_nontemporal_store(m1, M + j);
     __builtin_nontemporal_store(v0, V + i); __builtin_nontemporal_store(v1, V + j);
+    if (sh) {
+      adam_sh4(sh + 4 * i, p0);
+      adam_sh4(sh + 4 * j, p1);
+    }
   }
   if (i < n4) {
     adam_f4 p0 = P[i], m0 = M[i], v0 = V[i];
     adam4(p0, Gv[i], m0, v0, b1, b2, eps, step_size, sbc2, gs);
     P[i] = p0; M[i] = m0; V[i] = v0;
+    if (sh) adam_sh4(sh + 4 * i, p0);
   }
   {  // scalar tail (same roundings as adam4)
 #pragma clang fp contract(off)
@@ -497,6 +511,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
       v[k] = b2 * v[k] + (1.f - b2) * gx * gx;
       const float den = sqrtf(v[k]) / sbc2 + eps;
       p[k] = p[k] - step_size * (m[k] / den);
+      if (sh) sh[k] = (__bf16)p[k];
     }
   }
 }
@@ -727,20 +742,29 @@ extern "C" int savqa_scale_by(void* stream, const float* in, const float* scale,
   return check_launch("savqa_scale_by");
 }
 
-extern "C" int savqa_adam(void* stream, float* p, const float* g, float* m, float* v, int64_t n,
-                          float lr, float beta1, float beta2, float eps, float bc1, float bc2,
-                          float grad_scale) {
+extern "C" int savqa_adam_shadow(void* stream, float* p, const float* g, float* m, float* v,
+                                 int64_t n, float lr, float beta1, float beta2, float eps,
+                                 float bc1, float bc2, float grad_scale, void* shadow) {
   if (n <= 0) return 0;
   if ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) != 0)
     return fail(SAVQA_EINVAL, "savqa_adam: buffers must be 16-B aligned");
+  if (((uintptr_t)shadow & 7) != 0)
+    return fail(SAVQA_EINVAL, "savqa_adam_shadow: the bf16 shadow must be 8-B aligned");
   const float step_size = lr / bc1;
   const float sbc2 = sqrtf(bc2);
   int64_t blocks = (n / 4 + 255) / 256;
   if (blocks > SAVQA_ADAM_BLOCKS) blocks = SAVQA_ADAM_BLOCKS;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr,
-                     beta1, beta2, eps, step_size, sbc2, grad_scale);
+                     beta1, beta2, eps, step_size, sbc2, grad_scale, static_cast<__bf16*>(shadow));
   return check_launch("savqa_adam");
+}
+
+extern "C" int savqa_adam(void* stream, float* p, const float* g, float* m, float* v, int64_t n,
+                          float lr, float beta1, float beta2, float eps, float bc1, float bc2,
+                          float grad_scale) {
+  return savqa_adam_shadow(stream, p, g, m, v, n, lr, beta1, beta2, eps, bc1, bc2, grad_scale,
+                           nullptr);
 }
 
 static unsigned rows_grid(int64_t nrows) { return (unsigned)((nrows + 255) / 256); }

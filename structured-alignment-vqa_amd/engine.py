@@ -876,8 +876,20 @@ class LpShadow:
     def __init__(self, arena, fp8: bool):
         self.arena, self.fp8 = arena, fp8
         self.buf, self.key = None, None
+        self.buf_key = None  # the arena state the bf16 image `buf` matches
         self.q8 = {}
         self.pad = {}
+        arena.lp_shadow = self  # optim.Adam writes `buf` in its update pass (savqa_adam_shadow)
+
+    def current(self) -> bool:
+        """Whether `buf` matches the arena now (an optimizer step may then update it)."""
+        a = self.arena
+        return self.buf is not None and self.buf.device == a.flat.device and \
+            self.buf_key == a.state_key()
+
+    def arena_updated(self):
+        """The optimizer has just written every live parameter's bf16 image into `buf`."""
+        self.buf_key = self.arena.state_key()
 
     def refresh(self):
         a = self.arena
@@ -886,11 +898,13 @@ class LpShadow:
             return
         if self.buf is None or self.buf.device != a.flat.device:
             self.buf = torch.empty(a.n_live, dtype=torch.bfloat16, device=a.flat.device)
-        lo = 0
-        for t0, t1 in a.table_ranges() + [(a.n_live, a.n_live)]:
-            if t0 > lo:
-                ops.cast_bf16(a.flat[lo:t0], 1, t0 - lo, t0 - lo, self.buf[lo:t0], t0 - lo)
-            lo = max(lo, t1)
+        if self.buf_key != key:
+            lo = 0
+            for t0, t1 in a.table_ranges() + [(a.n_live, a.n_live)]:
+                if t0 > lo:
+                    ops.cast_bf16(a.flat[lo:t0], 1, t0 - lo, t0 - lo, self.buf[lo:t0], t0 - lo)
+                lo = max(lo, t1)
+            self.buf_key = key
         # the two weights that meet GloVe rows (K = 300): bf16 copies with rows zero-padded
         # to 304 columns (the pad is written once, at allocation)
         for name in self.PADDED:

@@ -645,8 +645,13 @@ def adam_rows(p, g, m, v, width, nrows, flags, lr, beta1, beta2, eps, bc1, bc2, 
          float(grad_scale))
 
 
-def adam(p, g, m, v, n, lr, beta1, beta2, eps, bc1, bc2, grad_scale=1.0):
-    # 28 B per parameter: p, m, v read and written, g read
-    _kcall("adam", 28 * int(n), 0, "savqa_adam", _stream(), _p(p), _p(g), _p(m), _p(v), int(n),
-           float(lr), float(beta1), float(beta2), float(eps), float(bc1), float(bc2),
-           float(grad_scale))
+def adam(p, g, m, v, n, lr, beta1, beta2, eps, bc1, bc2, grad_scale=1.0, shadow=None):
+    # 28 B per parameter: p, m, v read and written, g read (+2 B: the optional bf16 shadow)
+    if shadow is None:
+        _kcall("adam", 28 * int(n), 0, "savqa_adam", _stream(), _p(p), _p(g), _p(m), _p(v),
+               int(n), float(lr), float(beta1), float(beta2), float(eps), float(bc1), float(bc2),
+               float(grad_scale))
+    else:
+        _kcall("adam", 30 * int(n), 0, "savqa_adam_shadow", _stream(), _p(p), _p(g), _p(m),
+               _p(v), int(n), float(lr), float(beta1), float(beta2), float(eps), float(bc1),
+               float(bc2), float(grad_scale), _p(shadow))

@@ -9,10 +9,16 @@ torch.optim.Adam's update is exactly zero, so they are skipped bit-exactly.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
 from . import ops
+
+# optim.Adam refreshes the low-precision modes' bf16 weight image in its own pass
+# (SAVQA_ADAM_SHADOW=0: leave it to the forward's cast, for A/B runs)
+ADAM_SHADOW = os.environ.get("SAVQA_ADAM_SHADOW", "1") != "0"
 
 
 class Adam(torch.optim.Optimizer):
@@ -53,12 +59,17 @@ class Adam(torch.optim.Optimizer):
             ranges = works + self._coverage_gaps(reducer, works, a.n_live)
         rows = self._row_tables(reducer if active else None)
         lr, eps = grp["lr"], grp["eps"]
+        # the low-precision modes' bf16 weight image (engine.LpShadow over [0, n_live)), written
+        # by the same pass when it is current: its refresh then skips the cast of the arena
+        sh = getattr(a, "lp_shadow", None) if ADAM_SHADOW else None
+        shbuf = sh.buf if sh is not None and sh.current() else None
         for w, lo, hi in ranges:
             if w is not None:
                 w.wait()   # this stream waits for this bucket's all-reduce only
             for plo, phi in self._dense_pieces(lo, hi, rows):
                 ops.adam(a.flat[plo:phi], g[plo:phi], self.m[plo:phi], self.v[plo:phi], phi - plo,
-                         lr, b1, b2, eps, bc1, bc2, scale)
+                         lr, b1, b2, eps, bc1, bc2, scale,
+                         shadow=None if shbuf is None else shbuf[plo:phi])
         # row-tracked tables last: every bucket covering them has been waited for by now
         for n in rows:
             o, shp = a.offsets[n]
@@ -69,6 +80,8 @@ class Adam(torch.optim.Optimizer):
             if n not in rows:
                 a.mark_all_rows(n)  # updated densely: every row may hold Adam state now
         a.generation += 1  # low-precision weight shadows are stale now
+        if shbuf is not None:
+            sh.arena_updated()  # ... except the bf16 image of the arena, written above
         return loss
 
     def _row_tables(self, reducer):

@@ -93,3 +93,33 @@ def test_lowp_long_syb_sequence_runs_key_tiled(prec):
     assert _rel(clp, c32) < bar and _rel(slp, s32) < bar
     assert abs(llp - l32) < bar * abs(l32)
     assert float((glp - g32).norm() / g32.norm()) < 5 * bar
+
+
+def test_adam_writes_the_bf16_shadow_bit_exactly():
+    """optim.Adam writes the bf16 weight image in its update pass (savqa_adam_shadow) and the
+    next forward skips the cast of the arena: the image must equal a fresh round-to-nearest
+    cast of every live non-table parameter after each of three steps."""
+    from savqa_amd.data import model_args, synthetic_batch
+    from savqa_amd.loss import smoothed_loss
+    from savqa_amd.optim import Adam
+    b = synthetic_batch(4, Nv=36, Lq=14, Ns=59, topN=5, num_classes=60, seed=9, device=dev)
+    m = _model("bf16", seed=4)
+    m.train()
+    opt = Adam(m, lr=1e-3)
+    a = m._arena
+    for it in range(3):
+        lc, lv, ls, mil, _ = m(*model_args(b), decMask=True, mcb=False)
+        sh = m._engine._shadow
+        assert sh.buf_key == a.state_key()
+        loss, _ = smoothed_loss(lc, lv, ls, b["answer"], mil)
+        opt.zero_grad()
+        loss.backward()
+        assert sh.current()
+        opt.step()
+        assert sh.buf_key == a.state_key(), "the step did not write the shadow"
+        want = a.flat[:a.n_live].to(torch.bfloat16)
+        lo = 0
+        for t0, t1 in a.table_ranges() + [(a.n_live, a.n_live)]:
+            if t0 > lo:
+                assert torch.equal(sh.buf[lo:t0], want[lo:t0]), (it, lo, t0)
+            lo = max(lo, t1)
