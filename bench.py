@@ -259,6 +259,36 @@ def committed_traffic(variant, workload="cfg2"):
         return None
 
 
+def _self_launch(n):
+    """Run this command as `python -m torch.distributed.run --nproc-per-node n` (rendezvous on
+    127.0.0.1, a free port) in a child process and return its exit status. Called before any
+    HIP call, so the parent never holds a GPU context while its ranks run."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+def _rank_devices(dev, backend):
+    """(rank, local device index, PCI bus, uuid) of every rank, gathered over the group."""
+    p = torch.cuda.get_device_properties(dev)
+    me = {"rank": dist.get_rank() if dist.is_initialized() else 0, "device": dev.index,
+          "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+          "uuid": str(getattr(p, "uuid", ""))}
+    if not dist.is_initialized():
+        return [me]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, me)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -279,7 +309,16 @@ def main():
                     help="run both stacks on one stream (per-kernel profiling)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launcher-less form (`python bench.py --gpus N`): start the N ranks here, before
+        # anything touches the GPU, as a torch.distributed.run child (the driver's own
+        # launch line), and exit with its status -- one rank per GPU, main:517's mp.spawn role
+        return _self_launch(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} "
+              f"ranks", file=sys.stderr, flush=True)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("SAVQA_DIST_BACKEND", "nccl") != "nccl":  # rehearsal: ranks share GPUs
@@ -291,6 +330,10 @@ def main():
         # N>1 code path with several ranks on one GPU (RCCL refuses duplicate devices)
         backend = os.environ.get("SAVQA_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus "
+                  f"{args.gpus}", file=sys.stderr, flush=True)
+            return 2
 
     import savqa_amd  # noqa: F401
     from savqa_amd import ops
@@ -364,6 +407,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     final_loss = float(loss)
+    backend = dist.get_backend() if dist.is_initialized() else None
+    dist_info = {"backend": ("rccl" if backend == "nccl" else backend),
+                 "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+                 "ranks": _rank_devices(dev, backend)}
 
     value = world * B * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
@@ -433,13 +480,15 @@ def main():
             "model_tflops": round(value * fl / 1e12, 2),
             "model_mfma_frac": round(value * fl / 1e12 / (peak * world), 4),
             "loss": round(final_loss, 4),
+            "dist": dist_info,
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -78,9 +78,18 @@ typedef struct savqa_gemm_desc {
     float alpha, beta;
     int32_t relu, atomic, split_k, _pad2;
     float* colsum_a;   /* optional, a_trans=1 only: colsum_a[m] += sum_k A(m,k) (bias grad) */
+    float* ws; int64_t ws_elems;  /* optional split-K / tail-split workspace (fp32 elements,
+                          >= savqa_gemm_ws_elems(d)): the 128x128 fp32 / x6 kernels then store
+                          each K slice's partial tile (and its column sums) with plain stores
+                          and add the slices in a fixed order in a second pass -- results no
+                          longer depend on the order atomics land in, i.e. run to run
+                          deterministic (a c_rows scatter keeps its atomics) */
 } savqa_gemm_desc;
 
 int savqa_gemm(void* stream, const savqa_gemm_desc* d);
+/* fp32 elements of workspace *d's launch would use for split-K / tail-split slabs (0: the plan
+ * has no K split, or its epilogue cannot take slabs: c_rows scatter, row map, relu, mask) */
+int64_t savqa_gemm_ws_elems(const savqa_gemm_desc* d);
 
 /* The launch plan savqa_gemm would use for *d (no launch): out[0] = tile (16 / 32: skinny
  * kernels, 128), out[1] = split-K factor, out[2] = tail split factor (0: none),

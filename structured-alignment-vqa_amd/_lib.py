@@ -37,6 +37,7 @@ class GemmDesc(C.Structure):
         ("alpha", c_f), ("beta", c_f),
         ("relu", c_i32), ("atomic", c_i32), ("split_k", c_i32), ("_pad2", c_i32),
         ("colsum_a", c_p),
+        ("ws", c_p), ("ws_elems", c_i64),
     ]
 
 
@@ -80,6 +81,7 @@ _SIGS = {
     "savqa_struct_sizes": [c_p, c_i32],
     "savqa_gemm": [c_p, C.POINTER(GemmDesc)],
     "savqa_gemm_plan": [C.POINTER(GemmDesc), c_p],
+    "savqa_gemm_ws_elems": [C.POINTER(GemmDesc)],
     "savqa_colsum_acc": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
     "savqa_gemm_lp": [c_p, C.POINTER(GemmLpDesc)],
     "savqa_gemm_lp_supported": [C.POINTER(GemmLpDesc)],
@@ -152,7 +154,7 @@ _SIGS = {
     "savqa_adam_shadow": [c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_f, c_f, c_p],
 }
 
-_I64_RET = {"savqa_ln_bwd_workspace_bytes"}
+_I64_RET = {"savqa_ln_bwd_workspace_bytes", "savqa_gemm_ws_elems"}
 
 _lib = None
 

@@ -348,7 +348,7 @@ __device__ __forceinline__ void gemm_mainloop(
 // LDS rows and one thread per column sums them (LDS float atomics serialise: ~us per block)
 template <int PER, int ITERS, int BM>
 __device__ __forceinline__ void cs_fold(const f4 (&cs)[ITERS], float* smem, int64_t m0,
-                                        const savqa_gemm_desc& d) {
+                                        const savqa_gemm_desc& d, float* slab_cs) {
   static_assert(GEMM_NT % PER == 0 && 4 * PER == BM, "colsum layout");
   constexpr int ROWS = GEMM_NT / PER;
   f4 t = cs[0];
@@ -361,7 +361,10 @@ __device__ __forceinline__ void cs_fold(const f4 (&cs)[ITERS], float* smem, int6
     float v = 0.f;
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) v += smem[r * BM + i];
-    if (m0 + i < d.M) atomicAdd(&d.colsum_a[m0 + i], v);
+    if (m0 + i < d.M) {
+      if (slab_cs) slab_cs[m0 + i] = v;  // slab mode: this slice's row of column sums
+      else atomicAdd(&d.colsum_a[m0 + i], v);
+    }
   }
 }
 
@@ -376,24 +379,26 @@ __global__ __launch_bounds__(GEMM_NT, GEMM_OCC) __attribute__((amdgpu_waves_per_
   const int wm = wave >> 1, wn = wave & 1;
 
   const int bid = blockIdx.x;
-  int t;
+  int t, slice;
   int64_t kbeg, kend;
   bool first_split, atomic;
-  if (bid < gg.full) {
-    int slice;  // (split launches have no tail: grid.x == gg.full)
+  float* slab = nullptr;  // slab mode (GemmGrid): this block's partial-tile slab
+  if (bid < gg.full) {    // (split launches have no tail: grid.x == gg.full)
     split_remap(gg.full, t, slice);
     kbeg = (int64_t)slice * gg.kchunk;
     kend = min(d.K, kbeg + gg.kchunk);
     first_split = slice == 0;
     atomic = d.atomic || gridDim.y > 1;
+    if (gg.slab && gridDim.y > 1) slab = gg.slab + slice * gg.slab_stride;
   } else {
     const int u = bid - gg.full;
-    const int part = u % gg.tail_f;
+    slice = u % gg.tail_f;
     t = gg.tail_t0 + u / gg.tail_f;
-    kbeg = (int64_t)part * gg.tail_kchunk;
+    kbeg = (int64_t)slice * gg.tail_kchunk;
     kend = min(d.K, kbeg + gg.tail_kchunk);
-    first_split = part == 0;
+    first_split = slice == 0;
     atomic = true;
+    if (gg.slab) slab = gg.slab + slice * gg.slab_stride;
   }
   const int tn = t % gg.tiles_n;
   const int tm = t / gg.tiles_n;
@@ -428,13 +433,15 @@ __global__ __launch_bounds__(GEMM_NT, GEMM_OCC) __attribute__((amdgpu_waves_per_
   }
   if constexpr (AT) {
     if (do_cs) {  // block-uniform; smem is free after the main loop's last barrier
-      cs_fold<G::OA::PER, G::OA::ITERS, BM>(cs, smem, m0, d);
+      cs_fold<G::OA::PER, G::OA::ITERS, BM>(cs, smem, m0, d,
+                                            gg.slab_cs ? gg.slab_cs + slice * d.M : nullptr);
     }
   }
 
   // ---------------------------------------------------------------- epilogue
   static_assert(MI::FR == 16 && MI::NACC == 4, "16x16 accumulator layout");
-  gemm_epilogue16<FM, FN, WM, WN>(d, acc, m0, n0, wm, wn, lane, first_split, atomic);
+  gemm_epilogue16<FM, FN, WM, WN>(d, acc, m0, n0, wm, wn, lane, first_split, atomic, slab,
+                                  gg.slab_r0);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -806,7 +813,45 @@ struct GemmPlan {
   GemmGrid gg;
   int grid_x, nsplit;
   int64_t zero_row0;  // >= 0: rows [zero_row0, M) of C are zero-filled before the launch
+  int64_t ws_need;    // slab mode: workspace floats (0: the plan does not split K / cannot)
 };
+
+// Slab mode's second pass (savqa_gemm_desc.ws): rows [r0, rows) of C get the sum of the ns
+// partial slabs in slice order -- added to C (split-K: the atomic "C +=" semantics) or
+// assigned (tail split: those rows are written by the tail blocks only) -- and colsum_a the
+// ns rows of per-slice column sums. Four columns per thread when rows are 16-B vectors.
+__global__ __launch_bounds__(256) void gemm_slab_reduce_kernel(
+    float* __restrict__ C, int64_t ldc, const float* __restrict__ slab, int ns, int64_t stride,
+    int64_t r0, int64_t rows, int64_t N, int accumulate, int vec, float* __restrict__ colsum,
+    const float* __restrict__ slab_cs, int64_t M) {
+  const int64_t nr = rows - r0;
+  const int64_t per = vec ? N / 4 : N;
+  const int64_t total = nr * per;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < total;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = u / per, c = u - r * per;
+    if (vec) {
+      const float* sp = slab + r * N + 4 * c;
+      f4 v = *reinterpret_cast<const f4*>(sp);
+      for (int s = 1; s < ns; ++s) v += *reinterpret_cast<const f4*>(sp + s * stride);
+      f4* cp = reinterpret_cast<f4*>(C + (r0 + r) * ldc + 4 * c);
+      *cp = accumulate ? *cp + v : v;
+    } else {
+      const float* sp = slab + r * N + c;
+      float v = *sp;
+      for (int s = 1; s < ns; ++s) v += sp[s * stride];
+      float* cp = C + (r0 + r) * ldc + c;
+      *cp = accumulate ? *cp + v : v;
+    }
+  }
+  if (colsum && blockIdx.x == 0) {
+    for (int64_t m = threadIdx.x; m < M; m += blockDim.x) {
+      float v = slab_cs[m];
+      for (int s = 1; s < ns; ++s) v += slab_cs[s * M + m];
+      colsum[m] += v;
+    }
+  }
+}
 
 }  // namespace savqa
 
@@ -932,6 +977,28 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
       }
     }
   }
+  // slab mode: the partials of a K split go to the caller's workspace and are summed in a
+  // fixed order (fp32 / x6 kernels; identity row map and a linear epilogue; the x6 kernel's
+  // fallback to fp32 for unaligned operands keeps the same plan)
+  const bool slab_ok = (d.prec == 0 || d.prec == 6) && ident && !d.relu && !d.mask &&
+                       !d.rowscale && d.beta == 0.f;
+  p.ws_need = 0;
+  if (slab_ok && p.nsplit > 1 && d.atomic)
+    p.ws_need = (int64_t)p.nsplit * d.M * d.N + (d.colsum_a ? (int64_t)p.nsplit * d.M : 0);
+  else if (slab_ok && p.gg.tail_f > 1)
+    p.ws_need = (int64_t)p.gg.tail_f * (d.M - p.zero_row0) * d.N;
+  if (p.ws_need > 0 && d.ws && d.ws_elems >= p.ws_need) {
+    p.gg.slab = d.ws;
+    if (p.nsplit > 1) {
+      p.gg.slab_stride = d.M * d.N;
+      p.gg.slab_r0 = 0;
+      p.gg.slab_cs = d.colsum_a ? d.ws + (int64_t)p.nsplit * d.M * d.N : nullptr;
+    } else {
+      p.gg.slab_r0 = p.zero_row0;
+      p.gg.slab_stride = (d.M - p.zero_row0) * d.N;
+      p.zero_row0 = -1;  // the reduce pass assigns the tail rows: no zero fill
+    }
+  }
   return 0;
 }
 
@@ -964,6 +1031,19 @@ extern "C" int savqa_gemm_plan(const savqa_gemm_desc* dp, int32_t* out) {
   return 0;
 }
 
+extern "C" int64_t savqa_gemm_ws_elems(const savqa_gemm_desc* dp) {
+  if (!dp) return fail(SAVQA_EINVAL, "savqa_gemm_ws_elems: null descriptor");
+  savqa_gemm_desc d = *dp;
+  GemmPlan p{};
+  if (int rc = plan_gemm(d, p)) return rc;
+  const bool vecs = (d.lda % 4 == 0) && aligned16(d.A) && (d.ldb % 4 == 0) && aligned16(d.B);
+  if (p.tile == 128 && d.prec == 6 && !vecs) {  // savqa_gemm's fallback to the fp32 kernel
+    d.prec = 0;
+    if (int rc = plan_gemm(d, p)) return rc;
+  }
+  return p.ws_need;
+}
+
 extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   if (!dp) return fail(SAVQA_EINVAL, "savqa_gemm: null descriptor");
   savqa_gemm_desc d = *dp;
@@ -990,6 +1070,20 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
     savqa_launch_gemm_bf16(d, p.gg, p.grid_x, p.nsplit, s, avec, bvec);
   } else if (p.tile == 128) {
     dispatch_layout<128, 128, GEMM_BK>(d, p, s, avec, bvec);
+  }
+  if (p.tile == 128 && p.gg.slab) {  // slab mode: add the slices in order
+    const bool split = p.nsplit > 1;
+    const int64_t r0 = p.gg.slab_r0;
+    const int ns = split ? p.nsplit : p.gg.tail_f;
+    const int vec = (d.N % 4 == 0) && (d.ldc % 4 == 0) && aligned16(d.C);
+    const int64_t work = (d.M - r0) * (vec ? d.N / 4 : d.N);
+    const int blocks = (int)std::min<int64_t>(std::max<int64_t>((work + 255) / 256, 1),
+                                              (int64_t)cu_count() * 8);
+    hipLaunchKernelGGL(gemm_slab_reduce_kernel, dim3(blocks), dim3(256), 0, s, d.C, d.ldc,
+                       p.gg.slab, ns, p.gg.slab_stride, r0, d.M, d.N, split ? 1 : 0, vec,
+                       split ? d.colsum_a : nullptr, p.gg.slab_cs, d.M);
+  }
+  if (p.tile == 128) {
   } else if (p.tile == 16) {
     const int tn = p.gg.tiles_n;
     const dim3 g(p.grid_x), b(64 * SK_WAVES);

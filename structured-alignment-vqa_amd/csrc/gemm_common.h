@@ -14,9 +14,16 @@ constexpr int GEMM_NT = 256;
 // Block -> (tile, k range). Blocks [0, full) own whole tiles (or split-K slices along
 // blockIdx.y); blocks [full, gridDim.x) are the "tail": tiles [tail_t0, T) each cut into
 // tail_f k-slices so the last partial wave of tiles spreads over every CU.
+// Slab mode (savqa_gemm_desc.ws; gemm_f32_kernel / gemm_x6_kernel): split-K slice s stores its
+// partial tile to slab + s * slab_stride, a tail block of part p to slab + p * slab_stride,
+// as rows m - slab_r0 of N floats (plain stores), and slice s's column sums (colsum_a) to
+// slab_cs + s * M; gemm_slab_reduce_kernel then adds them in slice order.
 struct GemmGrid {
   int tiles_n, full, tail_t0, tail_f;
   int64_t kchunk, tail_kchunk;
+  float* slab;
+  float* slab_cs;
+  int64_t slab_stride, slab_r0;
 };
 
 // Epilogue of one output element (include/savqa.h formula), split per row / element.
@@ -81,10 +88,13 @@ __device__ __forceinline__ void epi_store(const savqa_gemm_desc& d, const EpiRow
 // ReLU-backward mask, residual) serialised a memory round trip per element.
 //   bias: FN values per lane and the mask bits (rows indexed by m) per fragment row, the
 //   residual per 16-row fragment (a whole tile's would spill).
+// slab != nullptr: the partial of this K slice goes to slab[(m - slab_r0) * N + n] with a
+// plain store (identity row map, linear epilogue: host-checked).
 template <int FM, int FN, int WM, int WN>
 __device__ __forceinline__ void gemm_epilogue16(const savqa_gemm_desc& d, const f4 (&acc)[FM][FN],
                                                 int64_t m0, int64_t n0, int wm, int wn, int lane,
-                                                bool first_split, bool atomic) {
+                                                bool first_split, bool atomic,
+                                                float* slab = nullptr, int64_t slab_r0 = 0) {
   constexpr int FR = 16, NACC = 4;
   auto row = [&](int r) { return 4 * (lane >> 4) + r; };
   const int col = lane & 15;
@@ -146,6 +156,10 @@ __device__ __forceinline__ void gemm_epilogue16(const savqa_gemm_desc& d, const 
                                 : !(d.mask[er.mr * d.ldmask + n] > 0.f)))
           v = 0.f;
         v += rv[r][j];
+        if (slab) {
+          slab[(m - slab_r0) * d.N + n] = v;
+          continue;
+        }
         float* cp = er.crow + n;
         if (atomic) atomicAdd(cp, v);
         else if (d.beta != 0.f) *cp = v + d.beta * *cp;

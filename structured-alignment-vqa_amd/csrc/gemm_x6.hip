@@ -14,6 +14,12 @@
 // accumulation is fp32 -- the accuracy of an fp32 GEMM (tests/test_kernels_gpu.py holds it to
 // the native fp32 kernel's error against fp64 on every cfg-2 step shape) at 6/16 of the fp32
 // MFMA's cycles per product.
+// Range: an infinite operand gives a0 = +-inf and a1 = a2 = 0, so its products are +-inf (NaN
+// for inf * 0) as in fp32. Finite |x| > 3.3895e38 (the largest bf16) rounds to a0 = +-inf too:
+// x6 then returns +-inf where an fp32 GEMM may still be finite (|x * b| < FLT_MAX), the only
+// finite inputs it does not reproduce. At the small end a1 / a2 of |x| < 2^-110 fall below
+// the fp32 / bf16 normal range (tests/test_kernels_gpu.py holds such operands to the native
+// kernel's error too).
 //
 // Tiling: 256 threads = 4 waves (2x2), 128x128 outputs, k-tile 32; each wave owns 64x64 =
 // 4x4 fragments of 16x16. Operand tiles are register-staged (float4 global loads issued one
@@ -68,7 +74,11 @@ __device__ __forceinline__ void split3(f4 v, bf16x4& p0, bf16x4& p1, bf16x4& p2)
   for (int h = 0; h < 2; ++h) {
     const float x = v[2 * h], y = v[2 * h + 1];
     t0[h] = pk_bf16(x, y);
-    const float rx = x - pk_lo(t0[h]), ry = y - pk_hi(t0[h]);
+    // a0 = +-inf (x infinite, or finite beyond the bf16 range and rounded up to inf): a1 = a2
+    // = 0, so a product stays +-inf (x - a0 would be NaN / -inf and the sum NaN)
+    const float x0 = pk_lo(t0[h]), y0 = pk_hi(t0[h]);
+    const float rx = __builtin_isinf(x0) ? 0.f : x - x0;
+    const float ry = __builtin_isinf(y0) ? 0.f : y - y0;
     t1[h] = pk_bf16(rx, ry);
     const float sx = rx - pk_lo(t1[h]), sy = ry - pk_hi(t1[h]);
     t2[h] = pk_bf16(sx, sy);
@@ -307,24 +317,26 @@ __global__ __launch_bounds__(GEMM_NT, X6_OCC) void gemm_x6_kernel(savqa_gemm_des
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int bid = blockIdx.x;
-  int t;
+  int t, slice;
   int64_t kbeg, kend;
   bool first_split, atomic;
-  if (bid < gg.full) {
-    int slice;  // (split launches have no tail: grid.x == gg.full)
+  float* slab = nullptr;  // slab mode: this block's partial-tile slab
+  if (bid < gg.full) {    // (split launches have no tail: grid.x == gg.full)
     split_remap(gg.full, t, slice);
     kbeg = (int64_t)slice * gg.kchunk;
     kend = min(d.K, kbeg + gg.kchunk);
     first_split = slice == 0;
     atomic = d.atomic || gridDim.y > 1;
+    if (gg.slab && gridDim.y > 1) slab = gg.slab + slice * gg.slab_stride;
   } else {
     const int u = bid - gg.full;
-    const int part = u % gg.tail_f;
+    slice = u % gg.tail_f;
     t = gg.tail_t0 + u / gg.tail_f;
-    kbeg = (int64_t)part * gg.tail_kchunk;
+    kbeg = (int64_t)slice * gg.tail_kchunk;
     kend = min(d.K, kbeg + gg.tail_kchunk);
-    first_split = part == 0;
+    first_split = slice == 0;
     atomic = true;
+    if (gg.slab) slab = gg.slab + slice * gg.slab_stride;
   }
   const int tn = t % gg.tiles_n, tm = t / gg.tiles_n;
   const int64_t m0 = (int64_t)tm * X6_TILE, n0 = (int64_t)tn * X6_TILE;
@@ -357,11 +369,15 @@ __global__ __launch_bounds__(GEMM_NT, X6_OCC) void gemm_x6_kernel(savqa_gemm_des
         float v = 0.f;
 #pragma unroll
         for (int r = 0; r < 8; ++r) v += red[r * X6_TILE + i];
-        if (m0 + i < d.M) atomicAdd(&d.colsum_a[m0 + i], v);
+        if (m0 + i < d.M) {
+          if (gg.slab_cs) gg.slab_cs[slice * d.M + m0 + i] = v;
+          else atomicAdd(&d.colsum_a[m0 + i], v);
+        }
       }
     }
   }
-  gemm_epilogue16<4, 4, 64, 64>(d, acc, m0, n0, wm, wn, lane, first_split, atomic);
+  gemm_epilogue16<4, 4, 64, 64>(d, acc, m0, n0, wm, wn, lane, first_split, atomic, slab,
+                                gg.slab_r0);
 }
 
 }  // namespace savqa

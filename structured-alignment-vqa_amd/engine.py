@@ -24,7 +24,7 @@ from __future__ import annotations
 
 import math
 import os
-import sys
+import weakref
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -178,20 +178,50 @@ HEAD_SITES = {"cls": 6, "cls_vis": 7, "cls_syb": 8}  # Dropout(inplace) in the h
 
 # Persistent Q|V buffers of the pruned encoder layers 0-1 (PRUNE_L01): the gathered GEMM
 # writes the question rows only, the node rows must read as zeros (finite Q / V: their weights
-# are exactly 0 and 0 * NaN would not be), and they stay zero across steps -- so the buffer is
-# zero-filled once instead of a 38-76 MB torch.zeros per layer per step. A buffer still held
-# by an earlier forward's saved state (no backward yet: two forwards in flight) is not reused.
-_QV_BUFS: Dict[tuple, torch.Tensor] = {}
+# are exactly 0 and 0 * NaN would not be) -- so a buffer is zero-filled when it is created or
+# its row layout (B, Nn, Lq) changes, instead of a 38-76 MB torch.zeros per layer per step.
+# The slots live in the layer's own weight dict (they die with the model) and at most
+# _QV_SLOTS are kept per layer. A slot is in use from the forward that fills it until the
+# backward that reads it (`_release_qv`) or until that forward's saved state is freed
+# without a backward (weakref), so two forwards in flight never share one.
+_QV_SLOTS = 2
 
 
-def _zeroed_qv(key, M: int, width: int, dev) -> torch.Tensor:
-    k = key + (M, width, str(dev))
-    buf = _QV_BUFS.get(k)
-    # references when free: the dict, `buf`, getrefcount's argument
-    if buf is None or sys.getrefcount(buf) > 3:
-        buf = torch.zeros(M, width, device=dev)
-        _QV_BUFS[k] = buf
-    return buf
+class _QvSlot:
+    __slots__ = ("buf", "layout", "owner")
+
+    def __init__(self, buf, layout):
+        self.buf, self.layout, self.owner = buf, layout, None
+
+    def free(self) -> bool:
+        return self.owner is None or self.owner() is None
+
+
+def _zeroed_qv(L: dict, saved, layout: tuple, M: int, width: int, dev):
+    """(buffer, slot) for one pruned layer; node rows of the buffer read as exact zeros."""
+    slots = L.setdefault("_qv", [])
+    free = [sl for sl in slots if sl.free() and sl.buf.shape == (M, width)
+            and sl.buf.device == dev]
+    slot = next((sl for sl in free if sl.layout == layout), None)
+    if slot is None and free:       # same size, other row layout: stale question rows
+        slot = free[0]
+        slot.buf.zero_()
+        slot.layout = layout
+    if slot is None:
+        slot = _QvSlot(torch.zeros(M, width, device=dev), layout)
+        stale = [sl for sl in slots if sl.free()]
+        if len(slots) >= _QV_SLOTS and stale:
+            slots.remove(stale[0])   # another shape: drop the oldest free slot
+        if len(slots) < _QV_SLOTS:
+            slots.append(slot)
+    slot.owner = weakref.ref(saved)
+    return slot.buf, slot
+
+
+def _release_qv(e: dict) -> None:
+    slot = e.pop("qv_slot", None)
+    if slot is not None:
+        slot.owner = None
 
 
 def _ln_stats(rows, dev):
@@ -262,7 +292,7 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
         if lp is None and i < 2 and Nn > 0 and PRUNE_L01:
             kb = _empty(M, d, dev=dev)
             ops.linear(x, L["Wqkv"][d:2 * d], L["bqkv"][d:2 * d], kb, relu=True)
-            qv = _zeroed_qv((L["Wqkv"].data_ptr(),), M, 2 * d, dev)
+            qv, qv_slot = _zeroed_qv(L, s, (B, Nn, Lq), M, 2 * d, dev)
             bqv = torch.cat((L["bqkv"][:d], L["bqkv"][2 * d:]))
             ops.gemm(x, L["Wqkv"], qv, B * Lq, 2 * d, d, lda=d, ldb=d, ldc=2 * d, b_trans=True,
                      a_rows=s.qrows, b_rows=_qv_wrows(d, dev), bias=bqv, relu=True, c_group=Lq,
@@ -275,7 +305,7 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
             else:
                 ops.gattn_fwd(qv, 2 * d, kb, d, qv[:, d:], 2 * d, G, flag, flag, B, T, T, H, o, d)
             qkv = None
-            e.update(qv=qv, kb=kb)
+            e.update(qv=qv, kb=kb, qv_slot=qv_slot)
         elif lp is not None:
             Lb = lp.W.enc[i]
             qkv = _bf(M, 3 * d, dev=dev)
@@ -499,6 +529,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
                      a_rows=s.qrows, b_rows=_qv_wrows(d, dev), c_group=Lq, c_stride=T,
                      c_offset=Nn, beta=1.0)
             del dqv, dk
+            _release_qv(e)   # the last read of the buffer is queued: the next forward may fill it
             dx = dxn
             if i > 0:
                 mark(f"enc_feed_forward_{i - 1}.normalization.gamma")

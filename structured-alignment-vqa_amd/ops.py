@@ -91,6 +91,9 @@ _probe = None
 # exact three-term bf16 splits, six products per pair (gemm_x6.hip; the engine's fp32 mode). Set per model (AttModel(...,
 # gemm_precision="bf16x3")) via gemm_precision(); the bf16 / fp8 modes use gemm_lp instead.
 PREC = {"fp32": 0, "fp32_native": 0, "bf16x3": 3, "fp32x6": 6}
+# fp32 / x6 K splits (split-K weight gradients, tail splits) through partial slabs summed in a
+# fixed order (savqa_gemm_desc.ws) instead of fp32 atomics: run-to-run deterministic
+GEMM_SLABS = os.environ.get("SAVQA_GEMM_SLABS", "1") != "0"
 _prec = 0
 class gemm_precision:
     """Context manager: GEMMs launched inside use the given product precision."""
@@ -177,6 +180,12 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
         plan = (C.c_int32 * 4)()
         call("savqa_gemm_plan", C.byref(d), C.cast(plan, C.c_void_p))
         return list(plan)
+    if GEMM_SLABS and d.prec != 3 and not (relu or mask is not None or rowscale is not None
+                                            or beta != 0.0 or c_rows is not None):
+        need = int(_lib.load().savqa_gemm_ws_elems(C.byref(d)))
+        if need > 0:
+            ws = _workspace(need, Cm.device)
+            d.ws, d.ws_elems = _p(ws), int(ws.numel())
     if _probe is None:
         call("savqa_gemm", _stream(), C.byref(d))
         return
@@ -225,24 +234,29 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
     return d
 
 
-_lp_ws = {}
+_ws = {}
 LP_SLABS = os.environ.get("SAVQA_LP_SLABS", "1") != "0"  # cfg 3: 17.86k -> 18.32k QA-samples/s
 
 
+def _workspace(need: int, dev) -> Tensor:
+    """The split-K slab workspace of the current (device, stream), grown to `need` fp32
+    elements: GEMMs on one stream run in order, so one buffer serves all of them."""
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), _stream())
+    ws = _ws.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.float32, device=dev)
+        _ws[key] = ws
+    return ws
+
+
 def lp_workspace(d, dev) -> Optional[Tensor]:
-    """The split-K slab workspace a savqa_gemm_lp launch of d needs (slices x M x N fp32), one
-    per (device, stream), grown as needed (None when d does not split K)."""
+    """The split-K slab workspace a savqa_gemm_lp launch of d needs (slices x M x N fp32)
+    (None when d does not split K)."""
     plan = (C.c_int32 * 4)()
     call("savqa_gemm_lp_plan", C.byref(d), C.cast(plan, C.c_void_p))
     if plan[1] <= 1:
         return None
-    need = int(plan[1]) * int(d.M) * int(d.N)
-    key = (dev.index if dev.index is not None else torch.cuda.current_device(), _stream())
-    ws = _lp_ws.get(key)
-    if ws is None or ws.numel() < need:
-        ws = torch.empty(need, dtype=torch.float32, device=dev)
-        _lp_ws[key] = ws
-    return ws
+    return _workspace(int(plan[1]) * int(d.M) * int(d.N), dev)
 
 
 def lp_variant(d) -> str:

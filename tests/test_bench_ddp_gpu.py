@@ -42,3 +42,23 @@ def test_bench_two_ranks_gloo_rehearsal(workload):
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 64
     assert d["value"] > 0 and d["ms_per_step"] > 0
     assert d["loss"] == d["loss"] and abs(d["loss"]) < 1e4   # finite
+
+
+def test_bench_launcherless_form_starts_n_ranks():
+    """`python bench.py --gpus 2` with no launcher starts its own two ranks (a
+    torch.distributed.run child) and reports the process group's world size, not 1."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    env = dict(os.environ, SAVQA_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--batch", "16", "--steps", "2",
+           "--warmup", "1", "--no-cpu-baseline", "--no-roofline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 32
+    assert d["dist"]["world_size"] == 2 and d["dist"]["backend"] == "gloo"
+    assert sorted(x["rank"] for x in d["dist"]["ranks"]) == [0, 1]

@@ -507,9 +507,9 @@ CFG2_SHAPES = [("NT", 18688, 1536, 512), ("NT", 18688, 2048, 512), ("NT", 18688,
 def test_gemm_x6_error_at_most_native(lay, M, N, K):
     """The x6 kernel is an fp32 GEMM: on every cfg-2 step shape (forward NT, dX NN, split-K
     dW TN with the bias-gradient column sums) its max error against fp64 is within 1.25x of
-    the native fp32 MFMA kernel's on the same inputs (measured: at or below it); 1.5x for the
-    split-K TN shapes, whose slices are added by fp32 atomics in a run-dependent order (one
-    suite run measured 1.084e-6 against the native kernel's 8.6e-7 at TN 2048x512x18688)."""
+    the native fp32 MFMA kernel's on the same inputs (measured: at or below it). The split-K
+    slices of both kernels are summed through slabs in a fixed order (ops.GEMM_SLABS), so
+    the comparison no longer depends on the order fp32 atomics land in."""
     O = ops()
     if lay == "NT":
         A, B = g(M, K, seed=90), g(N, K, seed=91)
@@ -531,8 +531,120 @@ def test_gemm_x6_error_at_most_native(lay, M, N, K):
         errs[prec] = float((out.double() - ref).abs().max() / ref.abs().max())
         if cs is not None:
             assert rel(cs, A.double().sum(0)) < 1e-5
-    assert errs[6] <= (1.5 if lay == "TN" else 1.25) * errs[0] + 1e-8, errs
+    assert errs[6] <= 1.25 * errs[0] + 1e-8, errs
     assert errs[6] < 5e-6, errs
+
+
+@pytest.mark.parametrize("prec", [0, 6])
+@pytest.mark.parametrize("case", ["splitk_dw", "tail"])
+def test_gemm_slabs_deterministic(prec, case, monkeypatch):
+    """K splits through partial slabs (savqa_gemm_desc.ws, ops.GEMM_SLABS): the split-K
+    weight gradient (with its fused bias-gradient column sums) and a tail-split forward with a
+    residual are bit-identical run to run, and agree with the atomic form to fp32 rounding."""
+    O = ops()
+    if case == "splitk_dw":
+        M, N, K = 2048, 512, 18688
+        A, B = g(K, M, seed=31), g(K, N, seed=32)
+        kw = dict(lda=M, ldb=N, ldc=N, a_trans=True, atomic=True, split_k=-1)
+        ref = A.double().t() @ B.double()
+    else:
+        M, N, K = 18688, 512, 2048
+        A, B = g(M, K, seed=33), g(N, K, seed=34)
+        R = g(M, N, seed=35)
+        kw = dict(lda=K, ldb=K, ldc=N, b_trans=True, resid=R, ldr=N)
+        ref = A.double() @ B.double().t() + R.double()
+    plan = O.gemm(A, B, None, M, N, K, prec=prec, plan_only=True, **kw)
+    assert plan[0] == 128 and (plan[1] > 1 if case == "splitk_dw" else plan[2] > 1), plan
+
+    def run():
+        out = torch.zeros(M, N, device=dev)
+        cs = torch.zeros(M, device=dev) if case == "splitk_dw" else None
+        O.gemm(A, B, out, M, N, K, prec=prec, colsum_a=cs, **kw)
+        torch.cuda.synchronize()
+        return out, cs
+    outs = [run() for _ in range(3)]
+    for o, c in outs[1:]:
+        assert torch.equal(o, outs[0][0])
+        if c is not None:
+            assert torch.equal(c, outs[0][1])
+    assert rel(outs[0][0], ref) < 2e-6
+    if case == "splitk_dw":
+        assert rel(outs[0][1], A.double().sum(0)) < 1e-5
+    monkeypatch.setattr(O, "GEMM_SLABS", False)
+    atom, _ = run()
+    assert rel(atom, outs[0][0]) < 2e-6
+
+
+def _wide(shape, lo, hi, seed):
+    """sign x 10^U(lo, hi): operands spanning many decades (fp32 normal range)."""
+    gen = torch.Generator().manual_seed(seed)
+    e = torch.empty(shape, dtype=torch.float64).uniform_(lo, hi, generator=gen)
+    s = torch.randint(0, 2, shape, generator=gen).double() * 2 - 1
+    return (s * torch.pow(10.0, e)).float().to(dev)
+
+
+@pytest.mark.parametrize("lay", ["NT", "NN", "TN"])
+@pytest.mark.parametrize("rng", ["wide", "tiny"])
+def test_gemm_x6_wide_dynamic_range(lay, rng):
+    """The exact three-term split over operands far from N(0, 1): 'wide' spans 24 decades
+    (a1 / a2 of the smallest values stay fp32-normal), 'tiny' puts A at 1e-37..1e-33, where
+    a1 / a2 fall below the fp32 / bf16 normal range while every product stays normal. Per
+    element the error against fp64 is measured relative to sum_k |a||b| (the fp32 GEMM's own
+    error scale, meaningful whatever an element's magnitude); x6 within 1.25x of native."""
+    O = ops()
+    M, N, K = (2048, 2048, 1024) if lay != "TN" else (2048, 1024, 4096)
+    alo, ahi, blo, bhi = (-12, 12, -12, 12) if rng == "wide" else (-37, -33, 1, 5)
+    if lay == "NT":
+        A, B = _wide((M, K), alo, ahi, 1), _wide((N, K), blo, bhi, 2)
+        kw = dict(lda=K, ldb=K, ldc=N, b_trans=True)
+        Am, Bm = A.double(), B.double().t()
+    elif lay == "NN":
+        A, B = _wide((M, K), alo, ahi, 3), _wide((K, N), blo, bhi, 4)
+        kw = dict(lda=K, ldb=N, ldc=N)
+        Am, Bm = A.double(), B.double()
+    else:
+        A, B = _wide((K, M), alo, ahi, 5), _wide((K, N), blo, bhi, 6)
+        kw = dict(lda=M, ldb=N, ldc=N, a_trans=True, atomic=True, split_k=-1)
+        Am, Bm = A.double().t(), B.double()
+    ref = Am @ Bm
+    scale = Am.abs() @ Bm.abs()
+    assert O.gemm(A, B, None, M, N, K, prec=6, plan_only=True, **kw)[0] == 128  # x6 kernel
+    errs = {}
+    for prec in (0, 6):
+        out = torch.zeros(M, N, device=dev)
+        O.gemm(A, B, out, M, N, K, prec=prec, **kw)
+        assert bool(torch.isfinite(out).all())
+        errs[prec] = float(((out.double() - ref).abs() / scale).max())
+    assert errs[6] <= 1.25 * errs[0] + 1e-9, errs
+    assert errs[6] < 1e-5, errs
+
+
+def test_gemm_x6_infinite_operands():
+    """+-inf operands: the split keeps a0 = +-inf with a1 = a2 = 0, so x6 returns the same
+    +-inf / NaN pattern as the native fp32 kernel (not NaN from inf - inf), and the finite
+    elements agree."""
+    O = ops()
+    M, N, K = 2048, 2048, 512
+    A, B = g(M, K, seed=61), g(N, K, seed=62)
+    A[3, 7] = float("inf")
+    A[100, 300] = float("-inf")
+    A[200, 10] = float("inf")
+    A[200, 11] = float("-inf")           # row 200: +inf and -inf terms -> NaN
+    B[50, 400] = float("inf")            # column 50: inf in the other operand
+    outs = {}
+    assert O.gemm(A, B, None, M, N, K, lda=K, ldb=K, ldc=N, b_trans=True, prec=6,
+                  plan_only=True)[0] == 128
+    for prec in (0, 6):
+        out = torch.zeros(M, N, device=dev)
+        O.gemm(A, B, out, M, N, K, lda=K, ldb=K, ldc=N, b_trans=True, prec=prec)
+        outs[prec] = out.cpu()
+    n, x = outs[0], outs[6]
+    assert torch.equal(torch.isnan(n), torch.isnan(x))
+    assert torch.equal(torch.isinf(n), torch.isinf(x))
+    assert torch.equal(torch.sign(n[torch.isinf(n)]), torch.sign(x[torch.isinf(x)]))
+    assert bool(torch.isinf(n).any()) and bool(torch.isnan(n).any())
+    fin = torch.isfinite(n)
+    assert rel(x[fin], n[fin]) < 1e-5
 
 
 @pytest.mark.parametrize("gather", ["b", "a", "ab"])
