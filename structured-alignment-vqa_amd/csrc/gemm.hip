@@ -827,8 +827,16 @@ __global__ __launch_bounds__(256) void gemm_slab_reduce_kernel(
   const int64_t nr = rows - r0;
   const int64_t per = vec ? N / 4 : N;
   const int64_t total = nr * per;
-  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < total;
+  const int64_t ncs = colsum ? M : 0;  // column sums: the last ncs work items
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < total + ncs;
        u += (int64_t)gridDim.x * blockDim.x) {
+    if (u >= total) {
+      const int64_t m = u - total;
+      float v = slab_cs[m];
+      for (int s = 1; s < ns; ++s) v += slab_cs[s * M + m];
+      colsum[m] += v;
+      continue;
+    }
     const int64_t r = u / per, c = u - r * per;
     if (vec) {
       const float* sp = slab + r * N + 4 * c;
@@ -842,13 +850,6 @@ __global__ __launch_bounds__(256) void gemm_slab_reduce_kernel(
       for (int s = 1; s < ns; ++s) v += sp[s * stride];
       float* cp = C + (r0 + r) * ldc + c;
       *cp = accumulate ? *cp + v : v;
-    }
-  }
-  if (colsum && blockIdx.x == 0) {
-    for (int64_t m = threadIdx.x; m < M; m += blockDim.x) {
-      float v = slab_cs[m];
-      for (int s = 1; s < ns; ++s) v += slab_cs[s * M + m];
-      colsum[m] += v;
     }
   }
 }
@@ -888,7 +889,19 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
     return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32), 3 (3xbf16) or 6 (fp32 x6)");
   // gemm_bf16_kernel / gemm_x6_kernel k-tile: 32; workgroups per CU the planner counts
   const int BK = d.prec ? 32 : (d.a_trans ? GEMM_BK_DW : GEMM_BK);
-  const int occ = d.prec == 6 ? 2 : GEMM_PLAN_OCC;
+  const bool planes = d.prec == 6 && d.ap && d.bp;  // gemm_x6p_kernel: one workgroup per CU
+  if (planes) {
+    const bool al = ((uintptr_t)d.ap & 15) == 0 && ((uintptr_t)d.bp & 15) == 0;
+    const bool ld8 = d.ldap % 8 == 0 && d.ldbp % 8 == 0 && d.psa % 8 == 0 && d.psb % 8 == 0;
+    const int64_t la = d.a_trans ? (d.M + 7) / 8 * 8 : d.K;
+    const int64_t lb = d.b_trans ? d.K : (d.N + 7) / 8 * 8;
+    if (!al || !ld8 || d.ldap < la || d.ldbp < lb)
+      return fail(SAVQA_EINVAL, "savqa_gemm: plane operands need 16-B alignment, ld / plane "
+                                "stride % 8 == 0 and ld >= the padded row length");
+    if ((d.a_trans && d.a_rows) || (!d.b_trans && d.b_rows))
+      return fail(SAVQA_EUNSUP, "savqa_gemm: plane operands with a k-row gather");
+  }
+  const int occ = planes ? 1 : d.prec == 6 ? 2 : GEMM_PLAN_OCC;
   const int slots = occ * cu_count();
   const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
   int split = d.split_k > 1 ? d.split_k : 1;
@@ -978,10 +991,9 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
     }
   }
   // slab mode: the partials of a K split go to the caller's workspace and are summed in a
-  // fixed order (fp32 / x6 kernels; identity row map and a linear epilogue; the x6 kernel's
-  // fallback to fp32 for unaligned operands keeps the same plan)
-  const bool slab_ok = (d.prec == 0 || d.prec == 6) && ident && !d.relu && !d.mask &&
-                       !d.rowscale && d.beta == 0.f;
+  // fixed order (fp32 / x6 kernels; identity row map and an epilogue linear in the
+  // accumulator -- row scale and ReLU-backward mask included, no ReLU / beta)
+  const bool slab_ok = (d.prec == 0 || d.prec == 6) && ident && !d.relu && d.beta == 0.f;
   p.ws_need = 0;
   if (slab_ok && p.nsplit > 1 && d.atomic)
     p.ws_need = (int64_t)p.nsplit * d.M * d.N + (d.colsum_a ? (int64_t)p.nsplit * d.M : 0);
@@ -1037,7 +1049,7 @@ extern "C" int64_t savqa_gemm_ws_elems(const savqa_gemm_desc* dp) {
   GemmPlan p{};
   if (int rc = plan_gemm(d, p)) return rc;
   const bool vecs = (d.lda % 4 == 0) && aligned16(d.A) && (d.ldb % 4 == 0) && aligned16(d.B);
-  if (p.tile == 128 && d.prec == 6 && !vecs) {  // savqa_gemm's fallback to the fp32 kernel
+  if (p.tile == 128 && d.prec == 6 && !(d.ap && d.bp) && !vecs) {  // savqa_gemm's fp32 fallback
     d.prec = 0;
     if (int rc = plan_gemm(d, p)) return rc;
   }
@@ -1048,13 +1060,16 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   if (!dp) return fail(SAVQA_EINVAL, "savqa_gemm: null descriptor");
   savqa_gemm_desc d = *dp;
   if (d.M == 0 || d.N == 0) return 0;
-  if (!d.A || !d.B || !d.C) return fail(SAVQA_EINVAL, "savqa_gemm: null operand");
+  const bool planes = d.prec == 6 && d.ap && d.bp;
+  if ((!planes && (!d.A || !d.B)) || !d.C) return fail(SAVQA_EINVAL, "savqa_gemm: null operand");
   GemmPlan p{};
   if (int rc = plan_gemm(d, p)) return rc;
+  if (planes && p.tile != 128 && (!d.A || !d.B))
+    return fail(SAVQA_EINVAL, "savqa_gemm: a skinny launch needs the fp32 operands");
   const int avec = (d.lda % 4 == 0) && aligned16(d.A);
   const int bvec = (d.ldb % 4 == 0) && aligned16(d.B);
   hipStream_t s = as_stream(stream);
-  if (p.tile == 128 && d.prec == 6 && (!avec || !bvec)) {
+  if (p.tile == 128 && d.prec == 6 && !planes && (!avec || !bvec)) {
     // operands that are not 16-B vectors (guarded loads only in the x6 kernel) take the fp32
     // kernel
     d.prec = 0;
@@ -1064,7 +1079,9 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
       hipMemset2DAsync(d.C + p.zero_row0 * d.ldc, d.ldc * sizeof(float), 0, d.N * sizeof(float),
                        d.M - p.zero_row0, s) != hipSuccess)
     return fail(SAVQA_EUNSUP, "savqa_gemm: tail zero-fill failed");
-  if (p.tile == 128 && d.prec == 6) {
+  if (p.tile == 128 && planes) {
+    savqa_launch_gemm_x6p(d, p.gg, p.grid_x, p.nsplit, s);
+  } else if (p.tile == 128 && d.prec == 6) {
     savqa_launch_gemm_x6(d, p.gg, p.grid_x, p.nsplit, s);
   } else if (p.tile == 128 && d.prec != 0) {
     savqa_launch_gemm_bf16(d, p.gg, p.grid_x, p.nsplit, s, avec, bvec);
@@ -1076,7 +1093,7 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
     const int64_t r0 = p.gg.slab_r0;
     const int ns = split ? p.nsplit : p.gg.tail_f;
     const int vec = (d.N % 4 == 0) && (d.ldc % 4 == 0) && aligned16(d.C);
-    const int64_t work = (d.M - r0) * (vec ? d.N / 4 : d.N);
+    const int64_t work = (d.M - r0) * (vec ? d.N / 4 : d.N) + (split && d.colsum_a ? d.M : 0);
     const int blocks = (int)std::min<int64_t>(std::max<int64_t>((work + 255) / 256, 1),
                                               (int64_t)cu_count() * 8);
     hipLaunchKernelGGL(gemm_slab_reduce_kernel, dim3(blocks), dim3(256), 0, s, d.C, d.ldc,

@@ -14,12 +14,15 @@
 // accumulation is fp32 -- the accuracy of an fp32 GEMM (tests/test_kernels_gpu.py holds it to
 // the native fp32 kernel's error against fp64 on every cfg-2 step shape) at 6/16 of the fp32
 // MFMA's cycles per product.
-// Range: an infinite operand gives a0 = +-inf and a1 = a2 = 0, so its products are +-inf (NaN
-// for inf * 0) as in fp32. Finite |x| > 3.3895e38 (the largest bf16) rounds to a0 = +-inf too:
-// x6 then returns +-inf where an fp32 GEMM may still be finite (|x * b| < FLT_MAX), the only
-// finite inputs it does not reproduce. At the small end a1 / a2 of |x| < 2^-110 fall below
-// the fp32 / bf16 normal range (tests/test_kernels_gpu.py holds such operands to the native
-// kernel's error too).
+// Range: operands must be finite with |x| <= 3.3895e38 (the largest bf16). An infinite x (or a
+// finite one that rounds to a bf16 infinity) gives a0 = +-inf and x - a0 = NaN, and even with
+// a1 = a2 forced to 0 the other operand's terms would still meet it as inf * b1 with b1 = 0 or
+// of the opposite sign (NaN, where fp32 gives +-inf): x6 cannot reproduce fp32's infinities,
+// so it does not try (a guard would cost 8 VALU per float4 of the split). What it does keep:
+// an output is non-finite exactly where the fp32 GEMM's is (NaN in place of +-inf), so
+// overflow still surfaces (tests/test_kernels_gpu.py::test_gemm_x6_infinite_operands). At the
+// small end a1 / a2 of |x| < 2^-110 fall below the fp32 normal range and stay exact as fp32 /
+// bf16 subnormals (the 'tiny' range test holds such operands to the native kernel's error).
 //
 // Tiling: 256 threads = 4 waves (2x2), 128x128 outputs, k-tile 32; each wave owns 64x64 =
 // 4x4 fragments of 16x16. Operand tiles are register-staged (float4 global loads issued one
@@ -74,11 +77,7 @@ __device__ __forceinline__ void split3(f4 v, bf16x4& p0, bf16x4& p1, bf16x4& p2)
   for (int h = 0; h < 2; ++h) {
     const float x = v[2 * h], y = v[2 * h + 1];
     t0[h] = pk_bf16(x, y);
-    // a0 = +-inf (x infinite, or finite beyond the bf16 range and rounded up to inf): a1 = a2
-    // = 0, so a product stays +-inf (x - a0 would be NaN / -inf and the sum NaN)
-    const float x0 = pk_lo(t0[h]), y0 = pk_hi(t0[h]);
-    const float rx = __builtin_isinf(x0) ? 0.f : x - x0;
-    const float ry = __builtin_isinf(y0) ? 0.f : y - y0;
+    const float rx = x - pk_lo(t0[h]), ry = y - pk_hi(t0[h]);
     t1[h] = pk_bf16(rx, ry);
     const float sx = rx - pk_lo(t1[h]), sy = ry - pk_hi(t1[h]);
     t2[h] = pk_bf16(sx, sy);
@@ -223,7 +222,16 @@ __device__ __forceinline__ f4 mma(bf16x8 a, bf16x8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// one k-tile: acc[i][j] += A_i B_j^T over 32 k, six products per term pair, smallest first
+// one k-tile: acc[i][j] += A_i B_j^T over 32 k, six products per term pair, smallest first.
+// Two-level accumulation (X6_TWO_LEVEL): the six products of a k-tile are summed into a
+// zero-started partial t and t is added to acc once per k-tile, so the running sum takes one
+// rounding per 32 k instead of one per MFMA (six per 32 k; the native kernel: eight). Where one
+// product dominates an output (operands spanning many decades, as real activations do) the
+// single-level form rounded that product's six slices at the big accumulator's ulp: up to
+// 1.5x the native kernel's error (tests/test_kernels_gpu.py::test_gemm_x6_wide_dynamic_range).
+#ifndef SAVQA_X6_TWO_LEVEL
+#define SAVQA_X6_TWO_LEVEL 1
+#endif
 __device__ __forceinline__ void x6_compute(const char* As, const char* Bs, int wm, int wn,
                                            int lane, f4 (&acc)[4][4]) {
   bf16x8 b[4][3];
@@ -236,18 +244,22 @@ __device__ __forceinline__ void x6_compute(const char* As, const char* Bs, int w
     bf16x8 a[3];
 #pragma unroll
     for (int p = 0; p < 3; ++p) a[p] = x6_frag(As + p * X6_PLANE, wm * 64 + 16 * i, lane);
+    f4 t[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[2], b[j][0], acc[i][j]);
+    for (int j = 0; j < 4; ++j)
+      t[j] = mma(a[2], b[j][0], SAVQA_X6_TWO_LEVEL ? f4{0.f, 0.f, 0.f, 0.f} : acc[i][j]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[1], b[j][1], acc[i][j]);
+    for (int j = 0; j < 4; ++j) t[j] = mma(a[1], b[j][1], t[j]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[0], b[j][2], acc[i][j]);
+    for (int j = 0; j < 4; ++j) t[j] = mma(a[0], b[j][2], t[j]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[1], b[j][0], acc[i][j]);
+    for (int j = 0; j < 4; ++j) t[j] = mma(a[1], b[j][0], t[j]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[0], b[j][1], acc[i][j]);
+    for (int j = 0; j < 4; ++j) t[j] = mma(a[0], b[j][1], t[j]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[0], b[j][0], acc[i][j]);
+    for (int j = 0; j < 4; ++j) t[j] = mma(a[0], b[j][0], t[j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = SAVQA_X6_TWO_LEVEL ? acc[i][j] + t[j] : t[j];
   }
 }
 
