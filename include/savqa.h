@@ -84,27 +84,12 @@ typedef struct savqa_gemm_desc {
                           and add the slices in a fixed order in a second pass -- results no
                           longer depend on the order atomics land in, i.e. run to run
                           deterministic (a c_rows scatter / row map keeps its atomics) */
-    /* optional with prec = 6: the operands as three bf16 PLANES each (savqa_split3's layout:
-     * plane q of A at ap + q*psa, A's row r (as indexed above: m, or k when a_trans) at
-     * r*ldap; likewise bp / ldbp / psb), read by LDS-DMA instead of splitting fp32 tiles in
-     * the k-loop (gemm_x6p.hip). A / B may then be null. Needs 16-B aligned planes, ld and
-     * plane strides % 8 == 0, ld >= the padded row length (K, or M / N rounded up to 8 for
-     * the m- / n-contiguous operands), and no k-row gather (a_rows with a_trans, b_rows
-     * without b_trans). */
-    const void* ap; int64_t ldap, psa;
-    const void* bp; int64_t ldbp, psb;
 } savqa_gemm_desc;
 
 int savqa_gemm(void* stream, const savqa_gemm_desc* d);
 /* fp32 elements of workspace *d's launch would use for split-K / tail-split slabs (0: the plan
  * has no K split, or its epilogue cannot take slabs: c_rows scatter, row map, relu, beta) */
 int64_t savqa_gemm_ws_elems(const savqa_gemm_desc* d);
-/* Exact three-term bf16 split of fp32 rows (the x6 product operands): for row r (X row
- * row_map ? row_map[r] : r) and column c < cols, x = p0 + p1 + p2 with p0 = bf16(x),
- * p1 = bf16(x - p0), p2 = x - p0 - p1 (exact); plane q at planes + q*ps (bf16 elements), row r
- * at r*ldp; columns [cols, ldp) are zero. ldp % 8 == 0, ps % 8 == 0, ps >= rows*ldp. */
-int savqa_split3(void* stream, const float* X, int64_t rows, int64_t cols, int64_t ldx,
-                 const int64_t* row_map, void* planes, int64_t ldp, int64_t ps);
 
 /* The launch plan savqa_gemm would use for *d (no launch): out[0] = tile (16 / 32: skinny
  * kernels, 128), out[1] = split-K factor, out[2] = tail split factor (0: none),

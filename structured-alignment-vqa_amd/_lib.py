@@ -38,8 +38,6 @@ class GemmDesc(C.Structure):
         ("relu", c_i32), ("atomic", c_i32), ("split_k", c_i32), ("_pad2", c_i32),
         ("colsum_a", c_p),
         ("ws", c_p), ("ws_elems", c_i64),
-        ("ap", c_p), ("ldap", c_i64), ("psa", c_i64),
-        ("bp", c_p), ("ldbp", c_i64), ("psb", c_i64),
     ]
 
 
@@ -84,7 +82,6 @@ _SIGS = {
     "savqa_gemm": [c_p, C.POINTER(GemmDesc)],
     "savqa_gemm_plan": [C.POINTER(GemmDesc), c_p],
     "savqa_gemm_ws_elems": [C.POINTER(GemmDesc)],
-    "savqa_split3": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_i64],
     "savqa_colsum_acc": [c_p, c_p, c_i64, c_i64, c_i64, c_p],
     "savqa_gemm_lp": [c_p, C.POINTER(GemmLpDesc)],
     "savqa_gemm_lp_supported": [C.POINTER(GemmLpDesc)],

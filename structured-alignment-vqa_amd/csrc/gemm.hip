@@ -889,19 +889,7 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
     return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32), 3 (3xbf16) or 6 (fp32 x6)");
   // gemm_bf16_kernel / gemm_x6_kernel k-tile: 32; workgroups per CU the planner counts
   const int BK = d.prec ? 32 : (d.a_trans ? GEMM_BK_DW : GEMM_BK);
-  const bool planes = d.prec == 6 && d.ap && d.bp;  // gemm_x6p_kernel: one workgroup per CU
-  if (planes) {
-    const bool al = ((uintptr_t)d.ap & 15) == 0 && ((uintptr_t)d.bp & 15) == 0;
-    const bool ld8 = d.ldap % 8 == 0 && d.ldbp % 8 == 0 && d.psa % 8 == 0 && d.psb % 8 == 0;
-    const int64_t la = d.a_trans ? (d.M + 7) / 8 * 8 : d.K;
-    const int64_t lb = d.b_trans ? d.K : (d.N + 7) / 8 * 8;
-    if (!al || !ld8 || d.ldap < la || d.ldbp < lb)
-      return fail(SAVQA_EINVAL, "savqa_gemm: plane operands need 16-B alignment, ld / plane "
-                                "stride % 8 == 0 and ld >= the padded row length");
-    if ((d.a_trans && d.a_rows) || (!d.b_trans && d.b_rows))
-      return fail(SAVQA_EUNSUP, "savqa_gemm: plane operands with a k-row gather");
-  }
-  const int occ = planes ? 1 : d.prec == 6 ? 2 : GEMM_PLAN_OCC;
+  const int occ = d.prec == 6 ? 2 : GEMM_PLAN_OCC;
   const int slots = occ * cu_count();
   const int64_t tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
   int split = d.split_k > 1 ? d.split_k : 1;
@@ -1049,7 +1037,7 @@ extern "C" int64_t savqa_gemm_ws_elems(const savqa_gemm_desc* dp) {
   GemmPlan p{};
   if (int rc = plan_gemm(d, p)) return rc;
   const bool vecs = (d.lda % 4 == 0) && aligned16(d.A) && (d.ldb % 4 == 0) && aligned16(d.B);
-  if (p.tile == 128 && d.prec == 6 && !(d.ap && d.bp) && !vecs) {  // savqa_gemm's fp32 fallback
+  if (p.tile == 128 && d.prec == 6 && !vecs) {  // savqa_gemm's fallback to the fp32 kernel
     d.prec = 0;
     if (int rc = plan_gemm(d, p)) return rc;
   }
@@ -1060,16 +1048,13 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   if (!dp) return fail(SAVQA_EINVAL, "savqa_gemm: null descriptor");
   savqa_gemm_desc d = *dp;
   if (d.M == 0 || d.N == 0) return 0;
-  const bool planes = d.prec == 6 && d.ap && d.bp;
-  if ((!planes && (!d.A || !d.B)) || !d.C) return fail(SAVQA_EINVAL, "savqa_gemm: null operand");
+  if (!d.A || !d.B || !d.C) return fail(SAVQA_EINVAL, "savqa_gemm: null operand");
   GemmPlan p{};
   if (int rc = plan_gemm(d, p)) return rc;
-  if (planes && p.tile != 128 && (!d.A || !d.B))
-    return fail(SAVQA_EINVAL, "savqa_gemm: a skinny launch needs the fp32 operands");
   const int avec = (d.lda % 4 == 0) && aligned16(d.A);
   const int bvec = (d.ldb % 4 == 0) && aligned16(d.B);
   hipStream_t s = as_stream(stream);
-  if (p.tile == 128 && d.prec == 6 && !planes && (!avec || !bvec)) {
+  if (p.tile == 128 && d.prec == 6 && (!avec || !bvec)) {
     // operands that are not 16-B vectors (guarded loads only in the x6 kernel) take the fp32
     // kernel
     d.prec = 0;
@@ -1079,9 +1064,7 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
       hipMemset2DAsync(d.C + p.zero_row0 * d.ldc, d.ldc * sizeof(float), 0, d.N * sizeof(float),
                        d.M - p.zero_row0, s) != hipSuccess)
     return fail(SAVQA_EUNSUP, "savqa_gemm: tail zero-fill failed");
-  if (p.tile == 128 && planes) {
-    savqa_launch_gemm_x6p(d, p.gg, p.grid_x, p.nsplit, s);
-  } else if (p.tile == 128 && d.prec == 6) {
+  if (p.tile == 128 && d.prec == 6) {
     savqa_launch_gemm_x6(d, p.gg, p.grid_x, p.nsplit, s);
   } else if (p.tile == 128 && d.prec != 0) {
     savqa_launch_gemm_bf16(d, p.gg, p.grid_x, p.nsplit, s, avec, bvec);

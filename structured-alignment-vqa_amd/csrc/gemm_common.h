@@ -177,6 +177,3 @@ int savqa_launch_gemm_bf16(const savqa_gemm_desc& d, const savqa::GemmGrid& gg, 
 // gemm_x6.hip: fp32 GEMM on bf16 matrix cores from exact three-term splits (desc.prec == 6)
 int savqa_launch_gemm_x6(const savqa_gemm_desc& d, const savqa::GemmGrid& gg, int grid_x,
                          int nsplit, hipStream_t s);
-// gemm_x6p.hip: the x6 products from pre-split bf16 plane operands (desc.ap / desc.bp)
-int savqa_launch_gemm_x6p(const savqa_gemm_desc& d, const savqa::GemmGrid& gg, int grid_x,
-                          int nsplit, hipStream_t s);

@@ -156,10 +156,9 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
          c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None, ldrv=0, rowvec_period=0,
          resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False, rowscale=None, relu=False,
          alpha=1.0, beta=0.0, atomic=False, split_k=1, colsum_a=None, prec=None,
-         plan_only=False, ap=None, bp=None):
+         plan_only=False):
     """Generic MFMA GEMM with fused epilogue (see savqa_gemm in include/savqa.h).
-    plan_only: no launch, return savqa_gemm_plan's [tile, split, tail slices, workgroups].
-    ap / bp: the operands' bf16 planes ([3, rows, ld] tensors from split3) for prec 6."""
+    plan_only: no launch, return savqa_gemm_plan's [tile, split, tail slices, workgroups]."""
     d = GemmDesc()
     d.prec = _prec if prec is None else int(prec)
     d.M, d.N, d.K = int(M), int(N), int(K)
@@ -178,10 +177,6 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
     d.alpha, d.beta = float(alpha), float(beta)
     d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
     d.colsum_a = _p(colsum_a)
-    if ap is not None:
-        d.ap, d.ldap, d.psa = _p(ap), int(ap.stride(1)), int(ap.stride(0))
-    if bp is not None:
-        d.bp, d.ldbp, d.psb = _p(bp), int(bp.stride(1)), int(bp.stride(0))
     if plan_only:
         plan = (C.c_int32 * 4)()
         call("savqa_gemm_plan", C.byref(d), C.cast(plan, C.c_void_p))
@@ -307,17 +302,6 @@ def gemm_lp(*args, slabs=False, **kw):
         key += (f" | {'T' if d.a_trans else 'N'}{'T' if d.b_trans else 'N'} {d.M}x{d.N}x{d.K}"
                 f" split{plan[1]} wg{plan[2]}")
     _probe.records.append((key, 2.0 * d.M * d.N * d.K, e0, e1))
-
-
-def split3(x: Tensor, rows: int, cols: int, ldx: int, row_map=None, out: Tensor = None) -> Tensor:
-    """Exact three-term bf16 split of fp32 rows (savqa_split3): a [3, rows, ldp] bf16 tensor,
-    ldp = cols rounded up to 8 (zero columns past cols), x = p0 + p1 + p2 elementwise."""
-    ldp = (int(cols) + 7) // 8 * 8
-    if out is None:
-        out = torch.empty(3, int(rows), ldp, dtype=torch.bfloat16, device=x.device)
-    call("savqa_split3", _stream(), _p(x), int(rows), int(cols), int(ldx), _p(row_map), _p(out),
-         int(out.stride(1)), int(out.stride(0)))
-    return out
 
 
 def cast_bf16(x: Tensor, rows: int, cols: int, ldi: int, out: Tensor, ldo: int, group=0,

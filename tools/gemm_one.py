@@ -9,8 +9,7 @@ import torch  # noqa: E402
 
 from savqa_amd import ops  # noqa: E402
 
-planes = sys.argv[5] == "fp32x6p"  # x6 products from pre-split bf16 planes (gemm_x6p.hip)
-lay, m, n, k, prec = sys.argv[1], *map(int, sys.argv[2:5]), ops.PREC[sys.argv[5].rstrip("p")]
+lay, m, n, k, prec = sys.argv[1], *map(int, sys.argv[2:5]), ops.PREC[sys.argv[5]]
 iters = int(sys.argv[6]) if len(sys.argv) > 6 else 20
 dev = "cuda"
 if lay == "NT":
@@ -23,9 +22,6 @@ else:
     A, B = torch.randn(k, m, device=dev), torch.randn(k, n, device=dev)
     kw = dict(lda=m, ldb=n, ldc=n, a_trans=True, atomic=True, split_k=-1)
 C = torch.zeros(m, n, device=dev)
-if planes:
-    kw["ap"] = ops.split3(A, *((m, k, k) if lay != "TN" else (k, m, m)))
-    kw["bp"] = ops.split3(B, *((n, k, k) if lay == "NT" else (k, n, n)))
 for _ in range(iters):
     ops.gemm(A, B, C, m, n, k, prec=prec, **kw)
 torch.cuda.synchronize()
