@@ -78,9 +78,48 @@ def layer_norm(x, gamma, beta, eps=1e-8):
     return gamma * (x - mean) / (std + eps) + beta
 
 
+# Test hook, branch-aligned references: {(site, call): bool mask} -- the ReLU of the call-th
+# call of Linear `site` keeps exactly the units the mask marks (y * mask: the same piecewise-
+# linear branch as the computation the masks came from), so an fp64 run follows the fp32
+# path's ReLU decisions and the two differ by rounding alone, not by units within rounding of
+# 0 that land on the other side (tests/branch_masks.py). Sites without a mask use F.relu.
+RELU_BRANCHES = None
+_relu_calls = {}
+
+
 def linear(x, P, name, relu=False):
     y = F.linear(x, P[name + ".weight"], P[name + ".bias"])
-    return F.relu(y) if relu else y
+    if not relu:
+        return y
+    if RELU_BRANCHES is not None:
+        k = _relu_calls.get(name, 0)
+        _relu_calls[name] = k + 1
+        if RELU_BRANCHES.get("_record"):     # record this run's own decisions instead
+            RELU_BRANCHES[(name, k)] = (y > 0).detach()
+            return F.relu(y)
+        m = RELU_BRANCHES.get((name, k))
+        if m is not None:
+            return y * m.reshape(y.shape).to(device=y.device, dtype=y.dtype)
+    return F.relu(y)
+
+
+class relu_branches:
+    """Context manager: run the oracle with the given ReLU branch masks (RELU_BRANCHES)."""
+
+    def __init__(self, masks):
+        self.masks = masks
+
+    def __enter__(self):
+        global RELU_BRANCHES
+        RELU_BRANCHES = self.masks
+        _relu_calls.clear()
+        return self
+
+    def __exit__(self, *exc):
+        global RELU_BRANCHES
+        RELU_BRANCHES = None
+        _relu_calls.clear()
+        return False
 
 
 def _heads(X, h):
