@@ -282,6 +282,26 @@ int savqa_gattn_bwd_flash(void* stream, const float* q, int64_t ldq, const float
                           int64_t dk, const float* dout, int64_t lddo, float* stats, float* dq, int64_t lddq, float* dk_, int64_t lddk,
                           float* dv, int64_t lddv);
 
+/* Single-query graph attention over long key sequences (T_q = 1: the decoder cross-attention
+ * at T_k > 128, AttModel_x3.py:279 -> modules.py:236-311), split over keys so every wave takes
+ * 64 keys of one (sample, head): same operator, layouts and ReLU-masked gradients as
+ * savqa_gattn_fwd / _bwd with T_q = 1 (q / o / dout / dq rows are samples; G is (B, 1, Tk)).
+ * stats: caller-owned [B*H*4] floats (16-B aligned) written by the forward (row max, softmax
+ * denominator, graph-weighted mass) and read by the backward; ws: scratch of at least
+ * savqa_gattn_q1s_ws_bytes(B, H, Tk) bytes, 16-B aligned (per-split partials, summed in a
+ * fixed order: deterministic). */
+int64_t savqa_gattn_q1s_ws_bytes(int64_t B, int64_t H, int64_t Tk);
+int savqa_gattn_fwd_q1s(void* stream, const float* q, int64_t ldq, const float* k, int64_t ldk,
+                        const float* v, int64_t ldv, const float* G, const float* kflag,
+                        const float* qflag, int64_t B, int64_t Tk, int64_t H, int64_t dk, float* o,
+                        int64_t ldo, float* stats, void* ws, int64_t ws_bytes);
+int savqa_gattn_bwd_q1s(void* stream, const float* q, int64_t ldq, const float* k, int64_t ldk,
+                        const float* v, int64_t ldv, const float* G, const float* kflag,
+                        const float* qflag, int64_t B, int64_t Tk, int64_t H, int64_t dk,
+                        const float* dout, int64_t lddo, const float* stats, float* dq,
+                        int64_t lddq, float* dk_, int64_t lddk, float* dv, int64_t lddv, void* ws,
+                        int64_t ws_bytes);
+
 /* ------------------------------------------------------------------------
  * Graph construction, AttModel_x3.py:103-122 (vis, node_graph == NULL) and
  * :229-247 (syb): graph_diag, graph (== graph_cross, aliased in the reference),

@@ -118,6 +118,12 @@ _SIGS = {
     "savqa_gattn_bwd_flash": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
                               c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p,
                               c_p, c_i64, c_p, c_i64, c_p, c_i64],
+    "savqa_gattn_q1s_ws_bytes": [c_i64, c_i64, c_i64],
+    "savqa_gattn_fwd_q1s": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i64,
+                            c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64],
+    "savqa_gattn_bwd_q1s": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i64,
+                            c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64,
+                            c_p, c_i64],
     "savqa_rel_entries_fwd": [c_p, c_p, c_i32, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p],
     "savqa_rel_entries_bwd": [c_p, c_p, c_i32, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p,
                               c_p, c_p],
@@ -154,7 +160,7 @@ _SIGS = {
     "savqa_adam_shadow": [c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_f, c_f, c_p],
 }
 
-_I64_RET = {"savqa_ln_bwd_workspace_bytes", "savqa_gemm_ws_elems"}
+_I64_RET = {"savqa_ln_bwd_workspace_bytes", "savqa_gemm_ws_elems", "savqa_gattn_q1s_ws_bytes"}
 
 _lib = None
 

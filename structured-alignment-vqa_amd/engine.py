@@ -359,7 +359,7 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
     if lp is not None:
         s.kv = _bf(M, 2 * nb * d, dev=dev)
         ops.linear_lp(xb, lp.W.Wkv, W.bkv, None, s.kv, relu=True)
-        if ops.use_flash(1, T):  # fp32 K/V for the key-tiled decoder cross-attention
+        if ops.use_flash(1, T) or ops.use_q1s(T):  # fp32 K/V for the long-key kernels
             s.kv32 = _empty(M, 2 * nb * d, dev=dev)
             ops.widen_bf16(s.kv, M, 2 * nb * d, 2 * nb * d, s.kv32, 2 * nb * d)
     else:
@@ -381,7 +381,14 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
         ops.linear(d1, L["Wqc"], L["bqc"], qc, relu=True)
         oc = _empty(B, d, dev=dev)
         kvi = s.kv[:, 2 * i * d:]
-        if ops.use_flash(1, T):
+        if ops.use_q1s(T):  # long key sequence: split over keys (attn_q1s.hip)
+            if s.kv32 is not None:
+                kvi = s.kv32[:, 2 * i * d:]
+            ast = _empty(B * H * 4, dev=dev)
+            ops.gattn_fwd_q1s(qc, d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6, f1, B,
+                              T, H, oc, d, ast)
+            e.update(ast=ast, q1s=True)
+        elif ops.use_flash(1, T):
             if s.kv32 is not None:
                 kvi = s.kv32[:, 2 * i * d:]
             ast = _empty(B * H * 4, dev=dev)
@@ -445,7 +452,13 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         ops.ln_bwd(dd2, e["zc"], *e["stc"], L["gc"], dzc, Lg["gc"], Lg["bc"])
         dqc = _empty(B, d, dev=dev)
         kvi, dkvi = s.kv[:, 2 * i * d:], dkv_att[:, 2 * i * d:]
-        if "ast" in e:
+        if e.get("q1s"):
+            if s.kv32 is not None:
+                kvi = s.kv32[:, 2 * i * d:]
+            ops.gattn_bwd_q1s(e["qc"], d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6,
+                              e["f1"], B, T, H, dzc, d, e["ast"], dqc, d, dkvi, 2 * nb * d,
+                              dkvi[:, d:], 2 * nb * d)
+        elif "ast" in e:
             if s.kv32 is not None:
                 kvi = s.kv32[:, 2 * i * d:]
             ops.gattn_bwd_flash(e["qc"], d, kvi, 2 * nb * d, kvi[:, d:], 2 * nb * d, s.dmask, s.f6,

@@ -502,6 +502,32 @@ def gattn_bwd_flash(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout,
            _p(dq), lddq, _p(dk_), lddk, _p(dv), lddv)
 
 
+def gattn_fwd_q1s(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tk, H, o, ldo, stats, dk=64):
+    """Single-query attention split over keys (T_q = 1, long T_k: csrc/attn_q1s.hip);
+    stats: [B*H*4] fp32 kept for gattn_bwd_q1s."""
+    ws = _workspace((int(_lib.load().savqa_gattn_q1s_ws_bytes(B, H, Tk)) + 3) // 4, q.device)
+    _kcall(f"gattn_fwd_q1s T1x{Tk}", _attn_bytes(q, B, 1, Tk, H, dk, 1 + 2 * Tk, 1),
+           4.0 * B * H * Tk * dk, "savqa_gattn_fwd_q1s", _stream(), _p(q), ldq, _p(k), ldk, _p(v),
+           ldv, _p(G), _p(kflag), _p(qflag), B, Tk, H, dk, _p(o), ldo, _p(stats), _p(ws),
+           ws.numel() * 4)
+
+
+def gattn_bwd_q1s(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tk, H, dout, lddo, stats, dq,
+                  lddq, dk_, lddk, dv, lddv, dk=64):
+    ws = _workspace((int(_lib.load().savqa_gattn_q1s_ws_bytes(B, H, Tk)) + 3) // 4, q.device)
+    _kcall(f"gattn_bwd_q1s T1x{Tk}", _attn_bytes(q, B, 1, Tk, H, dk, 2 + 2 * Tk, 1 + 2 * Tk),
+           10.0 * B * H * Tk * dk, "savqa_gattn_bwd_q1s", _stream(), _p(q), ldq, _p(k), ldk, _p(v),
+           ldv, _p(G), _p(kflag), _p(qflag), B, Tk, H, dk, _p(dout), lddo, _p(stats), _p(dq),
+           lddq, _p(dk_), lddk, _p(dv), lddv, _p(ws), ws.numel() * 4)
+
+
+def use_q1s(Tk: int) -> bool:
+    """The decoder's single-query cross-attention at T_k > 128 runs split over keys
+    (attn_q1s.hip). SAVQA_ATTN_Q1S=0 keeps it on the key-tiled kernels (A/B), =force uses it at
+    every T_k (parity tests on the golden shapes)."""
+    mode = os.environ.get("SAVQA_ATTN_Q1S", "1")
+    return mode == "force" or (mode != "0" and Tk > FULL_ROW_MAX_T)
+
 FULL_ROW_MAX_T = 128  # attn.hip's full-row kernels; longer sequences use the key-tiled path
 
 

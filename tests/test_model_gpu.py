@@ -51,13 +51,17 @@ def run(m, t, decMask):
 @pytest.mark.parametrize("case,flash,prec", [("full_b4", False, "fp32"),
                                              ("full_b2_nodec", False, "fp32"),
                                              ("full_b4", True, "fp32"),
+                                             ("full_b4", "q1s", "fp32"),
+                                             ("full_b2_nodec", "q1s", "fp32"),
                                              ("full_b4", False, "bf16x3")])
 def test_full_model_against_reference_golden(model, case, flash, prec, monkeypatch):
     """flash=True forces the key-tiled attention kernels (used beyond T = 128) on the
     golden shapes, so the long-sequence path is pinned by the reference's own vectors;
-    prec="bf16x3" runs the 128x128-tile GEMMs as three bf16 MFMAs per product and must
-    still meet the north-star fp32 tolerance."""
-    monkeypatch.setenv("SAVQA_ATTN_FLASH", "1" if flash else "0")
+    flash="q1s" forces the decoder cross-attention onto the split-key single-query kernels
+    (attn_q1s.hip, used beyond T_k = 128); prec="bf16x3" runs the 128x128-tile GEMMs as three
+    bf16 MFMAs per product and must still meet the north-star fp32 tolerance."""
+    monkeypatch.setenv("SAVQA_ATTN_FLASH", "1" if flash is True else "0")
+    monkeypatch.setenv("SAVQA_ATTN_Q1S", "force" if flash == "q1s" else "0")
     monkeypatch.setattr(model._engine, "gemm_precision", prec)
     from savqa_amd.loss import smoothed_loss
     from savqa_amd.optim import Adam
