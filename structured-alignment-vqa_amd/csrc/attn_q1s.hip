@@ -14,7 +14,7 @@
 //            max(nrm, 1e-12) * qflag; (m, Z, nrm) saved for the backward    (q1s_fwd_combine)
 // Backward (the single-query kernel's chain, attn.hip gattn_bwd_q1_kernel, with its two
 // whole-row sums taken over the splits): dn_j = (dO.v_j) qflag, bm_j = g_j P_j,
-//   t1 = sum_j dn_j bm_j (fp64, fixed order over the splits)               (q1s_bwd_t1)
+//   t1 = sum_j dn_j bm_j (fp64, fixed order over the splits); dV_j        (q1s_bwd_dv)
 //   dnrm = -t1 / sden^2 (0 in F.normalize's clamped branch), da_j = g_j (dn_j / sden + dnrm
 //   sgn bm_j), t2 = sum_j da_j P_j = t1 / sden + dnrm nrm (closed form), ds_j = P_j (da_j -
 //   t2) / 8; dK_j = ds_j q, dV_j = (bm_j / sden) qflag dO, dQ = sum_j ds_j k_j, each through
@@ -30,7 +30,10 @@
 
 namespace savqa {
 
-constexpr int QS_KEYS = 64;            // keys per wave (one split)
+#ifndef SAVQA_Q1S_KEYS
+#define SAVQA_Q1S_KEYS 64
+#endif
+constexpr int QS_KEYS = SAVQA_Q1S_KEYS;  // keys per wave (one split)
 constexpr int QS_IT = QS_KEYS / 4;     // 4 key rows per load instruction
 constexpr int QS_PART = 4 + ATT_DK;    // floats per forward partial: m, Z, W, pad, U[64]
 
@@ -41,6 +44,7 @@ struct Q1sArgs {
   float* part;        // forward partials [B * H * ns][QS_PART]
   double* t1;         // backward: [B * H * ns]
   float* dqp;         // backward: dQ partials [B * H * ns][64]
+  float* pdn;         // backward: (P_j, dn_j) of every key [B * H * ns][QS_KEYS][2]
 };
 
 __device__ __forceinline__ float rows4_max_s(float v) {
@@ -94,6 +98,10 @@ __global__ __launch_bounds__(256) void q1s_fwd_part_kernel(Q1sArgs p) {
   const int64_t kb = (int64_t)b * a.Tk;
   const int j0 = s * QS_KEYS;
   const f4v q4 = ld4(a.q + (int64_t)b * a.ldq + hd + 4 * c);
+  f4v v4[QS_IT];  // V rows issued with the K rows: one memory round trip per wave
+#pragma unroll
+  for (int it = 0; it < QS_IT; ++it)
+    v4[it] = ld4(a.v + (kb + min(j0 + 4 * it + kk, a.Tk - 1)) * a.ldv + hd + 4 * c);
   float x[QS_IT];
   q1s_scores(a, kb, j0, hd, kk, c, q4, x);
   float mx = -INFINITY;
@@ -109,8 +117,7 @@ __global__ __launch_bounds__(256) void q1s_fwd_part_kernel(Q1sArgs p) {
     const float gj = j < a.Tk ? a.G[kb + j] : 0.f;
     z += e;
     w += fabsf(gj) * e;
-    const f4v v4 = ld4(a.v + (kb + min(j, a.Tk - 1)) * a.ldv + hd + 4 * c);
-    u += (gj * e) * v4;
+    u += (gj * e) * v4[it];
   }
   z = rows4_sum_s(z);
   w = rows4_sum_s(w);
@@ -120,7 +127,9 @@ __global__ __launch_bounds__(256) void q1s_fwd_part_kernel(Q1sArgs p) {
   if (kk == 0) *reinterpret_cast<f4v*>(rec + 4 + 4 * c) = u;
 }
 
-// one wave per (b, h): lane d combines dimension d of U over the splits
+// one wave per (b, h): the split statistics a lane per split (64 at a time), then lane d
+// combines dimension d of U -- every load of a pass issued before its sums (latency-bound
+// otherwise: one dependent L2 round trip per split)
 __global__ __launch_bounds__(256) void q1s_fwd_combine_kernel(Q1sArgs p) {
   const AttnArgs& a = p.a;
   const int bh = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -129,22 +138,42 @@ __global__ __launch_bounds__(256) void q1s_fwd_combine_kernel(Q1sArgs p) {
   const int b = bh / a.H, h = bh - b * a.H;
   const float* rec = p.part + (int64_t)bh * p.ns * QS_PART;
   float m = -INFINITY;
-  for (int s = 0; s < p.ns; ++s) m = fmaxf(m, rec[s * QS_PART]);
+  for (int s0 = 0; s0 < p.ns; s0 += 64)
+    if (s0 + lane < p.ns) m = fmaxf(m, rec[(s0 + lane) * QS_PART]);
+  m = wave_max(m);
   float z = 0.f, w = 0.f, u = 0.f;
-  for (int s = 0; s < p.ns; ++s) {
-    const float sc = expf(rec[s * QS_PART] - m);
-    z += rec[s * QS_PART + 1] * sc;
-    w += rec[s * QS_PART + 2] * sc;
-    u += rec[s * QS_PART + 4 + lane] * sc;
+  for (int s0 = 0; s0 < p.ns; s0 += 64) {
+    float sc = 0.f;
+    if (s0 + lane < p.ns) {
+      const f4v st = *reinterpret_cast<const f4v*>(rec + (s0 + lane) * QS_PART);
+      sc = expf(st[0] - m);
+      z += st[1] * sc;
+      w += st[2] * sc;
+    }
+    const int n = min(64, p.ns - s0);
+    for (int r0 = 0; r0 < n; r0 += 16) {
+      float uv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float x = rec[(s0 + min(r0 + r, n - 1)) * QS_PART + 4 + lane];
+        uv[r] = r0 + r < n ? x : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) u += uv[r] * __shfl(sc, r0 + r);
+    }
   }
+  z = wave_sum(z);
+  w = wave_sum(w);
   const float nrm = w / z;
   const float sden = fmaxf(nrm, 1e-12f);
   a.o[(int64_t)b * a.ldo + h * ATT_DK + lane] = u / z / sden * a.qflag[b];
   if (lane == 0) *reinterpret_cast<f4v*>(p.stats + 4 * bh) = f4v{m, z, nrm, 0.f};
 }
 
-// per split: dn_j = (dO . v_j) qflag and the partial of t1 = sum_j dn_j g_j P_j (fp64)
-__global__ __launch_bounds__(256) void q1s_bwd_t1_kernel(Q1sArgs p) {
+// per split: P_j (the forward's row max and denominator), dn_j = (dO . v_j) qflag, dV_j =
+// (g_j P_j / sden) qflag dO through V's ReLU mask (needs only forward statistics), the partial
+// of t1 = sum_j dn_j g_j P_j (fp64), and (P_j, dn_j) kept for q1s_bwd_main
+__global__ __launch_bounds__(256) void q1s_bwd_dv_kernel(Q1sArgs p) {
   int b, h, s;
   if (!q1s_unit(p, b, h, s)) return;
   const AttnArgs& a = p.a;
@@ -153,26 +182,44 @@ __global__ __launch_bounds__(256) void q1s_bwd_t1_kernel(Q1sArgs p) {
   const int64_t kb = (int64_t)b * a.Tk;
   const int j0 = s * QS_KEYS;
   const f4v st = *reinterpret_cast<const f4v*>(p.stats + 4 * bh);
+  const float sden = fmaxf(st[2], 1e-12f);
   const float qf = a.qflag[b];
   const f4v q4 = ld4(a.q + (int64_t)b * a.ldq + hd + 4 * c);
   const f4v do4 = ld4(a.dout + (int64_t)b * a.lddo + hd + 4 * c);
+  f4v v4[QS_IT];
+#pragma unroll
+  for (int it = 0; it < QS_IT; ++it)
+    v4[it] = ld4(a.v + (kb + min(j0 + 4 * it + kk, a.Tk - 1)) * a.ldv + hd + 4 * c);
   float x[QS_IT];
   q1s_scores(a, kb, j0, hd, kk, c, q4, x);
+  const bool vv = vec_rows(a.dv, a.lddv);
+  float* pdn = p.pdn + ((int64_t)bh * p.ns + s) * QS_KEYS * 2;
   double t = 0.0;
 #pragma unroll
   for (int it = 0; it < QS_IT; ++it) {
     const int j = j0 + 4 * it + kk;
-    const f4v v4 = ld4(a.v + (kb + min(j, a.Tk - 1)) * a.ldv + hd + 4 * c);
-    const float dn = row16_sum((do4.x * v4.x + do4.y * v4.y) + (do4.z * v4.z + do4.w * v4.w)) * qf;
-    if (c == 0 && j < a.Tk) {
+    const float dn =
+        row16_sum((do4.x * v4[it].x + do4.y * v4[it].y) + (do4.z * v4[it].z + do4.w * v4[it].w)) * qf;
+    if (j < a.Tk) {
       const float P = expf(x[it] - st[0]) / st[1];
-      t += (double)dn * (double)(a.G[kb + j] * P);
+      const float bm = a.G[kb + j] * P;
+      if (c == 0) {
+        t += (double)dn * (double)bm;
+        *reinterpret_cast<float2*>(pdn + 2 * (4 * it + kk)) = make_float2(P, dn);
+      }
+      const float pj = bm / sden * qf;
+      f4v gv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gv[e] = v4[it][e] > 0.f ? pj * do4[e] : 0.f;
+      stx4(a.dv + (kb + j) * a.lddv + hd + 4 * c, gv, vv);
     }
   }
   t = wave_sum_d(t);
   if (lane == 0) p.t1[(int64_t)bh * p.ns + s] = t;
 }
 
+// per split: ds_j from (P_j, dn_j) and the whole-row t1, dK_j = ds_j q through K's ReLU mask,
+// and the split's dQ partial sum_j ds_j k_j
 __global__ __launch_bounds__(256) void q1s_bwd_main_kernel(Q1sArgs p) {
   int b, h, s;
   if (!q1s_unit(p, b, h, s)) return;
@@ -181,48 +228,39 @@ __global__ __launch_bounds__(256) void q1s_bwd_main_kernel(Q1sArgs p) {
   const int bh = b * a.H + h;
   const int64_t kb = (int64_t)b * a.Tk;
   const int j0 = s * QS_KEYS;
-  const f4v st = *reinterpret_cast<const f4v*>(p.stats + 4 * bh);
-  const float nrm = st[2], sden = fmaxf(nrm, 1e-12f);
-  double t1 = 0.0;
-  for (int r = 0; r < p.ns; ++r) t1 += p.t1[(int64_t)bh * p.ns + r];
+  f4v k4[QS_IT];
+#pragma unroll
+  for (int it = 0; it < QS_IT; ++it)
+    k4[it] = ld4(a.k + (kb + min(j0 + 4 * it + kk, a.Tk - 1)) * a.ldk + hd + 4 * c);
+  const float nrm = p.stats[4 * bh + 2], sden = fmaxf(nrm, 1e-12f);
+  double t1 = 0.0;  // lane r holds split r (64 at a time); the butterfly sum is the same in
+  for (int r0 = 0; r0 < p.ns; r0 += 64)  // every wave of (b, h)
+    if (r0 + lane < p.ns) t1 += p.t1[(int64_t)bh * p.ns + r0 + lane];
+  t1 = wave_sum_d(t1);
   const double dnrm_d = nrm >= 1e-12f ? -t1 / ((double)sden * (double)sden) : 0.0;
   const float dnrm = (float)dnrm_d;
   const float t2 = (float)(t1 / (double)sden + dnrm_d * (double)nrm);
-  const float qf = a.qflag[b];
   const f4v q4 = ld4(a.q + (int64_t)b * a.ldq + hd + 4 * c);
-  const f4v do4 = ld4(a.dout + (int64_t)b * a.lddo + hd + 4 * c);
-  float x[QS_IT];
-  q1s_scores(a, kb, j0, hd, kk, c, q4, x);
-  const bool vk = vec_rows(a.dk, a.lddk), vv = vec_rows(a.dv, a.lddv);
+  const float* pdn = p.pdn + ((int64_t)bh * p.ns + s) * QS_KEYS * 2;
+  const bool vk = vec_rows(a.dk, a.lddk);
   f4v dq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int it = 0; it < QS_IT; ++it) {
     const int j = j0 + 4 * it + kk;
-    const bool ok = j < a.Tk;
-    const int64_t row = kb + min(j, a.Tk - 1);
-    const f4v k4 = ld4(a.k + row * a.ldk + hd + 4 * c);
-    const f4v v4 = ld4(a.v + row * a.ldv + hd + 4 * c);
-    const float dn = row16_sum((do4.x * v4.x + do4.y * v4.y) + (do4.z * v4.z + do4.w * v4.w)) * qf;
-    const float P = ok ? expf(x[it] - st[0]) / st[1] : 0.f;
-    const float gj = ok ? a.G[row] : 0.f;
-    const float bm = gj * P;
+    if (j >= a.Tk) continue;
+    const float2 pd = *reinterpret_cast<const float2*>(pdn + 2 * (4 * it + kk));
+    const float gj = a.G[kb + j];
+    const float bm = gj * pd.x;
     const float sg = bm > 0.f ? 1.f : (bm < 0.f ? -1.f : 0.f);
-    const float da = (dn / sden + dnrm * sg) * gj;
-    float ds = P * (da - t2);
-    if (!ok || a.kflag[row] == 0.f) ds = 0.f;
+    const float da = (pd.y / sden + dnrm * sg) * gj;
+    float ds = pd.x * (da - t2);
+    if (a.kflag[kb + j] == 0.f) ds = 0.f;
     ds *= 0.125f;
-    const float pj = ok ? bm / sden * qf : 0.f;
-    dq += ds * k4;
-    if (ok) {
-      f4v gk, gv;
+    dq += ds * k4[it];
+    f4v gk;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        gk[e] = k4[e] > 0.f ? ds * q4[e] : 0.f;
-        gv[e] = v4[e] > 0.f ? pj * do4[e] : 0.f;
-      }
-      stx4(a.dk + row * a.lddk + hd + 4 * c, gk, vk);
-      stx4(a.dv + row * a.lddv + hd + 4 * c, gv, vv);
-    }
+    for (int e = 0; e < 4; ++e) gk[e] = k4[it][e] > 0.f ? ds * q4[e] : 0.f;
+    stx4(a.dk + (kb + j) * a.lddk + hd + 4 * c, gk, vk);
   }
   dq = xrow_sum_s(dq);
   if (kk == 0) *reinterpret_cast<f4v*>(p.dqp + ((int64_t)bh * p.ns + s) * ATT_DK + 4 * c) = dq;
@@ -235,7 +273,17 @@ __global__ __launch_bounds__(256) void q1s_bwd_dq_kernel(Q1sArgs p) {
   const int lane = threadIdx.x & 63;
   const int b = bh / a.H, h = bh - b * a.H;
   float v = 0.f;
-  for (int s = 0; s < p.ns; ++s) v += p.dqp[((int64_t)bh * p.ns + s) * ATT_DK + lane];
+  const float* src = p.dqp + (int64_t)bh * p.ns * ATT_DK + lane;
+  for (int r0 = 0; r0 < p.ns; r0 += 16) {
+    float x[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float y = src[(int64_t)min(r0 + r, p.ns - 1) * ATT_DK];
+      x[r] = r0 + r < p.ns ? y : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v += x[r];
+  }
   const int64_t qi = (int64_t)b * a.ldq + h * ATT_DK + lane;
   a.dq[(int64_t)b * a.lddq + h * ATT_DK + lane] = a.q[qi] > 0.f ? v : 0.f;
 }
@@ -258,7 +306,8 @@ using namespace savqa;
 extern "C" int64_t savqa_gattn_q1s_ws_bytes(int64_t B, int64_t H, int64_t Tk) {
   const int64_t units = B * H * (int64_t)q1s_ns(Tk);
   const int64_t fwd = units * QS_PART * (int64_t)sizeof(float);
-  const int64_t bwd = units * (int64_t)sizeof(double) + units * ATT_DK * (int64_t)sizeof(float);
+  const int64_t bwd = units * (int64_t)sizeof(double) + units * ATT_DK * (int64_t)sizeof(float) +
+                      units * QS_KEYS * 2 * (int64_t)sizeof(float);
   return std::max(fwd, bwd) + 256;
 }
 
@@ -272,6 +321,7 @@ static int q1s_ws(Q1sArgs& p, void* ws, int64_t ws_bytes, bool fwd, const char* 
   } else {
     p.t1 = reinterpret_cast<double*>(w);
     p.dqp = reinterpret_cast<float*>(w + ((units * (int64_t)sizeof(double) + 15) & ~(int64_t)15));
+    p.pdn = p.dqp + units * ATT_DK;
   }
   return 0;
 }
@@ -321,8 +371,8 @@ extern "C" int savqa_gattn_bwd_q1s(void* stream, const float* q, int64_t ldq, co
   if (int rc = q1s_ws(p, ws, ws_bytes, false, "savqa_gattn_bwd_q1s")) return rc;
   hipStream_t s = as_stream(stream);
   const unsigned blocks = (unsigned)(B * H * ((p.ns + 3) / 4));
-  hipLaunchKernelGGL(q1s_bwd_t1_kernel, dim3(blocks), dim3(256), 0, s, p);
-  if (int rc = check_launch("savqa_gattn_bwd_q1s(t1)")) return rc;
+  hipLaunchKernelGGL(q1s_bwd_dv_kernel, dim3(blocks), dim3(256), 0, s, p);
+  if (int rc = check_launch("savqa_gattn_bwd_q1s(dv)")) return rc;
   hipLaunchKernelGGL(q1s_bwd_main_kernel, dim3(blocks), dim3(256), 0, s, p);
   if (int rc = check_launch("savqa_gattn_bwd_q1s(main)")) return rc;
   hipLaunchKernelGGL(q1s_bwd_dq_kernel, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, s, p);

@@ -35,7 +35,13 @@ def main():
                     help="decoder cross-attention: one fp32 query per sample, K/V of T rows")
     ap.add_argument("--flash", action="store_true",
                     help="key-tiled kernels (T > 128: cfg 4, super-node relation graphs), fp32")
+    ap.add_argument("--q1s", action="store_true",
+                    help="decoder cross-attention at T_k > 128: split-key single-query kernels "
+                         "against the key-tiled ones with T_q = 1 (K/V rows of the 6-layer "
+                         "[B*T, 12 d] decoder buffer)")
     args = ap.parse_args()
+    if args.q1s:
+        return q1s_main(args)
     if args.q1:
         return q1_main(args)
     if args.flash:
@@ -114,6 +120,37 @@ def q1_main(args):
         bb = 2 * B * T * 2 * d * es
         print(f"q1 {dt} B={B} Tk={T}: fwd {tf*1e6:7.1f} us {fb/tf/1e9:6.0f} GB/s | "
               f"bwd {tb*1e6:7.1f} us {bb/tb/1e9:6.0f} GB/s", flush=True)
+
+
+def q1s_main(args):
+    H, dk = 8, 64
+    d = H * dk
+    ld = 12 * d
+    for B, T in ((args.B[0], t) for t in args.T):
+        q = torch.randn(B, d, device=dev).relu_()
+        kv = torch.randn(B * T, ld, device=dev).relu_()
+        G = (torch.rand(B, 1, T, device=dev) < 0.3).float()
+        kf, qf = torch.ones(B * T, device=dev), torch.ones(B, device=dev)
+        o, dout = torch.empty(B, d, device=dev), torch.randn(B, d, device=dev)
+        dq = torch.empty(B, d, device=dev)
+        dkv = torch.empty(B * T, ld, device=dev)
+        st = torch.empty(B * H * 4, device=dev)
+        res = {}
+        for name, fw, bw in (
+                ("q1s", lambda: ops.gattn_fwd_q1s(q, d, kv, ld, kv[:, d:], ld, G, kf, qf, B, T, H,
+                                                  o, d, st),
+                 lambda: ops.gattn_bwd_q1s(q, d, kv, ld, kv[:, d:], ld, G, kf, qf, B, T, H, dout,
+                                           d, st, dq, d, dkv, ld, dkv[:, d:], ld)),
+                ("flash", lambda: ops.gattn_fwd_flash(q, d, kv, ld, kv[:, d:], ld, G, kf, qf, B, 1,
+                                                      T, H, o, d, st),
+                 lambda: ops.gattn_bwd_flash(q, d, kv, ld, kv[:, d:], ld, G, kf, qf, B, 1, T, H,
+                                             dout, d, st, dq, d, dkv, ld, dkv[:, d:], ld))):
+            fw()
+            res[name] = (timeit(fw), timeit(bw))
+        fb = B * T * 2 * d * 4
+        print(f"T_q=1 B={B} Tk={T}: " + " | ".join(
+            f"{n} fwd {tf*1e6:6.1f} us ({fb/tf/1e9:5.0f} GB/s) bwd {tb*1e6:6.1f} us "
+            f"({3*fb/tb/1e9:5.0f} GB/s)" for n, (tf, tb) in res.items()), flush=True)
 
 
 if __name__ == "__main__":
