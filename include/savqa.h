@@ -343,10 +343,12 @@ int savqa_rel_entries_bwd(void* stream, const int64_t* loc, int32_t loc_w, int64
  * valid entries must be a prefix of each sample's slots (collate pads the tail); cum[b] =
  * valid positives of samples < b (int32 [B+1]); wsm[cum[b]+k] = softmax over the batch's
  * valid positives (:420); st (16 floats) = (P, m1, Z1, m2, Z2, err, mr, Zr, ...) for the
- * backward; err = 1 and mil_rel = NaN if the prefix layout is violated. */
+ * backward; err = 1 and mil_rel = NaN if the prefix layout is violated. Multi-workgroup with a
+ * fixed-order fold of per-chunk records (deterministic): ws holds savqa_rel_loss_ws_bytes. */
+int64_t savqa_rel_loss_ws_bytes(int64_t B, int64_t Lp, int64_t Ln);
 int savqa_rel_loss_fwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp, const float* sp,
                        const int64_t* neg_loc, int64_t Ln, const float* sn, float eps, int32_t* cum,
-                       float* wsm, float* st, float* mil_rel);
+                       float* wsm, float* st, float* mil_rel, void* ws, int64_t ws_bytes);
 /* macro[b, loc3] = sum over the node's (consecutive) entries, in order, of
  * wsm[loc4] * relf[b, loc4]  (:418-436: zero, then the reference's accumulation loop) */
 int savqa_rel_macro_fwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp, const float* st,
@@ -356,11 +358,12 @@ int savqa_rel_macro_fwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t
 int savqa_rel_macro_bwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp, const float* st,
                         const float* wsm, const float* relf, int64_t Ns, int64_t H, float* dmacro,
                         float* dwsm, float* drelf);
-/* dsp / dsn per slot from dmil (device scalar) through both logsumexps and the softmax path */
+/* dsp / dsn per slot from dmil (device scalar) through both logsumexps and the softmax path
+ * (ws: savqa_rel_loss_ws_bytes, as for the forward) */
 int savqa_rel_loss_bwd(void* stream, const int64_t* pos_loc, int64_t B, int64_t Lp, const float* sp,
                        const int64_t* neg_loc, int64_t Ln, const float* sn, float eps,
                        const int32_t* cum, const float* wsm, const float* dwsm, float* st,
-                       const float* dmil, float* dsp, float* dsn);
+                       const float* dmil, float* dsp, float* dsn, void* ws, int64_t ws_bytes);
 
 /* out = a*x + b*y over n floats (combining the MIL-NCE terms of the loss) */
 int savqa_axpby(void* stream, const float* x, const float* y, int64_t n, float a, float b,

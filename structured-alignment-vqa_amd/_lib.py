@@ -127,11 +127,13 @@ _SIGS = {
     "savqa_rel_entries_fwd": [c_p, c_p, c_i32, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p],
     "savqa_rel_entries_bwd": [c_p, c_p, c_i32, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p,
                               c_p, c_p],
-    "savqa_rel_loss_fwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p, c_p],
+    "savqa_rel_loss_ws_bytes": [c_i64, c_i64, c_i64],
+    "savqa_rel_loss_fwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p, c_p, c_p,
+                           c_i64],
     "savqa_rel_macro_fwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_i64, c_p],
     "savqa_rel_macro_bwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p],
     "savqa_rel_loss_bwd": [c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p, c_p,
-                           c_p, c_p, c_p],
+                           c_p, c_p, c_p, c_p, c_i64],
     "savqa_axpby": [c_p, c_p, c_p, c_i64, c_f, c_f, c_p],
     "savqa_collate": [c_p, C.POINTER(CollateField), c_i32, c_i64],
     "savqa_collate_edges": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p],
@@ -160,7 +162,8 @@ _SIGS = {
     "savqa_adam_shadow": [c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_f, c_f, c_p],
 }
 
-_I64_RET = {"savqa_ln_bwd_workspace_bytes", "savqa_gemm_ws_elems", "savqa_gattn_q1s_ws_bytes"}
+_I64_RET = {"savqa_ln_bwd_workspace_bytes", "savqa_gemm_ws_elems", "savqa_gattn_q1s_ws_bytes",
+            "savqa_rel_loss_ws_bytes"}
 
 _lib = None
 

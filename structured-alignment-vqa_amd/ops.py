@@ -648,9 +648,15 @@ def rel_entries_bwd(loc, B, L, obj, Nv, H, V, ldv, dval, dobj, dV):
          _p(V), int(ldv), _p(dval), _p(dobj), _p(dV))
 
 
+def _rel_ws(B, Lp, Ln, dev):
+    nb = int(_lib.load().savqa_rel_loss_ws_bytes(B, Lp, Ln))
+    return _workspace((nb + 3) // 4, dev), nb
+
+
 def rel_loss_fwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cum, wsm, st, mil_rel):
+    ws, nb = _rel_ws(B, Lp, Ln, sp.device)
     call("savqa_rel_loss_fwd", _stream(), _p(pos_loc), B, Lp, _p(sp), _p(neg_loc), Ln, _p(sn),
-         float(eps), _p(cum), _p(wsm), _p(st), _p(mil_rel))
+         float(eps), _p(cum), _p(wsm), _p(st), _p(mil_rel), _p(ws), nb)
 
 
 def rel_macro_fwd(pos_loc, B, Lp, st, wsm, relf, Ns, H, macro):
@@ -664,8 +670,9 @@ def rel_macro_bwd(pos_loc, B, Lp, st, wsm, relf, Ns, H, dmacro, dwsm, drelf):
 
 
 def rel_loss_bwd(pos_loc, B, Lp, sp, neg_loc, Ln, sn, eps, cum, wsm, dwsm, st, dmil, dsp, dsn):
+    ws, nb = _rel_ws(B, Lp, Ln, sp.device)
     call("savqa_rel_loss_bwd", _stream(), _p(pos_loc), B, Lp, _p(sp), _p(neg_loc), Ln, _p(sn),
-         float(eps), _p(cum), _p(wsm), _p(dwsm), _p(st), _p(dmil), _p(dsp), _p(dsn))
+         float(eps), _p(cum), _p(wsm), _p(dwsm), _p(st), _p(dmil), _p(dsp), _p(dsn), _p(ws), nb)
 
 
 def axpby(x, y, n, a, b, out):
