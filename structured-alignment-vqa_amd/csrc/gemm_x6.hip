@@ -3,26 +3,27 @@
 // Same operator, operand layouts, epilogues and launch plan as gemm_f32_kernel (gemm.hip);
 // only the products move from v_mfma_f32_16x16x4_f32 (64 FLOP/clk/SIMD) to
 // v_mfma_f32_16x16x32_bf16 (1024 FLOP/clk/SIMD). Every fp32 operand value is split EXACTLY
-// into three bf16 terms while its tile is staged,
-//   a = a0 + a1 + a2,  a0 = bf16(a), a1 = bf16(a - a0), a2 = a - a0 - a1
-// (round to nearest even; a - a0 and a - a0 - a1 are exact fp32 differences, and the last
-// remainder has at most 8 significant bits, so a2 is a bf16 value: the split loses nothing),
-// and each product is the sum of the six terms of order <= 2:
+// into three bf16 terms while its tile is staged (truncation split, SAVQA_X6_TRUNC):
+//   a0 = a with its low 16 mantissa bits cleared, a1 = (a - a0) likewise, a2 = a - a0 - a1
+// (both differences are exact fp32 values of a's sign, and the last remainder has at most 8
+// significant bits, so a2 is a bf16 value: the split loses nothing), and each product is the
+// sum of the six terms of order <= 2:
 //   a*b = a0 b0 + (a0 b1 + a1 b0) + (a0 b2 + a1 b1 + a2 b0)      [+ a1 b2 + a2 b1 + a2 b2]
-// The dropped bracket is below 2^-23 |a b| in the worst case (|a1| <= 2^-8 |a|, |a2| <= 2^-16
-// |a|; typically 2^-26), bf16 x bf16 products are exact in the fp32 accumulator, and the
+// The dropped bracket is below 2^-21 |a b| in the worst case (|a1| < 2^-7 |a|, |a2| < 2^-15
+// |a|; about 2^-25 on average, of ab's sign -- a rounded split would bound it by 2^-23 with
+// either sign), bf16 x bf16 products are exact in the fp32 accumulator, and the
 // accumulation is fp32 -- the accuracy of an fp32 GEMM (tests/test_kernels_gpu.py holds it to
 // the native fp32 kernel's error against fp64 on every cfg-2 step shape) at 6/16 of the fp32
 // MFMA's cycles per product.
-// Range: operands must be finite with |x| <= 3.3895e38 (the largest bf16). An infinite x (or a
-// finite one that rounds to a bf16 infinity) gives a0 = +-inf and x - a0 = NaN, and even with
-// a1 = a2 forced to 0 the other operand's terms would still meet it as inf * b1 with b1 = 0 or
-// of the opposite sign (NaN, where fp32 gives +-inf): x6 cannot reproduce fp32's infinities,
-// so it does not try (a guard would cost 8 VALU per float4 of the split). What it does keep:
-// an output is non-finite exactly where the fp32 GEMM's is (NaN in place of +-inf), so
-// overflow still surfaces (tests/test_kernels_gpu.py::test_gemm_x6_infinite_operands). At the
-// small end a1 / a2 of |x| < 2^-110 fall below the fp32 normal range and stay exact as fp32 /
-// bf16 subnormals (the 'tiny' range test holds such operands to the native kernel's error).
+// Range: every finite fp32 operand splits (truncation never rounds a term up to a bf16
+// infinity). An infinite operand gives a0 = +-inf and a - a0 = NaN, and the other operand's
+// terms would meet it as inf * b1 with b1 = 0 or of the opposite sign (NaN, where fp32 gives
+// +-inf): x6 cannot reproduce fp32's infinities, so it does not try (a guard would cost 8 VALU
+// per float4 of the split). What it does keep: an output is non-finite exactly where the fp32
+// GEMM's is (NaN in place of +-inf), so overflow still surfaces
+// (tests/test_kernels_gpu.py::test_gemm_x6_infinite_operands). At the small end a1 / a2 of
+// |x| < 2^-110 fall below the fp32 normal range and stay exact as fp32 / bf16 subnormals (the
+// 'tiny' range test holds such operands to the native kernel's error).
 //
 // Tiling: 256 threads = 4 waves (2x2), 128x128 outputs, k-tile 32; each wave owns 64x64 =
 // 4x4 fragments of 16x16. Operand tiles are register-staged (float4 global loads issued one
@@ -71,6 +72,33 @@ __device__ __forceinline__ uint32_t pk_bf16(float x, float y) {
 __device__ __forceinline__ float pk_lo(uint32_t p) { return __uint_as_float(p << 16); }
 __device__ __forceinline__ float pk_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
 
+#ifndef SAVQA_X6_TRUNC
+#define SAVQA_X6_TRUNC 1
+#endif
+#if SAVQA_X6_TRUNC
+// truncation split: a0 = a with its low 16 bits cleared (the upper halves of a pair packed by
+// one v_perm_b32), a - a0 exact and of the same sign, and so on. Per pair: 2 masks + 1 perm +
+// 1 packed subtract per term (v_pk_add_f32), 9 VALU against 11 for the rounded split, and no
+// term can round up to a bf16 infinity, so every finite fp32 operand splits.
+__device__ __forceinline__ void split3(f4 v, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  uint32_t t[3][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    f2 x = f2{v[2 * h], v[2 * h + 1]};
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const uint32_t ux = __float_as_uint(x[0]), uy = __float_as_uint(x[1]);
+      t[p][h] = __builtin_amdgcn_perm(uy, ux, 0x07060302u);
+      if (p < 2) x = x - f2{__uint_as_float(ux & 0xffff0000u), __uint_as_float(uy & 0xffff0000u)};
+    }
+  }
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  p0 = __builtin_bit_cast(bf16x4, u2{t[0][0], t[0][1]});
+  p1 = __builtin_bit_cast(bf16x4, u2{t[1][0], t[1][1]});
+  p2 = __builtin_bit_cast(bf16x4, u2{t[2][0], t[2][1]});
+}
+#else
 __device__ __forceinline__ void split3(f4 v, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
   uint32_t t0[2], t1[2], t2[2];
 #pragma unroll
@@ -87,6 +115,7 @@ __device__ __forceinline__ void split3(f4 v, bf16x4& p0, bf16x4& p1, bf16x4& p2)
   p1 = __builtin_bit_cast(bf16x4, u2{t1[0], t1[1]});
   p2 = __builtin_bit_cast(bf16x4, u2{t2[0], t2[1]});
 }
+#endif
 
 __device__ __forceinline__ void put3(char* img, int off, f4 v) {
   bf16x4 p0, p1, p2;

@@ -584,16 +584,19 @@ def _wide(shape, lo, hi, seed):
 
 
 @pytest.mark.parametrize("lay", ["NT", "NN", "TN"])
-@pytest.mark.parametrize("rng", ["wide", "tiny"])
+@pytest.mark.parametrize("rng", ["wide", "tiny", "huge"])
 def test_gemm_x6_wide_dynamic_range(lay, rng):
     """The exact three-term split over operands far from N(0, 1): 'wide' spans 24 decades
     (a1 / a2 of the smallest values stay fp32-normal), 'tiny' puts A at 1e-37..1e-33, where
-    a1 / a2 fall below the fp32 / bf16 normal range while every product stays normal. Per
+    a1 / a2 fall below the fp32 / bf16 normal range while every product stays normal, 'huge'
+    puts A at 3.35e38..3.40e38, next to FLT_MAX, where a rounded bf16 a0 would be +-inf (the
+    truncation split keeps every finite operand) and B at 1e-33..1e-31 (its terms stay normal). Per
     element the error against fp64 is measured relative to sum_k |a||b| (the fp32 GEMM's own
     error scale, meaningful whatever an element's magnitude); x6 within 1.25x of native."""
     O = ops()
     M, N, K = (2048, 2048, 1024) if lay != "TN" else (2048, 1024, 4096)
-    alo, ahi, blo, bhi = (-12, 12, -12, 12) if rng == "wide" else (-37, -33, 1, 5)
+    alo, ahi, blo, bhi = {"wide": (-12, 12, -12, 12), "tiny": (-37, -33, 1, 5),
+                          "huge": (38.525, 38.5315, -33, -31)}[rng]
     if lay == "NT":
         A, B = _wide((M, K), alo, ahi, 1), _wide((N, K), blo, bhi, 2)
         kw = dict(lda=K, ldb=K, ldc=N, b_trans=True)
