@@ -112,7 +112,9 @@ int savqa_gemm_plan(const savqa_gemm_desc* d, int32_t* out);
  *   v = acc*alpha + bias[n] + rowvec[(m % rowvec_period)*ldrv + n]  (bias/rowvec/resid:
  *       first K slice only) ; v = relu ? max(v,0) : v ;
  *   v = (mask && !(mask[mr*ldmask+n] > 0)) ? 0 : v   mr = mask_arows ? a_rows[m] : m
- *       (mask_type SAVQA_DT_BF16 or SAVQA_DT_F32) ; v += resid[m*ldr + n]
+ *       (mask_type SAVQA_DT_BF16 or SAVQA_DT_F32; SAVQA_DT_BITS: the gate is bit (n & 7) of
+ *       byte ((uint8_t*)mask)[mr*ldmask + n/8], ldmask in bytes, bf16-only outputs Cb with
+ *       N % 8 == 0 and no C / resid / rowvec / atomic) ; v += resid[m*ldr + n]
  *   crow(m) = (m / c_group)*c_stride + m % c_group + c_offset  (c_group <= 0: identity)
  *   C[crow*ldc + n] = v  (atomic: +=)      Cb[crow*ldcb + n] = bf16(v)  (not with atomic)
  * split_k > 1 / < 0 (auto) requires atomic = 1 and C. savqa_gemm_lp_supported() says
@@ -121,6 +123,7 @@ int savqa_gemm_plan(const savqa_gemm_desc* d, int32_t* out);
 #define SAVQA_DT_F32 0
 #define SAVQA_DT_BF16 1
 #define SAVQA_DT_FP8 2
+#define SAVQA_DT_BITS 3  /* mask_type only: one bit per element (see savqa_gemm_lp_desc) */
 typedef struct savqa_gemm_lp_desc {
     int64_t M, N, K;
     const void* A; int64_t lda; int32_t a_trans; int32_t a_type;
@@ -150,6 +153,10 @@ typedef struct savqa_gemm_lp_desc {
                                bias gradient of dW = dY^T X), summed in fp32 from the staged A
                                tiles by the 128x128 kernel; other kernels add it in a separate
                                column-sum pass */
+    uint8_t* bits_out; int64_t ldbits;  /* optional, bf16-only outputs (Cb; N % 8 == 0; no C /
+                               resid / rowvec / atomic): bit (n & 7) of byte bits_out[crow*ldbits
+                               + n/8] = (Cb[crow*ldcb + n] > 0) -- the ReLU gate of this output
+                               as a SAVQA_DT_BITS mask, 1/16 of the bf16 output's bytes */
 } savqa_gemm_lp_desc;
 
 int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* d);

@@ -63,6 +63,7 @@ class GemmLpDesc(C.Structure):
         ("c_rows", c_p), ("n_store", c_i64),
         ("ws", c_p), ("ws_elems", c_i64),
         ("colsum_a", c_p),
+        ("bits_out", c_p), ("ldbits", c_i64),
     ]
 
 

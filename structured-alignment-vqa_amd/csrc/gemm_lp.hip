@@ -21,6 +21,8 @@
 // 4 consecutive output COLUMNS of one row: 16-B fp32 / 8-B bf16 epilogue stores.
 #include "gemm_common.h"
 
+#include <type_traits>
+
 #include <algorithm>
 
 namespace savqa {
@@ -253,8 +255,26 @@ __host__ __device__ __forceinline__ bool lp_wide_epilogue(const savqa_gemm_lp_de
   auto al = [](const void* p, int b) { return (((uintptr_t)p) & (b - 1)) == 0; };
   if (!d.Cb || d.C || d.resid || d.rowvec || d.atomic || d.N % 8) return false;
   if ((d.ldcb & 7) || !al(d.Cb, 16)) return false;
-  if (d.mask && (d.mask_type != SAVQA_DT_BF16 || (d.ldmask & 7) || !al(d.mask, 16))) return false;
+  if (d.mask && d.mask_type != SAVQA_DT_BITS &&
+      (d.mask_type != SAVQA_DT_BF16 || (d.ldmask & 7) || !al(d.mask, 16)))
+    return false;
   return true;
+}
+
+// the gate bytes of one lane in the wide map (SAVQA_DT_BITS mask: bits 0-7 = its 8 columns of
+// rows rb + 8q + lane/8), one zero-extended byte per register so a prefetch holds no wait
+__device__ __forceinline__ void lp_wide_bits(const savqa_gemm_lp_desc& d, uint32_t (&mb)[8],
+                                             int64_t rb, int64_t col0, int lane,
+                                             int64_t col_hi = -1) {
+  const int64_t n = ecol(col0, col_hi < 0 ? col0 + 32 : col_hi, 8 * (lane & 7));
+  const int64_t nc = n < d.N ? n : d.N - 8;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    int64_t m = rb + 8 * q + (lane >> 3);
+    m = m < d.M ? m : d.M - 1;
+    const int64_t mr = d.mask_arows ? d.a_rows[m] : m;
+    mb[q] = static_cast<const uint8_t*>(d.mask)[mr * d.ldmask + (nc >> 3)];
+  }
 }
 
 // the mask rows of one lane in the wide map (rows rb + 8q + lane/8, columns col0 + 8(lane%8))
@@ -272,11 +292,13 @@ __device__ __forceinline__ void lp_wide_mask(const savqa_gemm_lp_desc& d, bf16x8
   }
 }
 
-template <bool HAVE_MASK>
+// MK: 0 no mask, 1 bf16 mask values (mk), 2 gate bits (mb); d.bits_out: this output's gate
+// bits, one byte per lane and row (computed from the stored bf16 values)
+template <int MK>
 __device__ __forceinline__ void lp_pass_wide(const savqa_gemm_lp_desc& d, const char* reg,
                                              int64_t rb, int64_t col0, bool first_split,
-                                             const bf16x8 (&mk)[8], int lane,
-                                             int64_t col_hi = -1) {
+                                             const bf16x8 (&mk)[8], const uint32_t (&mb)[8],
+                                             int lane, int64_t col_hi = -1) {
   const int c8 = lane & 7, r8 = lane >> 3;
   const bool ident = d.c_group <= 0;
   const int64_t n = ecol(col0, col_hi < 0 ? col0 + 32 : col_hi, 8 * c8);
@@ -305,11 +327,17 @@ __device__ __forceinline__ void lp_pass_wide(const savqa_gemm_lp_desc& d, const 
         hi[r] = fmaxf(hi[r], 0.f);
       }
     }
-    if constexpr (HAVE_MASK) {
+    if constexpr (MK == 1) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         if (!((float)mk[q][r] > 0.f)) lo[r] = 0.f;
         if (!((float)mk[q][4 + r] > 0.f)) hi[r] = 0.f;
+      }
+    } else if constexpr (MK == 2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!((mb[q] >> r) & 1u)) lo[r] = 0.f;
+        if (!((mb[q] >> (4 + r)) & 1u)) hi[r] = 0.f;
       }
     }
     if (m < d.M && nok) {
@@ -321,6 +349,15 @@ __device__ __forceinline__ void lp_pass_wide(const savqa_gemm_lp_desc& d, const 
       const bf16x4 l = __builtin_convertvector(lo, bf16x4), h = __builtin_convertvector(hi, bf16x4);
       *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(d.Cb) + cr * d.ldcb + n) =
           bf16x8{l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+      if (d.bits_out) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          bits |= (uint32_t)((float)l[r] > 0.f) << r;
+          bits |= (uint32_t)((float)h[r] > 0.f) << (4 + r);
+        }
+        d.bits_out[cr * d.ldbits + (n >> 3)] = (uint8_t)bits;
+      }
     }
   }
 }
@@ -334,6 +371,14 @@ __device__ __forceinline__ void lp_pass_wide(const savqa_gemm_lp_desc& d, const 
 // lines; atomic outputs read one float per lane so a wave instruction adds 256 contiguous
 // bytes (the full-rate shape of global float atomics). The caller has barriered the
 // workgroup after its last k-tile read.
+template <int I, int N, class F>
+__device__ __forceinline__ void lp_static_for(F& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    lp_static_for<I + 1, N>(f);
+  }
+}
+
 template <int FM, int FN>
 __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&acc)[FM][FN],
                                             char* reg, int64_t row0, int64_t col0,
@@ -345,8 +390,18 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
   const bool ident = d.c_group <= 0;
   const bool vec_c = (d.ldc & 3) == 0 && (((uintptr_t)d.C) & 15) == 0;
   const bool vec_cb = (d.ldcb & 3) == 0 && (((uintptr_t)d.Cb) & 7) == 0;
+  // gate bits of every pass, loaded before the first image write (8 registers per pass)
+  const bool bits = d.mask && d.mask_type == SAVQA_DT_BITS && !d.atomic && !tail_atomic;
+  uint32_t mbits[FM / 4][8];
+  if (bits) {
 #pragma unroll
-  for (int pass = 0; pass < FM / 4; ++pass) {
+    for (int pass = 0; pass < FM / 4; ++pass)
+      lp_wide_bits(d, mbits[pass], row0 + rstep * pass, col0, lane, col_hi);
+  }
+  // passes of 64 rows as a compile-time loop: a runtime pass index would put the
+  // accumulators in scratch when the body is too large for the unroller
+  auto pass_body = [&](auto pc) {
+    constexpr int pass = decltype(pc)::value;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -405,11 +460,13 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
     } else if (lp_wide_epilogue(d)) {
       const int64_t rb = row0 + rstep * pass;
       bf16x8 mk[8];
-      if (d.mask) {
+      if (bits) {
+        lp_pass_wide<2>(d, reg, rb, col0, first_split, mk, mbits[pass], lane, col_hi);
+      } else if (d.mask) {
         lp_wide_mask(d, mk, rb, col0, lane, col_hi);
-        lp_pass_wide<true>(d, reg, rb, col0, first_split, mk, lane, col_hi);
+        lp_pass_wide<1>(d, reg, rb, col0, first_split, mk, mbits[0], lane, col_hi);
       } else {
-        lp_pass_wide<false>(d, reg, rb, col0, first_split, mk, lane, col_hi);
+        lp_pass_wide<0>(d, reg, rb, col0, first_split, mk, mbits[0], lane, col_hi);
       }
     } else if (lp_vec_epilogue(d)) {
       // 16 lanes per row, 4 rows per instruction, groups of G instructions per pass, each
@@ -528,7 +585,8 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
     }
-  }
+  };
+  lp_static_for<0, FM / 4>(pass_body);
 }
 
 // Split-K slab epilogue (128 x 128 kernel): the slice's partial tile goes to its own slab
@@ -606,6 +664,7 @@ template <int PRE>
 struct LpPre {
   f4 r[PRE == 1 ? 8 : 1];
   bf16x8 m[PRE == 2 ? 8 : 1];
+  uint32_t mb[8];  // PRE == 3: the gate bytes (SAVQA_DT_BITS mask), loaded before the k-loop
 
   __device__ __forceinline__ void load(const savqa_gemm_lp_desc& d, int64_t row0, int64_t col0,
                                        int lane) {
@@ -620,6 +679,7 @@ struct LpPre {
       }
     }
     if constexpr (PRE == 2) lp_wide_mask(d, this->m, row0, col0, lane);
+    if constexpr (PRE == 3) lp_wide_bits(d, this->mb, row0, col0, lane);
   }
 };
 
@@ -638,7 +698,12 @@ __device__ __forceinline__ void lp_epilogue_pre(const savqa_gemm_lp_desc& d, f4 
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is complete
   __builtin_amdgcn_wave_barrier();
   if constexpr (PRE == 2) {
-    lp_pass_wide<true>(d, reg, row0, col0, true, pre.m, lane);
+    lp_pass_wide<1>(d, reg, row0, col0, true, pre.m, pre.mb, lane);
+    return;
+  }
+  if constexpr (PRE == 3) {
+    bf16x8 unused[8];
+    lp_pass_wide<2>(d, reg, row0, col0, true, unused, pre.mb, lane);
     return;
   }
   const bool ident = d.c_group <= 0;
@@ -727,8 +792,8 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   LpPre<PRE> pre;
-  if constexpr (PRE != 0) {
-    if (nt == 0 && !tail) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
+  if constexpr (PRE != 0) {  // (the gate bytes cost 8 registers: loaded before the k-loop)
+    if ((nt == 0 || PRE == 3) && !tail) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
   }
   // fused bias gradient (savqa_gemm_lp_desc.colsum_a, dW launches): the first column tile of
   // each row block also sums its staged A^T tiles over k, thread (rg, cg) four k rows of 8
@@ -796,7 +861,7 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
       if (kt + 1 < nt) {  // next k-tile into the other buffer (read one barrier ago)
         stage(smem + ((kt + 1) & 1) * 2 * LP_IMG, kt + 1);
         stage_scales((kt + 1) & 1, kt + 1);
-      } else if constexpr (PRE != 0) {  // last k-tile: epilogue operands under its MFMAs
+      } else if constexpr (PRE == 1 || PRE == 2) {  // last k-tile: epilogue operands under its MFMAs
         if (!tail) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
       }
       if constexpr (FP8) {
@@ -1250,7 +1315,13 @@ static bool lp_ok(const savqa_gemm_lp_desc& d, const char** msg) {
   if (d.a_rows && d.a_trans) return no("a_rows needs a_trans = 0");
   if (d.colsum_a && (!d.a_trans || fp8)) return no("colsum_a needs a_trans = 1 and bf16 operands");
   if (d.mask && d.mask_arows && !d.a_rows) return no("mask_arows needs a_rows");
-  if (d.mask && d.mask_type != SAVQA_DT_BF16 && d.mask_type != SAVQA_DT_F32) return no("mask_type");
+  if (d.mask && d.mask_type != SAVQA_DT_BF16 && d.mask_type != SAVQA_DT_F32 &&
+      d.mask_type != SAVQA_DT_BITS)
+    return no("mask_type");
+  if (((d.mask && d.mask_type == SAVQA_DT_BITS) || d.bits_out) && !lp_wide_epilogue(d))
+    return no("bit masks / bits_out need a bf16-only output (Cb, N % 8 == 0, no C / resid / "
+              "rowvec / atomic)");
+  if (d.bits_out && d.ldbits < (d.N + 7) / 8) return no("ldbits < N / 8");
   if (d.rowvec && d.rowvec_period <= 0) return no("rowvec_period");
   if (!al16(d.A) || !al16(d.B)) return no("operands must be 16-B aligned");
   if (fp8) {
@@ -1276,7 +1347,8 @@ struct LpPlan {
   int var, split, nsplit;
   int64_t tiles, per;
   int bn;
-  int pre;  // gemm_lp_kernel's epilogue-operand prefetch (LpPre): 0 none, 1 resid, 2 bf16 mask
+  int pre;  // gemm_lp_kernel's epilogue-operand prefetch (LpPre): 0 none, 1 resid, 2 bf16 mask,
+            // 3 gate bits
   // tail split (variant 1, unsplit): tiles [tail_t0, tiles) in tail_f k-slices, rows
   // [zero_row0, M) of C zero-filled first; tail_f = 1: none
   int tail_f;
@@ -1328,7 +1400,7 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
   p.pre = 0;
   if (p.var == 1 && !fp8 && p.nsplit == 1 && !d.atomic && !d.rowvec && lp_vec_epilogue(d)) {
     if (d.resid && !d.mask) p.pre = 1;
-    else if (d.mask && lp_wide_epilogue(d)) p.pre = 2;
+    else if (d.mask && lp_wide_epilogue(d)) p.pre = d.mask_type == SAVQA_DT_BITS ? 3 : 2;
   }
   // Tail split (as savqa_gemm's): the tiles of the last, partial round of workgroups are split
   // over K (zero-filled C, atomic fp32 adds, bias / residual / row vector on slice 0) so that
@@ -1461,6 +1533,7 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   do {                                                                                        \
     if (pre == 1) hipLaunchKernelGGL((gemm_lp_kernel<AT_, BT_, false, 1>), grid, block, 0, s, a); \
     else if (pre == 2) hipLaunchKernelGGL((gemm_lp_kernel<AT_, BT_, false, 2>), grid, block, 0, s, a); \
+    else if (pre == 3) hipLaunchKernelGGL((gemm_lp_kernel<AT_, BT_, false, 3>), grid, block, 0, s, a); \
     else hipLaunchKernelGGL((gemm_lp_kernel<AT_, BT_, false, 0>), grid, block, 0, s, a);     \
   } while (0)
     if (!d.a_trans && d.b_trans) SAVQA_LP1(false, true);

@@ -70,6 +70,10 @@ def _qv_wrows(d: int, dev) -> torch.Tensor:
 # F.normalize clamp decision reads it) and gets gradient in the clamped case, so K stays
 # computed for every row; Q and V only for the question rows (node rows zero).
 PRUNE_L01 = True
+# bf16 / fp8 modes: the encoder FFN's first Linear also writes its ReLU gate as bits
+# (savqa_gemm_lp_desc.bits_out), and the dX of the second Linear reads those instead of the
+# bf16 activations (SAVQA_DT_BITS mask: 1/16 of the bytes). SAVQA_LP_BITS=0: the bf16 mask.
+LP_BITS = os.environ.get("SAVQA_LP_BITS", "1") != "0"
 
 
 # ----------------------------------------------------------------------------- weights
@@ -338,9 +342,12 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
         st1 = _ln_stats(M, dev)
         ops.ln_fwd(o, L["g1"], L["b1"], y1, *st1, r=x, z_out=z1, yb=y1b)
         z2 = _empty(M, d, dev=dev)
+        hbits = None
         if lp is not None:
             h = _bf(M, 4 * d, dev=dev)
-            ops.linear_lp(y1b, Lb["W1"], L["c1"], None, h, relu=True)
+            # the ReLU gate of h as bits (1/16 of h's bytes): the mask of the dX of W2
+            hbits = torch.empty(M, 4 * d // 8, dtype=torch.uint8, device=dev) if LP_BITS else None
+            ops.linear_lp(y1b, Lb["W1"], L["c1"], None, h, relu=True, bits_out=hbits)
             ops.linear_lp(h, Lb["W2"], L["c2"], z2, resid=y1)
         else:
             h = _empty(M, 4 * d, dev=dev)
@@ -351,7 +358,7 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
         st2 = _ln_stats(M, dev)
         fn = _empty(M, dev=dev)
         ops.ln_fwd(z2, L["g2"], L["b2"], xn, *st2, flag=fn, yb=xnb)
-        e.update(qkv=qkv, z1=z1, st1=st1, y1=y1, y1b=y1b, h=h, z2=z2, st2=st2, xb=xb)
+        e.update(qkv=qkv, z1=z1, st1=st1, y1=y1, y1b=y1b, h=h, hbits=hbits, z2=z2, st2=st2, xb=xb)
         s.enc.append(e)
         x, flag, xb = xn, fn, xnb
     s.x6, s.f6, s.x6b = x, flag, xb
@@ -507,7 +514,10 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
             ops.ln_bwd(dx, e["z2"], *e["st2"], L["g2"], dz2, Lg["g2"], Lg["b2"], dzb=dz2b)
             ops.linear_dw_lp(dz2b, e["h"], Lg["W2"], Lg["c2"], rows=M)
             dh = _bf(M, 4 * d, dev=dev)
-            ops.linear_dx_lp(dz2b, Lb["W2"], None, dh, rows=M, mask=e["h"], ldmask=4 * d)
+            if e["hbits"] is not None:
+                ops.linear_dx_lp(dz2b, Lb["W2"], None, dh, rows=M, mask=e["hbits"], ldmask=d // 2)
+            else:
+                ops.linear_dx_lp(dz2b, Lb["W2"], None, dh, rows=M, mask=e["h"], ldmask=4 * d)
             del dz2b
             ops.linear_dw_lp(dh, e["y1b"], Lg["W1"], Lg["c1"], rows=M)
             ops.linear_dx_lp(dh, Lb["W1"], dy1, rows=M, resid=dz2)

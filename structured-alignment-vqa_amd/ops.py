@@ -202,7 +202,7 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
 
 
 # ------------------------------------------------------------------------------ low precision
-DT = {torch.float32: 0, torch.bfloat16: 1, torch.float8_e4m3fn: 2}
+DT = {torch.float32: 0, torch.bfloat16: 1, torch.float8_e4m3fn: 2, torch.uint8: 3}  # uint8: bits
 
 
 def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int, a_trans=False,
@@ -210,7 +210,7 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
             ldc=0, Cb=None, ldcb=0, c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None,
             ldrv=0, rowvec_period=0, resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False,
             alpha=1.0, relu=False, atomic=False, split_k=1, tile_hint=0, c_rows=None,
-            n_store=0, ws=None, colsum_a=None):
+            n_store=0, ws=None, colsum_a=None, bits_out=None, ldbits=0):
     """savqa_gemm_lp_desc for bf16 / fp8 operands (include/savqa.h). ws: split-K partial-slab
     workspace (fp32 tensor), see lp_workspace."""
     d = _lib.GemmLpDesc()
@@ -232,6 +232,7 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
     if ws is not None:
         d.ws, d.ws_elems = _p(ws), int(ws.numel())
     d.colsum_a = _p(colsum_a)
+    d.bits_out, d.ldbits = _p(bits_out), int(ldbits)
     return d
 
 
@@ -341,23 +342,26 @@ def colsum_bf16(X: Tensor, rows: int, cols: int, ldx: int, out: Tensor):
 def linear_lp(X: Tensor, W: Tensor, b: Optional[Tensor], out: Optional[Tensor] = None,
               outb: Optional[Tensor] = None, *, relu=False, rows: Optional[int] = None,
               a_rows=None, rowvec=None, rowvec_period=0, resid=None, c_group=0, c_stride=0,
-              c_offset=0, ldo=None, x_scale=None, w_scale=None):
+              c_offset=0, ldo=None, x_scale=None, w_scale=None, bits_out=None):
     """nn.Linear forward on low-precision operands: X [M][K] and W [N][K] both bf16, or both
     fp8-e4m3 with e8m0 block scales x_scale [M][K/32] / w_scale [N][K/32]; fp32 `out` and/or
-    bf16 `outb` (same row map)."""
+    bf16 `outb` (same row map). bits_out (uint8 [M][N/8], bf16-only output): the output's
+    (> 0) bits, the ReLU gate a later linear_dx_lp reads as its mask."""
     N, K = W.shape
     M = rows if rows is not None else (a_rows.numel() if a_rows is not None else X.numel() // K)
     ld = ldo if ldo is not None else N
     gemm_lp(X, W, M, N, K, lda=K, ldb=K, b_trans=True, a_rows=a_rows, a_scale=x_scale,
             lds_a=K // 32, b_scale=w_scale, lds_b=K // 32, C=out, ldc=ld, Cb=outb, ldcb=ld,
             c_group=c_group, c_stride=c_stride, c_offset=c_offset, bias=b, rowvec=rowvec, ldrv=N,
-            rowvec_period=rowvec_period, resid=resid, ldr=N, relu=relu)
+            rowvec_period=rowvec_period, resid=resid, ldr=N, relu=relu, bits_out=bits_out,
+            ldbits=(bits_out.shape[-1] if bits_out is not None else 0))
 
 
 def linear_dx_lp(dY: Tensor, W: Tensor, dX: Optional[Tensor] = None,
                  dXb: Optional[Tensor] = None, *, rows: int, a_rows=None, mask=None, ldmask=0,
                  mask_arows=False, resid=None):
-    """dX = dY W on bf16 operands (W the bf16 shadow [N][K]); mask: bf16 ReLU gate."""
+    """dX = dY W on bf16 operands (W the bf16 shadow [N][K]); mask: the ReLU gate, bf16 values
+    or a uint8 bit image (linear_lp's bits_out; ldmask in bytes)."""
     N, K = W.shape
     gemm_lp(dY, W, rows, K, N, lda=N, ldb=K, a_rows=a_rows, C=dX, ldc=K, Cb=dXb, ldcb=K,
             mask=mask, ldmask=ldmask, mask_arows=mask_arows, resid=resid, ldr=K)

@@ -262,6 +262,90 @@ def test_bf16_only_output_wide_stores(hint, mask, arows, N):
     assert (Cb[untouched].float() == 7.0).all()
 
 
+def _packbits(x):
+    """(x > 0) as the SAVQA_DT_BITS layout: bit (n & 7) of byte [m][n / 8]."""
+    b = (x > 0).to(torch.uint8).view(x.shape[0], -1, 8)
+    w = (2 ** torch.arange(8, device=x.device, dtype=torch.int32)).view(1, 1, 8)
+    return (b.int() * w).sum(-1).to(torch.uint8)
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("hint", [0, 1, 3, 4, 5])
+@pytest.mark.parametrize("N", [2048, 264])
+def test_bits_out_is_the_relu_gate_of_the_bf16_output(hint, N, fp8):
+    """bits_out (the FFN's first Linear, bias + ReLU, bf16 only): bit (n & 7) of byte [m][n/8]
+    is (Cb > 0), through a c_group row map and M / N edge tiles, on every kernel variant (fp8:
+    the 128 x 128 fp8 kernel)."""
+    O = ops()
+    if fp8 and hint not in (0, 1):
+        pytest.skip("fp8 runs the 128 x 128 kernel only")
+    M, K, T, G = 1300, 512 if fp8 else 320, 50, 14
+    A, W = bf((M, K), 31), bf((N, K), 32)
+    bias = torch.randn(N, device=dev)
+    Cn = M // G * T + T
+    Cb = torch.zeros(Cn, N, device=dev, dtype=torch.bfloat16)
+    bits = torch.full((Cn, N // 8), 0xA5, device=dev, dtype=torch.uint8)
+    kw = dict(Cb=Cb, ldcb=N, c_group=G, c_stride=T, c_offset=3, bias=bias, relu=True,
+              bits_out=bits, ldbits=N // 8, tile_hint=hint)
+    if fp8:
+        qa, sa = torch.empty(M, K, device=dev, dtype=torch.float8_e4m3fn), \
+            torch.empty(M, K // 32, device=dev, dtype=torch.uint8)
+        qw, sw = torch.empty(N, K, device=dev, dtype=torch.float8_e4m3fn), \
+            torch.empty(N, K // 32, device=dev, dtype=torch.uint8)
+        O.quant_fp8(A.float(), M, K, K, qa, K, sa, K // 32)
+        O.quant_fp8(W.float(), N, K, K, qw, K, sw, K // 32)
+        O.gemm_lp(qa, qw, M, N, K, lda=K, ldb=K, b_trans=True, a_scale=sa, lds_a=K // 32,
+                  b_scale=sw, lds_b=K // 32, **kw)
+    else:
+        O.gemm_lp(A, W, M, N, K, lda=K, ldb=K, b_trans=True, **kw)
+    crow = (torch.arange(M, device=dev) // G) * T + torch.arange(M, device=dev) % G + 3
+    assert float(Cb[crow].float().abs().max()) > 0
+    assert torch.equal(bits[crow].cpu(), _packbits(Cb[crow].float()).cpu())
+    untouched = torch.ones(Cn, dtype=torch.bool, device=dev)
+    untouched[crow] = False
+    assert (bits[untouched] == 0xA5).all()
+
+
+@pytest.mark.parametrize("hint", [0, 1, 3, 4, 5])
+@pytest.mark.parametrize("arows,M,N", [(False, 1300, 2048), (False, 37376 // 4, 2048),
+                                       (True, 1300, 264), (False, 700, 136)])
+def test_bits_mask_equals_the_bf16_mask(hint, arows, M, N):
+    """The ReLU-backward dX of a bf16-only output gated by a SAVQA_DT_BITS mask (prefetched
+    before the k-loop on the 128 x 128 kernel, per epilogue on the 256-row kernels) is bit for
+    bit the output gated by the bf16 values the bits came from, through the mask's A-row
+    gather."""
+    O = ops()
+    K = 512
+    src = bf((M + 200, K), 35)
+    rows = torch.randperm(M + 200, device=dev)[:M].contiguous() if arows else None
+    A = src if arows else src[:M].contiguous()
+    W = bf((K, N), 36)
+    h = torch.relu(bf((M + 200 if arows else M, N), 37).float()).to(torch.bfloat16)
+    hb = _packbits(h.float())
+    outs = []
+    for mk, ld in ((h, N), (hb, N // 8)):
+        Cb = torch.full((M, N), 7.0, device=dev, dtype=torch.bfloat16)
+        O.gemm_lp(A, W, M, N, K, lda=K, ldb=N, a_rows=rows, Cb=Cb, ldcb=N, mask=mk, ldmask=ld,
+                  mask_arows=arows, tile_hint=hint)
+        outs.append(Cb.cpu())
+    assert torch.equal(outs[0], outs[1])
+    assert float((outs[1] == 0).float().mean()) > 0.3   # the gate took effect
+    Ad = (src[rows] if arows else A).double()
+    ref = torch.where((h[rows] if arows else h).double() > 0, Ad @ W.double(), 0.0)
+    assert rel(outs[1].float(), ref) < 8e-3
+
+
+def test_bits_need_the_wide_bf16_epilogue():
+    """A bit mask or bits_out with an fp32 output (no wide bf16 epilogue) is refused."""
+    O = ops()
+    A, W = bf((256, 128), 38), bf((256, 128), 39)
+    C = torch.empty(256, 256, device=dev)
+    bits = torch.zeros(256, 32, device=dev, dtype=torch.uint8)
+    for kw in (dict(mask=bits, ldmask=32), dict(bits_out=bits, ldbits=32)):
+        d = O.lp_desc(A, W, 256, 256, 128, lda=128, ldb=128, b_trans=True, C=C, ldc=256, **kw)
+        assert O._lib.load().savqa_gemm_lp_supported(ctypes.byref(d)) == 0
+
+
 @pytest.mark.parametrize("rows,cols,ld", [(5, 520, 520), (37376, 2048, 2048), (1000, 300, 300),
                                            (777, 512, 1024)])
 def test_colsum_bf16_shapes(rows, cols, ld):

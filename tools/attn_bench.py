@@ -141,6 +141,9 @@ def q1s_main(args):
                                                   o, d, st),
                  lambda: ops.gattn_bwd_q1s(q, d, kv, ld, kv[:, d:], ld, G, kf, qf, B, T, H, dout,
                                            d, st, dq, d, dkv, ld, dkv[:, d:], ld)),
+                ("q1", lambda: ops.gattn_fwd(q, d, kv, ld, kv[:, d:], ld, G, kf, qf, B, 1, T, H, o, d),
+                 lambda: ops.gattn_bwd(q, d, kv, ld, kv[:, d:], ld, G, kf, qf, B, 1, T, H, dout, d,
+                                       dq, d, dkv, ld, dkv[:, d:], ld)),
                 ("flash", lambda: ops.gattn_fwd_flash(q, d, kv, ld, kv[:, d:], ld, G, kf, qf, B, 1,
                                                       T, H, o, d, st),
                  lambda: ops.gattn_bwd_flash(q, d, kv, ld, kv[:, d:], ld, G, kf, qf, B, 1, T, H,

@@ -44,6 +44,12 @@ def bf16_case(lay, m, n, k, out, hint=0):
         mk = torch.randn(m, n, device=dev).to(BF)
         f = lambda: ops.gemm_lp(A, B, m, n, k, Cb=Cb, ldcb=n, mask=mk, ldmask=n, tile_hint=hint,
                                 **kw)
+    elif out == "bf16bits":  # the same gate as a SAVQA_DT_BITS image (engine.LP_BITS)
+        Cb = torch.empty(m, n, device=dev, dtype=BF)
+        w = 2 ** torch.arange(8, device=dev, dtype=torch.int32)
+        mk = ((torch.randn(m, n // 8, 8, device=dev) > 0).int() * w).sum(-1).to(torch.uint8)
+        f = lambda: ops.gemm_lp(A, B, m, n, k, Cb=Cb, ldcb=n, mask=mk, ldmask=n // 8,
+                                tile_hint=hint, **kw)
     elif out == "f32resid":  # FFN conv2 forward / dX with the residual: fp32 out + resid
         C = torch.empty(m, n, device=dev)
         R = torch.randn(m, n, device=dev)
@@ -87,7 +93,8 @@ def main():
              ("dx qkv", "NN", Ms, 512, 1536, "f32"), ("dx kv", "NN", Ms, 512, 6144, "f32"),
              ("dw qkv", "TN", 1536, 512, Ms, "atomic"), ("dw ffn1", "TN", 2048, 512, Ms, "atomic"),
              ("dw ffn2", "TN", 512, 2048, Ms, "atomic"), ("dw kv", "TN", 6144, 512, Ms, "atomic"),
-             ("dx ffn2 m", "NN", Ms, 2048, 512, "bf16mask"), ("fwd ffn2 r", "NT", Ms, 512, 2048, "f32resid"),
+             ("dx ffn2 m", "NN", Ms, 2048, 512, "bf16mask"), ("dx ffn2 b", "NN", Ms, 2048, 512, "bf16bits"),
+             ("fwd ffn2 r", "NT", Ms, 512, 2048, "f32resid"),
              ("dx ffn1 r", "NN", Ms, 512, 2048, "f32resid")]
     hints = [0] + ([1, 3, 5] if "--variants" in sys.argv else [])
     if "--square" in sys.argv:  # structure check at 8192^3 / 4096^3 (cdna guide's reference shapes)
