@@ -1,6 +1,6 @@
 set -eo pipefail
-SAVQA_BENCH_PREC=fp32x6 timeout -k 10 300 python -u tools/gemm_bench.py 2>&1 | grep -v amdgpu.ids > gpurun_out/x6_shapes.txt
-cat gpurun_out/x6_shapes.txt
-bash tools/profile_round.sh r05 cfg4
-bash tools/profile_round.sh r05 cfg5
-bash tools/profile_round.sh r05 rel
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_cfg2.json 2> gpurun_out/bench_cfg2.err
+for w in cfg3 cfg4 cfg5 rel; do
+  timeout -k 10 300 python -u bench.py --workload $w --no-cpu-baseline > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err
+done
+for w in cfg2 cfg3 cfg4 cfg5 rel; do python -c "import json;d=json.load(open('gpurun_out/bench_$w.json'));r=d['roofline'];print('$w', d['value'], d['ms_per_step'], r['kernel'], r['frac'], r.get('traffic'), (d.get('cpu_baseline') or {}).get('value'))"; done
