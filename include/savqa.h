@@ -166,6 +166,11 @@ int savqa_gemm_lp_supported(const savqa_gemm_lp_desc* d);
  * out[1] = K slices, out[2] = workgroups, out[3] = epilogue operand prefetched under the
  * last k-tile (variant 1: 0 none, 1 the residual, 2 the bf16 mask). */
 int savqa_gemm_lp_plan(const savqa_gemm_lp_desc* d, int32_t* out);
+/* fp32 elements of d.ws that let the launch of *d store partial slabs instead of adding fp32
+ * atomics: split-K weight gradients (slices x M x N) and the split-off last round of tiles of
+ * long-K launches into fp32 C (tail slices x rows x N, then one ordered reduce that assigns
+ * those rows: deterministic, no zero fill). 0 = no slab use. */
+int64_t savqa_gemm_lp_ws_elems(const savqa_gemm_lp_desc* d);
 
 /* Conversions feeding the low-precision operands (output row of input row r: ro(r) =
  * (r / group)*stride + r % group + offset, or r when group <= 0 -- e.g. the question rows

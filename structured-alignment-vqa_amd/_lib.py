@@ -87,6 +87,7 @@ _SIGS = {
     "savqa_gemm_lp": [c_p, C.POINTER(GemmLpDesc)],
     "savqa_gemm_lp_supported": [C.POINTER(GemmLpDesc)],
     "savqa_gemm_lp_plan": [C.POINTER(GemmLpDesc), c_p],
+    "savqa_gemm_lp_ws_elems": [C.POINTER(GemmLpDesc)],
     "savqa_cast_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64],
     "savqa_widen_bf16": [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64],
     "savqa_mark_rows": [c_p, c_p, c_i64, c_i64, c_p],
@@ -164,7 +165,7 @@ _SIGS = {
 }
 
 _I64_RET = {"savqa_ln_bwd_workspace_bytes", "savqa_gemm_ws_elems", "savqa_gattn_q1s_ws_bytes",
-            "savqa_rel_loss_ws_bytes"}
+            "savqa_rel_loss_ws_bytes", "savqa_gemm_lp_ws_elems"}
 
 _lib = None
 

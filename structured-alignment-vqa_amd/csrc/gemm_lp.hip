@@ -68,6 +68,8 @@ struct LpArgs {
   int full, tail_t0, tail_f;
   int64_t tail_kchunk;
   float* slab;            // split-K partial slabs [slice][M][N] (savqa_gemm_lp_desc.ws), or null
+  float* tail_slab;       // tail-split partial slabs [slice][M - tail_r0][N] (same workspace),
+  int64_t tail_r0;        // or null: the tail tiles' slices then add into C atomically
   int dbg;                // diagnostic builds only (SAVQA_LP_DIAG=1, tools/lp_bench.py --dbg):
                           // 1 = skip the MFMAs, 2 = skip the k-loop DMAs, 4 = skip the
                           // epilogue; production builds compile every test of it away
@@ -598,7 +600,8 @@ __device__ __forceinline__ void lp_epilogue(const savqa_gemm_lp_desc& d, f4 (&ac
 // vector / residual on slice 0; N % 4 == 0.
 __device__ __forceinline__ void lp_epilogue_slab(const savqa_gemm_lp_desc& d, const f4 (&acc)[4][4],
                                                  int64_t row0, int64_t col0, bool first_split,
-                                                 int lane, float* __restrict__ slab) {
+                                                 int lane, float* __restrict__ slab,
+                                                 int64_t r0 = 0) {
   const int ri = lane & 15, g = lane >> 4;
   f4 bv[4];
 #pragma unroll
@@ -626,29 +629,31 @@ __device__ __forceinline__ void lp_epilogue_slab(const savqa_gemm_lp_desc& d, co
           if (d.resid) v[r] += d.resid[m * d.ldr + n + r];
         }
       }
-      *reinterpret_cast<f4*>(slab + m * d.N + n) = v;
+      *reinterpret_cast<f4*>(slab + (m - r0) * d.N + n) = v;
     }
   }
 }
 
-// C[m][n] += sum over the ns slabs (fixed order), four columns per thread
+// C[r0 + m][n] (+)= sum over the ns slabs [ns][rows][N] (fixed order), four columns per thread;
+// assign: the split-off tail tiles' rows (C = sum), else split-K accumulation (C += sum)
 __global__ __launch_bounds__(256) void lp_slab_reduce_kernel(const float* __restrict__ slab, int ns,
-                                                             int64_t M, int64_t N,
+                                                             int64_t rows, int64_t N,
                                                              float* __restrict__ C, int64_t ldc,
-                                                             int vec) {
+                                                             int vec, int64_t r0, int assign) {
   const int64_t n4 = N / 4;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= M * n4) return;
+  if (t >= rows * n4) return;
   const int64_t m = t / n4, n = 4 * (t - m * n4);
-  const int64_t plane = M * N;
+  const int64_t plane = rows * N;
   f4 acc = *reinterpret_cast<const f4*>(slab + m * N + n);
   for (int k = 1; k < ns; ++k) acc += *reinterpret_cast<const f4*>(slab + k * plane + m * N + n);
-  float* cp = C + m * ldc + n;
+  float* cp = C + (r0 + m) * ldc + n;
   if (vec) {
-    *reinterpret_cast<f4*>(cp) += acc;
+    f4* c4 = reinterpret_cast<f4*>(cp);
+    *c4 = assign ? acc : *c4 + acc;
   } else {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) cp[r] += acc[r];
+    for (int r = 0; r < 4; ++r) cp[r] = assign ? acc[r] : cp[r] + acc[r];
   }
 }
 
@@ -928,6 +933,9 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   if (PRE == 0 && !FP8 && args.slab && !tail)
     lp_epilogue_slab(d, acc, m0 + wm * 64, n0 + wn * 64, first_split, lane,
                      args.slab + (int64_t)slice * d.M * d.N);
+  else if (tail && args.tail_slab)
+    lp_epilogue_slab(d, acc, m0 + wm * 64, n0 + wn * 64, first_split, lane,
+                     args.tail_slab + (int64_t)slice * (d.M - args.tail_r0) * d.N, args.tail_r0);
   else if (tail)
     lp_epilogue<4, 4>(d, acc, smem + wave * 16384, m0 + wm * 64, n0 + wn * 64, first_split, lane,
                       64, -1, true);
@@ -1353,7 +1361,18 @@ struct LpPlan {
   // [zero_row0, M) of C zero-filled first; tail_f = 1: none
   int tail_f;
   int64_t tail_t0, tail_per, zero_row0;
+  bool tail_slab;  // the tail slices store partial slabs (d.ws) instead of adding atomically
 };
+
+// tail splits need >= 64 k-tiles: with atomic adds into a zero-filled C the epilogue and the
+// fill cost a third of a K = 512 launch (K = 2048 shapes were 20-40 % slower); with partial
+// slabs and one ordered reduce (deterministic, no fill) K = 2048 / 1536 shapes were 0-6 %
+// slower and cfg 3 1.2 % (tools/lp_bench.py, interleaved), K = 6144 7 % faster than atomics
+#ifndef SAVQA_LP_TAIL_MIN_NK_SLAB
+#define SAVQA_LP_TAIL_MIN_NK_SLAB 64
+#endif
+constexpr int LP_TAIL_MIN_NK = 64, LP_TAIL_MIN_NK_SLAB = SAVQA_LP_TAIL_MIN_NK_SLAB;
+static bool lp_al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
   LpPlan p{};
@@ -1423,23 +1442,47 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
     const char* r1 = (const char*)(d.resid + (d.M - 1) * d.ldr + d.N);
     if (r0 < c1 && c0 < r1) tail_ok = false;
   }
-  if (tail_ok && p.tiles > slots && nk >= 64) {
+  // slabs: a workspace was given (its size is checked below) and the slab rows are whole f4s
+  const bool slab_ok = d.ws && d.N % 4 == 0 && lp_al16(d.ws);
+  if (tail_ok && p.tiles > slots && nk >= (slab_ok ? LP_TAIL_MIN_NK_SLAB : LP_TAIL_MIN_NK)) {
     const int64_t tn = (d.N + p.bn - 1) / p.bn;
     int64_t r = p.tiles % slots;
-    r = (r + tn - 1) / tn * tn;  // whole rows of tiles: one contiguous zero-fill
+    r = (r + tn - 1) / tn * tn;  // whole rows of tiles: one contiguous zero-fill / slab
     if (r > 0 && r < p.tiles) {
       int64_t f = slots / r;
       if (f > nk / 4) f = nk / 4;
       if (f >= 2) {
-        p.tail_per = (nk + f - 1) / f;
-        p.tail_f = (int)((nk + p.tail_per - 1) / p.tail_per);
-        p.tail_t0 = p.tiles - r;
-        p.zero_row0 = (p.tail_t0 / tn) * bm;
-        p.pre = 0;  // the prefetching instantiations have no tail path
+        const int64_t per = (nk + f - 1) / f;
+        const int tf = (int)((nk + per - 1) / per);
+        const int64_t r0 = ((p.tiles - r) / tn) * bm;
+        const bool slab = slab_ok && d.ws_elems >= (int64_t)tf * (d.M - r0) * d.N;
+        if (slab || nk >= LP_TAIL_MIN_NK) {
+          p.tail_per = per;
+          p.tail_f = tf;
+          p.tail_t0 = p.tiles - r;
+          p.zero_row0 = r0;
+          p.tail_slab = slab;
+          p.pre = 0;  // the prefetching instantiations have no tail path
+        }
       }
     }
   }
   return p;
+}
+
+// fp32 workspace elements the plan of d can use for partial slabs (split-K and tail split)
+static int64_t lp_ws_need(const savqa_gemm_lp_desc& d0) {
+  savqa_gemm_lp_desc d = d0;
+  static float probe[4] __attribute__((aligned(16)));
+  d.ws = probe;                 // any aligned non-null pointer: the plan only tests it
+  d.ws_elems = INT64_MAX;
+  const LpPlan p = lp_plan(d);
+  int64_t need = 0;
+  if (p.var == 1 && d.a_type != SAVQA_DT_FP8 && p.nsplit > 1 && d.C && !d.Cb && !d.relu &&
+      !d.mask && !d.c_rows && d.n_store == 0 && d.c_group <= 0 && d.N % 4 == 0)
+    need = (int64_t)p.nsplit * d.M * d.N;
+  if (p.tail_slab) need = std::max(need, (int64_t)p.tail_f * (d.M - p.zero_row0) * d.N);
+  return need;
 }
 
 }  // namespace savqa
@@ -1449,6 +1492,12 @@ using namespace savqa;
 extern "C" int savqa_gemm_lp_supported(const savqa_gemm_lp_desc* d) {
   const char* msg = nullptr;
   return d && lp_ok(*d, &msg) ? 1 : 0;
+}
+
+extern "C" int64_t savqa_gemm_lp_ws_elems(const savqa_gemm_lp_desc* d) {
+  const char* msg = nullptr;
+  if (!d || !lp_ok(*d, &msg)) return 0;
+  return lp_ws_need(*d);
 }
 
 extern "C" int savqa_gemm_lp_plan(const savqa_gemm_lp_desc* d, int32_t* out) {
@@ -1492,8 +1541,10 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
                      !d.mask && !d.c_rows && d.n_store == 0 && d.c_group <= 0 && d.N % 4 == 0 &&
                      ((uintptr_t)d.ws & 15) == 0 && d.ws_elems >= (int64_t)p.nsplit * d.M * d.N;
   a.slab = slabs ? d.ws : nullptr;
+  a.tail_slab = p.tail_slab ? d.ws : nullptr;
+  a.tail_r0 = p.tail_slab ? p.zero_row0 : 0;
   hipStream_t s = as_stream(stream);
-  if (p.zero_row0 >= 0 &&
+  if (p.zero_row0 >= 0 && !p.tail_slab &&
       hipMemset2DAsync(d.C + p.zero_row0 * d.ldc, d.ldc * sizeof(float), 0, d.N * sizeof(float),
                        d.M - p.zero_row0, s) != hipSuccess)
     return fail(SAVQA_EUNSUP, "savqa_gemm_lp: tail zero-fill failed");
@@ -1545,11 +1596,14 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   if (d.colsum_a && var != 1) {  // the fused column sum lives in the 128 x 128 kernel only
     if (int rc = savqa_colsum_bf16(stream, d.A, d.K, d.M, d.lda, d.colsum_a)) return rc;
   }
-  if (slabs) {
+  if (slabs || p.tail_slab) {
+    if (int rc = check_launch("savqa_gemm_lp")) return rc;
     const int vec = (d.ldc % 4 == 0) && (((uintptr_t)d.C & 15) == 0);
-    const int64_t n = d.M * (d.N / 4);
+    const int64_t r0 = p.tail_slab ? p.zero_row0 : 0, rows = d.M - r0;
+    const int64_t n = rows * (d.N / 4);
     hipLaunchKernelGGL(lp_slab_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                       d.ws, p.nsplit, d.M, d.N, d.C, d.ldc, vec);
+                       d.ws, p.tail_slab ? p.tail_f : p.nsplit, rows, d.N, d.C, d.ldc, vec, r0,
+                       p.tail_slab ? 1 : 0);
   }
   return check_launch("savqa_gemm_lp");
 }

@@ -238,6 +238,7 @@ def lp_desc(A: Tensor, B: Tensor, M: int, N: int, K: int, *, lda: int, ldb: int,
 
 _ws = {}
 LP_SLABS = os.environ.get("SAVQA_LP_SLABS", "1") != "0"  # cfg 3: 17.86k -> 18.32k QA-samples/s
+LP_TAIL_SLABS = os.environ.get("SAVQA_LP_TAIL_SLABS", "1") != "0"
 
 
 def _workspace(need: int, dev) -> Tensor:
@@ -252,13 +253,10 @@ def _workspace(need: int, dev) -> Tensor:
 
 
 def lp_workspace(d, dev) -> Optional[Tensor]:
-    """The split-K slab workspace a savqa_gemm_lp launch of d needs (slices x M x N fp32)
-    (None when d does not split K)."""
-    plan = (C.c_int32 * 4)()
-    call("savqa_gemm_lp_plan", C.byref(d), C.cast(plan, C.c_void_p))
-    if plan[1] <= 1:
-        return None
-    return _workspace(int(plan[1]) * int(d.M) * int(d.N), dev)
+    """The partial-slab workspace a savqa_gemm_lp launch of d can use (split-K: slices x M x N
+    fp32; a split-off last round of tiles: tail slices x rows x N), None when it uses none."""
+    need = int(_lib.load().savqa_gemm_lp_ws_elems(C.byref(d)))
+    return _workspace(need, dev) if need > 0 else None
 
 
 def lp_variant(d) -> str:
@@ -282,9 +280,11 @@ def lp_supported(d) -> bool:
 
 def gemm_lp(*args, slabs=False, **kw):
     """Low-precision-operand MFMA GEMM (savqa_gemm_lp): same arguments as lp_desc; slabs: give a
-    split-K launch its partial-slab workspace (no fp32 atomics)."""
+    split-K launch its partial-slab workspace (no fp32 atomics). A long-K launch into fp32 C
+    whose last round of tiles is split over K gets its tail workspace unless
+    SAVQA_LP_TAIL_SLABS=0 (those slices then add atomically into a zero-filled C)."""
     d = lp_desc(*args, **kw)
-    if slabs and LP_SLABS:
+    if LP_SLABS and (slabs or (not d.atomic and LP_TAIL_SLABS)):
         ws = lp_workspace(d, args[0].device)
         if ws is not None:
             d.ws, d.ws_elems = _p(ws), int(ws.numel())

@@ -493,22 +493,23 @@ def _lp_plan(O, d):
     return list(plan)
 
 
+@pytest.mark.parametrize("mode,K", [("atomic", 6144), ("slab", 6144), ("slab", 4096)])
 @pytest.mark.parametrize("lay,epi,ldc_pad", [("NT", "resid", 0), ("NN", "bias", 8),
                                              ("NT", "rowvec", 0), ("NN", "resid_bias", 16)])
-def test_bf16_tail_split_last_round(lay, epi, ldc_pad):
+def test_bf16_tail_split_last_round(lay, epi, ldc_pad, mode, K, monkeypatch):
     """Tail split: the tiles of the last, partial round of workgroups (M = 18688, N = 512:
-    584 tiles over 512 slots, K = 6144) are split over K with atomic fp32 adds into a
-    zero-filled C;
-    bias / residual / row vector are added by slice 0 only, and a strided C (ldc > N) keeps
-    its other columns."""
+    584 tiles over 512 slots) are split over K -- with fp32 atomic adds into a zero-filled C
+    (K >= 64 k-tiles, no workspace), or into partial slabs reduced in slice order (the
+    workspace ops.gemm_lp attaches): bias / residual / row vector are added by
+    slice 0 only, a strided C (ldc > N) keeps its other columns, and the slab form is
+    bit-identical run to run."""
     O = ops()
-    M, N, K = 18688, 512, 6144
+    monkeypatch.setattr(O, "LP_TAIL_SLABS", mode == "slab")
+    M, N = 18688, 512
     bt = lay[1] == "T"
     A = bf((M, K), 31)
     B = bf((N, K) if bt else (K, N), 32)
     ldc = N + ldc_pad
-    Cfull = torch.full((M, ldc), 7.0, device=dev)
-    C = Cfull[:, :N]
     kw = {}
     ref = A.double() @ (B.t() if bt else B).double()
     if "resid" in epi:
@@ -524,16 +525,27 @@ def test_bf16_tail_split_last_round(lay, epi, ldc_pad):
         rv = torch.randn(P, N, device=dev)
         kw.update(rowvec=rv, ldrv=N, rowvec_period=P)
         ref = ref + rv.double().repeat(M // P + 1, 1)[:M]
-    d = O.lp_desc(A, B, M, N, K, lda=K, ldb=K if bt else N, b_trans=bt, C=C, ldc=ldc, **kw)
-    plan = _lp_plan(O, d)
-    tiles = ((M + 127) // 128) * (N // 128)  # 146 x 4
-    assert plan[0] == 1 and plan[1] == 1 and plan[2] > tiles, plan  # tail blocks present
-    O.gemm_lp(A, B, M, N, K, lda=K, ldb=K if bt else N, b_trans=bt, C=C, ldc=ldc, **kw)
-    torch.cuda.synchronize()
-    err = float((C.double() - ref).abs().max() / ref.abs().max())
-    assert err < 2e-5, err
-    if ldc_pad:
-        assert bool((Cfull[:, N:] == 7.0).all())
+    outs = []
+    for _ in range(2 if mode == "slab" else 1):
+        Cfull = torch.full((M, ldc), 7.0, device=dev)
+        C = Cfull[:, :N]
+        d = O.lp_desc(A, B, M, N, K, lda=K, ldb=K if bt else N, b_trans=bt, C=C, ldc=ldc, **kw)
+        if mode == "slab":
+            ws = O.lp_workspace(d, dev)
+            assert ws is not None
+            d.ws, d.ws_elems = ws.data_ptr(), ws.numel()
+        plan = _lp_plan(O, d)
+        tiles = ((M + 127) // 128) * (N // 128)  # 146 x 4
+        assert plan[0] == 1 and plan[1] == 1 and plan[2] > tiles, plan  # tail blocks present
+        O.gemm_lp(A, B, M, N, K, lda=K, ldb=K if bt else N, b_trans=bt, C=C, ldc=ldc, **kw)
+        torch.cuda.synchronize()
+        err = float((C.double() - ref).abs().max() / ref.abs().max())
+        assert err < 2e-5, err
+        if ldc_pad:
+            assert bool((Cfull[:, N:] == 7.0).all())
+        outs.append(C.clone())
+    if mode == "slab":
+        assert torch.equal(outs[0], outs[1])
 
 
 def test_fp8_cfg5_region_feature_shape():
