@@ -1392,9 +1392,13 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
   if (!fp8) {
     const bool split = d.split_k > 1 || d.split_k < 0;
     const int h = d.tile_hint & 255;
+    // (round 5, tools/lp_bench.py --variants: the 128 x 128 kernel with split-K slabs beats the
+    // 256 x 256 one with atomics on the M = 6144 dW, 322 vs 344 us; the 256 x 256 kernel wins
+    // the N = 2048 forward too, 104 vs 109 us)
+    const bool slab_dw = split && d.ws && !d.mask && !d.relu && !d.Cb && d.N % 4 == 0;
     if (h == 1 || h == 3 || h == 4 || h == 5) p.var = h;
-    else if (d.N >= 4096 || (split && d.a_trans && d.M >= 4096 && d.N >= 256) ||
-             (!d.a_trans && !d.b_trans && d.N >= 2048 && d.M >= 8192))
+    else if (d.N >= 4096 || (split && d.a_trans && d.M >= 4096 && d.N >= 256 && !slab_dw) ||
+             (!d.a_trans && d.N >= 2048 && d.M >= 8192))
       p.var = 5;
   }
   const int bm = p.var == 1 ? 128 : 256;
