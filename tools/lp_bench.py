@@ -96,7 +96,7 @@ def main():
              ("dx ffn2 m", "NN", Ms, 2048, 512, "bf16mask"), ("dx ffn2 b", "NN", Ms, 2048, 512, "bf16bits"),
              ("fwd ffn2 r", "NT", Ms, 512, 2048, "f32resid"),
              ("dx ffn1 r", "NN", Ms, 512, 2048, "f32resid")]
-    hints = [0] + ([1, 3, 5] if "--variants" in sys.argv else [])
+    hints = [0] + ([1, 3, 4, 5] if "--variants" in sys.argv else [])
     if "--square" in sys.argv:  # structure check at 8192^3 / 4096^3 (cdna guide's reference shapes)
         hints = [1, 3, 5]
         cases = [(f"sq{n}", lay, n, n, n, "bf16") for n in (4096, 8192) for lay in ("NT", "NN", "TN")]
