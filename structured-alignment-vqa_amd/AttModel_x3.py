@@ -350,8 +350,11 @@ class AttModel(nn.Module):
         if not self.only_obj:  # relation branch inputs (micro_negative_rel ids are unused, :391)
             tensors = tensors + (i64(micro_positive_rel), i64(micro_positive_rel_loc),
                                  i64(micro_negative_rel_loc))
-            self._check_relation_locs(tensors[-2], tensors[-1], vis_fea.shape[1],
-                                      macro_ipt.shape[1], tensors[-3].shape[1])
+            # the bounds check runs on a side stream; the engine waits for its verdict only
+            # before launching the first kernel that reads these tables
+            self._engine.pending_rel_check = self._check_relation_locs(
+                tensors[-2], tensors[-1], vis_fea.shape[1], macro_ipt.shape[1],
+                tensors[-3].shape[1])
         live = self._live_params()
         red = self.__dict__.get("_reducer")
         if red is not None and live:
@@ -363,25 +366,53 @@ class AttModel(nn.Module):
     def _check_relation_locs(self, pos, neg, n_obj, n_macro, n_rel):
         """The reference indexes rels_bilinear / new_macro_ipt with these columns
         (AttModel_x3.py:401-437) and fails with IndexError on a bad one; the kernels would
-        read outside their buffers instead, so the listed rows are bounds-checked here
-        (one device reduction + one host read per relation-mode step)."""
+        read outside their buffers instead, so the listed rows are bounds-checked: one device
+        reduction on a side stream (after the producers of the tables on the caller's stream)
+        into pinned host memory. Returns the wait: it raises IndexError for a bad table and
+        synchronises with that reduction only -- a host read of the flag right here stalled the
+        host until the GPU had drained the previous step, ~1.6 ms of the relation workload's
+        step of launches the GPU then waited for. Shape errors raise at once."""
         nrel = self.MIL_NCE.num_relations
+        dev = pos.device
+        cur = torch.cuda.current_stream(dev)
+        st = self.__dict__.get("_rel_check_stream")
+        if st is None or st.device != dev:
+            st = torch.cuda.Stream(device=dev)
+            object.__setattr__(self, "_rel_check_stream", st)
+            object.__setattr__(self, "_rel_check_host", torch.zeros(1, dtype=torch.bool,
+                                                                  pin_memory=True))
+        flag = self._rel_check_host
         bad = []
         for loc, w in ((pos, 5), (neg, 4)):
             if loc.numel() == 0:
                 continue
             if loc.dim() != 3 or loc.shape[2] < w:
                 raise IndexError(f"relation locations need shape (B, L, >={w}), got {tuple(loc.shape)}")
-            v = loc[..., 3] >= 0
-            b = (loc[..., 0] < 0) | (loc[..., 0] >= n_obj) | (loc[..., 1] < 0) | \
-                (loc[..., 1] >= n_obj) | (loc[..., 2] < 0) | (loc[..., 2] >= nrel) | \
-                (loc[..., 3] >= n_macro)
-            if w == 5:
-                b = b | (loc[..., 4] < 0) | (loc[..., 4] >= n_rel)
-            bad.append((v & b).any())
-        if bad and bool(torch.stack(bad).any()):
-            raise IndexError("relation location out of range (objects / categories "
-                             f"< {nrel} / macro nodes / positive words)")
+            bad.append((loc, w))
+        if not bad:
+            return lambda: None
+        st.wait_stream(cur)
+        with torch.cuda.stream(st):
+            flags = []
+            for loc, w in bad:
+                loc.record_stream(st)
+                v = loc[..., 3] >= 0
+                b = (loc[..., 0] < 0) | (loc[..., 0] >= n_obj) | (loc[..., 1] < 0) | \
+                    (loc[..., 1] >= n_obj) | (loc[..., 2] < 0) | (loc[..., 2] >= nrel) | \
+                    (loc[..., 3] >= n_macro)
+                if w == 5:
+                    b = b | (loc[..., 4] < 0) | (loc[..., 4] >= n_rel)
+                flags.append((v & b).any())
+            flag.copy_(torch.stack(flags).any().reshape(1), non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(st)
+
+        def wait():
+            done.synchronize()
+            if bool(flag[0]):
+                raise IndexError("relation location out of range (objects / categories "
+                                 f"< {nrel} / macro nodes / positive words)")
+        return wait
 
     def _live_params(self):
         """The live Parameters (those the backward writes gradients for) when a graph is being

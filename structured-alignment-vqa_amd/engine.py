@@ -650,7 +650,7 @@ class MilSaved:
 
 def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb, T_syb: int,
                 mil_out: torch.Tensor, eps: float = 1e-6, rel=None,
-                mil_rel_out: Optional[torch.Tensor] = None, lp=None) -> MilSaved:
+                mil_rel_out: Optional[torch.Tensor] = None, lp=None, rel_check=None) -> MilSaved:
     """MIL_NCE.forward (AttModel_x3.py:352-441): the only_obj branch, plus the relation
     branch (:382-437) when rel = (pos_rel [B,Lp], pos_loc [B,Lp,5], neg_loc [B,Ln,4]).
     Writes relu(new_macro W_ipt^T + b) into the node rows of the syb stack's cat buffer
@@ -698,6 +698,8 @@ def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb
     ops.mil_fwd(s.Pf, s.Nf, s.vv, omask, B * Nv, K, Hm, eps, obj, ws, mil_out)
     ops.index_put_rows(s.loc, B, Nv, Ns, Hm, obj, s.macro)
     s.obj = obj
+    if rel_check is not None:
+        rel_check()  # the tables' bounds verdict, before the first kernel that reads them
     if rel is not None:
         s.rel = _rel_forward(W, s, rel, Ns, Hm, eps, mil_rel_out)
     if lp is not None:
@@ -1003,6 +1005,9 @@ class ModelEngine:
         self.gemm_precision = gemm_precision
         self.nb, self.d, self.H = num_blocks, hidden, heads
         self._shadow = None
+        # AttModel's relation bounds check: a wait that raises for a bad table, called before
+        # the first relation kernel is launched (set per forward, consumed by _forward)
+        self.pending_rel_check = None
         self.rebind()
 
     @property
@@ -1167,6 +1172,17 @@ class ModelEngine:
         s_vis, s_syb = self._streams(dev)
         s_vis.wait_stream(main)
         s_syb.wait_stream(main)
+        # the visual stack reads no relation table: its launches go first, so the relation
+        # bounds check (AttModel._check_relation_locs) has landed by the time the relation
+        # branch needs its verdict (mil_forward), and the GPU has the visual stack's work
+        with torch.cuda.stream(s_vis):
+            if lp_vis is None:
+                cat_vis = _empty(B * Tv, Dv, dev=dev)
+                ops.copy_rows(vis.reshape(B * Nv, Dv), B * Nv, Dv, Dv, cat_vis, Dv, Nv, Tv, 0)
+            sv = stack_forward(self.vis, cat_vis, B, Nv, Lq, inp["q_ipt"], inp["vis_mask"],
+                               inp["q_mask"], inp["q_graph"], None, decMask, H, d, drop,
+                               VIS_SITES, lp=lp_vis)
+        check, self.pending_rel_check = self.pending_rel_check, None
         with torch.cuda.stream(s_syb):
             mil_val = _empty((), dev=dev)
             if lp_syb is None:
@@ -1179,17 +1195,10 @@ class ModelEngine:
             ms = mil_forward(self.mil, vis, inp["macro_ipt"], inp["macro_obj_loc"],
                              inp["micro_positive_obj"], inp["micro_negative_obj"],
                              inp["micro_obj_mask"], cat_syb, Ts, mil_val, rel=rel,
-                             mil_rel_out=mil_rel, lp=lp_mil)
+                             mil_rel_out=mil_rel, lp=lp_mil, rel_check=check)
             ss = stack_forward(self.syb, cat_syb, B, Ns, Lq, inp["q_ipt"], inp["macro_mask"],
                                inp["q_mask"], inp["q_graph"], inp["macro_graph"], decMask, H, d,
                                drop, SYB_SITES, lp=lp_syb)
-        with torch.cuda.stream(s_vis):
-            if lp_vis is None:
-                cat_vis = _empty(B * Tv, Dv, dev=dev)
-                ops.copy_rows(vis.reshape(B * Nv, Dv), B * Nv, Dv, Dv, cat_vis, Dv, Nv, Tv, 0)
-            sv = stack_forward(self.vis, cat_vis, B, Nv, Lq, inp["q_ipt"], inp["vis_mask"],
-                               inp["q_mask"], inp["q_graph"], None, decMask, H, d, drop,
-                               VIS_SITES, lp=lp_vis)
         main.wait_stream(s_vis)
         main.wait_stream(s_syb)
         for t in (sv.out, ss.out, mil_val) + ((mil_rel,) if mil_rel is not None else ()):

@@ -102,6 +102,12 @@ def test_relation_locations_out_of_range_raise(col, value):
     b = synthetic_relation_batch(2, Nv=4, Lq=5, topN=2, num_relations=4, num_classes=12,
                                  seed=3, device="cuda")
     m(*model_args_rel(b), decMask=True, mcb=False)  # in range: runs
+    keep = int(b["micro_positive_rel_loc"][1, 3, col])
     b["micro_positive_rel_loc"][1, 3, col] = value
     with pytest.raises(IndexError):
         m(*model_args_rel(b), decMask=True, mcb=False)
+    # the check is per forward (asynchronous, AttModel._check_relation_locs): a valid batch
+    # after the failed one runs
+    b["micro_positive_rel_loc"][1, 3, col] = keep
+    lc, *_ = m(*model_args_rel(b), decMask=True, mcb=False)
+    assert bool(torch.isfinite(lc).all())
