@@ -146,13 +146,15 @@ typedef struct savqa_gemm_lp_desc {
                                zero-padded to a multiple of 8 columns, C rows n_store wide) */
     float* ws; int64_t ws_elems;  /* optional split-K workspace (fp32 elements): a split-K
                                launch into fp32 C with a linear epilogue (no relu / mask / Cb /
-                               c_rows / n_store / row map) and ws_elems >= slices*M*N stores
-                               each K slice's partial tile with plain stores and then adds the
-                               slices into C in one pass (C += sum), instead of fp32 atomics */
+                               c_rows / row map; n_store a multiple of 4) and ws_elems >=
+                               slices*M*(N + (colsum_a != 0)) stores each K slice's partial tile
+                               (and column sums) with plain stores and then adds the slices into
+                               C (and colsum_a) in one pass in slice order (C += sum), instead
+                               of fp32 atomics */
     float* colsum_a;        /* optional, a_trans = 1, bf16: colsum_a[m] += sum_k A(m, k) (the
                                bias gradient of dW = dY^T X), summed in fp32 from the staged A
                                tiles by the 128x128 kernel; other kernels add it in a separate
-                               column-sum pass */
+                               (atomic) column-sum pass */
     uint8_t* bits_out; int64_t ldbits;  /* optional, bf16-only outputs (Cb; N % 8 == 0; no C /
                                resid / rowvec / atomic): bit (n & 7) of byte bits_out[crow*ldbits
                                + n/8] = (Cb[crow*ldcb + n] > 0) -- the ReLU gate of this output
@@ -218,11 +220,11 @@ int savqa_ln_fwd(void* stream, const float* x, const float* xscale, const float*
                  void* yb /* optional bf16 copy of y (the next low-precision GEMM's operand) */);
 
 /* Backward of the above: dz = dLN/dz (+ dz_add), dgamma += ..., dbeta += ...
- * Column sums land in the caller's slot workspace `ws` first (ws_bytes >=
- * savqa_ln_bwd_workspace_bytes(cols), 16-B aligned, ZERO-FILLED before its first use);
- * a second tiny kernel on the same stream folds them into dgamma/dbeta and re-zeroes
- * the slots, so one workspace serves every later call on the same stream (calls on
- * concurrently running streams need one workspace each). */
+ * Per-workgroup column sums land in the caller's workspace `ws` first (ws_bytes >=
+ * savqa_ln_bwd_workspace_bytes(cols), 16-B aligned, no initial contents needed);
+ * a second tiny kernel on the same stream adds them into dgamma/dbeta in a fixed
+ * order (bit-identical run to run), so one workspace serves every later call on the
+ * same stream (calls on concurrently running streams need one workspace each). */
 int64_t savqa_ln_bwd_workspace_bytes(int64_t cols);
 int savqa_ln_bwd(void* stream, const float* dy, const float* z, const float* mean,
                  const float* rden, const float* stdv, const float* gamma,

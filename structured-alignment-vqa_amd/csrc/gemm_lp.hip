@@ -70,6 +70,8 @@ struct LpArgs {
   float* slab;            // split-K partial slabs [slice][M][N] (savqa_gemm_lp_desc.ws), or null
   float* tail_slab;       // tail-split partial slabs [slice][M - tail_r0][N] (same workspace),
   int64_t tail_r0;        // or null: the tail tiles' slices then add into C atomically
+  float* cs_slab;         // split-K launches with slabs: the fused column sum's per-slice
+                          // partials [slice][M] (after the C slabs), else null (atomics)
   int dbg;                // diagnostic builds only (SAVQA_LP_DIAG=1, tools/lp_bench.py --dbg):
                           // 1 = skip the MFMAs, 2 = skip the k-loop DMAs, 4 = skip the
                           // epilogue; production builds compile every test of it away
@@ -634,16 +636,30 @@ __device__ __forceinline__ void lp_epilogue_slab(const savqa_gemm_lp_desc& d, co
   }
 }
 
-// C[r0 + m][n] (+)= sum over the ns slabs [ns][rows][N] (fixed order), four columns per thread;
-// assign: the split-off tail tiles' rows (C = sum), else split-K accumulation (C += sum)
+// C[r0 + m][n] (+)= sum over the ns slabs [ns][rows][N] (fixed order), four columns per thread,
+// columns < nst stored (n_store; a multiple of 4); assign: the split-off tail tiles' rows
+// (C = sum), else split-K accumulation (C += sum). Blocks from cs_blk0 on add the fused column
+// sum's ns partials [ns][cs_n] (cs_slab) into colsum in the same slice order.
 __global__ __launch_bounds__(256) void lp_slab_reduce_kernel(const float* __restrict__ slab, int ns,
-                                                             int64_t rows, int64_t N,
+                                                             int64_t rows, int64_t N, int64_t nst,
                                                              float* __restrict__ C, int64_t ldc,
-                                                             int vec, int64_t r0, int assign) {
+                                                             int vec, int64_t r0, int assign,
+                                                             int64_t cs_blk0,
+                                                             const float* __restrict__ cs_slab,
+                                                             int64_t cs_n, float* __restrict__ colsum) {
+  if ((int64_t)blockIdx.x >= cs_blk0) {
+    const int64_t m = ((int64_t)blockIdx.x - cs_blk0) * 256 + threadIdx.x;
+    if (m >= cs_n) return;
+    float v = cs_slab[m];
+    for (int k = 1; k < ns; ++k) v += cs_slab[k * cs_n + m];
+    colsum[m] += v;
+    return;
+  }
   const int64_t n4 = N / 4;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= rows * n4) return;
   const int64_t m = t / n4, n = 4 * (t - m * n4);
+  if (n >= nst) return;
   const int64_t plane = rows * N;
   f4 acc = *reinterpret_cast<const f4*>(slab + m * N + n);
   for (int k = 1; k < ns; ++k) acc += *reinterpret_cast<const f4*>(slab + k * plane + m * N + n);
@@ -925,7 +941,10 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
         float v = 0.f;
 #pragma unroll
         for (int g = 0; g < 16; ++g) v += red[g * 128 + threadIdx.x];
-        atomicAdd(&d.colsum_a[m0 + threadIdx.x], v);
+        if (args.cs_slab && !tail)  // (block-uniform) added in slice order by the slab reduce
+          args.cs_slab[(int64_t)slice * d.M + m0 + threadIdx.x] = v;
+        else
+          atomicAdd(&d.colsum_a[m0 + threadIdx.x], v);
       }
       __syncthreads();  // the epilogue reuses the LDS
     }
@@ -1483,8 +1502,8 @@ static int64_t lp_ws_need(const savqa_gemm_lp_desc& d0) {
   const LpPlan p = lp_plan(d);
   int64_t need = 0;
   if (p.var == 1 && d.a_type != SAVQA_DT_FP8 && p.nsplit > 1 && d.C && !d.Cb && !d.relu &&
-      !d.mask && !d.c_rows && d.n_store == 0 && d.c_group <= 0 && d.N % 4 == 0)
-    need = (int64_t)p.nsplit * d.M * d.N;
+      !d.mask && !d.c_rows && d.n_store % 4 == 0 && d.c_group <= 0 && d.N % 4 == 0)
+    need = (int64_t)p.nsplit * d.M * (d.N + (d.colsum_a ? 1 : 0));
   if (p.tail_slab) need = std::max(need, (int64_t)p.tail_f * (d.M - p.zero_row0) * d.N);
   return need;
 }
@@ -1542,9 +1561,11 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
   // split-K slabs instead of atomics (savqa_gemm_lp_desc.ws): 128 x 128 kernel, plain
   // accumulation into fp32 C with a linear epilogue
   const bool slabs = d.ws && var == 1 && !fp8 && p.nsplit > 1 && d.C && !d.Cb && !d.relu &&
-                     !d.mask && !d.c_rows && d.n_store == 0 && d.c_group <= 0 && d.N % 4 == 0 &&
-                     ((uintptr_t)d.ws & 15) == 0 && d.ws_elems >= (int64_t)p.nsplit * d.M * d.N;
+                     !d.mask && !d.c_rows && d.n_store % 4 == 0 && d.c_group <= 0 &&
+                     d.N % 4 == 0 && ((uintptr_t)d.ws & 15) == 0 &&
+                     d.ws_elems >= (int64_t)p.nsplit * d.M * (d.N + (d.colsum_a ? 1 : 0));
   a.slab = slabs ? d.ws : nullptr;
+  a.cs_slab = slabs && d.colsum_a ? d.ws + (int64_t)p.nsplit * d.M * d.N : nullptr;
   a.tail_slab = p.tail_slab ? d.ws : nullptr;
   a.tail_r0 = p.tail_slab ? p.zero_row0 : 0;
   hipStream_t s = as_stream(stream);
@@ -1604,10 +1625,12 @@ extern "C" int savqa_gemm_lp(void* stream, const savqa_gemm_lp_desc* dp) {
     if (int rc = check_launch("savqa_gemm_lp")) return rc;
     const int vec = (d.ldc % 4 == 0) && (((uintptr_t)d.C & 15) == 0);
     const int64_t r0 = p.tail_slab ? p.zero_row0 : 0, rows = d.M - r0;
-    const int64_t n = rows * (d.N / 4);
-    hipLaunchKernelGGL(lp_slab_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                       d.ws, p.tail_slab ? p.tail_f : p.nsplit, rows, d.N, d.C, d.ldc, vec, r0,
-                       p.tail_slab ? 1 : 0);
+    const int64_t n = rows * (d.N / 4), blk = (n + 255) / 256;
+    const int64_t cs_blk = a.cs_slab ? (d.M + 255) / 256 : 0;
+    hipLaunchKernelGGL(lp_slab_reduce_kernel, dim3((unsigned)(blk + cs_blk)), dim3(256), 0, s,
+                       d.ws, p.tail_slab ? p.tail_f : p.nsplit, rows, d.N,
+                       d.n_store > 0 ? d.n_store : d.N, d.C, d.ldc, vec, r0, p.tail_slab ? 1 : 0,
+                       blk, a.cs_slab, d.M, d.colsum_a);
   }
   return check_launch("savqa_gemm_lp");
 }

@@ -90,17 +90,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 
 // Backward. 512-thread workgroups (8 waves), two per CU: each wave walks rows with a
 // grid stride, keeping its dgamma/dbeta partial sums in registers; the 8 waves fold
-// them through per-wave LDS rows and the workgroup adds once per column into one of
-// LN_SLOTS partial copies (the caller's workspace: 512 adders on ONE address serialise in L2
-// and cost ~35 us per launch; 32 per address run at the chip's atomic rate), which
-// ln_bwd_reduce_kernel then folds into dgamma/dbeta (and re-zeroes). NV (float4 per
+// them through per-wave LDS rows and the workgroup stores its partial row ws[block][2 cols]
+// (the caller's workspace, plain stores), which ln_bwd_reduce_kernel then adds in block
+// order into dgamma/dbeta: deterministic (round 4 added the partials atomically into 16
+// slots, i.e. in arrival order; 512 adders on ONE address serialised in L2). NV (float4 per
 // lane = cols/256) is a template parameter, and the row loop is software-pipelined two
 // deep: the loads of row r+stride are in flight while row r is reduced and written
 // (one row's loads in flight per wave left every wave waiting on HBM latency).
 constexpr int LN_BWD_WAVES = 8;
-constexpr int LN_SLOTS = 16;
-// grid cap: 1024 / 2048 blocks with 32 / 64 slots measured slower standalone (18688 x 512:
-// 22.9 us = 5.0 TB/s at 512 blocks / 16 slots; 25.1 / 27.9 / 41.9 us) and equal in-step
+// grid cap: round 4 measured 1024 / 2048 blocks slower standalone (18688 x 512: 22.9 us =
+// 5.0 TB/s at 512 blocks; 25.1 / 27.9 / 41.9 us) and equal in-step
 constexpr int LN_BWD_BLOCKS = 512;
 
 template <int NV, bool ADD>
@@ -216,32 +215,45 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(const float* 
     reinterpret_cast<float4*>(&red[w][1][0])[lane + 64 * i] = db[i];
   }
   __syncthreads();
-  float* slot = ws + (blockIdx.x % LN_SLOTS) * 2 * cols;
+  float* part = ws + (int64_t)blockIdx.x * 2 * cols;
   for (int c = threadIdx.x; c < 2 * cols; c += blockDim.x) {
     const int a = c >= cols, cc = c - a * cols;
     float t = 0.f;
 #pragma unroll
     for (int ww = 0; ww < LN_BWD_WAVES; ++ww) t += red[ww][a][cc];
-    atomicAdd(&slot[c], t);
+    part[c] = t;
   }
 }
 
-// dgamma[c] += sum_s ws[s][0][c]; dbeta[c] += sum_s ws[s][1][c]; the slots are re-zeroed
-__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(float* __restrict__ ws, int cols,
-                                                            float* __restrict__ dgamma,
+// dgamma[c] += sum_b ws[b][0][c]; dbeta[c] += sum_b ws[b][1][c] over the nb block partials in
+// a fixed order: 4 row groups of 64 columns per workgroup, group r summing blocks r, r + 4, ...
+// (eight loads in flight), then the 4 group sums in order
+__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(const float* __restrict__ ws, int cols,
+                                                            int nb, float* __restrict__ dgamma,
                                                             float* __restrict__ dbeta) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * cols) return;
+  __shared__ float red[4][64];
+  const int rg = threadIdx.x >> 6, lc = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + lc;
   float sacc = 0.f;
+  if (c < 2 * cols) {
+    int b = rg;
+    for (; b + 28 < nb; b += 32) {
+      float x[8];
 #pragma unroll
-  for (int k = 0; k < LN_SLOTS; ++k) {
-    sacc += ws[k * 2 * cols + t];
-    ws[k * 2 * cols + t] = 0.f;
+      for (int u = 0; u < 8; ++u) x[u] = ws[(int64_t)(b + 4 * u) * 2 * cols + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sacc += x[u];
+    }
+    for (; b < nb; b += 4) sacc += ws[(int64_t)b * 2 * cols + c];
   }
-  if (t < cols) {
-    if (dgamma) dgamma[t] += sacc;
+  red[rg][lc] = sacc;
+  __syncthreads();
+  if (rg != 0 || c >= 2 * cols) return;
+  const float t = ((red[0][lc] + red[1][lc]) + red[2][lc]) + red[3][lc];
+  if (c < cols) {
+    if (dgamma) dgamma[c] += t;
   } else if (dbeta) {
-    dbeta[t - cols] += sacc;
+    dbeta[c - cols] += t;
   }
 }
 
@@ -276,7 +288,7 @@ extern "C" int savqa_ln_fwd(void* stream, const float* x, const float* xscale, c
 }
 
 extern "C" int64_t savqa_ln_bwd_workspace_bytes(int64_t cols) {
-  return (int64_t)sizeof(float) * LN_SLOTS * 2 * cols;
+  return (int64_t)sizeof(float) * LN_BWD_BLOCKS * 2 * cols;  // one partial row per block
 }
 
 extern "C" int savqa_ln_bwd(void* stream, const float* dy, const float* z, const float* mean,
@@ -306,8 +318,8 @@ extern "C" int savqa_ln_bwd(void* stream, const float* dy, const float* z, const
 #undef SAVQA_LNB
   }
   if (int rc = check_launch("savqa_ln_bwd")) return rc;
-  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((unsigned)((2 * cols + 255) / 256)), dim3(256), 0, st,
-                     ws, (int)cols, dgamma, dbeta);
+  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((unsigned)((2 * cols + 63) / 64)), dim3(256), 0, st,
+                     ws, (int)cols, (int)blocks, dgamma, dbeta);
   return check_launch("savqa_ln_bwd");
 }
 

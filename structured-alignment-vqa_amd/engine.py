@@ -794,15 +794,16 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
     dvv = torch.empty_like(s.vv)
     n = B * Nv * K
     if s.Eg is not None:
-        # bf16 dPf / dNf straight from the MIL-NCE backward; dW = dP^T Eg and the table
-        # scatter dE[ids] += dP Ws on the 304-column padded operands (pad columns not stored)
+        # bf16 dPf / dNf straight from the MIL-NCE backward; dW = dP^T Eg (+ the bias's column
+        # sums, both through split-K slabs: fixed order) and the table scatter dE[ids] += dP Ws
+        # on the 304-column padded operands (pad columns not stored)
         dPb = _bf(n, Hm, dev=dev)
         dNb = _bf(n, Hm, dev=dev)
         ops.mil_bwd_bf16(s.Pf, s.Nf, s.vv, s.mask, B * Nv, K, Hm, eps, dobj, dmil, dPb, dNb, dvv)
         for dY, ids, eg in ((dPb, s.pos, s.Eg[0]), (dNb, s.neg, s.Eg[1])):
             ops.gemm_lp(dY, eg, Hm, GLOVE_PAD, n, lda=Hm, ldb=GLOVE_PAD, a_trans=True, C=G.Ws,
-                        ldc=GLOVE_D, atomic=True, split_k=-1, n_store=GLOVE_D)
-            ops.colsum_bf16(dY, n, Hm, Hm, G.bs)
+                        ldc=GLOVE_D, atomic=True, split_k=-1, n_store=GLOVE_D, slabs=True,
+                        colsum_a=G.bs)
             ops.gemm_lp(dY, lp.Ws, n, GLOVE_PAD, Hm, lda=Hm, ldb=GLOVE_PAD, C=G.E, ldc=GLOVE_D,
                         atomic=True, split_k=-1, c_rows=ids, n_store=GLOVE_D)
         del dPb, dNb

@@ -419,9 +419,9 @@ def _rccl_worker(port, q):
     all-reduces issued from the two stacks' backward streams, the row-sparse stack tables
     with the static-cap id list, per-bucket Adam waiting on each bucket's work) against the
     same 2 steps with no reducer. At world 1 every collective is an identity: after the first
-    step every deterministic gradient and update is bit-identical, and the LayerNorm gamma / beta
-    and MIL-NCE table gradients (still fp32 atomics in run-dependent order) agree to fp32
-    rounding, as do both steps as a whole."""
+    step every deterministic gradient and update is bit-identical, and the MIL-NCE table
+    gradient (still fp32 atomics in run-dependent order) agrees to fp32 rounding, as do both
+    steps as a whole."""
     import os
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -460,12 +460,12 @@ def _rccl_worker(port, q):
                 torch.cuda.synchronize()
                 rec.append((a.grad[:a.n_live].cpu().clone(), a.flat[:a.n_live].cpu().clone()))
             out[forced] = (rec, nworks, init)
-        # gradients still summed by fp32 atomics in run-dependent order (everything else --
-        # every GEMM's K split included -- is deterministic, ops.GEMM_SLABS): LayerNorm
-        # gamma / beta (per-column partial slots) and the MIL-NCE GloVe table (scatter-add of
+        # the one gradient still summed by fp32 atomics in run-dependent order (everything
+        # else -- every GEMM's K split (ops.GEMM_SLABS) and the LayerNorm gamma / beta column
+        # sums included -- is added in a fixed order): the MIL-NCE GloVe table (scatter-add of
         # duplicate object ids)
         nd = [(a.offsets[n][0], a.offsets[n][0] + a.offsets[n][1].numel()) for n in a.live_names
-              if n.endswith((".gamma", ".beta")) or n == "MIL_NCE.syb_emb.weight"]
+              if n == "MIL_NCE.syb_emb.weight"]
         out["nd"] = nd
         q.put((_to_numpy(out), None))
     except Exception:

@@ -134,19 +134,56 @@ def test_bf16_dw_fused_colsum(M, N, K, hint, slabs, monkeypatch):
     """The bias gradient fused into the dW launch (savqa_gemm_lp_desc.colsum_a): the first
     column tile of each row block sums its staged dY^T tiles over its k range (every split-K
     slice, zero-filled past K, edge rows past N dropped); the 256-wide kernels (hint 5) add it
-    in a separate column-sum pass. Accumulates into an existing gradient."""
+    in a separate column-sum pass. Accumulates into an existing gradient. With slabs the
+    slices' column sums go to [slice][N] partials the slab reduce adds in slice order: dW and
+    db bit-identical run to run."""
     O = ops()
     monkeypatch.setattr(O, "LP_SLABS", slabs)
     dY = bf((K, N), 13)
     X = bf((K, M), 14)
     W0 = torch.randn(N, M, device=dev)
     b0 = torch.randn(N, device=dev)
-    dW, db = W0.clone(), b0.clone()
-    O.gemm_lp(dY, X, N, M, K, lda=N, ldb=M, a_trans=True, C=dW, ldc=M, atomic=True,
-              split_k=-1, tile_hint=hint, colsum_a=db, slabs=slabs)
+    outs = []
+    for _ in range(2):
+        dW, db = W0.clone(), b0.clone()
+        O.gemm_lp(dY, X, N, M, K, lda=N, ldb=M, a_trans=True, C=dW, ldc=M, atomic=True,
+                  split_k=-1, tile_hint=hint, colsum_a=db, slabs=slabs)
+        outs.append((dW, db))
+    dW, db = outs[0]
     ref = dY.double().t() @ X.double()
     assert rel(dW - W0, ref) < 2e-5
     assert rel(db - b0, dY.double().sum(0)) < 1e-5
+    if slabs and hint in (0, 1):
+        assert torch.equal(outs[1][0], dW) and torch.equal(outs[1][1], db)
+
+
+@pytest.mark.parametrize("n", [18560, 2400])
+def test_bf16_dw_slabs_n_store_colsum(n, monkeypatch):
+    """The MIL-NCE object MLP's weight gradient: dW[:, :300] += dY^T Eg on the 304-column
+    padded operand (n_store = 300, rows of C 300 wide) with the bias's column sums fused, through
+    split-K slabs (the reduce stores only the first 300 columns): matches fp64, leaves the
+    neighbouring rows alone and is bit-identical run to run."""
+    O = ops()
+    monkeypatch.setattr(O, "LP_SLABS", True)
+    H = 1024
+    dY = bf((n, H), 51)
+    Eg = torch.zeros(n, 304, device=dev, dtype=torch.bfloat16)
+    Eg[:, :300] = bf((n, 300), 52)
+    G0, b0 = torch.randn(H, 300, device=dev), torch.randn(H, device=dev)
+    outs = []
+    for _ in range(2):
+        G, b = G0.clone(), b0.clone()
+        O.gemm_lp(dY, Eg, H, 304, n, lda=H, ldb=304, a_trans=True, C=G, ldc=300, atomic=True,
+                  split_k=-1, n_store=300, slabs=True, colsum_a=b)
+        outs.append((G, b))
+    d = O.lp_desc(dY, Eg, H, 304, n, lda=H, ldb=304, a_trans=True, C=G0, ldc=300, atomic=True,
+                  split_k=-1, n_store=300, colsum_a=b0)
+    assert O.lp_workspace(d, dev) is not None, "the launch must take the slab path"
+    G, b = outs[0]
+    ref = dY.double().t() @ Eg[:, :300].double()
+    assert rel(G - G0, ref) < 2e-5
+    assert rel(b - b0, dY.double().sum(0)) < 1e-5
+    assert torch.equal(outs[1][0], G) and torch.equal(outs[1][1], b)
 
 
 def test_bf16_epilogues_rows_mask_resid_rowvec():

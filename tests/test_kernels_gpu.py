@@ -216,6 +216,34 @@ def test_layernorm_fwd_bwd():
     assert rel(db, bd.grad) < 1e-5
 
 
+@pytest.mark.parametrize("R,Cc", [(18688, 512), (4099, 1024), (7, 256)])
+def test_layernorm_bwd_param_grads_fixed_order(R, Cc):
+    """dgamma/dbeta: per-workgroup partials added in block order (512 partial rows at the
+    cfg-2 shape), accumulated into the caller's buffers, and bit-identical run to run."""
+    O = ops()
+    x = g(R, Cc, seed=40)
+    gam, bet = g(Cc, seed=41) * 0.2 + 1, g(Cc, seed=42) * 0.2
+    y, z = torch.empty_like(x), torch.empty_like(x)
+    mean, rden, std = (torch.empty(R, device=dev) for _ in range(3))
+    O.ln_fwd(x, gam, bet, y, mean, rden, std, z_out=z)
+    dy = g(R, Cc, seed=43)
+    g0, b0 = g(Cc, seed=44), g(Cc, seed=45)
+    outs = []
+    for _ in range(3):
+        dz = torch.empty_like(x)
+        dg, db = g0.clone(), b0.clone()
+        O.ln_bwd(dy, z, mean, rden, std, gam, dz, dg, db)
+        outs.append((dz, dg, db))
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            assert torch.equal(a, b)
+    zd = x.double()
+    nrm = (zd - zd.mean(-1, keepdim=True)) / (zd.std(-1, keepdim=True) + 1e-8)
+    dyd = dy.double()
+    assert rel(outs[0][1], g0.double() + (dyd * nrm).sum(0)) < 1e-5
+    assert rel(outs[0][2], b0.double() + dyd.sum(0)) < 1e-5
+
+
 def _attn_ref(Q, K, V, G, kf, qf, h=8):
     """modules.py:246-301 core on already-projected (post-ReLU) Q, K, V."""
     B, Tq, D = Q.shape
