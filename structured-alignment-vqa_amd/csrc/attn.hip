@@ -1324,6 +1324,201 @@ void gattn_bwd_q1_kernel(AttnArgsT<TQ, TKV> a) {
   }
 }
 
+// Single-query path split over the 4 waves of a workgroup (SAVQA_ATT_Q1W, the default): one
+// workgroup per (b, h); wave w takes keys [4 NI w, 4 NI (w + 1)) as NI iterations of 4 key
+// rows (lane = (key slot kk, float4 chunk c) as above) and keeps its K / V rows in registers
+// from the first load to the last use. The softmax max and sum, the L1 norm, the adjoint's
+// t1 / t2 and the output / dQ partials cross the waves through LDS, one slot per wave (and per
+// exchange: no slot is reused, so each exchange costs one barrier), folded in wave order: every
+// lane and every rerun sees the same bits. One (b, h) is then one load round trip for 16 NI
+// keys spread over 4 waves, where the one-wave kernels above walk ceil(T_k / 4) iterations and
+// read K / V twice (their register arrays do not hold the rows between the passes).
+#ifndef SAVQA_ATT_Q1W
+#define SAVQA_ATT_Q1W 1
+#endif
+
+__device__ __forceinline__ float q1w_sum4(const float* r) { return (r[0] + r[1]) + (r[2] + r[3]); }
+__device__ __forceinline__ float q1w_max4(const float* r) {
+  return fmaxf(fmaxf(r[0], r[1]), fmaxf(r[2], r[3]));
+}
+
+// K / V rows, graph weights and key flags of this wave's keys (rows past T_k clamped to the
+// last one: valid addresses, masked at use)
+template <int NI, typename TQ, typename TKV>
+__device__ __forceinline__ void q1w_load(const AttnArgsT<TQ, TKV>& a, int b, int hd, int j0, int kk,
+                                         int c, f4v (&k4)[NI], f4v (&v4)[NI], float (&gg)[NI],
+                                         float (&kf)[NI]) {
+  const int64_t kb = (int64_t)b * a.Tk;
+  const float* grow = a.G + kb;
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    const int j = j0 + 4 * it + kk;
+    const int64_t row = kb + min(j, a.Tk - 1);
+    k4[it] = ldx4(a.k + row * a.ldk + hd + 4 * c);
+    v4[it] = ldx4(a.v + row * a.ldv + hd + 4 * c);
+    gg[it] = j < a.Tk ? grow[min(j, a.Tk - 1)] : 0.f;
+    kf[it] = a.kflag[row];
+  }
+}
+
+// softmax over all 4 waves' keys -> aa (0 past T_k), bm = g * aa; red: 2 x 4 LDS slots
+template <int NI>
+__device__ __forceinline__ void q1w_softmax(const f4v q4, const f4v (&k4)[NI], const float (&gg)[NI],
+                                            const float (&kf)[NI], int j0, int kk, int Tk, int w,
+                                            int lane, float (*red)[4], float (&aa)[NI],
+                                            float (&bm)[NI]) {
+  float s[NI], mx = -INFINITY;
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    const f4v k = k4[it];
+    const float d = row16_sum((q4.x * k.x + q4.y * k.y) + (q4.z * k.z + q4.w * k.w));
+    const int j = j0 + 4 * it + kk;
+    s[it] = j < Tk ? (kf[it] == 0.f ? ATT_MASKED : d * 0.125f) : -INFINITY;
+    mx = fmaxf(mx, s[it]);
+  }
+  mx = rows4_max(mx);
+  if (lane == 0) red[0][w] = mx;
+  __syncthreads();
+  const float M = q1w_max4(red[0]);
+  float sum = 0.f;
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    aa[it] = j0 + 4 * it + kk < Tk ? expf(s[it] - M) : 0.f;
+    sum += aa[it];
+  }
+  sum = rows4_sum(sum);
+  if (lane == 0) red[1][w] = sum;
+  __syncthreads();
+  const float Z = q1w_sum4(red[1]);
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    aa[it] = aa[it] / Z;
+    bm[it] = gg[it] * aa[it];
+  }
+}
+
+template <int NI, typename TQ, typename TKV>
+__global__ __launch_bounds__(256) void gattn_fwd_q1w_kernel(AttnArgsT<TQ, TKV> a) {
+  __shared__ float red[3][4];
+  __shared__ f4v ured[4][16];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);  // the heads of a sample on one XCD
+  const int b = bh / a.H, h = bh % a.H, hd = h * ATT_DK;
+  const int kk = lane >> 4, c = lane & 15;
+  const int j0 = 4 * NI * w;
+  const f4v q4 = ldx4(a.q + (int64_t)b * a.ldq + hd + 4 * c);
+  f4v k4[NI], v4[NI];
+  float gg[NI], kf[NI], aa[NI], bm[NI];
+  q1w_load<NI>(a, b, hd, j0, kk, c, k4, v4, gg, kf);
+  q1w_softmax<NI>(q4, k4, gg, kf, j0, kk, a.Tk, w, lane, red, aa, bm);
+  float nr = 0.f;
+  f4v u = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    nr += fabsf(bm[it]);
+    u += bm[it] * v4[it];  // 0 past T_k (g = 0 there)
+  }
+  nr = rows4_sum(nr);
+  u = xrow_sum(u);
+  if (lane == 0) red[2][w] = nr;
+  if (kk == 0) ured[w][c] = u;
+  __syncthreads();
+  const float sden = fmaxf(q1w_sum4(red[2]), 1e-12f);
+  if (a.att && c == 0) {
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int j = j0 + 4 * it + kk;
+      if (j < a.Tk) a.att[((int64_t)h * a.B + b) * a.Tk + j] = bm[it] / sden;
+    }
+  }
+  if (w == 0 && kk == 0) {
+    const f4v o = ((ured[0][c] + ured[1][c]) + (ured[2][c] + ured[3][c])) * (a.qflag[b] / sden);
+    stx4(a.o + (int64_t)b * a.ldo + hd + 4 * c, o, vec_rows(a.o, a.ldo));
+  }
+}
+
+template <int NI, typename TQ, typename TKV>
+__global__ __launch_bounds__(256) void gattn_bwd_q1w_kernel(AttnArgsT<TQ, TKV> a) {
+  __shared__ float red[5][4];
+  __shared__ f4v qred[4][16];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bh / a.H, h = bh % a.H, hd = h * ATT_DK;
+  const int kk = lane >> 4, c = lane & 15;
+  const int j0 = 4 * NI * w;
+  const int64_t kb = (int64_t)b * a.Tk;
+  const f4v q4 = ldx4(a.q + (int64_t)b * a.ldq + hd + 4 * c);
+  const f4v do4 = ld4(a.dout + (int64_t)b * a.lddo + hd + 4 * c);
+  const float qf = a.qflag[b];
+  f4v k4[NI], v4[NI];
+  float gg[NI], kf[NI], aa[NI], bm[NI];
+  q1w_load<NI>(a, b, hd, j0, kk, c, k4, v4, gg, kf);
+  q1w_softmax<NI>(q4, k4, gg, kf, j0, kk, a.Tk, w, lane, red, aa, bm);
+  // dP_j = dO . V_j ; dN = dP * qf ; t1 = sum dN bm, with the L1 norm in the same exchange
+  float dn[NI], t1 = 0.f, nr = 0.f;
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    const f4v v = v4[it];
+    const float x = row16_sum((do4.x * v.x + do4.y * v.y) + (do4.z * v.z + do4.w * v.w)) * qf;
+    dn[it] = j0 + 4 * it + kk < a.Tk ? x : 0.f;
+    t1 += dn[it] * bm[it];
+    nr += fabsf(bm[it]);
+  }
+  t1 = rows4_sum(t1);
+  nr = rows4_sum(nr);
+  if (lane == 0) {
+    red[2][w] = nr;
+    red[3][w] = t1;
+  }
+  __syncthreads();
+  const float nrm = q1w_sum4(red[2]);
+  const float sden = fmaxf(nrm, 1e-12f);
+  const float dnrm = nrm >= 1e-12f ? -q1w_sum4(red[3]) / (sden * sden) : 0.f;
+  float t2 = 0.f;
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    const float sg = bm[it] > 0.f ? 1.f : (bm[it] < 0.f ? -1.f : 0.f);
+    dn[it] = (dn[it] / sden + dnrm * sg) * gg[it];  // da
+    t2 += dn[it] * aa[it];
+  }
+  t2 = rows4_sum(t2);
+  if (lane == 0) red[4][w] = t2;
+  __syncthreads();
+  t2 = q1w_sum4(red[4]);
+  const bool vk = vec_rows(a.dk, a.lddk), vv = vec_rows(a.dv, a.lddv);
+  f4v dq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    const int j = j0 + 4 * it + kk;
+    const bool ok = j < a.Tk;
+    float ds = aa[it] * (dn[it] - t2);
+    if (!ok || kf[it] == 0.f) ds = 0.f;
+    ds *= 0.125f;
+    const float pj = ok ? bm[it] / sden * qf : 0.f;
+    dq += ds * k4[it];
+    if (ok) {
+      f4v gk, gv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gk[e] = k4[it][e] > 0.f ? ds * q4[e] : 0.f;
+        gv[e] = v4[it][e] > 0.f ? pj * do4[e] : 0.f;
+      }
+      const int64_t row = kb + j;
+      stx4(a.dk + row * a.lddk + hd + 4 * c, gk, vk);
+      stx4(a.dv + row * a.lddv + hd + 4 * c, gv, vv);
+    }
+  }
+  dq = xrow_sum(dq);
+  if (kk == 0) qred[w][c] = dq;
+  __syncthreads();
+  if (w == 0 && kk == 0) {
+    f4v r = (qred[0][c] + qred[1][c]) + (qred[2][c] + qred[3][c]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = q4[e] > 0.f ? r[e] : 0.f;
+    stx4(a.dq + (int64_t)b * a.lddq + hd + 4 * c, r, vec_rows(a.dq, a.lddq));
+  }
+}
+
 template <typename TQ, typename TKV>
 static int validate(const AttnArgsT<TQ, TKV>& a, int64_t dk, const char* who) {
   constexpr uintptr_t AQ = sizeof(TQ) * 4 - 1, AK = sizeof(TKV) * 4 - 1;  // 4-element vector loads
@@ -1352,7 +1547,16 @@ static int launch_fwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const ch
   const int path = attn_path(a);
   if (path != 2 && !std::is_same<TQ, TKV>::value)
     return fail(SAVQA_EUNSUP, std::string(who) + ": fp32 Q with bf16 K/V needs T_q = 1");
-  if (path == 2) {
+  if (path == 2 && SAVQA_ATT_Q1W) {
+    const dim3 g((unsigned)(B * H));
+    switch ((Tk + 15) / 16) {
+#define SAVQA_Q1W_CASE(N)                                                                      \
+  case N: hipLaunchKernelGGL((gattn_fwd_q1w_kernel<N, TQ, TKV>), g, dim3(256), 0, s, a); break;
+      SAVQA_Q1W_CASE(1) SAVQA_Q1W_CASE(2) SAVQA_Q1W_CASE(3) SAVQA_Q1W_CASE(4)
+      SAVQA_Q1W_CASE(5) SAVQA_Q1W_CASE(6) SAVQA_Q1W_CASE(7) SAVQA_Q1W_CASE(8)
+#undef SAVQA_Q1W_CASE
+    }
+  } else if (path == 2) {
     const dim3 g((unsigned)((B * H + 3) / 4));
     switch (q1_nit(Tk)) {
       case 8: hipLaunchKernelGGL((gattn_fwd_q1_kernel<8, TQ, TKV>), g, dim3(256), 0, s, a); break;
@@ -1403,6 +1607,17 @@ static int launch_bwd(AttnArgsT<TQ, TKV>& a, int64_t dk, hipStream_t s, const ch
     return fail(SAVQA_EUNSUP, std::string(who) + ": fp32 Q with bf16 K/V needs T_q = 1");
   if (((a.lddo & 3) || (((uintptr_t)a.dout) & 15)))
     return fail(SAVQA_EINVAL, std::string(who) + ": dO must be 16-B aligned with ld % 4 == 0");
+  if (path == 2 && SAVQA_ATT_Q1W) {
+    const dim3 g((unsigned)(B * H));
+    switch ((Tk + 15) / 16) {
+#define SAVQA_Q1W_CASE(N)                                                                      \
+  case N: hipLaunchKernelGGL((gattn_bwd_q1w_kernel<N, TQ, TKV>), g, dim3(256), 0, s, a); break;
+      SAVQA_Q1W_CASE(1) SAVQA_Q1W_CASE(2) SAVQA_Q1W_CASE(3) SAVQA_Q1W_CASE(4)
+      SAVQA_Q1W_CASE(5) SAVQA_Q1W_CASE(6) SAVQA_Q1W_CASE(7) SAVQA_Q1W_CASE(8)
+#undef SAVQA_Q1W_CASE
+    }
+    return check_launch(who);
+  }
   if (path == 2) {
     const dim3 g((unsigned)((B * H + 3) / 4));
     switch (q1_nit(Tk)) {

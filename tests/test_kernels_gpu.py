@@ -266,7 +266,9 @@ def _attn_ref(Q, K, V, G, kf, qf, h=8):
                                            (4, 1, 50, "cross"), (2, 16, 16, "self"),
                                            (1, 5, 3, "cross"), (2, 100, 7, "cross"),
                                            (3, 1, 128, "cross"), (2, 1, 5, "cross"),
-                                           (2, 1, 3, "cross"), (3, 4, 33, "cross")])
+                                           (2, 1, 3, "cross"), (3, 4, 33, "cross"),
+                                           (3, 1, 17, "cross"), (2, 1, 65, "cross"),
+                                           (2, 1, 16, "cross")])
 def test_graph_attention_fwd_bwd(B, Tq, Tk, kind):
     O = ops()
     H, D = 8, 512
@@ -305,6 +307,37 @@ def test_graph_attention_fwd_bwd(B, Tq, Tk, kind):
     assert rel(dq.view(B, Tq, D), Qr.grad * mq) < 5e-5
     assert rel(dk.view(B, Tk, D), Kr.grad * mk) < 5e-5
     assert rel(dv.view(B, Tk, D), Vr.grad * mv) < 5e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_single_query_attention_one_key_and_reruns(dt):
+    """T_q = 1 kernels (one workgroup per (sample, head), keys split over its 4 waves): with one
+    key the softmax weight is exactly 1, so dQ and dK are exactly 0 as in the reference (the
+    cross-wave sums add exact zeros); at T_k = 73 / 128 reruns are bit-identical."""
+    O = ops()
+    H, D = 8, 512
+    for B, Tk in ((3, 1), (4, 73), (2, 128)):
+        Q = g(B, D, seed=70, relu=True)
+        kv = g(B * Tk, 2 * D, seed=71, relu=True).to(dt)
+        G = torch.ones(B, 1, Tk, device=dev)
+        G[:, :, ::3] = 0.5
+        kf, qf = torch.ones(B, Tk, device=dev), torch.ones(B, 1, device=dev)
+        dO = g(B, D, seed=72)
+        outs = []
+        for _ in range(2):
+            o = torch.empty(B, D, device=dev)
+            dq = torch.empty(B, D, device=dev)
+            dkv = torch.empty(B * Tk, 2 * D, device=dev, dtype=dt)
+            O.gattn_fwd(Q, D, kv, 2 * D, kv[:, D:], 2 * D, G, kf, qf, B, 1, Tk, H, o, D)
+            O.gattn_bwd(Q, D, kv, 2 * D, kv[:, D:], 2 * D, G, kf, qf, B, 1, Tk, H, dO, D, dq, D,
+                        dkv, 2 * D, dkv[:, D:], 2 * D)
+            outs.append((o, dq, dkv))
+        for a, b_ in zip(*outs):
+            assert torch.equal(a, b_)
+        o, dq, dkv = outs[0]
+        if Tk == 1:
+            assert int((dq != 0).sum()) == 0 and int((dkv[:, :D] != 0).sum()) == 0
+            assert torch.equal(o, kv[:, D:].float())   # P = 1 (G / |G| = 1) times V
 
 
 @pytest.mark.parametrize("B,Tq,Tk,kind", [(3, 50, 50, "self"), (2, 73, 73, "self"),

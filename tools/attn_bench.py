@@ -106,15 +106,16 @@ def q1_main(args):
     es = 2 if args.bf16 else 4
     for B, T in ((args.B[0], t) for t in args.T):
         q = torch.randn(B, d, device=dev).relu_()
-        kv = torch.randn(B * T, 2 * d, device=dev).relu_().to(dt)
+        # the model's layout: the 6 decoder layers' K / V side by side in one [B T, 12 d] buffer
+        kv = torch.randn(B * T, 12 * d, device=dev).relu_().to(dt)
         G = (torch.rand(B, 1, T, device=dev) < 0.3).float()
         kf, qf = torch.ones(B * T, device=dev), torch.ones(B, device=dev)
         o, dout = torch.empty(B, d, device=dev), torch.randn(B, d, device=dev)
         dq = torch.empty(B, d, device=dev)
-        dkv = torch.empty(B * T, 2 * d, device=dev, dtype=dt)
-        f = lambda: ops.gattn_fwd(q, d, kv, 2 * d, kv[:, d:], 2 * d, G, kf, qf, B, 1, T, H, o, d)
-        g = lambda: ops.gattn_bwd(q, d, kv, 2 * d, kv[:, d:], 2 * d, G, kf, qf, B, 1, T, H, dout,
-                                  d, dq, d, dkv, 2 * d, dkv[:, d:], 2 * d)
+        dkv = torch.empty(B * T, 12 * d, device=dev, dtype=dt)
+        f = lambda: ops.gattn_fwd(q, d, kv, 12 * d, kv[:, d:], 12 * d, G, kf, qf, B, 1, T, H, o, d)
+        g = lambda: ops.gattn_bwd(q, d, kv, 12 * d, kv[:, d:], 12 * d, G, kf, qf, B, 1, T, H, dout,
+                                  d, dq, d, dkv, 12 * d, dkv[:, d:], 12 * d)
         tf, tb = timeit(f), timeit(g)
         fb = B * T * 2 * d * es
         bb = 2 * B * T * 2 * d * es
