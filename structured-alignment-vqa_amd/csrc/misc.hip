@@ -282,6 +282,191 @@ __global__ __launch_bounds__(256) void mil_bwd_kernel(
   }
 }
 
+// Single-pass forms (SAVQA_MIL_SPLIT, the default, for H <= 1024 and topN <= 8): one 256-thread
+// workgroup per (b, n) row, thread t owning float4 column t of every candidate row, so the P / N
+// rows are read once and held in registers from the scores to the outputs (the one-wave kernels
+// above read them again for the outputs: P twice forward, P and N twice backward). The per-k dot
+// products cross the 4 waves through LDS, folded in wave order (deterministic, every thread the
+// same bits); the softmax / LSE scalars are then formed redundantly by every thread.
+#ifndef SAVQA_MIL_SPLIT
+#define SAVQA_MIL_SPLIT 1
+#endif
+constexpr int MIL_SPLIT_H = 1024, MIL_SPLIT_K = 8;
+
+template <int NV>
+__device__ __forceinline__ void mil_fold(float (&x)[NV], float (*red)[4]) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const float t = wave_sum(x[k]);
+    if (lane == 0) red[k][w] = t;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) x[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+}
+
+__device__ __forceinline__ float mil_dot4(const float4& a, const float4& b) {
+  return (a.x * b.x + a.y * b.y) + (a.z * b.z + a.w * b.w);
+}
+
+template <int KC>
+__global__ __launch_bounds__(256) void mil_fwd_split_kernel(const float* __restrict__ Pf,
+                                                            const float* __restrict__ Nf,
+                                                            const float* __restrict__ v,
+                                                            const int32_t* __restrict__ mask,
+                                                            int H, float eps,
+                                                            float* __restrict__ obj,
+                                                            float* __restrict__ term) {
+  __shared__ float red[2 * KC][4];
+  const int64_t bn = blockIdx.x;
+  const int i = threadIdx.x, h4 = H / 4;
+  const bool act = i < h4;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 vv = act ? reinterpret_cast<const float4*>(v + bn * H)[i] : z;
+  float4 pp[KC];
+  float sc[2 * KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const int64_t off = (bn * KC + k) * h4 + i;
+    pp[k] = act ? reinterpret_cast<const float4*>(Pf)[off] : z;
+    const float4 qq = act ? reinterpret_cast<const float4*>(Nf)[off] : z;
+    sc[k] = mil_dot4(pp[k], vv);
+    sc[KC + k] = mil_dot4(qq, vv);
+  }
+  mil_fold<2 * KC>(sc, red);
+  // softmax over k of the raw positive scores (AttModel_x3.py:372-373)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) mx = fmaxf(mx, sc[k]);
+  float den = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) { sc[k] = expf(sc[k] - mx); den += sc[k]; }
+  if (act) {
+    float4 o = z;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const float w = sc[k] / den;
+      o.x = fmaf(w, pp[k].x, o.x); o.y = fmaf(w, pp[k].y, o.y);
+      o.z = fmaf(w, pp[k].z, o.z); o.w = fmaf(w, pp[k].w, o.w);
+    }
+    reinterpret_cast<float4*>(obj + bn * H)[i] = o;
+  }
+  if (threadIdx.x == 0) {  // LSE_k(clamp(mask*s-, eps)) (AttModel_x3.py:367)
+    float m2 = -INFINITY, sn[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      sn[k] = fmaxf((float)mask[bn * KC + k] * sc[KC + k], eps);
+      m2 = fmaxf(m2, sn[k]);
+    }
+    float s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) s2 += expf(sn[k] - m2);
+    term[bn] = (eps + logf((float)KC)) - (m2 + logf(s2));
+  }
+}
+
+template <int KC, typename TO>
+__global__ __launch_bounds__(256) void mil_bwd_split_kernel(
+    const float* __restrict__ Pf, const float* __restrict__ Nf, const float* __restrict__ v,
+    const int32_t* __restrict__ mask, int64_t BN, int H, float eps,
+    const float* __restrict__ dobj, const float* __restrict__ dmil, TO* __restrict__ dPf,
+    TO* __restrict__ dNf, float* __restrict__ dv) {
+  __shared__ float red[3 * KC][4];
+  const int64_t bn = blockIdx.x;
+  const int i = threadIdx.x, h4 = H / 4;
+  const bool act = i < h4;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 vv = act ? reinterpret_cast<const float4*>(v + bn * H)[i] : z;
+  const float4 g = act && dobj ? reinterpret_cast<const float4*>(dobj + bn * H)[i] : z;
+  float4 pp[KC], qq[KC];
+  float sc[3 * KC];  // [0, KC) s+, [KC, 2KC) s-, [2KC, 3KC) dobj . P_k
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const int64_t off = (bn * KC + k) * h4 + i;
+    pp[k] = act ? reinterpret_cast<const float4*>(Pf)[off] : z;
+    qq[k] = act ? reinterpret_cast<const float4*>(Nf)[off] : z;
+    sc[k] = mil_dot4(pp[k], vv);
+    sc[KC + k] = mil_dot4(qq[k], vv);
+    sc[2 * KC + k] = mil_dot4(g, pp[k]);
+  }
+  mil_fold<3 * KC>(sc, red);
+  // softmax weights w and their backward dsp = w*(dw - sum w dw)
+  float sp[KC], dsp[KC], dsn[KC];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) mx = fmaxf(mx, sc[k]);
+  float den = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) { sp[k] = expf(sc[k] - mx); den += sp[k]; }
+  float wdw = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) { sp[k] = sp[k] / den; wdw += sp[k] * sc[2 * KC + k]; }
+#pragma unroll
+  for (int k = 0; k < KC; ++k) dsp[k] = sp[k] * (sc[2 * KC + k] - wdw);
+  // term = LSE(eps) - LSE(snc): d snc_k = -dterm * softmax_k(snc); clamp passes where >= eps
+  const float dterm = (*dmil) / (2.f * (float)BN);
+  {
+    float m2 = -INFINITY, snc[KC], mk[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      mk[k] = (float)mask[bn * KC + k];
+      snc[k] = fmaxf(mk[k] * sc[KC + k], eps);
+      m2 = fmaxf(m2, snc[k]);
+    }
+    float s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) { dsn[k] = expf(snc[k] - m2); s2 += dsn[k]; }
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const float d_snc = -dterm * (dsn[k] / s2);
+      dsn[k] = (mk[k] * sc[KC + k] >= eps) ? d_snc * mk[k] : 0.f;
+    }
+  }
+  if (!act) return;
+  float4 acc = z;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const int64_t off = (bn * KC + k) * H + 4 * i;
+    const float4 p = pp[k], q = qq[k];
+    float4 dp, dn;
+    dp.x = p.x > 0.f ? sp[k] * g.x + dsp[k] * vv.x : 0.f;
+    dp.y = p.y > 0.f ? sp[k] * g.y + dsp[k] * vv.y : 0.f;
+    dp.z = p.z > 0.f ? sp[k] * g.z + dsp[k] * vv.z : 0.f;
+    dp.w = p.w > 0.f ? sp[k] * g.w + dsp[k] * vv.w : 0.f;
+    dn.x = q.x > 0.f ? dsn[k] * vv.x : 0.f;
+    dn.y = q.y > 0.f ? dsn[k] * vv.y : 0.f;
+    dn.z = q.z > 0.f ? dsn[k] * vv.z : 0.f;
+    dn.w = q.w > 0.f ? dsn[k] * vv.w : 0.f;
+    mil_store4(dPf + off, dp);
+    mil_store4(dNf + off, dn);
+    acc.x += dsp[k] * p.x + dsn[k] * q.x;
+    acc.y += dsp[k] * p.y + dsn[k] * q.y;
+    acc.z += dsp[k] * p.z + dsn[k] * q.z;
+    acc.w += dsp[k] * p.w + dsn[k] * q.w;
+  }
+  float4 o;
+  o.x = vv.x > 0.f ? acc.x : 0.f; o.y = vv.y > 0.f ? acc.y : 0.f;
+  o.z = vv.z > 0.f ? acc.z : 0.f; o.w = vv.w > 0.f ? acc.w : 0.f;
+  reinterpret_cast<float4*>(dv + bn * H)[i] = o;
+}
+
+static bool mil_split_ok(int64_t K, int64_t H) {
+  return SAVQA_MIL_SPLIT && K <= MIL_SPLIT_K && H <= MIL_SPLIT_H;
+}
+
+#define SAVQA_MIL_K_SWITCH(K, LAUNCH) \
+  switch (K) {                        \
+    case 1: LAUNCH(1); break;         \
+    case 2: LAUNCH(2); break;         \
+    case 3: LAUNCH(3); break;         \
+    case 4: LAUNCH(4); break;         \
+    case 5: LAUNCH(5); break;         \
+    case 6: LAUNCH(6); break;         \
+    case 7: LAUNCH(7); break;         \
+    default: LAUNCH(8); break;        \
+  }
+
 // macro[b*Ns + loc[b,n]] = obj[b*Nv + n], n ascending (last write wins, as the
 // reference's index_put on CPU); one block per sample keeps that order.
 __global__ void index_put_rows_kernel(const int64_t* __restrict__ loc, int64_t Nv, int64_t Ns,
@@ -672,11 +857,37 @@ extern "C" int savqa_mil_fwd(void* stream, const float* Pf, const float* Nf, con
   if (K <= 0 || K > MIL_KMAX || H % 4 != 0)
     return fail(SAVQA_EUNSUP, "savqa_mil_fwd: need 1 <= topN <= 16 and H % 4 == 0");
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(mil_fwd_kernel, dim3((BN + 3) / 4), dim3(256), 0, s, Pf, Nf, v, mask, BN,
-                     (int)K, (int)H, eps, obj, ws);
+  if (mil_split_ok(K, H)) {
+#define SAVQA_MIL_FWD(KC)                                                                     \
+  hipLaunchKernelGGL((mil_fwd_split_kernel<KC>), dim3((unsigned)BN), dim3(256), 0, s, Pf, Nf, v, \
+                     mask, (int)H, eps, obj, ws)
+    SAVQA_MIL_K_SWITCH(K, SAVQA_MIL_FWD)
+#undef SAVQA_MIL_FWD
+  } else {
+    hipLaunchKernelGGL(mil_fwd_kernel, dim3((BN + 3) / 4), dim3(256), 0, s, Pf, Nf, v, mask, BN,
+                       (int)K, (int)H, eps, obj, ws);
+  }
   hipLaunchKernelGGL(mean_reduce_kernel, dim3(1), dim3(1024), 0, s, ws, BN, 1.f / (2.f * (float)BN),
                      mil_out);
   return check_launch("savqa_mil_fwd");
+}
+
+template <typename TO>
+static int mil_bwd_launch(hipStream_t s, const float* Pf, const float* Nf, const float* v,
+                          const int32_t* mask, int64_t BN, int64_t K, int64_t H, float eps,
+                          const float* dobj, const float* dmil, TO* dPf, TO* dNf, float* dv,
+                          const char* who) {
+  if (mil_split_ok(K, H)) {
+#define SAVQA_MIL_BWD(KC)                                                                      \
+  hipLaunchKernelGGL((mil_bwd_split_kernel<KC, TO>), dim3((unsigned)BN), dim3(256), 0, s, Pf, Nf, \
+                     v, mask, BN, (int)H, eps, dobj, dmil, dPf, dNf, dv)
+    SAVQA_MIL_K_SWITCH(K, SAVQA_MIL_BWD)
+#undef SAVQA_MIL_BWD
+  } else {
+    hipLaunchKernelGGL(mil_bwd_kernel<TO>, dim3((BN + 3) / 4), dim3(256), 0, s, Pf, Nf, v, mask, BN,
+                       (int)K, (int)H, eps, dobj, dmil, dPf, dNf, dv);
+  }
+  return check_launch(who);
 }
 
 extern "C" int savqa_mil_bwd(void* stream, const float* Pf, const float* Nf, const float* v,
@@ -686,9 +897,8 @@ extern "C" int savqa_mil_bwd(void* stream, const float* Pf, const float* Nf, con
   if (BN <= 0) return 0;
   if (K <= 0 || K > MIL_KMAX || H % 4 != 0)
     return fail(SAVQA_EUNSUP, "savqa_mil_bwd: need 1 <= topN <= 16 and H % 4 == 0");
-  hipLaunchKernelGGL(mil_bwd_kernel<float>, dim3((BN + 3) / 4), dim3(256), 0, as_stream(stream), Pf,
-                     Nf, v, mask, BN, (int)K, (int)H, eps, dobj, dmil, dPf, dNf, dv);
-  return check_launch("savqa_mil_bwd");
+  return mil_bwd_launch<float>(as_stream(stream), Pf, Nf, v, mask, BN, K, H, eps, dobj, dmil, dPf,
+                               dNf, dv, "savqa_mil_bwd");
 }
 
 extern "C" int savqa_mil_bwd_bf16(void* stream, const float* Pf, const float* Nf, const float* v,
@@ -698,10 +908,9 @@ extern "C" int savqa_mil_bwd_bf16(void* stream, const float* Pf, const float* Nf
   if (BN <= 0) return 0;
   if (K <= 0 || K > MIL_KMAX || H % 4 != 0)
     return fail(SAVQA_EUNSUP, "savqa_mil_bwd_bf16: need 1 <= topN <= 16 and H % 4 == 0");
-  hipLaunchKernelGGL(mil_bwd_kernel<__bf16>, dim3((BN + 3) / 4), dim3(256), 0, as_stream(stream), Pf,
-                     Nf, v, mask, BN, (int)K, (int)H, eps, dobj, dmil,
-                     static_cast<__bf16*>(dPf), static_cast<__bf16*>(dNf), dv);
-  return check_launch("savqa_mil_bwd_bf16");
+  return mil_bwd_launch<__bf16>(as_stream(stream), Pf, Nf, v, mask, BN, K, H, eps, dobj, dmil,
+                                static_cast<__bf16*>(dPf), static_cast<__bf16*>(dNf), dv,
+                                "savqa_mil_bwd_bf16");
 }
 
 extern "C" int savqa_index_put_rows(void* stream, const int64_t* loc, int64_t B, int64_t Nv,
