@@ -286,24 +286,29 @@ __global__ __launch_bounds__(256) void mil_bwd_kernel(
 // workgroup per (b, n) row, thread t owning float4 column t of every candidate row, so the P / N
 // rows are read once and held in registers from the scores to the outputs (the one-wave kernels
 // above read them again for the outputs: P twice forward, P and N twice backward). The per-k dot
-// products cross the 4 waves through LDS, folded in wave order (deterministic, every thread the
-// same bits); the softmax / LSE scalars are then formed redundantly by every thread.
+// products are summed in exactly the one-wave kernels' order -- lane l adds its columns l,
+// l + 64, l + 128, l + 192 in sequence (here: the 4 waves' partials of lane l, exchanged through
+// LDS), then the same wave tree -- so the scores, and the forward's object features, are
+// bit-identical to theirs (the gradients up to the compiler's FMA-contraction choices), and every
+// thread holds the same bits; the softmax / LSE scalars are then formed redundantly per thread.
 #ifndef SAVQA_MIL_SPLIT
 #define SAVQA_MIL_SPLIT 1
 #endif
 constexpr int MIL_SPLIT_H = 1024, MIL_SPLIT_K = 8;
 
 template <int NV>
-__device__ __forceinline__ void mil_fold(float (&x)[NV], float (*red)[4]) {
+__device__ __forceinline__ void mil_fold(float (&x)[NV], float (*part)[4][64]) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const float t = wave_sum(x[k]);
-    if (lane == 0) red[k][w] = t;
-  }
+  for (int k = 0; k < NV; ++k) part[k][w][lane] = x[k];
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < NV; ++k) x[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+  for (int k = 0; k < NV; ++k) {
+    float a = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a += part[k][r][lane];
+    x[k] = wave_sum(a);
+  }
 }
 
 __device__ __forceinline__ float mil_dot4(const float4& a, const float4& b) {
@@ -318,7 +323,7 @@ __global__ __launch_bounds__(256) void mil_fwd_split_kernel(const float* __restr
                                                             int H, float eps,
                                                             float* __restrict__ obj,
                                                             float* __restrict__ term) {
-  __shared__ float red[2 * KC][4];
+  __shared__ float red[2 * KC][4][64];
   const int64_t bn = blockIdx.x;
   const int i = threadIdx.x, h4 = H / 4;
   const bool act = i < h4;
@@ -372,7 +377,7 @@ __global__ __launch_bounds__(256) void mil_bwd_split_kernel(
     const int32_t* __restrict__ mask, int64_t BN, int H, float eps,
     const float* __restrict__ dobj, const float* __restrict__ dmil, TO* __restrict__ dPf,
     TO* __restrict__ dNf, float* __restrict__ dv) {
-  __shared__ float red[3 * KC][4];
+  __shared__ float red[3 * KC][4][64];
   const int64_t bn = blockIdx.x;
   const int i = threadIdx.x, h4 = H / 4;
   const bool act = i < h4;

@@ -452,7 +452,8 @@ def test_graph_build_matches_oracle():
 @pytest.mark.parametrize("K,H", [(5, 64), (5, 1024), (8, 1000), (1, 512), (9, 64), (5, 1028)])
 def test_mil_core_fwd_bwd(K, H):
     """MIL-NCE core (AttModel_x3.py:358-373) against fp64 autograd: the single-pass
-    one-workgroup-per-row kernels (topN <= 8, H <= 1024) and the one-wave kernels past them."""
+    one-workgroup-per-row kernels (topN <= 8, H <= 1024; their scores are summed in the one-wave
+    kernels' order: the same object features bit for bit) and the one-wave kernels past them."""
     O = ops()
     B, Nv, eps = 3, 7, 1e-6
     Pf = g(B * Nv * K, H, seed=60, relu=True) * 0.2
