@@ -226,30 +226,38 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(const float* 
 }
 
 // dgamma[c] += sum_b ws[b][0][c]; dbeta[c] += sum_b ws[b][1][c] over the nb block partials in
-// a fixed order: 4 row groups of 64 columns per workgroup, group r summing blocks r, r + 4, ...
-// (eight loads in flight), then the 4 group sums in order
-__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(const float* __restrict__ ws, int cols,
-                                                            int nb, float* __restrict__ dgamma,
-                                                            float* __restrict__ dbeta) {
-  __shared__ float red[4][64];
+// a fixed order: 16 row groups of 64 columns per 1024-thread workgroup, group r summing blocks
+// r, r + 16, ... (all of its <= 32 loads issued in batches of 8), then the 16 group sums as a
+// fixed pairwise tree. (4 row groups left each thread 128 loads deep at nb = 512: ~16 latency
+// rounds on 16 workgroups; the relation workload lost ~1 %.)
+constexpr int LN_RED_GROUPS = 16;
+__global__ __launch_bounds__(1024) void ln_bwd_reduce_kernel(const float* __restrict__ ws, int cols,
+                                                             int nb, float* __restrict__ dgamma,
+                                                             float* __restrict__ dbeta) {
+  __shared__ float red[LN_RED_GROUPS][64];
   const int rg = threadIdx.x >> 6, lc = threadIdx.x & 63;
   const int c = blockIdx.x * 64 + lc;
   float sacc = 0.f;
   if (c < 2 * cols) {
     int b = rg;
-    for (; b + 28 < nb; b += 32) {
+    for (; b + 7 * LN_RED_GROUPS < nb; b += 8 * LN_RED_GROUPS) {
       float x[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = ws[(int64_t)(b + 4 * u) * 2 * cols + c];
+      for (int u = 0; u < 8; ++u) x[u] = ws[(int64_t)(b + LN_RED_GROUPS * u) * 2 * cols + c];
 #pragma unroll
       for (int u = 0; u < 8; ++u) sacc += x[u];
     }
-    for (; b < nb; b += 4) sacc += ws[(int64_t)b * 2 * cols + c];
+    for (; b < nb; b += LN_RED_GROUPS) sacc += ws[(int64_t)b * 2 * cols + c];
   }
   red[rg][lc] = sacc;
   __syncthreads();
+#pragma unroll
+  for (int h = LN_RED_GROUPS / 2; h > 0; h >>= 1) {
+    if (rg < h) red[rg][lc] += red[rg + h][lc];
+    __syncthreads();
+  }
   if (rg != 0 || c >= 2 * cols) return;
-  const float t = ((red[0][lc] + red[1][lc]) + red[2][lc]) + red[3][lc];
+  const float t = red[0][lc];
   if (c < cols) {
     if (dgamma) dgamma[c] += t;
   } else if (dbeta) {
@@ -318,7 +326,7 @@ extern "C" int savqa_ln_bwd(void* stream, const float* dy, const float* z, const
 #undef SAVQA_LNB
   }
   if (int rc = check_launch("savqa_ln_bwd")) return rc;
-  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((unsigned)((2 * cols + 63) / 64)), dim3(256), 0, st,
+  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((unsigned)((2 * cols + 63) / 64)), dim3(1024), 0, st,
                      ws, (int)cols, (int)blocks, dgamma, dbeta);
   return check_launch("savqa_ln_bwd");
 }
