@@ -1478,7 +1478,9 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
         const int64_t per = (nk + f - 1) / f;
         const int tf = (int)((nk + per - 1) / per);
         const int64_t r0 = ((p.tiles - r) / tn) * bm;
-        const bool slab = slab_ok && d.ws_elems >= (int64_t)tf * (d.M - r0) * d.N;
+        // (the slab epilogue is linear only -- no ReLU-backward gate: a masked launch keeps
+        // the atomic tail, whose epilogue applies the mask)
+        const bool slab = slab_ok && !d.mask && d.ws_elems >= (int64_t)tf * (d.M - r0) * d.N;
         if (slab || nk >= LP_TAIL_MIN_NK) {
           p.tail_per = per;
           p.tail_f = tf;

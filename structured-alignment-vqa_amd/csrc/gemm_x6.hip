@@ -303,12 +303,66 @@ __device__ __forceinline__ int x6_mode(const savqa_gemm_desc& d, int64_t m0, int
   return ((kend - kbeg) % X6_BK == 0) ? 1 : 2;
 }
 
+// Split accumulators (SAVQA_X6_HILO): the dominant product a0 b0 accumulates in acc (hi), the
+// five smaller ones (a2 b0, a1 b0, a1 b1, a0 b1, a0 b2: each below 2^-7 |ab|) in a second set
+// lo, and hi + lo is formed once after the k-loop. hi takes one rounding per 32 k at the
+// output's scale (the native fp32 kernel: eight), the small products round at lo's ulp, at
+// least 2^7 finer -- more accurate than two-level, and no per-k-tile adds (whose latency behind
+// the last MFMA of each partial cost cfg 2 3.5 %). Loop order is B-plane-major: b0's fragments
+// meet a0 / a1 / a2, b1's a0 / a1, b2's a0 -- 28 fragment registers instead of 60, paid for by
+// re-reading A fragments (36 ds_read_b128 per wave per k-tile instead of 24).
+#ifndef SAVQA_X6_HILO
+#define SAVQA_X6_HILO 1
+#endif
+__device__ __forceinline__ void x6_compute_hilo(const char* As, const char* Bs, int wm, int wn,
+                                                int lane, f4 (&hi)[4][4], f4 (&lo)[4][4]) {
+  bf16x8 b[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b[j] = x6_frag(Bs, wn * 64 + 16 * j, lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bf16x8 a2 = x6_frag(As + 2 * X6_PLANE, wm * 64 + 16 * i, lane);
+    const bf16x8 a1 = x6_frag(As + X6_PLANE, wm * 64 + 16 * i, lane);
+    const bf16x8 a0 = x6_frag(As, wm * 64 + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lo[i][j] = mma(a2, b[j], lo[i][j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lo[i][j] = mma(a1, b[j], lo[i][j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hi[i][j] = mma(a0, b[j], hi[i][j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b[j] = x6_frag(Bs + X6_PLANE, wn * 64 + 16 * j, lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bf16x8 a1 = x6_frag(As + X6_PLANE, wm * 64 + 16 * i, lane);
+    const bf16x8 a0 = x6_frag(As, wm * 64 + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lo[i][j] = mma(a1, b[j], lo[i][j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lo[i][j] = mma(a0, b[j], lo[i][j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b[j] = x6_frag(Bs + 2 * X6_PLANE, wn * 64 + 16 * j, lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bf16x8 a0 = x6_frag(As, wm * 64 + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lo[i][j] = mma(a0, b[j], lo[i][j]);
+  }
+}
+
 template <bool AT, bool BT, int MODE>
 __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem, int64_t m0,
                                             int64_t n0, int64_t kbeg, int64_t kend, int ntiles,
                                             f4 (&acc)[4][4], bool do_cs, f4& cs) {
   X6Operand<!AT> la;
   X6Operand<BT> lb;
+  f4 lo[4][4];  // SAVQA_X6_HILO: the small products' accumulators
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lo[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -338,7 +392,10 @@ __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem
     lb.template store<S>(smem + 3 * X6_PLANE, tid);
     if (tt + X6_DEPTH < ntiles) load(set, kbeg + (int64_t)(tt + X6_DEPTH) * X6_BK);
     __syncthreads();
-    x6_compute(smem, smem + 3 * X6_PLANE, wm, wn, lane, acc);
+    if constexpr (SAVQA_X6_HILO)
+      x6_compute_hilo(smem, smem + 3 * X6_PLANE, wm, wn, lane, acc, lo);
+    else
+      x6_compute(smem, smem + 3 * X6_PLANE, wm, wn, lane, acc);
   };
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, X6_DEPTH - 1>;
@@ -347,6 +404,12 @@ __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem
   for (int tt = 0; tt < ntiles; tt += X6_DEPTH) {
     step(S0{}, tt);
     if (X6_DEPTH > 1 && tt + 1 < ntiles) step(S1{}, tt + 1);
+  }
+  if constexpr (SAVQA_X6_HILO) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] += lo[i][j];
   }
   __syncthreads();  // LDS is reused by the colsum fold
 }

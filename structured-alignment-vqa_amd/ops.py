@@ -41,9 +41,13 @@ class GemmProbe:
     """Optional per-launch timing of savqa_gemm with HIP events on the launch stream
     (bench.py's roofline measurement). Off unless a probe is installed."""
 
-    def __init__(self, detail: bool = False):
+    def __init__(self, detail: bool = False, keep: bool = False):
         self.records = []  # (variant, flops, start_event, end_event)
         self.detail = detail  # key launches by shape + fused options too (breakdowns)
+        # keep: also a copy of every launch's descriptor, aligned with records, as
+        # ("gemm" | "lp", desc) -- tools/gemm_replay.py re-issues them on their own buffers
+        self.keep = keep
+        self.descs = []
 
     @staticmethod
     def shape_key(d):
@@ -199,6 +203,8 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
     if _probe.detail:
         key += " | " + GemmProbe.shape_key(d)
     _probe.records.append((key, 2.0 * M * N * K, e0, e1))
+    if _probe.keep:
+        _probe.descs.append(("gemm", GemmDesc.from_buffer_copy(d)))
 
 
 # ------------------------------------------------------------------------------ low precision
@@ -303,6 +309,8 @@ def gemm_lp(*args, slabs=False, **kw):
         key += (f" | {'T' if d.a_trans else 'N'}{'T' if d.b_trans else 'N'} {d.M}x{d.N}x{d.K}"
                 f" split{plan[1]} wg{plan[2]}")
     _probe.records.append((key, 2.0 * d.M * d.N * d.K, e0, e1))
+    if _probe.keep:
+        _probe.descs.append(("lp", _lib.GemmLpDesc.from_buffer_copy(d)))
 
 
 def cast_bf16(x: Tensor, rows: int, cols: int, ldi: int, out: Tensor, ldo: int, group=0,

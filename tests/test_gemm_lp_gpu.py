@@ -530,6 +530,30 @@ def _lp_plan(O, d):
     return list(plan)
 
 
+@pytest.mark.parametrize("mtype", ["bf16", "f32"])
+def test_bf16_tail_split_masked_fp32_out(mtype):
+    """A ReLU-backward dX into fp32 C (a bf16 or fp32 gate operand) whose last round of tiles is
+    split over K: the slab tail epilogue is linear only, so a masked launch keeps the atomic
+    tail (slab tails once dropped the gate) -- with the tail workspace offered,
+    the plan takes none, and the gate is applied on every row, the tail's included."""
+    O = ops()
+    M, N, K = 18688, 512, 6144
+    A, B = bf((M, K), 41), bf((K, N), 42)
+    pre = torch.randn(M, N, device=dev)
+    mk, ldm = (pre.to(torch.bfloat16) if mtype == "bf16" else pre), N
+    C = torch.full((M, N), 7.0, device=dev)
+    d = O.lp_desc(A, B, M, N, K, lda=K, ldb=N, C=C, ldc=N, mask=mk, ldmask=ldm)
+    assert O.lp_workspace(d, dev) is None
+    plan = _lp_plan(O, d)
+    assert plan[0] == 1 and plan[2] > ((M + 127) // 128) * (N // 128), plan  # atomic tail
+    O.gemm_lp(A, B, M, N, K, lda=K, ldb=N, C=C, ldc=N, mask=mk, ldmask=ldm)
+    torch.cuda.synchronize()
+    ref = (A.double() @ B.double()) * (pre > 0).double()
+    err = float((C.double() - ref).abs().max() / ref.abs().max())
+    assert err < 2e-5, err
+    assert bool((C[pre <= 0] == 0).all())
+
+
 @pytest.mark.parametrize("mode,K", [("atomic", 6144), ("slab", 6144), ("slab", 4096)])
 @pytest.mark.parametrize("lay,epi,ldc_pad", [("NT", "resid", 0), ("NN", "bias", 8),
                                              ("NT", "rowvec", 0), ("NN", "resid_bias", 16)])
