@@ -307,6 +307,14 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--serial", action="store_true",
                     help="run both stacks on one stream (per-kernel profiling)")
+    ap.add_argument("--bucket-mb", type=float, default=64.0,
+                    help="N > 1: all-reduce bucket size of the streamed gradient exchange")
+    ap.add_argument("--bwd-gate", default=None,
+                    help="N > 1: backward schedule (engine.vis_gate): auto (= enc4 with an "
+                         "all-reduce), concurrent, enc1..enc6, dec, syb_first")
+    ap.add_argument("--comm-steps", type=int, default=2,
+                    help="N > 1: untimed diagnostic steps after the timed region whose "
+                         "collectives are HIP-event timed (the line's 'comm' report)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -355,8 +363,10 @@ def main():
     model.train()
     if args.serial:
         model._engine.concurrent = False
+    if args.bwd_gate:
+        model._engine.bwd_order = args.bwd_gate
     opt = Adam(model, lr=1e-4)
-    reducer = GradReducer(model._arena) if world > 1 else None
+    reducer = GradReducer(model._arena, bucket_mb=args.bucket_mb) if world > 1 else None
     if reducer:
         model.attach_reducer(reducer, batch_size=B)
     if W.get("rel"):
@@ -402,11 +412,31 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    comm = None
+    if world > 1:
+        # per-rank diagnosis of the exchange (untimed steps): this rank's own step time from
+        # the timed region, and over --comm-steps steps with HIP events around every
+        # collective the summed collective time, the part that outlasted the backward
+        # (exposed), and the dense / row bytes
+        mine = {"rank": rank, "ms_per_step": round(elapsed / args.steps * 1e3, 3)}
+        if args.comm_steps > 0:
+            reducer.time_collectives(True)
+            for _ in range(args.comm_steps):
+                step()
+            mine.update(reducer.comm_summary() or {})
+            reducer.time_collectives(False)
+        ranks_c = [None] * world
+        dist.all_gather_object(ranks_c, mine)
+        eng = model._engine
+        comm = {"bucket_mb": args.bucket_mb, "bwd_order": eng.bwd_order,
+                "bwd_schedule": (eng.AUTO_GATE if eng.multi_rank else "concurrent")
+                if eng.bwd_order == "auto" else eng.bwd_order,
+                "diag_steps": args.comm_steps, "ranks": ranks_c}
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
-    final_loss = float(loss)
+    final_loss = float(loss.detach())
     backend = dist.get_backend() if dist.is_initialized() else None
     dist_info = {"backend": ("rccl" if backend == "nccl" else backend),
                  "world_size": dist.get_world_size() if dist.is_initialized() else 1,
@@ -481,6 +511,7 @@ def main():
             "model_mfma_frac": round(value * fl / 1e12 / (peak * world), 4),
             "loss": round(final_loss, 4),
             "dist": dist_info,
+            "comm": comm,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -447,6 +447,17 @@ int savqa_index_put_rows(void* stream, const int64_t* loc, int64_t B, int64_t Nv
 int savqa_index_get_rows(void* stream, const int64_t* loc, int64_t B, int64_t Nv, int64_t Ns,
                          int64_t H, const float* dmacro, float* dobj);
 
+/* Deterministic embedding-table gradient (the backward of nn.Embedding's row gather,
+ * modules.py:32-46 / AttModel_x3.py:96-99, :352-360 -- torch accumulates it with index_add):
+ * table[sid[j]][:cols] += sum of T[perm[k]][:cols] over the run of positions k with
+ * sid[k] == sid[j], added in run order. sid: the R row ids sorted ascending, perm: the stable
+ * sort's permutation (equal ids keep their row order), so the sum has ONE order whatever the
+ * schedule: run-to-run bit-identical, unlike an atomic scatter. T: the dense rows dY W of
+ * the GEMM that used to scatter. cols, ldt, ldtab multiples of 4; T, table 16-B aligned. */
+int savqa_segment_add_rows(void* stream, const float* T, int64_t ldt, const int64_t* perm,
+                           const int64_t* sid, int64_t R, int64_t cols, float* table,
+                           int64_t ldtab);
+
 /* ------------------------------------------------------------------------
  * Loss, main_itp_ddp_tar_super_node.py:335-361 + label_smoothing modules.py:461-463:
  *   lsm = (lsm(vis)+lsm(syb)+lsm(concat))/3; y = (1-eps)*onehot + eps/C

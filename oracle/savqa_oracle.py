@@ -96,6 +96,8 @@ def linear(x, P, name, relu=False):
         _relu_calls[name] = k + 1
         if RELU_BRANCHES.get("_record"):     # record this run's own decisions instead
             RELU_BRANCHES[(name, k)] = (y > 0).detach()
+            if RELU_BRANCHES.get("_pre") is not None:  # and the pre-activations themselves
+                RELU_BRANCHES["_pre"][(name, k)] = y.detach()
             return F.relu(y)
         m = RELU_BRANCHES.get((name, k))
         if m is not None:

@@ -347,6 +347,8 @@ class AttModel(nn.Module):
         tensors = (vis_t, i32(vis_mask), i64(q_ipt), i32(q_mask), i32(q_graph), i64(macro_ipt),
                    i32(macro_mask), i32(macro_graph), i64(macro_obj_loc), i64(micro_positive_obj),
                    i64(micro_negative_obj), i32(micro_obj_mask))
+        # a check left over from a forward that raised must never answer for this one
+        self._engine.pending_rel_check = None
         if not self.only_obj:  # relation branch inputs (micro_negative_rel ids are unused, :391)
             tensors = tensors + (i64(micro_positive_rel), i64(micro_positive_rel_loc),
                                  i64(micro_negative_rel_loc))

@@ -153,6 +153,7 @@ _SIGS = {
     "savqa_mil_bwd_bf16": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_p, c_p,
                            c_p],
     "savqa_index_put_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
+    "savqa_segment_add_rows": [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_p, c_i64],
     "savqa_index_get_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "savqa_loss_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f, c_p, c_i32, c_p, c_p, c_p, c_p],
     "savqa_scale_by": [c_p, c_p, c_p, c_i64, c_p],

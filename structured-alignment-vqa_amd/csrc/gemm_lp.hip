@@ -54,6 +54,36 @@ __device__ __forceinline__ void glds16(const void* src, lds_void* dst) {
   __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
 }
 
+// The same LDS-DMA as an asm statement hipcc does not see (cdna_hip_programming.md 5.7,
+// the M0 save / restore recipe). hipcc treats a pending __builtin_amdgcn_global_load_lds as a
+// write to LDS it cannot tell apart from the k-tile being read, and waits vmcnt(0) before the
+// first ds_read after it: in the 128 x 128 kernel that drained the NEXT k-tile's DMAs before
+// every k-tile's MFMAs (the .s showed s_waitcnt vmcnt(0) at the loop head) -- no overlap of
+// staging and compute at all. Hidden in asm, the DMAs stay in flight; the kernel counts them
+// itself (lp_wait_vm before each barrier).
+#ifndef SAVQA_LP_ASM_DMA
+#define SAVQA_LP_ASM_DMA 1
+#endif
+template <int BYTES>
+__device__ __forceinline__ void glds_asm(const void* src, lds_void* dst) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+  unsigned keep;
+  if constexpr (BYTES == 16)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(l) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(l) : "memory");
+}
+template <int BYTES>
+__device__ __forceinline__ void glds_k(const void* src, lds_void* dst) {  // the k-loop's DMAs
+  if constexpr (SAVQA_LP_ASM_DMA) glds_asm<BYTES>(src, dst);
+  else if constexpr (BYTES == 16) __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+  else __builtin_amdgcn_global_load_lds(src, dst, 4, 0, 0);
+}
+
 // 16 zero bytes: the LDS-DMA source of every operand granule past the end of K (the last,
 // partial k-tile of a K that is not a multiple of the k-tile)
 __device__ __attribute__((aligned(16))) uint4 g_lp_zero[1];
@@ -123,17 +153,86 @@ struct LpStage {
   __device__ __forceinline__ void issue(char* img, int wave, int64_t t) const {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      glds16(p[u] + t * step, (lds_void*)(img + (4 * wave + u) * 1024));
+      glds_k<16>(p[u] + t * step, (lds_void*)(img + (4 * wave + u) * 1024));
   }
 
   // partial last k-tile: granules at k >= krem (within the tile) load zeros
   __device__ __forceinline__ void issue_tail(char* img, int wave, int64_t t, int krem) const {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      glds16(koff[u] < krem ? (const void*)(p[u] + t * step) : (const void*)g_lp_zero,
-             (lds_void*)(img + (4 * wave + u) * 1024));
+      glds_k<16>(koff[u] < krem ? (const void*)(p[u] + t * step) : (const void*)g_lp_zero,
+                 (lds_void*)(img + (4 * wave + u) * 1024));
   }
 };
+
+// L2 prefetch of a future k-tile (SAVQA_LP_PF k-tiles beyond the one being staged; bf16
+// 128 x 128 kernel): every lane touches one 128-B line of its workgroup's operand tiles -- waves
+// 0-1 the A tile's 128 lines, waves 2-3 the B tile's -- by a 4-byte LDS-DMA into a dummy slot
+// (no VGPR destination, nothing reads it). A k-loop launch whose operands come cold from HBM
+// (the split-K weight gradients of a training step read activations written long before: in-step
+// they ran 1.2x their back-to-back time, profiles/r06_cfg3_gemm_replay.txt) otherwise waits a
+// full HBM latency per k-tile, since only the next k-tile is in flight; with the prefetch the
+// stage DMAs hit L2. The wait at the end of a k-tile becomes vmcnt(1) (the newest prefetch may
+// stay in flight; LDS-DMAs complete in issue order) with a raw barrier.
+// Measured (tools/gemm_replay.py, cfg-3 in-step launches, interleaved builds on one box):
+// with the DMAs in asm, the split-K dW 140 -> 106 us in-step; prefetching 2 or 4 k-tiles ahead
+// on top made it slower again (126-142 us: a line request per lane per k-tile through the
+// TA), so the prefetch is built but off.
+#ifndef SAVQA_LP_PF
+#define SAVQA_LP_PF 0
+#endif
+constexpr int LP_PF = SAVQA_LP_PF;
+constexpr int LP_PF_BYTES = LP_PF > 0 ? 1024 : 0;  // dummy LDS-DMA slots, 256 B per wave
+
+struct LpPf {
+  const char* base;  // this lane's line at k-tile 0 (k-row 0 of the tile for T images)
+  int64_t step;      // bytes per k-tile
+  int64_t krow, kmax;  // T image: this lane's k row within the launch; last valid row (K - 1)
+  int64_t ld_b;        // T image: bytes per k row
+  bool t;
+
+  template <bool T>
+  __device__ __forceinline__ void setup(const void* b0, int64_t ld, int esz,
+                                        const int64_t* __restrict__ rows, int64_t r0, int64_t lim,
+                                        int64_t kbeg, int64_t K, int q) {
+    const char* b = static_cast<const char*>(b0);
+    t = T;
+    if constexpr (!T) {  // tile row q (one 128-B line: 64 bf16 of k)
+      int64_t m = r0 + q;
+      m = m < lim ? m : lim - 1;
+      const int64_t rr = rows ? rows[m] : m;
+      base = b + (rr * ld + kbeg) * esz;
+      step = LP_KB;
+      krow = kmax = 0;
+      ld_b = 0;
+    } else {             // k row q / 2, columns 64 (q & 1) .. +63 of the tile
+      int64_t c = r0 + 64 * (q & 1);
+      c = c + 8 <= lim ? c : lim - 8;
+      base = b + c * esz;
+      krow = kbeg + (q >> 1);
+      kmax = K - 1;
+      ld_b = ld * esz;
+      step = 64;
+    }
+  }
+
+  __device__ __forceinline__ void issue(int64_t kt, lds_void* dummy) const {
+    const char* src;
+    if (t) {
+      int64_t k = krow + kt * step;
+      k = k < kmax ? k : kmax;
+      src = base + k * ld_b;
+    } else {
+      src = base + kt * step;
+    }
+    glds_k<4>(src, dummy);
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void lp_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 // bf16 fragment of 16 rows (R image) / 16 columns (T image), k 32kk + 8g .. +7 per lane
 template <bool T>
@@ -774,7 +873,11 @@ template <bool AT, bool BT, bool FP8, int PRE>
 __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   const savqa_gemm_lp_desc& d = args.d;
   // fp8: + two 1-KB e8m0 scale images [A rows 0..127 | B rows 0..127][4 blocks of 32 k]
-  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * LP_IMG + (FP8 ? 2048 : 0)];
+  // (+ the L2 prefetch's dummy DMA slots, bf16 only: ONE shared array -- a second __shared__
+  // object makes hipcc wait vmcnt(0) before every k-tile's first LDS read)
+  constexpr bool PFON = !FP8 && LP_PF > 0;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * LP_IMG + (FP8 ? 2048 : 0) +
+                                                      (PFON ? LP_PF_BYTES : 0)];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -806,6 +909,13 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   LpStage<!BT, FP8> sb;
   sa.setup(d.A, d.lda, esz, AT ? nullptr : d.a_rows, m0, d.M, kbeg, wave, lane);
   sb.setup(d.B, d.ldb, esz, nullptr, n0, d.N, kbeg, wave, lane);
+  LpPf pf;
+  if constexpr (PFON) {
+    const int q = 64 * (wave & 1) + lane;
+    if (wave < 2) pf.setup<AT>(d.A, d.lda, esz, AT ? nullptr : d.a_rows, m0, d.M, kbeg, d.K, q);
+    else pf.setup<!BT>(d.B, d.ldb, esz, nullptr, n0, d.N, kbeg, d.K, q);
+  }
+  lds_void* const pf_dummy = (lds_void*)(smem + 2 * 2 * LP_IMG + 256 * wave);
 
   f4 acc[4][4];
 #pragma unroll
@@ -846,8 +956,7 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   char* const sc_img = smem + 2 * 2 * LP_IMG;  // fp8 only: [buffer][A 512 B | B 512 B]
   auto stage_scales = [&](int buf, int64_t kt) {
     if constexpr (FP8)
-      __builtin_amdgcn_global_load_lds(scp + kt * 4, (lds_void*)(sc_img + buf * 1024 + wave * 256),
-                                       4, 0, 0);
+      glds_k<4>(scp + kt * 4, (lds_void*)(sc_img + buf * 1024 + wave * 256));
   };
   int sca[4], scb[4];
   auto read_scales = [&](int buf) {
@@ -874,7 +983,8 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
   if (nt > 0) {
     stage(smem, 0);
     stage_scales(0, 0);
-    __syncthreads();  // vmcnt(0) + barrier: stage 0 landed for every wave
+    lp_wait_vm<0>();  // (asm DMAs: __syncthreads() does not wait for them)
+    __syncthreads();  // stage 0 landed for every wave
     for (int kt = 0; kt < nt; ++kt) {
       const char* ia = smem + (kt & 1) * 2 * LP_IMG;
       const char* ib = ia + LP_IMG;
@@ -884,6 +994,10 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
         stage_scales((kt + 1) & 1, kt + 1);
       } else if constexpr (PRE == 1 || PRE == 2) {  // last k-tile: epilogue operands under its MFMAs
         if (!tail) pre.load(d, m0 + wm * 64, n0 + wn * 64, lane);
+      }
+      const bool pf_now = PFON && kt + 1 + LP_PF < nt;  // (uniform)
+      if constexpr (PFON) {
+        if (pf_now) pf.issue(kt + 1 + LP_PF, pf_dummy);
       }
       if constexpr (FP8) {
         i32x8 a[4], b[4];
@@ -924,7 +1038,12 @@ __global__ __launch_bounds__(LP_NT, LP_OCC) void gemm_lp_kernel(LpArgs args) {
           }
         }
       }
-      __syncthreads();  // k-tile kt+1 landed; buffer kt free for k-tile kt+2
+      // k-tile kt+1 landed (everything but the newest prefetch), this wave's LDS reads of
+      // buffer kt done; then the barrier: buffer kt free for k-tile kt+2
+      if (pf_now) lp_wait_vm<1>();
+      else lp_wait_vm<0>();
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
     }
   }
 
@@ -1198,7 +1317,7 @@ struct LpHalf {
   __device__ __forceinline__ void issue(char* img, int wave, int64_t t, int krem) const {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
-      glds16(krem >= 64 || koff[u] < krem ? (const void*)(p[u] + t * step) : (const void*)g_lp_zero,
+      glds_k<16>(krem >= 64 || koff[u] < krem ? (const void*)(p[u] + t * step) : (const void*)g_lp_zero,
              (lds_void*)(img + (2 * wave + u) * 1024));
   }
 };

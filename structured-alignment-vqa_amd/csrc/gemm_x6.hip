@@ -314,6 +314,14 @@ __device__ __forceinline__ int x6_mode(const savqa_gemm_desc& d, int64_t m0, int
 #ifndef SAVQA_X6_HILO
 #define SAVQA_X6_HILO 1
 #endif
+#ifndef SAVQA_X6_REREAD
+#define SAVQA_X6_REREAD 0
+#endif
+// (hipcc keeps the A fragments of the first section live for the later ones unless a compiler
+// barrier forces the re-reads: SAVQA_X6_REREAD)
+__device__ __forceinline__ void x6_reread_fence() {
+  if constexpr (SAVQA_X6_REREAD) asm volatile("" ::: "memory");
+}
 __device__ __forceinline__ void x6_compute_hilo(const char* As, const char* Bs, int wm, int wn,
                                                 int lane, f4 (&hi)[4][4], f4 (&lo)[4][4]) {
   bf16x8 b[4];
@@ -331,6 +339,7 @@ __device__ __forceinline__ void x6_compute_hilo(const char* As, const char* Bs, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) hi[i][j] = mma(a0, b[j], hi[i][j]);
   }
+  x6_reread_fence();
 #pragma unroll
   for (int j = 0; j < 4; ++j) b[j] = x6_frag(Bs + X6_PLANE, wn * 64 + 16 * j, lane);
 #pragma unroll
@@ -342,6 +351,7 @@ __device__ __forceinline__ void x6_compute_hilo(const char* As, const char* Bs, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) lo[i][j] = mma(a0, b[j], lo[i][j]);
   }
+  x6_reread_fence();
 #pragma unroll
   for (int j = 0; j < 4; ++j) b[j] = x6_frag(Bs + 2 * X6_PLANE, wn * 64 + 16 * j, lane);
 #pragma unroll

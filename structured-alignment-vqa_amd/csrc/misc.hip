@@ -487,6 +487,31 @@ __global__ void index_put_rows_kernel(const int64_t* __restrict__ loc, int64_t N
   }
 }
 
+// Deterministic row scatter-add (savqa_segment_add_rows): one wave per sorted position j;
+// the wave at the start of a run of equal ids sums the run's rows of T in run order (the
+// stable sort keeps equal ids in their original row order) and adds the sum to the table row
+// -- one writer per row, a fixed order, no atomics. Columns in float4s (cols % 4 == 0).
+__global__ __launch_bounds__(256) void segment_add_rows_kernel(
+    const float* __restrict__ T, int64_t ldt, const int64_t* __restrict__ perm,
+    const int64_t* __restrict__ sid, int64_t R, int64_t cols, float* __restrict__ table,
+    int64_t ldtab) {
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (j >= R) return;
+  const int64_t id = sid[j];
+  if (j > 0 && sid[j - 1] == id) return;  // not the start of a run (wave-uniform)
+  int64_t end = j + 1;
+  while (end < R && sid[end] == id) ++end;
+  float* dst = table + id * ldtab;
+  for (int64_t c = 4 * lane; c < cols; c += 256) {
+    v4 acc = *reinterpret_cast<const v4*>(T + perm[j] * ldt + c);
+    for (int64_t k = j + 1; k < end; ++k) acc += *reinterpret_cast<const v4*>(T + perm[k] * ldt + c);
+    v4* o = reinterpret_cast<v4*>(dst + c);
+    *o = *o + acc;
+  }
+}
+
 __global__ void index_get_rows_kernel(const int64_t* __restrict__ loc, int64_t Nv, int64_t Ns,
                                       int64_t H, const float* __restrict__ dmacro,
                                       float* __restrict__ dobj) {
@@ -628,7 +653,7 @@ __global__ void scatter_rows_kernel(const float* __restrict__ g, const int64_t* 
 // m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2; p -= (lr/bc1) m / (sqrt(v)/sqrt(bc2) + eps).
 // Streaming, 28 B/param: each thread moves 2 float4 of p, g, m, v per iteration with
 // non-temporal loads/stores (11 GB per step at the cfg-2 arena never fits in cache).
-// grid cap of the grid-stride Adam launch (A/B knob; tools/adam_bench.py over 457M params,
+// grid cap of the grid-stride Adam launch (A/B knob; round 3, a since-removed Adam micro-bench over 457M params,
 // interleaved runs: 8192 blocks 2.17-2.37 ms, 32768 2.05-2.32 ms, i.e. ~4% within noise)
 #ifndef SAVQA_ADAM_BLOCKS
 #define SAVQA_ADAM_BLOCKS 32768
@@ -924,6 +949,18 @@ extern "C" int savqa_index_put_rows(void* stream, const int64_t* loc, int64_t B,
   hipLaunchKernelGGL(index_put_rows_kernel, dim3(B), dim3(256), 0, as_stream(stream), loc, Nv, Ns, H,
                      obj, macro);
   return check_launch("savqa_index_put_rows");
+}
+
+extern "C" int savqa_segment_add_rows(void* stream, const float* T, int64_t ldt,
+                                      const int64_t* perm, const int64_t* sid, int64_t R,
+                                      int64_t cols, float* table, int64_t ldtab) {
+  if (R <= 0 || cols <= 0) return 0;
+  if (cols % 4 || ldt % 4 || ldtab % 4 || ((uintptr_t)T & 15) || ((uintptr_t)table & 15))
+    return fail(SAVQA_EUNSUP, "savqa_segment_add_rows: needs 16-B aligned rows (cols, ldt, "
+                              "ldtab multiples of 4)");
+  hipLaunchKernelGGL(segment_add_rows_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0,
+                     as_stream(stream), T, ldt, perm, sid, R, cols, table, ldtab);
+  return check_launch("savqa_segment_add_rows");
 }
 
 extern "C" int savqa_index_get_rows(void* stream, const int64_t* loc, int64_t B, int64_t Nv,

@@ -61,6 +61,11 @@ class GradReducer:
     optimizer can update each bucket as soon as ITS all-reduce lands (Adam of the early
     buckets overlaps the all-reduce of the last ones)."""
 
+    # collective timing of diagnostic steps (time_collectives): off by default
+    stats = None
+    _comm = None
+    _bwd_end = None
+
     def __init__(self, arena, bucket_mb: float = 64.0, group=None, filler: int = 400000,
                  force: bool = False):
         self.arena = arena
@@ -93,6 +98,12 @@ class GradReducer:
         self.trace: List = []
         self._rows_done = set()     # arena offsets of the tables exchanged by rows this step
         self.rows_exchanged = 0     # tables exchanged by rows in the current step
+        # collective timing (diagnostic steps only, bench.py's N > 1 "comm" report): None = off;
+        # a list = every collective of the step issued from a side stream bracketed by HIP
+        # events, [(kind, bytes, e_start, e_landed)], plus the end of the backward
+        self.stats = None
+        self._comm = None
+        self._bwd_end = None
 
     def add_sparse_table(self, lo: int, hi: int, width: int):
         """Exchange arena range [lo, hi) (a row-major table of `width`-wide rows) by the
@@ -106,7 +117,58 @@ class GradReducer:
         flags then get the union of every rank's ids, so Adam may update it row by row)."""
         return self.active and offset in self._rows_done
 
+    def time_collectives(self, on: bool = True):
+        """Diagnostic mode for the next steps: each collective is issued from a side stream
+        that first waits for the producing stream, with an event before the issue and one
+        after the collective has landed (the side stream waits for it), so comm_summary() can
+        report the exchange's busy time, how much of it outlasted the backward, and the
+        bytes. Off (None) in timed steps: the normal path issues on the producer stream."""
+        self.stats = [] if on else None
+
+    def _timed(self, kind: str, nbytes: int, issue):
+        if self.stats is None or not torch.cuda.is_available():
+            return issue()
+        cur = torch.cuda.current_stream()
+        if self._comm is None or self._comm.device != cur.device:
+            self._comm = torch.cuda.Stream(device=cur.device)
+        s = self._comm
+        s.wait_stream(cur)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s):
+            e0.record(s)
+            w = issue()
+            w.wait()
+            e1.record(s)
+        self.stats.append((kind, int(nbytes), e0, e1))
+        return w
+
+    def comm_summary(self):
+        """Of the last step run with time_collectives(): collectives issued, the sum of
+        their durations (each starts once its data is final and the previous one has
+        landed), the part of the exchange that ended after the backward did (exposed), and
+        bytes per kind (dense all-reduce buffers; row all-gather outputs)."""
+        if not self.stats:
+            return None
+        torch.cuda.synchronize()
+        busy = sum(e0.elapsed_time(e1) for _, _, e0, e1 in self.stats)
+        exposed = None
+        if self._bwd_end is not None:
+            exposed = max(0.0, max(self._bwd_end.elapsed_time(e1) for *_, e1 in self.stats))
+        by = {}
+        for kind, nb, _, _ in self.stats:
+            by[kind] = by.get(kind, 0) + nb
+        out = {"collectives": len(self.stats), "allreduce_ms": round(busy, 3),
+               "exposed_ms": None if exposed is None else round(exposed, 3),
+               "dense_MB": round(by.get("dense", 0) / 2 ** 20, 2),
+               "rows_MB": round(by.get("rows", 0) / 2 ** 20, 2),
+               "rows_tables": sum(1 for k, *_ in self.stats if k == "rows")}
+        return out
+
     def begin(self):
+        self._bwd_end = None
+        if self.stats is not None:
+            self.stats = []
         self._rows_done = set()
         self.works = []
         self.pending = {}
@@ -179,7 +241,8 @@ class GradReducer:
 
     def _dense(self, lo: int, hi: int):
         g = self.arena.grad
-        w = dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        w = self._timed("dense", (hi - lo) * g.element_size(), lambda: dist.all_reduce(
+            g[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         self.works.append((w, lo, hi))
         self.trace.append(("dense", lo, hi))
 
@@ -212,7 +275,8 @@ class GradReducer:
         buf = table.index_select(0, ids[self.rank])
         buf.mul_(first.unsqueeze(1).to(buf.dtype))
         outs = [torch.empty_like(buf) for _ in range(self.world)]
-        w = dist.all_gather(outs, buf, group=self.group, async_op=True)
+        w = self._timed("rows", buf.numel() * buf.element_size() * self.world,
+                        lambda: dist.all_gather(outs, buf, group=self.group, async_op=True))
         self.works.append((_RowsWork(w, table, union, ids, outs), t0, t1))
         self.trace.append(("rows", t0, t1))
         self.rows_exchanged += 1
@@ -249,6 +313,10 @@ class GradReducer:
         """Issue what is pending; return ([(work, lo, hi)...] in issue order, 1/world)."""
         if not self.active:
             return [], 1.0
+        if self.stats is not None and torch.cuda.is_available():
+            # the backward has been issued on this stream: its end, for comm_summary()
+            self._bwd_end = torch.cuda.Event(enable_timing=True)
+            self._bwd_end.record()
         self._flush_all()
         works, self.works = self.works, []
         return works, 1.0 / self.world

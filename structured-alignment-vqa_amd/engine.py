@@ -43,6 +43,20 @@ def _bf(*shape, dev):
     return torch.empty(*shape, dtype=torch.bfloat16, device=dev)
 
 
+def _table_grad(dY: torch.Tensor, W: torch.Tensor, ids: torch.Tensor, table: torch.Tensor,
+                rows: int):
+    """Embedding-table gradient table[ids] += dY W (nn.Embedding's backward, index_add):
+    deterministic by default -- the dense rows, then savqa_segment_add_rows in sorted-id order
+    (ops.DET_SCATTER) -- else the GEMM's atomic scatter epilogue."""
+    if ops.DET_SCATTER:
+        cols = W.shape[1]
+        T = _empty(rows, cols, dev=dY.device)
+        ops.linear_dx(dY, W, T, rows=rows)
+        ops.segment_add_rows(T, cols, ids, cols, table, table.stride(0))
+    else:
+        ops.linear_dx(dY, W, table, rows=rows, c_rows=ids, atomic=True)
+
+
 def _rows_index(B: int, T: int, start: int, count: int, dev) -> torch.Tensor:
     """int64 row ids b*T + start + t for t < count (gather index into a [B,T,...] buffer)."""
     return (torch.arange(B, device=dev, dtype=torch.int64).unsqueeze(1) * T
@@ -607,7 +621,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         ops.linear_dx(dx, W.Win, dq, rows=B * Lq, a_rows=qrows, mask=s.cat, ldmask=s.cat.shape[1],
                       mask_arows=True)
     ops.linear_dw(dq, W.E, G.Wq, G.bq, rows=B * Lq, x_rows=s.q_flat)
-    ops.linear_dx(dq, W.Wq, G.E, rows=B * Lq, c_rows=s.q_flat, atomic=True)
+    _table_grad(dq, W.Wq, s.q_flat, G.E, B * Lq)
     G.arena.mark_rows(G.table, s.q_flat)  # the table's gradient rows of this step
     del dq
     if not want_node_grad:
@@ -789,7 +803,7 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
         drelf = rel["drelf"]
         ops.rowscale_mask(drelf, None, rel["relf"], B * Lp, Hm, drelf)  # ReLU of syb_mlp
         ops.linear_dw(drelf, W.E, G.Ws, G.bs, rows=B * Lp, x_rows=rel["pos_rel"])
-        ops.linear_dx(drelf, W.Ws, G.E, rows=B * Lp, c_rows=rel["pos_rel"], atomic=True)
+        _table_grad(drelf, W.Ws, rel["pos_rel"], G.E, B * Lp)
         G.arena.mark_rows(G.table, rel["pos_rel"])
     dvv = torch.empty_like(s.vv)
     n = B * Nv * K
@@ -804,16 +818,23 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
             ops.gemm_lp(dY, eg, Hm, GLOVE_PAD, n, lda=Hm, ldb=GLOVE_PAD, a_trans=True, C=G.Ws,
                         ldc=GLOVE_D, atomic=True, split_k=-1, n_store=GLOVE_D, slabs=True,
                         colsum_a=G.bs)
-            ops.gemm_lp(dY, lp.Ws, n, GLOVE_PAD, Hm, lda=Hm, ldb=GLOVE_PAD, C=G.E, ldc=GLOVE_D,
-                        atomic=True, split_k=-1, c_rows=ids, n_store=GLOVE_D)
+            if ops.DET_SCATTER:  # dense rows, then the sorted-id segment sums (_table_grad)
+                T = _empty(n, GLOVE_PAD, dev=dev)
+                ops.gemm_lp(dY, lp.Ws, n, GLOVE_PAD, Hm, lda=Hm, ldb=GLOVE_PAD, C=T,
+                            ldc=GLOVE_PAD)
+                ops.segment_add_rows(T, GLOVE_PAD, ids, GLOVE_D, G.E, G.E.stride(0))
+                del T
+            else:
+                ops.gemm_lp(dY, lp.Ws, n, GLOVE_PAD, Hm, lda=Hm, ldb=GLOVE_PAD, C=G.E,
+                            ldc=GLOVE_D, atomic=True, split_k=-1, c_rows=ids, n_store=GLOVE_D)
         del dPb, dNb
     else:
         dPf, dNf = torch.empty_like(s.Pf), torch.empty_like(s.Nf)
         ops.mil_bwd(s.Pf, s.Nf, s.vv, s.mask, B * Nv, K, Hm, eps, dobj, dmil, dPf, dNf, dvv)
         ops.linear_dw(dPf, W.E, G.Ws, G.bs, rows=n, x_rows=s.pos)
         ops.linear_dw(dNf, W.E, G.Ws, G.bs, rows=n, x_rows=s.neg)
-        ops.linear_dx(dPf, W.Ws, G.E, rows=n, c_rows=s.pos, atomic=True)
-        ops.linear_dx(dNf, W.Ws, G.E, rows=n, c_rows=s.neg, atomic=True)
+        _table_grad(dPf, W.Ws, s.pos, G.E, n)
+        _table_grad(dNf, W.Ws, s.neg, G.E, n)
     # the table's gradient rows of this step: the positive / negative object words
     G.arena.mark_rows(G.table, s.pos)
     G.arena.mark_rows(G.table, s.neg)
@@ -1184,24 +1205,28 @@ class ModelEngine:
                                inp["q_mask"], inp["q_graph"], None, decMask, H, d, drop,
                                VIS_SITES, lp=lp_vis)
         check, self.pending_rel_check = self.pending_rel_check, None
-        with torch.cuda.stream(s_syb):
-            mil_val = _empty((), dev=dev)
-            if lp_syb is None:
-                cat_syb = _empty(B * Ts, Dv, dev=dev)
-            rel, mil_rel = None, None
-            if "micro_positive_rel_loc" in inp:
-                rel = (inp["micro_positive_rel"], inp["micro_positive_rel_loc"],
-                       inp["micro_negative_rel_loc"])
-                mil_rel = _empty((), dev=dev)
-            ms = mil_forward(self.mil, vis, inp["macro_ipt"], inp["macro_obj_loc"],
-                             inp["micro_positive_obj"], inp["micro_negative_obj"],
-                             inp["micro_obj_mask"], cat_syb, Ts, mil_val, rel=rel,
-                             mil_rel_out=mil_rel, lp=lp_mil, rel_check=check)
-            ss = stack_forward(self.syb, cat_syb, B, Ns, Lq, inp["q_ipt"], inp["macro_mask"],
-                               inp["q_mask"], inp["q_graph"], inp["macro_graph"], decMask, H, d,
-                               drop, SYB_SITES, lp=lp_syb)
-        main.wait_stream(s_vis)
-        main.wait_stream(s_syb)
+        # (a relation row the reference could not index raises IndexError from mil_forward:
+        # the main stream still joins both side streams, whose work is already queued)
+        try:
+            with torch.cuda.stream(s_syb):
+                mil_val = _empty((), dev=dev)
+                if lp_syb is None:
+                    cat_syb = _empty(B * Ts, Dv, dev=dev)
+                rel, mil_rel = None, None
+                if "micro_positive_rel_loc" in inp:
+                    rel = (inp["micro_positive_rel"], inp["micro_positive_rel_loc"],
+                           inp["micro_negative_rel_loc"])
+                    mil_rel = _empty((), dev=dev)
+                ms = mil_forward(self.mil, vis, inp["macro_ipt"], inp["macro_obj_loc"],
+                                 inp["micro_positive_obj"], inp["micro_negative_obj"],
+                                 inp["micro_obj_mask"], cat_syb, Ts, mil_val, rel=rel,
+                                 mil_rel_out=mil_rel, lp=lp_mil, rel_check=check)
+                ss = stack_forward(self.syb, cat_syb, B, Ns, Lq, inp["q_ipt"], inp["macro_mask"],
+                                   inp["q_mask"], inp["q_graph"], inp["macro_graph"], decMask, H, d,
+                                   drop, SYB_SITES, lp=lp_syb)
+        finally:
+            main.wait_stream(s_vis)
+            main.wait_stream(s_syb)
         for t in (sv.out, ss.out, mil_val) + ((mil_rel,) if mil_rel is not None else ()):
             t.record_stream(main)
         (lc, lv, ls), hs = heads_forward(self.head, sv.out, ss.out, d, drop)

@@ -441,9 +441,10 @@ _ln_ws = {}
 
 
 def ln_workspace(cols: int, dev) -> Tensor:
-    """The caller-owned, zero-filled slot workspace of savqa_ln_bwd for the current stream
-    (the library re-zeroes it after every call, so one per (device, stream) is reused;
-    the two stacks' streams run LN backwards concurrently and get one each)."""
+    """The caller-owned workspace of savqa_ln_bwd for the current stream: 512 x 2 x cols
+    floats of per-block gamma / beta partial rows, written with plain stores and summed in
+    block order by the library (no initial contents needed; one per (device, stream) is
+    reused, the two stacks' streams run LN backwards concurrently and get one each)."""
     key = (dev.index if dev.index is not None else torch.cuda.current_device(), _stream())
     nbytes = int(_lib.load().savqa_ln_bwd_workspace_bytes(int(cols)))
     ws = _ln_ws.get(key)
@@ -611,6 +612,19 @@ def mil_bwd_bf16(Pf, Nf, v, mask, BN, K, H, eps, dobj, dmil, dPf, dNf, dv):
 def mil_bwd(Pf, Nf, v, mask, BN, K, H, eps, dobj, dmil, dPf, dNf, dv):
     call("savqa_mil_bwd", _stream(), _p(Pf), _p(Nf), _p(v), _p(mask), BN, K, H, float(eps),
          _p(dobj), _p(dmil), _p(dPf), _p(dNf), _p(dv))
+
+
+# Embedding-table gradients (the GloVe-row scatters dE[ids] += dY W) through a dense GEMM and
+# savqa_segment_add_rows over the stably sorted ids (one order per row: run-to-run
+# bit-identical) instead of the GEMM's atomic scatter epilogue (SAVQA_DET_SCATTER=0)
+DET_SCATTER = os.environ.get("SAVQA_DET_SCATTER", "1") != "0"
+
+
+def segment_add_rows(T: Tensor, ldt: int, ids: Tensor, cols: int, table: Tensor, ldtab: int):
+    """table[ids[r]][:cols] += T[r][:cols] for every row r, summed per id in row order."""
+    sid, perm = torch.sort(ids.reshape(-1), stable=True)
+    call("savqa_segment_add_rows", _stream(), _p(T), int(ldt), _p(perm), _p(sid), int(sid.numel()),
+         int(cols), _p(table), int(ldtab))
 
 
 def index_put_rows(loc, B, Nv, Ns, H, obj, macro):

@@ -9,7 +9,11 @@ Sites the HIP path does not compute have no mask (the oracle's own ReLU runs the
 decoder self-attention's Q / K (one key: softmax == 1, exactly zero gradient) and the detached
 macro projection (AttModel_x3.py:354). In encoder layers 0-1 the node rows' Q / V are not
 computed either (their attention weights are exactly 0: engine.PRUNE_L01); their mask is 0."""
+import re
+
 import torch
+
+_PRUNED = re.compile(r"enc_self_attention_[01]\.(Q|V)_proj")
 
 
 def capture(model):
@@ -91,3 +95,28 @@ class _null:
 
     def __exit__(self, *exc):
         return False
+
+
+def mask_disagreement(O, params, batch, hip, names, tol=1e-4, **kw):
+    """The HIP forward's ReLU decisions against the fp64 oracle's OWN (an unaligned fp64 run
+    that records its pre-activations): per site, the units where they differ must sit within
+    tol x the site's largest |pre-activation| of 0 (rounding can flip those, a wrong gate flips
+    units anywhere) and be rare. Returns {site: (flips, units, worst |pre| / max |pre|)}."""
+    rec = {"_record": True, "_pre": {}}
+    oracle_grads(O, params, batch, rec, torch.float64, "cuda", names, **kw)
+    pre = rec["_pre"]
+    out = {}
+    for key, m in hip.items():
+        y = pre.get(key)
+        if y is None or _PRUNED.search(key[0]):  # node rows of layers 0-1: masks are "don't
+            continue                             # care" zeros there (module docstring)
+        y = y.reshape(m.shape).to(m.device)
+        flip = m != (y > 0)
+        n = int(flip.sum())
+        scale = float(y.abs().max())
+        worst = float(y[flip].abs().max()) / max(scale, 1e-300) if n else 0.0
+        out[key] = (n, m.numel(), worst)
+    bad = {k: v for k, v in out.items() if v[2] > tol or v[0] > max(8, v[1] // 1000)}
+    assert not bad, bad
+    assert out, "no site compared"
+    return out

@@ -42,6 +42,34 @@ def test_bench_two_ranks_gloo_rehearsal(workload):
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 64
     assert d["value"] > 0 and d["ms_per_step"] > 0
     assert d["loss"] == d["loss"] and abs(d["loss"]) < 1e4   # finite
+    # the per-rank exchange diagnosis: every rank's own step time, the
+    # collectives' summed time, the part that outlasted the backward, and the bytes; the two
+    # stack tables go by rows, the rest densely (the whole live range, 457M floats at cfg 2)
+    c = d["comm"]
+    assert c["bucket_mb"] == 64.0 and c["bwd_schedule"] == "enc4" and c["diag_steps"] == 2
+    assert sorted(r["rank"] for r in c["ranks"]) == [0, 1]
+    for r in c["ranks"]:
+        assert r["ms_per_step"] > 0 and r["allreduce_ms"] > 0 and r["exposed_ms"] >= 0
+        assert r["rows_tables"] == 2 and r["rows_MB"] > 0
+        assert r["dense_MB"] > 500 and r["collectives"] > 10, r
+
+
+def test_bench_comm_flags_two_ranks():
+    """--bucket-mb / --bwd-gate reach the reducer and the engine (the first real SCALE run
+    can sweep them) and are echoed in the line's comm report."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    env = dict(os.environ, SAVQA_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+           "--batch", "16", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+           "--no-roofline", "--bucket-mb", "256", "--bwd-gate", "concurrent", "--comm-steps", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith('{"metric"')][0])
+    c = d["comm"]
+    assert c["bucket_mb"] == 256.0 and c["bwd_schedule"] == "concurrent"
+    assert c["diag_steps"] == 1 and len(c["ranks"]) == 2
 
 
 def test_bench_launcherless_form_starts_n_ranks():

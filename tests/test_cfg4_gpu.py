@@ -99,6 +99,11 @@ def test_cfg4_full_depth_against_oracle(model, batch):
     errs = {n: _rel(mine[n], ref[n]) for n in heads}
     for n in heads:
         assert errs[n] < 1e-3, (n, errs)
+    # the masks the comparison aligns on are themselves checked: against the
+    # fp64 oracle's own decisions, HIP flips only units within rounding of 0
+    flips = branch_masks.mask_disagreement(O, params, b, masks, deep, **kw)
+    print(f"cfg4 ReLU sites compared {len(flips)}, flipped units "
+          f"{sum(v[0] for v in flips.values())}")
     r64, _ = branch_masks.oracle_grads(O, params, b, masks, torch.float64, dev, deep, **kw)
     r32, _ = branch_masks.oracle_grads(O, params, b, masks, torch.float32, "cpu", deep, **kw)
     for n in deep:

@@ -198,6 +198,11 @@ def test_cfg2_gradients_branch_aligned_fp64(model):
     box = []
     mine, _ = _hip_step(model, b, ALIGNED, box)
     masks = box[0]
+    # the masks the comparison aligns on, against the fp64 oracle's own decisions: HIP flips
+    # only units within rounding of 0 (a gating bug would flip units anywhere)
+    flips = branch_masks.mask_disagreement(O, params, b, masks, ALIGNED)
+    print(f"\nReLU sites compared {len(flips)}, flipped units "
+          f"{sum(v[0] for v in flips.values())} of {sum(v[1] for v in flips.values())}")
     t0 = time.perf_counter()
     ref, _ = branch_masks.oracle_grads(O, params, b, masks, torch.float64, "cuda", ALIGNED)
     t64 = time.perf_counter() - t0

@@ -621,9 +621,15 @@ def test_gemm_slabs_deterministic(prec, case, monkeypatch):
     plan = O.gemm(A, B, None, M, N, K, prec=prec, plan_only=True, **kw)
     assert plan[0] == 128 and (plan[1] > 1 if case == "splitk_dw" else plan[2] > 1), plan
 
+    # the weight gradient ACCUMULATES (the slab reduce's C += sum, colsum += sum branch, which
+    # runs every step since GEMM_SLABS became the default): start from an existing gradient
+    gen = torch.Generator(device=dev).manual_seed(36)
+    c0 = torch.randn(M, N, generator=gen, device=dev) if case == "splitk_dw" else None
+    s0 = torch.randn(M, generator=gen, device=dev) if case == "splitk_dw" else None
+
     def run():
-        out = torch.zeros(M, N, device=dev)
-        cs = torch.zeros(M, device=dev) if case == "splitk_dw" else None
+        out = c0.clone() if c0 is not None else torch.zeros(M, N, device=dev)
+        cs = s0.clone() if s0 is not None else None
         O.gemm(A, B, out, M, N, K, prec=prec, colsum_a=cs, **kw)
         torch.cuda.synchronize()
         return out, cs
@@ -632,9 +638,10 @@ def test_gemm_slabs_deterministic(prec, case, monkeypatch):
         assert torch.equal(o, outs[0][0])
         if c is not None:
             assert torch.equal(c, outs[0][1])
-    assert rel(outs[0][0], ref) < 5e-6
     if case == "splitk_dw":
-        assert rel(outs[0][1], A.double().sum(0)) < 1e-5
+        ref = ref + c0.double()
+        assert rel(outs[0][1].double() - s0.double(), A.double().sum(0)) < 1e-5
+    assert rel(outs[0][0], ref) < 5e-6
     monkeypatch.setattr(O, "GEMM_SLABS", False)
     atom, _ = run()
     assert rel(atom, outs[0][0]) < 5e-6

@@ -112,6 +112,8 @@ def main():
     ap.add_argument("--hints", default="",
                     help="lp weight-gradient launches (TN, no mask): also replay under these "
                          "tile_hint kernel variants, e.g. 1,3,4,5 (hot / cold)")
+    ap.add_argument("--hints-all", action="store_true",
+                    help="--hints on every bf16 launch (forward / dX too), not only the dW")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     m, step = build(a.workload, dev)
@@ -160,8 +162,9 @@ def main():
             shape = key.split(" | ", 1)[1]
             print(f"{shape:58s} {n:3d} {us / n:8.1f} {rep:8.1f} {fr:8.1f} {cold:8.1f}"
                   f" {fl / (us / n) / 1e6:9.1f} {fl / rep / 1e6:8.1f}")
-            if a.hints and kind == "lp" and d.a_trans and not d.mask and not d.bits_out \
-                    and not d.Cb and d.a_type == 1:
+            if a.hints and kind == "lp" and d.a_type == 1 and not d.bits_out and \
+                    not (d.mask and d.mask_type == 3) and (a.hints_all or (d.a_trans and not
+                                                                          d.mask and not d.Cb)):
                 for h in [int(x) for x in a.hints.split(",")]:
                     dh = type(d).from_buffer_copy(d)
                     dh.tile_hint = h
