@@ -515,8 +515,8 @@ __device__ __forceinline__ void sk_full4(const float* __restrict__ base, int64_t
 // straight-line (every slot's MFMAs, then its reload D groups ahead), so hipcc's counted
 // vmcnt waits for exactly the slot it consumes; guards only in the drain. Fewer than D
 // groups: all loads first, then the MFMAs (one round trip).
-template <int D, class LD, class MM>
-__device__ __forceinline__ void sk_ring(int64_t g0, int ng, float (&a)[D][4], float (&b)[D][4],
+template <int D, int W, class LD, class MM>
+__device__ __forceinline__ void sk_ring(int64_t g0, int ng, float (&a)[D][W], float (&b)[D][W],
                                         LD&& load, MM&& mma) {
   if (ng >= D) {
 #pragma unroll
@@ -641,6 +641,103 @@ __global__ __launch_bounds__(64 * NW) void gemm_skinny_kernel(savqa_gemm_desc d,
         }
       }
     }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[w][(r & 3) + 8 * (r >> 2) + 4 * q][i] = acc[r];
+  __syncthreads();
+  const bool ident = d.c_rows == nullptr && d.c_group >= d.M && d.c_offset == 0;
+  for (int e = threadIdx.x; e < 32 * 32; e += 64 * NW) {
+    const int r = e >> 5, c = e & 31;
+    const int64_t m = m0 + r, n = n0 + c;
+    if (m >= d.M || n >= d.N) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) v += red[ww][r][c];
+    const EpiRow er = epi_row(d, m, ident);
+    epi_store(d, er, m, n, v, true, d.atomic != 0);
+  }
+  if constexpr (AT) {
+    if (d.colsum_a && n0 == 0) {
+      __syncthreads();
+      float* flat = &red[0][0][0];
+      flat[threadIdx.x] = cs;  // 64 * NW partials: (wave, half q, i)
+      __syncthreads();
+      if (threadIdx.x < 32 && m0 + threadIdx.x < d.M) {
+        float sum = 0.f;
+        for (int j = 0; j < 2 * NW; ++j) sum += flat[j * 32 + threadIdx.x];
+        atomicAdd(&d.colsum_a[m0 + threadIdx.x], sum);
+      }
+    }
+  }
+}
+
+// bf16-product variant of gemm_skinny_kernel (savqa_gemm_desc.prec = 1: the low-precision
+// modes' decoder / head Linears at M = B rows, whose operands are fp32 activations): the same
+// 32x32 tile, K split over the 8 waves and LDS fold, but groups of 16 k -- lane half q takes
+// k = 16g + 8q .. +7 of its row (two b128 loads on a k-contiguous operand), rounds them to
+// bf16 (RNE, autocast's rounding of a Linear's operands) and issues ONE
+// v_mfma_f32_32x32x16_bf16 per group instead of eight v_mfma_f32_32x32x2_f32 (32 against 512
+// SIMD cycles); fp32 accumulation, the fp32 epilogue. The bias-gradient column sums (AT) add
+// the fp32 values.
+template <bool AT, bool BT, int NW, bool AV, bool BV>
+__global__ __launch_bounds__(64 * NW) void gemm_skinny_bf_kernel(savqa_gemm_desc d, int tiles_n,
+                                                                 int avec, int bvec) {
+  typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+  __shared__ float red[NW][32][33];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = blockIdx.x;
+  const int64_t m0 = (int64_t)(t / tiles_n) * 32, n0 = (int64_t)(t % tiles_n) * 32;
+  const int64_t ngrp = (d.K + 15) / 16;
+  const int64_t g0 = ngrp * w / NW, g1 = ngrp * (w + 1) / NW;
+  const int64_t gf = min(g1, max(g0, d.K / 16));  // [g0, gf): groups wholly inside K
+  const int i = lane & 31, q = lane >> 5;
+  const int64_t am = m0 + i, bn = n0 + i;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float cs = 0.f;
+  const bool aok = am < d.M, bok = bn < d.N;
+  auto mma = [&](const float (&aa)[8], const float (&bb)[8]) {
+    bfx8 x, y;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xa = aok ? aa[j] : 0.f;
+      cs += xa;
+      x[j] = (__bf16)xa;
+      y[j] = (__bf16)(bok ? bb[j] : 0.f);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc, 0, 0, 0);
+  };
+  const float* ab = sk_base<!AT>(d.A, d.lda, AT ? nullptr : d.a_rows, am, d.M);
+  const float* bb_ = sk_base<BT>(d.B, d.ldb, BT ? d.b_rows : nullptr, bn, d.N);
+  constexpr int D = 4;
+  float a[D][8], b[D][8];
+  auto load = [&](int64_t g, float (&aa)[8], float (&bx)[8]) {
+    const int64_t k = g * 16 + 8 * q;
+    float t4[4];
+    sk_full4<!AT, AV>(ab, d.lda, k, t4);
+    aa[0] = t4[0]; aa[1] = t4[1]; aa[2] = t4[2]; aa[3] = t4[3];
+    sk_full4<!AT, AV>(ab, d.lda, k + 4, t4);
+    aa[4] = t4[0]; aa[5] = t4[1]; aa[6] = t4[2]; aa[7] = t4[3];
+    sk_full4<BT, BV>(bb_, d.ldb, k, t4);
+    bx[0] = t4[0]; bx[1] = t4[1]; bx[2] = t4[2]; bx[3] = t4[3];
+    sk_full4<BT, BV>(bb_, d.ldb, k + 4, t4);
+    bx[4] = t4[0]; bx[5] = t4[1]; bx[6] = t4[2]; bx[7] = t4[3];
+  };
+  sk_ring<D>(g0, (int)(gf - g0), a, b, load, mma);
+  if (gf < g1) {  // the partial group at the end of K (one wave at most)
+    float aa[8], bx[8], t4[4];
+    const int64_t k = gf * 16 + 8 * q;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      sk_load4<!AT>(d.A, d.lda, d.a_rows, am, d.M, k + 4 * h, d.K, avec, t4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) aa[4 * h + j] = t4[j];
+      sk_load4<BT>(d.B, d.ldb, d.b_rows, bn, d.N, k + 4 * h, d.K, bvec, t4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bx[4 * h + j] = t4[j];
+    }
+    mma(aa, bx);
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[w][(r & 3) + 8 * (r >> 2) + 4 * q][i] = acc[r];
@@ -885,8 +982,10 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.rowvec && d.rowvec_period <= 0) return fail(SAVQA_EINVAL, "savqa_gemm: rowvec_period");
   if (d.split_k < 0 && !d.atomic) return fail(SAVQA_EINVAL, "savqa_gemm: auto split-K needs atomic=1");
   if (d.colsum_a && !d.a_trans) return fail(SAVQA_EINVAL, "savqa_gemm: colsum_a needs a_trans=1");
+  if (d.prec == 1) d.prec = 6;  // bf16 products: the skinny launches only (savqa_gemm), x6 else
   if (d.prec != 0 && d.prec != 3 && d.prec != 6)
-    return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32), 3 (3xbf16) or 6 (fp32 x6)");
+    return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32), 1 (bf16 skinny, x6 "
+                              "otherwise), 3 (3xbf16) or 6 (fp32 x6)");
   // gemm_bf16_kernel / gemm_x6_kernel k-tile: 32; workgroups per CU the planner counts
   const int BK = d.prec ? 32 : (d.a_trans ? GEMM_BK_DW : GEMM_BK);
   const int occ = d.prec == 6 ? 2 : GEMM_PLAN_OCC;
@@ -1049,6 +1148,8 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   savqa_gemm_desc d = *dp;
   if (d.M == 0 || d.N == 0) return 0;
   if (!d.A || !d.B || !d.C) return fail(SAVQA_EINVAL, "savqa_gemm: null operand");
+  const bool bf_skinny = d.prec == 1;  // (plan_gemm maps it to 6 for the 128 x 128 tiles)
+  if (bf_skinny) d.prec = 6;
   GemmPlan p{};
   if (int rc = plan_gemm(d, p)) return rc;
   const int avec = (d.lda % 4 == 0) && aligned16(d.A);
@@ -1091,6 +1192,13 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
     else if (!d.a_trans) SAVQA_SK_LAUNCH(gemm_skinny16_kernel, false, false);
     else if (!d.b_trans) SAVQA_SK_LAUNCH(gemm_skinny16_kernel, true, false);
     else SAVQA_SK_LAUNCH(gemm_skinny16_kernel, true, true);
+  } else if (bf_skinny && !((d.a_trans && d.a_rows) || (!d.b_trans && d.b_rows))) {
+    const dim3 g(p.grid_x), b(64 * SK_WAVES);
+    const int tn = p.gg.tiles_n;
+    if (!d.a_trans && d.b_trans) SAVQA_SK_LAUNCH(gemm_skinny_bf_kernel, false, true);
+    else if (!d.a_trans) SAVQA_SK_LAUNCH(gemm_skinny_bf_kernel, false, false);
+    else if (!d.b_trans) SAVQA_SK_LAUNCH(gemm_skinny_bf_kernel, true, false);
+    else SAVQA_SK_LAUNCH(gemm_skinny_bf_kernel, true, true);
   } else {
     const dim3 g(p.grid_x), b(64 * SK_WAVES);
     const int tn = p.gg.tiles_n;

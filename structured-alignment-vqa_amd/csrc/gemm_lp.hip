@@ -1510,6 +1510,10 @@ struct LpPlan {
 #define SAVQA_LP_TAIL_MIN_NK_SLAB 64
 #endif
 constexpr int LP_TAIL_MIN_NK = 64, LP_TAIL_MIN_NK_SLAB = SAVQA_LP_TAIL_MIN_NK_SLAB;
+constexpr int LP_TAIL_MIN_NK_PLAN = 64;  // (bf16 k-tiles) the 256 x 256 round rule's K bound
+#ifndef SAVQA_LP3_ROUND_COST
+#define SAVQA_LP3_ROUND_COST 17  // one 256 x 256 round in tenths of a 128 x 128 round
+#endif
 static bool lp_al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
@@ -1538,6 +1542,20 @@ static LpPlan lp_plan(const savqa_gemm_lp_desc& d) {
     else if (d.N >= 4096 || (split && d.a_trans && d.M >= 4096 && d.N >= 256 && !slab_dw) ||
              (!d.a_trans && d.N >= 2048 && d.M >= 8192))
       p.var = 5;
+    else if (!split && !d.a_trans && !d.c_rows && (d.K + 63) / 64 < LP_TAIL_MIN_NK_PLAN) {
+      // Round 6, with both kernels' LDS-DMAs pipelined (glds_asm): by the rounds each takes
+      // (2 x CUs 128 x 128 slots, CUs 256 x 256 slots), the 8-phase kernel wins once
+      // 1.7 x its rounds < the 128 x 128 kernel's -- one of its rounds costs ~1.7 of the
+      // other's at these K (tools/gemm_replay.py --hints 1,5 on the cfg-3 launches, cold:
+      // NN 25600x512x2048 116 -> 98 us, NT 92160x1024x304 176 -> 146, NT 37376x1536x512
+      // 112 -> 98; NN 37376x512x2048 stays 128 x 128, 158 vs 175). Long K keeps the
+      // 128 x 128 kernel and its tail split.
+      const int64_t t1 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
+      const int64_t t3 = ((d.M + 255) / 256) * ((d.N + 255) / 256);
+      const int64_t s1 = lp_slots(), s3 = std::max(1, lp_slots() / LP_OCC);
+      const int64_t r1 = (t1 + s1 - 1) / s1, r3 = (t3 + s3 - 1) / s3;
+      if (SAVQA_LP3_ROUND_COST * r3 < 10 * r1) p.var = 5;
+    }
   }
   const int bm = p.var == 1 ? 128 : 256;
   p.bn = (p.var == 3 || p.var == 5) ? 256 : 128;

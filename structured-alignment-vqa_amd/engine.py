@@ -84,6 +84,11 @@ def _qv_wrows(d: int, dev) -> torch.Tensor:
 # F.normalize clamp decision reads it) and gets gradient in the clamped case, so K stays
 # computed for every row; Q and V only for the question rows (node rows zero).
 PRUNE_L01 = True
+# Off by default: measured (interleaved, round 6) cfg 3 +0.9 %, cfg 5 +1.1 %, but the bf16
+# precision suite's deep-gradient bar (1.25x autocast's error) failed at 1.26x on
+# att_syb.enc_self_attention_5.Q_proj (the bf16 products of the chain's backward; with them in
+# the forward only there was no gain and the same failure)
+LP_SKINNY_BF16 = os.environ.get("SAVQA_LP_SKINNY_BF16", "0") != "0"
 # bf16 / fp8 modes: the encoder FFN's first Linear also writes its ReLU gate as bits
 # (savqa_gemm_lp_desc.bits_out), and the dX of the second Linear reads those instead of the
 # bf16 activations (SAVQA_DT_BITS mask: 1/16 of the bytes). SAVQA_LP_BITS=0: the bf16 mask.
@@ -1036,6 +1041,8 @@ class ModelEngine:
     def lp_mode(self):
         return self.gemm_precision in LP_MODES
 
+    # SAVQA_LP_SKINNY_BF16=1: the M = B decoder / head chain of the bf16 / fp8 modes on bf16
+    # products (gemm.hip gemm_skinny_bf_kernel) instead of its fp32 skinny kernels
     def _fp32_kernel_precision(self):
         """Product precision of the fp32-storage GEMMs (ops.PREC): bf16x3 in that mode,
         fp32 otherwise (incl. the GEMMs the low-precision modes keep in fp32): the x6 kernel
@@ -1044,6 +1051,8 @@ class ModelEngine:
             return "bf16x3"
         if self.gemm_precision == "fp32_native" or FP32_GEMM == "native":
             return "fp32_native"
+        if self.gemm_precision in ("bf16", "fp8") and LP_SKINNY_BF16:
+            return "bf16sk"
         return "fp32x6"
 
     def rebind(self):

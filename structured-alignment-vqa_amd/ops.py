@@ -64,10 +64,13 @@ class GemmProbe:
         call("savqa_gemm_plan", C.byref(d), C.cast(plan, C.c_void_p))
         lay = f"{str(bool(d.a_trans)).lower()},{str(bool(d.b_trans)).lower()}"
         if plan[0] == 32:
+            kg = (d.a_trans and d.a_rows) or (not d.b_trans and d.b_rows)
+            if d.prec == 1 and not kg:
+                return f"gemm_skinny_bf_kernel<{lay}>"
             return f"gemm_skinny_kernel<{lay}>"
         if plan[0] == 16:
             return f"gemm_skinny16_kernel<{lay}>"
-        if d.prec == 6:  # (savqa_gemm's fallback: operands that are not 16-B vectors)
+        if d.prec in (1, 6):  # (savqa_gemm's fallback: operands that are not 16-B vectors)
             al = all(p % 16 == 0 and ld % 4 == 0 for p, ld in ((d.A, d.lda), (d.B, d.ldb)))
             if al:
                 return f"gemm_x6_kernel<{lay}>"
@@ -94,7 +97,10 @@ _probe = None
 # MFMA (exact fp32, the ops-level default), 3 = 3xbf16 split products (~2^-16), 6 = fp32 from
 # exact three-term bf16 splits, six products per pair (gemm_x6.hip; the engine's fp32 mode). Set per model (AttModel(...,
 # gemm_precision="bf16x3")) via gemm_precision(); the bf16 / fp8 modes use gemm_lp instead.
-PREC = {"fp32": 0, "fp32_native": 0, "bf16x3": 3, "fp32x6": 6}
+# "bf16sk" (1): the low-precision modes' fp32-storage GEMMs -- bf16 products on the skinny
+# (M = B row) launches (gemm_skinny_bf_kernel: operands rounded to bf16 as autocast rounds a
+# Linear's), x6 on the 128x128 ones
+PREC = {"fp32": 0, "fp32_native": 0, "bf16x3": 3, "fp32x6": 6, "bf16sk": 1}
 # fp32 / x6 K splits (split-K weight gradients, tail splits) through partial slabs summed in a
 # fixed order (savqa_gemm_desc.ws) instead of fp32 atomics: run-to-run deterministic
 # ("dw": split-K weight gradients only, the tail splits keep their atomics)

@@ -568,8 +568,9 @@ CFG2_SHAPES = [("NT", 18688, 1536, 512), ("NT", 18688, 2048, 512), ("NT", 18688,
                ("TN", 2048, 512, 18688), ("TN", 512, 2048, 18688), ("TN", 6144, 512, 18688)]
 
 
+@pytest.mark.parametrize("x6", [6])
 @pytest.mark.parametrize("lay,M,N,K", CFG2_SHAPES)
-def test_gemm_x6_error_at_most_native(lay, M, N, K):
+def test_gemm_x6_error_at_most_native(lay, M, N, K, x6):
     """The x6 kernel is an fp32 GEMM: on every cfg-2 step shape (forward NT, dX NN, split-K
     dW TN with the bias-gradient column sums) its max error against fp64 is within 1.25x of
     the native fp32 MFMA kernel's on the same inputs (measured: at or below it). The split-K
@@ -589,15 +590,15 @@ def test_gemm_x6_error_at_most_native(lay, M, N, K):
         kw = dict(lda=M, ldb=N, ldc=N, a_trans=True, atomic=True, split_k=-1)
         ref = A.double().t() @ B.double()
     errs = {}
-    for prec in (0, 6):
+    for prec in (0, x6):
         out = torch.zeros(M, N, device=dev)
         cs = torch.zeros(M, device=dev) if lay == "TN" else None
         O.gemm(A, B, out, M, N, K, colsum_a=cs, prec=prec, **kw)
         errs[prec] = float((out.double() - ref).abs().max() / ref.abs().max())
         if cs is not None:
             assert rel(cs, A.double().sum(0)) < 1e-5
-    assert errs[6] <= 1.25 * errs[0] + 1e-8, errs
-    assert errs[6] < 5e-6, errs
+    assert errs[x6] <= 1.25 * errs[0] + 1e-8, errs
+    assert errs[x6] < 5e-6, errs
 
 
 @pytest.mark.parametrize("prec", [0, 6])
@@ -655,9 +656,10 @@ def _wide(shape, lo, hi, seed):
     return (s * torch.pow(10.0, e)).float().to(dev)
 
 
+@pytest.mark.parametrize("x6", [6])
 @pytest.mark.parametrize("lay", ["NT", "NN", "TN"])
 @pytest.mark.parametrize("rng", ["wide", "tiny", "huge"])
-def test_gemm_x6_wide_dynamic_range(lay, rng):
+def test_gemm_x6_wide_dynamic_range(lay, rng, x6):
     """The exact three-term split over operands far from N(0, 1): 'wide' spans 24 decades
     (a1 / a2 of the smallest values stay fp32-normal), 'tiny' puts A at 1e-37..1e-33, where
     a1 / a2 fall below the fp32 / bf16 normal range while every product stays normal, 'huge'
@@ -683,18 +685,18 @@ def test_gemm_x6_wide_dynamic_range(lay, rng):
         Am, Bm = A.double().t(), B.double()
     ref = Am @ Bm
     scale = Am.abs() @ Bm.abs()
-    assert O.gemm(A, B, None, M, N, K, prec=6, plan_only=True, **kw)[0] == 128  # x6 kernel
+    assert O.gemm(A, B, None, M, N, K, prec=x6, plan_only=True, **kw)[0] == 128  # x6 kernel
     errs, rms = {}, {}
-    for prec in (0, 6):
+    for prec in (0, x6):
         out = torch.zeros(M, N, device=dev)
         O.gemm(A, B, out, M, N, K, prec=prec, **kw)
         assert bool(torch.isfinite(out).all())
         e = (out.double() - ref).abs() / scale
         errs[prec], rms[prec] = float(e.max()), float(e.pow(2).mean().sqrt())
-    print(f"x6 wide-range {rng} {lay}: max {errs}, rms {rms}")
-    assert rms[6] <= 1.25 * rms[0] + 1e-10, (errs, rms)
-    assert errs[6] <= 1.25 * errs[0] + 1e-9, (errs, rms)
-    assert errs[6] < 1e-5, errs
+    print(f"x6 wide-range {rng} {lay} prec {x6}: max {errs}, rms {rms}")
+    assert rms[x6] <= 1.25 * rms[0] + 1e-10, (errs, rms)
+    assert errs[x6] <= 1.25 * errs[0] + 1e-9, (errs, rms)
+    assert errs[x6] < 1e-5, errs
 
 
 def test_gemm_x6_infinite_operands():
@@ -745,3 +747,33 @@ def test_gemm_k_row_gathers(gather, N, fp32k):
     Bg = B[ib] if "b" in gather else B
     ref = Ag.double().t() @ Bg.double()
     assert rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("lay,M,N,K", [("NT", 512, 2048, 512), ("NN", 1024, 512, 2048),
+                                       ("TN", 512, 2048, 512), ("NT", 300, 914, 1000),
+                                       ("NN", 512, 1024, 914), ("TN", 914, 512, 520),
+                                       ("TT", 512, 512, 512)])
+def test_gemm_skinny_bf16_products(lay, M, N, K):
+    """prec = 1 (ops.PREC "bf16sk", the low-precision modes' decoder / head chain): the skinny
+    launches round both operands to bf16 (RNE) and accumulate the exact products in fp32
+    (gemm_skinny_bf_kernel) -- held to the fp64 product of the bf16-rounded operands, incl. K
+    not a multiple of 16 (the guarded last group), M / N edge tiles, the TN bias-gradient
+    column sums (of the fp32 values) and a residual epilogue."""
+    O = ops()
+    at, bt = lay[0] == "T", lay[1] == "T"
+    A = g(K, M, seed=71) if at else g(M, K, seed=71)
+    B = g(N, K, seed=72) if bt else g(K, N, seed=72)
+    kw = dict(lda=M if at else K, ldb=K if bt else N, ldc=N, a_trans=at, b_trans=bt)
+    assert O.gemm(A, B, None, M, N, K, prec=1, plan_only=True, **kw)[0] == 32  # skinny
+    Ar = (A.t() if at else A).to(torch.bfloat16).double()
+    Br = (B.t() if bt else B).to(torch.bfloat16).double()
+    R = torch.randn(M, N, device=dev)
+    out = torch.empty(M, N, device=dev)
+    cs = torch.zeros(M, device=dev) if at else None
+    O.gemm(A, B, out, M, N, K, prec=1, resid=None if at else R, ldr=N, colsum_a=cs, **kw)
+    ref = Ar @ Br + (0 if at else R.double())
+    assert rel(out, ref) < 1e-5
+    exact = (A.t() if at else A).double() @ (B.t() if bt else B).double()
+    assert rel(out - (0 if at else R), exact) > 1e-4  # really bf16 products, not fp32 ones
+    if cs is not None:
+        assert rel(cs, A.double().sum(0)) < 1e-5
