@@ -54,6 +54,8 @@ int savqa_struct_sizes(int64_t* out, int32_t n);
  * Non-atomic launches with a linear epilogue (relu=0, beta=0, C not aliasing resid) may
  * split the last partial wave of tiles over K internally (zero-fill + atomics): results
  * then differ from a single-pass launch only in fp32 summation order.
+ * prec 1: the skinny (M = B row) launches round both operands to bf16 and use one bf16 MFMA
+ * per 16 k (gemm_skinny_bf_kernel; k-row gathers stay fp32), the 128x128 ones run as prec 6.
  * prec (128x128-tile launches; the skinny kernel stays fp32): 3 = each operand split into
  * bf16 hi + lo (lo = bf16(x - hi)) and a*b ~ ah*bh + ah*bl + al*bh on
  * v_mfma_f32_32x32x16_bf16: ~2^-16 relative per product (the "bf16x3" mode). The bf16
@@ -62,8 +64,9 @@ int savqa_struct_sizes(int64_t* out, int32_t n);
 typedef struct savqa_gemm_desc {
     int64_t M, N, K;
     const float* A; int64_t lda; int32_t a_trans;
-    int32_t prec;      /* products: 0 fp32 MFMA (exact), 3 3xbf16 split, 6 fp32 from exact
-                          three-term bf16 splits (six bf16 MFMA products, gemm_x6.hip) */
+    int32_t prec;      /* products: 0 fp32 MFMA (exact), 1 bf16 on the skinny launches (x6
+                          else), 3 3xbf16 split, 6 fp32 from exact three-term bf16 splits
+                          (six bf16 MFMA products, gemm_x6.hip) */
     const int64_t* a_rows;
     const float* B; int64_t ldb; int32_t b_trans; int32_t _pad1;
     const int64_t* b_rows;

@@ -982,10 +982,11 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.rowvec && d.rowvec_period <= 0) return fail(SAVQA_EINVAL, "savqa_gemm: rowvec_period");
   if (d.split_k < 0 && !d.atomic) return fail(SAVQA_EINVAL, "savqa_gemm: auto split-K needs atomic=1");
   if (d.colsum_a && !d.a_trans) return fail(SAVQA_EINVAL, "savqa_gemm: colsum_a needs a_trans=1");
-  if (d.prec == 1) d.prec = 6;  // bf16 products: the skinny launches only (savqa_gemm), x6 else
+  if (d.prec == 1 || d.prec == 5) d.prec = 6;  // 1: bf16 products on the skinny launches only,
+                                                // 5: x6 two-level (savqa_gemm); x6 else
   if (d.prec != 0 && d.prec != 3 && d.prec != 6)
     return fail(SAVQA_EINVAL, "savqa_gemm: prec must be 0 (fp32), 1 (bf16 skinny, x6 "
-                              "otherwise), 3 (3xbf16) or 6 (fp32 x6)");
+                              "otherwise), 3 (3xbf16), 5 (x6 two-level) or 6 (fp32 x6)");
   // gemm_bf16_kernel / gemm_x6_kernel k-tile: 32; workgroups per CU the planner counts
   const int BK = d.prec ? 32 : (d.a_trans ? GEMM_BK_DW : GEMM_BK);
   const int occ = d.prec == 6 ? 2 : GEMM_PLAN_OCC;
@@ -1149,7 +1150,8 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
   if (d.M == 0 || d.N == 0) return 0;
   if (!d.A || !d.B || !d.C) return fail(SAVQA_EINVAL, "savqa_gemm: null operand");
   const bool bf_skinny = d.prec == 1;  // (plan_gemm maps it to 6 for the 128 x 128 tiles)
-  if (bf_skinny) d.prec = 6;
+  const bool x6_two_level = d.prec == 5;
+  if (bf_skinny || x6_two_level) d.prec = 6;
   GemmPlan p{};
   if (int rc = plan_gemm(d, p)) return rc;
   const int avec = (d.lda % 4 == 0) && aligned16(d.A);
@@ -1166,7 +1168,7 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
                        d.M - p.zero_row0, s) != hipSuccess)
     return fail(SAVQA_EUNSUP, "savqa_gemm: tail zero-fill failed");
   if (p.tile == 128 && d.prec == 6) {
-    savqa_launch_gemm_x6(d, p.gg, p.grid_x, p.nsplit, s);
+    savqa_launch_gemm_x6(d, p.gg, p.grid_x, p.nsplit, s, x6_two_level);
   } else if (p.tile == 128 && d.prec != 0) {
     savqa_launch_gemm_bf16(d, p.gg, p.grid_x, p.nsplit, s, avec, bvec);
   } else if (p.tile == 128) {

@@ -176,4 +176,4 @@ int savqa_launch_gemm_bf16(const savqa_gemm_desc& d, const savqa::GemmGrid& gg, 
                            int nsplit, hipStream_t s, int avec, int bvec);
 // gemm_x6.hip: fp32 GEMM on bf16 matrix cores from exact three-term splits (desc.prec == 6)
 int savqa_launch_gemm_x6(const savqa_gemm_desc& d, const savqa::GemmGrid& gg, int grid_x,
-                         int nsplit, hipStream_t s);
+                         int nsplit, hipStream_t s, bool two_level);

@@ -314,6 +314,13 @@ __device__ __forceinline__ int x6_mode(const savqa_gemm_desc& d, int64_t m0, int
 #ifndef SAVQA_X6_HILO
 #define SAVQA_X6_HILO 1
 #endif
+#ifndef SAVQA_X6_TL_MASK
+#define SAVQA_X6_TL_MASK 0  // layouts on the two-level form instead: 1 NT, 2 NN, 4 TN / TT
+#endif
+template <bool AT, bool BT, bool HL>
+constexpr bool x6_hilo() {
+  return HL && SAVQA_X6_HILO && !((SAVQA_X6_TL_MASK & (AT ? 4 : (BT ? 1 : 2))) != 0);
+}
 #ifndef SAVQA_X6_REREAD
 #define SAVQA_X6_REREAD 0
 #endif
@@ -362,7 +369,7 @@ __device__ __forceinline__ void x6_compute_hilo(const char* As, const char* Bs, 
   }
 }
 
-template <bool AT, bool BT, int MODE>
+template <bool AT, bool BT, int MODE, bool HL>
 __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem, int64_t m0,
                                             int64_t n0, int64_t kbeg, int64_t kend, int ntiles,
                                             f4 (&acc)[4][4], bool do_cs, f4& cs) {
@@ -402,7 +409,7 @@ __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem
     lb.template store<S>(smem + 3 * X6_PLANE, tid);
     if (tt + X6_DEPTH < ntiles) load(set, kbeg + (int64_t)(tt + X6_DEPTH) * X6_BK);
     __syncthreads();
-    if constexpr (SAVQA_X6_HILO)
+    if constexpr (x6_hilo<AT, BT, HL>())
       x6_compute_hilo(smem, smem + 3 * X6_PLANE, wm, wn, lane, acc, lo);
     else
       x6_compute(smem, smem + 3 * X6_PLANE, wm, wn, lane, acc);
@@ -415,7 +422,7 @@ __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem
     step(S0{}, tt);
     if (X6_DEPTH > 1 && tt + 1 < ntiles) step(S1{}, tt + 1);
   }
-  if constexpr (SAVQA_X6_HILO) {
+  if constexpr (x6_hilo<AT, BT, HL>()) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -424,7 +431,12 @@ __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem
   __syncthreads();  // LDS is reused by the colsum fold
 }
 
-template <bool AT, bool BT>
+// HL: the hi / lo accumulators (x6_compute_hilo); false: the two-level form (x6_compute),
+// which adds each k-tile's partial into the accumulator with a VALU (RNE) add instead of
+// inside the MFMA -- savqa_gemm_desc.prec = 5, for launches whose outputs feed a rounding-
+// sensitive chain (the engine's decoder K / V projection: a softmax over T keys in all 6
+// decoder layers)
+template <bool AT, bool BT, bool HL>
 __global__ __launch_bounds__(GEMM_NT, X6_OCC) void gemm_x6_kernel(savqa_gemm_desc d, GemmGrid gg) {
   __shared__ __attribute__((aligned(16))) char smem[6 * X6_PLANE];  // A planes 0-2, B planes 0-2
   const int lane = threadIdx.x & 63;
@@ -466,11 +478,11 @@ __global__ __launch_bounds__(GEMM_NT, X6_OCC) void gemm_x6_kernel(savqa_gemm_des
   if (ntiles > 0) {
     const int mode = x6_mode<AT, BT>(d, m0, n0, kbeg, kend);
     if (mode == 1)
-      x6_mainloop<AT, BT, 1>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      x6_mainloop<AT, BT, 1, HL>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     else if (mode == 2)
-      x6_mainloop<AT, BT, 2>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      x6_mainloop<AT, BT, 2, HL>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     else
-      x6_mainloop<AT, BT, 0>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      x6_mainloop<AT, BT, 0, HL>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
   }
   if constexpr (AT) {
     if (do_cs) {  // block-uniform; LDS is free after the main loop's last barrier
@@ -498,12 +510,19 @@ __global__ __launch_bounds__(GEMM_NT, X6_OCC) void gemm_x6_kernel(savqa_gemm_des
 
 // Launch of the x6 kernels on a plan made by savqa_gemm (gemm.hip): grid (grid_x, nsplit).
 int savqa_launch_gemm_x6(const savqa_gemm_desc& d, const savqa::GemmGrid& gg, int grid_x,
-                         int nsplit, hipStream_t s) {
+                         int nsplit, hipStream_t s, bool two_level) {
   using namespace savqa;
   const dim3 g(grid_x, nsplit), b(GEMM_NT);
-  if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, true>), g, b, 0, s, d, gg);
-  else if (!d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, false>), g, b, 0, s, d, gg);
-  else if (d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<true, false>), g, b, 0, s, d, gg);
-  else hipLaunchKernelGGL((gemm_x6_kernel<true, true>), g, b, 0, s, d, gg);
+  if (two_level) {
+    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, true, false>), g, b, 0, s, d, gg);
+    else if (!d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, false, false>), g, b, 0, s, d, gg);
+    else if (d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<true, false, false>), g, b, 0, s, d, gg);
+    else hipLaunchKernelGGL((gemm_x6_kernel<true, true, false>), g, b, 0, s, d, gg);
+    return 0;
+  }
+  if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, true, true>), g, b, 0, s, d, gg);
+  else if (!d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, false, true>), g, b, 0, s, d, gg);
+  else if (d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<true, false, true>), g, b, 0, s, d, gg);
+  else hipLaunchKernelGGL((gemm_x6_kernel<true, true, true>), g, b, 0, s, d, gg);
   return 0;
 }

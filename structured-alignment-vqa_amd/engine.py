@@ -89,6 +89,8 @@ PRUNE_L01 = True
 # att_syb.enc_self_attention_5.Q_proj (the bf16 products of the chain's backward; with them in
 # the forward only there was no gain and the same failure)
 LP_SKINNY_BF16 = os.environ.get("SAVQA_LP_SKINNY_BF16", "0") != "0"
+# the decoder K / V projection on x6's two-level form (ops.x6_two_level; =0: hi / lo like the rest)
+KV_TWO_LEVEL = os.environ.get("SAVQA_KV_TWO_LEVEL", "1") != "0"
 # bf16 / fp8 modes: the encoder FFN's first Linear also writes its ReLU gate as bits
 # (savqa_gemm_lp_desc.bits_out), and the dX of the second Linear reads those instead of the
 # bf16 activations (SAVQA_DT_BITS mask: 1/16 of the bytes). SAVQA_LP_BITS=0: the bf16 mask.
@@ -390,7 +392,11 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
             ops.widen_bf16(s.kv, M, 2 * nb * d, 2 * nb * d, s.kv32, 2 * nb * d)
     else:
         s.kv = _empty(M, 2 * nb * d, dev=dev)
-        ops.linear(x, W.Wkv, W.bkv, s.kv, relu=True)
+        # (two-level x6: these K / V feed the softmax over T keys of all six decoder layers;
+        # with the hi / lo accumulators a cfg-4 decoder K-projection gradient landed 2x the
+        # CPU fp32 oracle's distance to fp64, with two-level 1.4x: DESIGN.md 5, round 6)
+        ops.linear(x, W.Wkv, W.bkv, s.kv, relu=True,
+                   prec=ops.x6_two_level() if KV_TWO_LEVEL else None)
     dec = _empty(B, d, dev=dev)
     ops.dec_init(W.dec_emb, 2, math.sqrt(d), W.dec_pos, B, d, dec, drop=drop, site=sites[2])
     fdec = _empty(B, dev=dev)

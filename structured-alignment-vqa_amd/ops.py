@@ -70,7 +70,7 @@ class GemmProbe:
             return f"gemm_skinny_kernel<{lay}>"
         if plan[0] == 16:
             return f"gemm_skinny16_kernel<{lay}>"
-        if d.prec in (1, 6):  # (savqa_gemm's fallback: operands that are not 16-B vectors)
+        if d.prec in (1, 5, 6):  # (savqa_gemm's fallback: operands that are not 16-B vectors)
             al = all(p % 16 == 0 and ld % 4 == 0 for p, ld in ((d.A, d.lda), (d.B, d.ldb)))
             if al:
                 return f"gemm_x6_kernel<{lay}>"
@@ -101,6 +101,15 @@ _probe = None
 # (M = B row) launches (gemm_skinny_bf_kernel: operands rounded to bf16 as autocast rounds a
 # Linear's), x6 on the 128x128 ones
 PREC = {"fp32": 0, "fp32_native": 0, "bf16x3": 3, "fp32x6": 6, "bf16sk": 1}
+# prec 5: x6 in its two-level form (gemm_x6.hip: VALU adds of each k-tile's partial, no hi / lo
+# accumulators), for launches whose outputs feed a rounding-sensitive chain (x6_two_level)
+X6_TWO_LEVEL = 5
+
+
+def x6_two_level() -> int:
+    """The precision to pass a launch that wants x6's two-level accumulation: 5 when the
+    current mode is x6, the current mode otherwise."""
+    return X6_TWO_LEVEL if _prec == 6 else _prec
 # fp32 / x6 K splits (split-K weight gradients, tail splits) through partial slabs summed in a
 # fixed order (savqa_gemm_desc.ws) instead of fp32 atomics: run-to-run deterministic
 # ("dw": split-K weight gradients only, the tail splits keep their atomics)
@@ -392,14 +401,14 @@ def linear_dw_lp(dY: Tensor, X: Tensor, dW: Tensor, db: Optional[Tensor], *, row
 
 def linear(X: Tensor, W: Tensor, b: Optional[Tensor], out: Tensor, *, relu=False,
            rows: Optional[int] = None, a_rows=None, rowvec=None, rowvec_period=0, resid=None,
-           c_group=0, c_stride=0, c_offset=0, ldx=None, ldo=None, rowscale=None):
+           c_group=0, c_stride=0, c_offset=0, ldx=None, ldo=None, rowscale=None, prec=None):
     """out = act(X W^T + b [+ rowvec]) [+ resid]  -- nn.Linear forward (W is [out, in])."""
     N, K = W.shape
     M = rows if rows is not None else (a_rows.numel() if a_rows is not None else X.numel() // K)
     gemm(X, W, out, M, N, K, lda=ldx if ldx is not None else K, ldb=K,
          ldc=ldo if ldo is not None else N, b_trans=True, a_rows=a_rows, bias=b, rowvec=rowvec,
          ldrv=N, rowvec_period=rowvec_period, resid=resid, ldr=N, relu=relu, c_group=c_group,
-         c_stride=c_stride, c_offset=c_offset, rowscale=rowscale)
+         c_stride=c_stride, c_offset=c_offset, rowscale=rowscale, prec=prec)
 
 
 def linear_dx(dY: Tensor, W: Tensor, dX: Tensor, *, rows: int, a_rows=None, mask=None,
