@@ -87,7 +87,23 @@ typedef struct savqa_gemm_desc {
                           and add the slices in a fixed order in a second pass -- results no
                           longer depend on the order atomics land in, i.e. run to run
                           deterministic (a c_rows scatter / row map keeps its atomics) */
+    const void* b_planes;  /* optional, x6 (prec 5 / 6) launches with !a_trans only: B as the
+                          x6 kernel's LDS images, pre-split by savqa_x6_weight_planes for
+                          exactly this B (same N, K, layout); the kernel then DMAs B's three
+                          bf16 planes instead of loading and splitting B (the weights of the
+                          forward / dX GEMMs: split once per optimizer step, not per tile).
+                          Results are bit-identical to the launch without it. NULL: off */
 } savqa_gemm_desc;
+
+/* The x6 kernel's bf16 plane images of a GEMM's B operand (the N x K operand of
+ * savqa_gemm's formula; b_trans = 1: B(n, k) = Bp[n * ldb + k], else B(n, k) = Bp[k * ldb + n]):
+ * for every 128-row n tile and 32-wide k tile, 3 planes x 128 x 32 bf16 (24 KB) at
+ * out + (nt * ceil(K / 32) + kt) * 24576 bytes, each value split exactly into the three
+ * truncated bf16 terms gemm_x6 makes, in its swizzled order; zeros past N and K.
+ * out: savqa_x6_weight_planes_bytes(N, K) bytes, 16-B aligned. */
+int64_t savqa_x6_weight_planes_bytes(int64_t N, int64_t K);
+int savqa_x6_weight_planes(void* stream, const float* Bp, int64_t ldb, int32_t b_trans, int64_t N,
+                           int64_t K, void* out);
 
 int savqa_gemm(void* stream, const savqa_gemm_desc* d);
 /* fp32 elements of workspace *d's launch would use for split-K / tail-split slabs (0: the plan

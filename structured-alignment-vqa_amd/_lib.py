@@ -38,6 +38,7 @@ class GemmDesc(C.Structure):
         ("relu", c_i32), ("atomic", c_i32), ("split_k", c_i32), ("_pad2", c_i32),
         ("colsum_a", c_p),
         ("ws", c_p), ("ws_elems", c_i64),
+        ("b_planes", c_p),
     ]
 
 
@@ -154,6 +155,8 @@ _SIGS = {
                            c_p],
     "savqa_index_put_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "savqa_segment_add_rows": [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_p, c_i64],
+    "savqa_x6_weight_planes": [c_p, c_p, c_i64, c_i32, c_i64, c_i64, c_p],
+    "savqa_x6_weight_planes_bytes": [c_i64, c_i64],
     "savqa_index_get_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "savqa_loss_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f, c_p, c_i32, c_p, c_p, c_p, c_p],
     "savqa_scale_by": [c_p, c_p, c_p, c_i64, c_p],
@@ -166,7 +169,7 @@ _SIGS = {
 }
 
 _I64_RET = {"savqa_ln_bwd_workspace_bytes", "savqa_gemm_ws_elems", "savqa_gattn_q1s_ws_bytes",
-            "savqa_rel_loss_ws_bytes", "savqa_gemm_lp_ws_elems"}
+            "savqa_rel_loss_ws_bytes", "savqa_gemm_lp_ws_elems", "savqa_x6_weight_planes_bytes"}
 
 _lib = None
 

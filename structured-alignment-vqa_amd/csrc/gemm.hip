@@ -1167,6 +1167,11 @@ extern "C" int savqa_gemm(void* stream, const savqa_gemm_desc* dp) {
       hipMemset2DAsync(d.C + p.zero_row0 * d.ldc, d.ldc * sizeof(float), 0, d.N * sizeof(float),
                        d.M - p.zero_row0, s) != hipSuccess)
     return fail(SAVQA_EUNSUP, "savqa_gemm: tail zero-fill failed");
+  // pre-split B planes (savqa_gemm_desc.b_planes): x6 128x128 launches with a k-contiguous,
+  // 16-B-vector A and no B row gather; anything else ignores them
+  if (d.b_planes && !(p.tile == 128 && d.prec == 6 && !d.a_trans && !d.b_rows && avec &&
+                      aligned16(d.b_planes)))
+    d.b_planes = nullptr;
   if (p.tile == 128 && d.prec == 6) {
     savqa_launch_gemm_x6(d, p.gg, p.grid_x, p.nsplit, s, x6_two_level);
   } else if (p.tile == 128 && d.prec != 0) {

@@ -247,6 +247,23 @@ __device__ __forceinline__ bf16x8 x6_frag(const char* img, int base, int lane) {
   return *reinterpret_cast<const bf16x8*>(img + r * X6_ROWB + (((lane >> 4) ^ x6_swz(r)) << 4));
 }
 
+// 16-B LDS-DMA from an asm statement (hipcc does not track it, so it neither drains it at the
+// next LDS read nor at __syncthreads(); the x6 loop counts it itself): the pre-split B planes
+// (savqa_gemm_desc.b_planes). M0 is saved and restored (cdna_hip_programming.md 5.7).
+typedef __attribute__((address_space(3))) void x6_lds_void;
+__device__ __forceinline__ void x6_dma16(const void* src, char* dst) {
+  const uint32_t l =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(x6_lds_void*)dst);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void x6_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 __device__ __forceinline__ f4 mma(bf16x8 a, bf16x8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -369,7 +386,7 @@ __device__ __forceinline__ void x6_compute_hilo(const char* As, const char* Bs, 
   }
 }
 
-template <bool AT, bool BT, int MODE, bool HL>
+template <bool AT, bool BT, int MODE, bool HL, bool BP>
 __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem, int64_t m0,
                                             int64_t n0, int64_t kbeg, int64_t kend, int ntiles,
                                             f4 (&acc)[4][4], bool do_cs, f4& cs) {
@@ -414,6 +431,57 @@ __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem
     else
       x6_compute(smem, smem + 3 * X6_PLANE, wm, wn, lane, acc);
   };
+  if constexpr (BP) {
+    // B from its pre-split planes (savqa_x6_weight_planes): 24 KB per k-tile, DMA'd one k-tile
+    // ahead into the other half of a double buffer (6 x 1 KB per wave); A as usual. Before the
+    // barrier that precedes k-tile tt's MFMAs, tt's DMA must have landed: the wave issued at
+    // least 4 A loads and 6 DMAs after it (k-tile tt+1), so vmcnt(10) retires it.
+    static_assert(!AT, "planes: the A operand must be the k-contiguous one");
+    const int64_t KT = (d.K + X6_BK - 1) / X6_BK;
+    const char* bsrc = static_cast<const char*>(d.b_planes) +
+                       ((n0 / X6_TILE) * KT + kbeg / X6_BK) * (3 * X6_PLANE) + wave * 6 * 1024 +
+                       lane * 16;
+    auto dma_b = [&](int buf, int tt) {
+      char* dst = smem + 3 * X6_PLANE + buf * 3 * X6_PLANE + wave * 6 * 1024;
+      const char* src = bsrc + (int64_t)tt * (3 * X6_PLANE);
+#pragma unroll
+      for (int u = 0; u < 6; ++u) x6_dma16(src + u * 1024, dst + u * 1024);
+    };
+    auto load_a = [&](int64_t k0) {
+      if (MODE == 1 || (MODE == 2 && k0 + X6_BK <= kend))
+        la.template load_fast<0>(d.lda, k0, tid);
+      else
+        la.template load_slow<0>(d.A, d.lda, d.a_rows, d.M, m0, k0, kend, tid);
+    };
+    load_a(kbeg);
+    dma_b(0, 0);
+    for (int tt = 0; tt < ntiles; ++tt) {
+      if (tt > 0) __syncthreads();  // every wave has read k-tile tt-1's planes
+      la.template store<0>(smem, tid);
+      const bool nx = tt + 1 < ntiles;  // (uniform)
+      if (nx) {
+        load_a(kbeg + (int64_t)(tt + 1) * X6_BK);
+        dma_b((tt + 1) & 1, tt + 1);
+        x6_wait_vm<10>();
+      } else {
+        x6_wait_vm<0>();
+      }
+      __syncthreads();
+      const char* Bs = smem + 3 * X6_PLANE + (tt & 1) * 3 * X6_PLANE;
+      if constexpr (x6_hilo<AT, BT, HL>())
+        x6_compute_hilo(smem, Bs, wm, wn, lane, acc, lo);
+      else
+        x6_compute(smem, Bs, wm, wn, lane, acc);
+    }
+    if constexpr (x6_hilo<AT, BT, HL>()) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += lo[i][j];
+    }
+    __syncthreads();
+    return;
+  }
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, X6_DEPTH - 1>;
   load(S0{}, kbeg);
@@ -436,9 +504,10 @@ __device__ __forceinline__ void x6_mainloop(const savqa_gemm_desc& d, char* smem
 // inside the MFMA -- savqa_gemm_desc.prec = 5, for launches whose outputs feed a rounding-
 // sensitive chain (the engine's decoder K / V projection: a softmax over T keys in all 6
 // decoder layers)
-template <bool AT, bool BT, bool HL>
+template <bool AT, bool BT, bool HL, bool BP>
 __global__ __launch_bounds__(GEMM_NT, X6_OCC) void gemm_x6_kernel(savqa_gemm_desc d, GemmGrid gg) {
-  __shared__ __attribute__((aligned(16))) char smem[6 * X6_PLANE];  // A planes 0-2, B planes 0-2
+  // A planes 0-2, B planes 0-2 (BP: B planes double-buffered, 72 KB: still two per CU)
+  __shared__ __attribute__((aligned(16))) char smem[(BP ? 9 : 6) * X6_PLANE];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -478,11 +547,11 @@ __global__ __launch_bounds__(GEMM_NT, X6_OCC) void gemm_x6_kernel(savqa_gemm_des
   if (ntiles > 0) {
     const int mode = x6_mode<AT, BT>(d, m0, n0, kbeg, kend);
     if (mode == 1)
-      x6_mainloop<AT, BT, 1, HL>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      x6_mainloop<AT, BT, 1, HL, BP>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     else if (mode == 2)
-      x6_mainloop<AT, BT, 2, HL>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      x6_mainloop<AT, BT, 2, HL, BP>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
     else
-      x6_mainloop<AT, BT, 0, HL>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
+      x6_mainloop<AT, BT, 0, HL, BP>(d, smem, m0, n0, kbeg, kend, ntiles, acc, do_cs, cs);
   }
   if constexpr (AT) {
     if (do_cs) {  // block-uniform; LDS is free after the main loop's last barrier
@@ -513,16 +582,71 @@ int savqa_launch_gemm_x6(const savqa_gemm_desc& d, const savqa::GemmGrid& gg, in
                          int nsplit, hipStream_t s, bool two_level) {
   using namespace savqa;
   const dim3 g(grid_x, nsplit), b(GEMM_NT);
-  if (two_level) {
-    if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, true, false>), g, b, 0, s, d, gg);
-    else if (!d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, false, false>), g, b, 0, s, d, gg);
-    else if (d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<true, false, false>), g, b, 0, s, d, gg);
-    else hipLaunchKernelGGL((gemm_x6_kernel<true, true, false>), g, b, 0, s, d, gg);
+#define SAVQA_X6_GO(AT_, BT_, HL_, BP_) \
+  hipLaunchKernelGGL((gemm_x6_kernel<AT_, BT_, HL_, BP_>), g, b, 0, s, d, gg)
+  if (d.b_planes && !d.a_trans) {  // (the caller checked the planes' fit: savqa_gemm)
+    if (two_level) {
+      if (d.b_trans) SAVQA_X6_GO(false, true, false, true);
+      else SAVQA_X6_GO(false, false, false, true);
+    } else {
+      if (d.b_trans) SAVQA_X6_GO(false, true, true, true);
+      else SAVQA_X6_GO(false, false, true, true);
+    }
     return 0;
   }
-  if (!d.a_trans && d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, true, true>), g, b, 0, s, d, gg);
-  else if (!d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<false, false, true>), g, b, 0, s, d, gg);
-  else if (d.a_trans && !d.b_trans) hipLaunchKernelGGL((gemm_x6_kernel<true, false, true>), g, b, 0, s, d, gg);
-  else hipLaunchKernelGGL((gemm_x6_kernel<true, true, true>), g, b, 0, s, d, gg);
+  if (two_level) {
+    if (!d.a_trans && d.b_trans) SAVQA_X6_GO(false, true, false, false);
+    else if (!d.a_trans && !d.b_trans) SAVQA_X6_GO(false, false, false, false);
+    else if (d.a_trans && !d.b_trans) SAVQA_X6_GO(true, false, false, false);
+    else SAVQA_X6_GO(true, true, false, false);
+    return 0;
+  }
+  if (!d.a_trans && d.b_trans) SAVQA_X6_GO(false, true, true, false);
+  else if (!d.a_trans && !d.b_trans) SAVQA_X6_GO(false, false, true, false);
+  else if (d.a_trans && !d.b_trans) SAVQA_X6_GO(true, false, true, false);
+  else SAVQA_X6_GO(true, true, true, false);
+#undef SAVQA_X6_GO
   return 0;
+}
+
+// ------------------------------------------------------------------ pre-split B planes
+namespace savqa {
+// one workgroup per (n tile, k tile): the 128 x 32 B tile split like X6Operand<ROW>::store
+// (thread u -> row u / 8, k 4 (u % 8)), zeros past N / K
+__global__ __launch_bounds__(256) void x6_planes_kernel(const float* __restrict__ Bp, int64_t ldb,
+                                                        int b_trans, int64_t N, int64_t K,
+                                                        int64_t KT, char* __restrict__ out) {
+  const int64_t nt = blockIdx.x / KT, kt = blockIdx.x - nt * KT;
+  char* img = out + (int64_t)blockIdx.x * (3 * X6_PLANE);
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int u = threadIdx.x + 256 * it;
+    const int r = u >> 3, k4 = 4 * (u & 7);
+    const int64_t n = nt * X6_TILE + r, k = kt * X6_BK + k4;
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    if (n < N) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (k + e < K) v[e] = b_trans ? Bp[n * ldb + k + e] : Bp[(k + e) * ldb + n];
+    }
+    put3(img, x6_off(r, k4), v);
+  }
+}
+}  // namespace savqa
+
+extern "C" int64_t savqa_x6_weight_planes_bytes(int64_t N, int64_t K) {
+  if (N <= 0 || K <= 0) return 0;
+  return ((N + 127) / 128) * ((K + 31) / 32) * 3 * (int64_t)savqa::X6_PLANE;
+}
+
+extern "C" int savqa_x6_weight_planes(void* stream, const float* Bp, int64_t ldb, int32_t b_trans,
+                                      int64_t N, int64_t K, void* out) {
+  using namespace savqa;
+  if (N <= 0 || K <= 0) return 0;
+  if (!Bp || !out || ((uintptr_t)out & 15))
+    return fail(SAVQA_EINVAL, "savqa_x6_weight_planes: null operand or unaligned output");
+  const int64_t KT = (K + X6_BK - 1) / X6_BK, NT = (N + X6_TILE - 1) / X6_TILE;
+  hipLaunchKernelGGL(x6_planes_kernel, dim3((unsigned)(NT * KT)), dim3(256), 0, as_stream(stream),
+                     Bp, ldb, b_trans, N, K, KT, static_cast<char*>(out));
+  return check_launch("savqa_x6_weight_planes");
 }

@@ -298,9 +298,9 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
             ops.posadd_dropout(s.x0, W.pos, B, T, d, drop, sites[0], sites[1], s.x0)
             ops.cast_bf16(s.x0, M, d, d, xb, d)
     elif drop is None:
-        ops.linear(cat, W.Win, W.bin, s.x0, rowvec=W.pos, rowvec_period=T)
+        ops.linear(cat, W.Win, W.bin, s.x0, rowvec=W.pos, rowvec_period=T, wp=True)
     else:
-        ops.linear(cat, W.Win, W.bin, s.x0)
+        ops.linear(cat, W.Win, W.bin, s.x0, wp=True)
         ops.posadd_dropout(s.x0, W.pos, B, T, d, drop, sites[0], sites[1], s.x0)
     flag = _empty(M, dev=dev)
     ops.rowflag(s.x0, M, d, d, flag)
@@ -316,7 +316,7 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
         o = _empty(M, d, dev=dev)
         if lp is None and i < 2 and Nn > 0 and PRUNE_L01:
             kb = _empty(M, d, dev=dev)
-            ops.linear(x, L["Wqkv"][d:2 * d], L["bqkv"][d:2 * d], kb, relu=True)
+            ops.linear(x, L["Wqkv"][d:2 * d], L["bqkv"][d:2 * d], kb, relu=True, wp=True)
             qv, qv_slot = _zeroed_qv(L, s, (B, Nn, Lq), M, 2 * d, dev)
             bqv = torch.cat((L["bqkv"][:d], L["bqkv"][2 * d:]))
             ops.gemm(x, L["Wqkv"], qv, B * Lq, 2 * d, d, lda=d, ldb=d, ldc=2 * d, b_trans=True,
@@ -349,7 +349,7 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
                               B, T, T, H, o, d)
         else:
             qkv = _empty(M, 3 * d, dev=dev)
-            ops.linear(x, L["Wqkv"], L["bqkv"], qkv, relu=True)
+            ops.linear(x, L["Wqkv"], L["bqkv"], qkv, relu=True, wp=True)
             if ops.use_flash(T, T):  # key-tiled path: keeps the per-row statistics
                 ast = _empty(B * H * T * 4, dev=dev)
                 ops.gattn_fwd_flash(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, G, flag,
@@ -372,8 +372,8 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
             ops.linear_lp(h, Lb["W2"], L["c2"], z2, resid=y1)
         else:
             h = _empty(M, 4 * d, dev=dev)
-            ops.linear(y1, L["W1"], L["c1"], h, relu=True)
-            ops.linear(h, L["W2"], L["c2"], z2, resid=y1)
+            ops.linear(y1, L["W1"], L["c1"], h, relu=True, wp=True)
+            ops.linear(h, L["W2"], L["c2"], z2, resid=y1, wp=True)
         xn = _empty(M, d, dev=dev)
         xnb = _bf(M, d, dev=dev) if lp is not None else None
         st2 = _ln_stats(M, dev)
@@ -396,7 +396,7 @@ def stack_forward(W: StackWeights, cat: torch.Tensor, B: int, Nn: int, Lq: int,
         # with the hi / lo accumulators a cfg-4 decoder K-projection gradient landed 2x the
         # CPU fp32 oracle's distance to fp64, with two-level 1.4x: DESIGN.md 5, round 6)
         ops.linear(x, W.Wkv, W.bkv, s.kv, relu=True,
-                   prec=ops.x6_two_level() if KV_TWO_LEVEL else None)
+                   prec=ops.x6_two_level() if KV_TWO_LEVEL else None, wp=True)
     dec = _empty(B, d, dev=dev)
     ops.dec_init(W.dec_emb, 2, math.sqrt(d), W.dec_pos, B, d, dec, drop=drop, site=sites[2])
     fdec = _empty(B, dev=dev)
@@ -525,7 +525,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
         ops.linear_dx_lp(dkv, lp.W.Wkv, dx, rows=M)
     else:
         ops.linear_dw(dkv, s.x6, G.Wkv, G.bkv, rows=M)
-        ops.linear_dx(dkv, W.Wkv, dx, rows=M)
+        ops.linear_dx(dkv, W.Wkv, dx, rows=M, wp=True)
     del dkv
     mark(f"enc_feed_forward_{len(W.enc) - 1}.normalization.gamma")
     for i in reversed(range(len(W.enc))):
@@ -550,9 +550,9 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
             ops.ln_bwd(dx, e["z2"], *e["st2"], L["g2"], dz2, Lg["g2"], Lg["b2"])
             ops.linear_dw(dz2, e["h"], Lg["W2"], Lg["c2"], rows=M)
             dh = _empty(M, 4 * d, dev=dev)
-            ops.linear_dx(dz2, L["W2"], dh, rows=M, mask=e["h"], ldmask=4 * d)
+            ops.linear_dx(dz2, L["W2"], dh, rows=M, mask=e["h"], ldmask=4 * d, wp=True)
             ops.linear_dw(dh, e["y1"], Lg["W1"], Lg["c1"], rows=M)
-            ops.linear_dx(dh, L["W1"], dy1, rows=M, resid=dz2)
+            ops.linear_dx(dh, L["W1"], dy1, rows=M, resid=dz2, wp=True)
         del dh
         dz1 = _empty(M, d, dev=dev)
         ops.ln_bwd(dy1, e["z1"], *e["st1"], L["g1"], dz1, Lg["g1"], Lg["b1"])
@@ -568,7 +568,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
                               T, H, dz1, d, dqv, 2 * d, dk, d, dqv[:, d:], 2 * d)
             dxn = _empty(M, d, dev=dev)
             ops.linear_dw(dk, e["x"], Lg["Wqkv"][d:2 * d], Lg["bqkv"][d:2 * d], rows=M)
-            ops.linear_dx(dk, L["Wqkv"][d:2 * d], dxn, rows=M, resid=dz1)
+            ops.linear_dx(dk, L["Wqkv"][d:2 * d], dxn, rows=M, resid=dz1, wp=True)
             for off in (0, 2 * d):  # dW_q, dW_v over the question rows (k-row gathers)
                 ops.gemm(dqv[:, off // 2:], e["x"], Lg["Wqkv"][off:off + d], d, d, B * Lq,
                          lda=2 * d, ldb=d, ldc=d, a_trans=True, a_rows=s.qrows, b_rows=s.qrows,
@@ -603,7 +603,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
             ops.linear_dx_lp(dqkv, Lb["Wqkv"], dxn, rows=M, resid=dz1)
         else:
             ops.linear_dw(dqkv, e["x"], Lg["Wqkv"], Lg["bqkv"], rows=M)
-            ops.linear_dx(dqkv, L["Wqkv"], dxn, rows=M, resid=dz1)
+            ops.linear_dx(dqkv, L["Wqkv"], dxn, rows=M, resid=dz1, wp=True)
         dx = dxn
         if i > 0:
             mark(f"enc_feed_forward_{i - 1}.normalization.gamma")
@@ -629,7 +629,7 @@ def stack_backward(W: StackWeights, G: StackWeights, s: StackSaved, dout: torch.
     else:
         ops.linear_dw(dx, s.cat, G.Win, G.bin, rows=M)
         dq = _empty(B * Lq, D2, dev=dev)
-        ops.linear_dx(dx, W.Win, dq, rows=B * Lq, a_rows=qrows, mask=s.cat, ldmask=s.cat.shape[1],
+        ops.linear_dx(dx, W.Win, dq, rows=B * Lq, a_rows=qrows, mask=s.cat, ldmask=s.cat.shape[1], wp=True,
                       mask_arows=True)
     ops.linear_dw(dq, W.E, G.Wq, G.bq, rows=B * Lq, x_rows=s.q_flat)
     _table_grad(dq, W.Wq, s.q_flat, G.E, B * Lq)
@@ -1182,6 +1182,7 @@ class ModelEngine:
         visual stack and the MIL-NCE + semantic stack run on two HIP streams: one stack's
         latency-bound decoder phase and GEMM tails overlap the other's big GEMMs.
         drop = (seed, p): training-mode dropout (None in eval or at p = 0)."""
+        ops.WP_KEY = self.arena.state_key()  # the weights' pre-split x6 planes follow it
         d, H = self.d, self.H
         vis = inp["vis_fea"]
         dev = vis.device

@@ -72,8 +72,8 @@ class GemmProbe:
             return f"gemm_skinny16_kernel<{lay}>"
         if d.prec in (1, 5, 6):  # (savqa_gemm's fallback: operands that are not 16-B vectors)
             al = all(p % 16 == 0 and ld % 4 == 0 for p, ld in ((d.A, d.lda), (d.B, d.ldb)))
-            if al:
-                return f"gemm_x6_kernel<{lay}>"
+            if al:  # third argument: hi / lo accumulators (prec 5: the two-level form)
+                return f"gemm_x6_kernel<{lay},{str(d.prec != 5).lower()}>"
             return f"gemm_f32_kernel<{plan[0]},{plan[0]},{lay}>"
         if d.prec:
             return f"gemm_bf16_kernel<{lay},{d.prec}>"
@@ -165,6 +165,30 @@ def _attn_bytes(q, B, Tq, Tk, H, dk, n_in, n_out):
     return rows * (n_in + n_out) + B * Tq * Tk * 4
 
 
+# Pre-split x6 planes of GEMM weights (savqa_x6_weight_planes): a weight's B operand split
+# into the x6 kernel's three bf16 plane images once per optimizer step instead of by every
+# 128x128 tile that reads it (savqa_gemm_desc.b_planes; bit-identical results). The engine
+# sets WP_KEY to the parameter arena's state key at every forward; planes made under another
+# key are rebuilt at their next use, on the stream of that use.
+X6_PLANES = os.environ.get("SAVQA_X6_PLANES", "1") != "0"
+WP_KEY = None
+_wplanes = {}
+
+
+def weight_planes(W: Tensor, b_trans: bool, N: int, K: int, ldb: int) -> Tensor:
+    key = (W.data_ptr(), bool(b_trans), int(N), int(K), int(ldb), W.device)
+    e = _wplanes.get(key)
+    if e is not None and e[1] == WP_KEY:
+        return e[0]
+    buf = e[0] if e is not None else torch.empty(
+        int(_lib.load().savqa_x6_weight_planes_bytes(int(N), int(K))), dtype=torch.uint8,
+        device=W.device)
+    call("savqa_x6_weight_planes", _stream(), _p(W), int(ldb), int(bool(b_trans)), int(N),
+         int(K), _p(buf))
+    _wplanes[key] = (buf, WP_KEY)
+    return buf
+
+
 def set_gemm_probe(probe):
     global _probe
     _probe = probe
@@ -175,7 +199,7 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
          c_group=0, c_stride=0, c_offset=0, bias=None, rowvec=None, ldrv=0, rowvec_period=0,
          resid=None, ldr=0, mask=None, ldmask=0, mask_arows=False, rowscale=None, relu=False,
          alpha=1.0, beta=0.0, atomic=False, split_k=1, colsum_a=None, prec=None,
-         plan_only=False):
+         plan_only=False, b_planes=False):
     """Generic MFMA GEMM with fused epilogue (see savqa_gemm in include/savqa.h).
     plan_only: no launch, return savqa_gemm_plan's [tile, split, tail slices, workgroups]."""
     d = GemmDesc()
@@ -196,6 +220,8 @@ def gemm(A: Tensor, B: Tensor, Cm: Tensor, M: int, N: int, K: int, *, lda: int, 
     d.alpha, d.beta = float(alpha), float(beta)
     d.relu, d.atomic, d.split_k = int(bool(relu)), int(bool(atomic)), int(split_k)
     d.colsum_a = _p(colsum_a)
+    if b_planes and X6_PLANES and d.prec in (5, 6) and not a_trans and b_rows is None:
+        d.b_planes = _p(weight_planes(B, b_trans, N, K, ldb))
     if plan_only:
         plan = (C.c_int32 * 4)()
         call("savqa_gemm_plan", C.byref(d), C.cast(plan, C.c_void_p))
@@ -401,20 +427,22 @@ def linear_dw_lp(dY: Tensor, X: Tensor, dW: Tensor, db: Optional[Tensor], *, row
 
 def linear(X: Tensor, W: Tensor, b: Optional[Tensor], out: Tensor, *, relu=False,
            rows: Optional[int] = None, a_rows=None, rowvec=None, rowvec_period=0, resid=None,
-           c_group=0, c_stride=0, c_offset=0, ldx=None, ldo=None, rowscale=None, prec=None):
+           c_group=0, c_stride=0, c_offset=0, ldx=None, ldo=None, rowscale=None, prec=None,
+           wp=False):
     """out = act(X W^T + b [+ rowvec]) [+ resid]  -- nn.Linear forward (W is [out, in])."""
     N, K = W.shape
     M = rows if rows is not None else (a_rows.numel() if a_rows is not None else X.numel() // K)
     gemm(X, W, out, M, N, K, lda=ldx if ldx is not None else K, ldb=K,
          ldc=ldo if ldo is not None else N, b_trans=True, a_rows=a_rows, bias=b, rowvec=rowvec,
          ldrv=N, rowvec_period=rowvec_period, resid=resid, ldr=N, relu=relu, c_group=c_group,
-         c_stride=c_stride, c_offset=c_offset, rowscale=rowscale, prec=prec)
+         c_stride=c_stride, c_offset=c_offset, rowscale=rowscale, prec=prec, b_planes=wp)
 
 
 def linear_dx(dY: Tensor, W: Tensor, dX: Tensor, *, rows: int, a_rows=None, mask=None,
               ldmask=0, mask_arows=False, resid=None, ldr=None, c_rows=None, atomic=False,
-              beta=0.0, lddy=None, lddx=None):
-    """dX = dY W  (mask: ReLU-backward gate of the producer of X; c_rows: scatter-add)."""
+              beta=0.0, lddy=None, lddx=None, wp=False):
+    """dX = dY W  (mask: ReLU-backward gate of the producer of X; c_rows: scatter-add;
+    wp: W's pre-split x6 planes, see weight_planes)."""
     N, K = W.shape  # dY has N cols, dX has K cols
     # a pure scatter-add (the GloVe-table gradient: few output tiles, K = 2048) may split K
     # across workgroups: every slice adds its partial with the same atomics
@@ -422,7 +450,7 @@ def linear_dx(dY: Tensor, W: Tensor, dX: Tensor, *, rows: int, a_rows=None, mask
     gemm(dY, W, dX, rows, K, N, lda=lddy if lddy is not None else N, ldb=K,
          ldc=lddx if lddx is not None else K, a_rows=a_rows, mask=mask, ldmask=ldmask,
          mask_arows=mask_arows, resid=resid, ldr=ldr if ldr is not None else K, c_rows=c_rows,
-         atomic=atomic, beta=beta, split_k=split)
+         atomic=atomic, beta=beta, split_k=split, b_planes=wp)
 
 
 def linear_dw(dY: Tensor, X: Tensor, dW: Tensor, db: Optional[Tensor], *, rows: int,

@@ -777,3 +777,38 @@ def test_gemm_skinny_bf16_products(lay, M, N, K):
     assert rel(out - (0 if at else R), exact) > 1e-4  # really bf16 products, not fp32 ones
     if cs is not None:
         assert rel(cs, A.double().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("prec", [6, 5])
+@pytest.mark.parametrize("lay,M,N,K", [("NT", 18688, 2048, 512), ("NT", 1000, 300, 520),
+                                       ("NN", 18688, 512, 2048), ("NN", 777, 1000, 300),
+                                       ("NT", 18688, 512, 2048), ("NN", 18688, 512, 6144)])
+def test_gemm_x6_weight_planes_bit_identical(lay, M, N, K, prec):
+    """savqa_gemm_desc.b_planes (ops.weight_planes: the weight split into the x6 kernel's three
+    bf16 plane images once, DMA'd into a double-buffered LDS image by the kernel): the same
+    split values meet the same MFMAs, so the outputs are BIT-identical to the launch that
+    splits B itself -- M / N / K edges, the tail split (N = 512 at 18688 rows), the two-level
+    form (prec 5), an A row gather, a residual and a ReLU-backward mask."""
+    O = ops()
+    bt = lay == "NT"
+    A = g(M, K, seed=81)
+    B = g(N, K, seed=82) if bt else g(K, N, seed=82)
+    kw = dict(lda=K, ldb=K if bt else N, ldc=N, b_trans=bt, prec=prec)
+    R = g(M, N, seed=83)
+    H = g(M, N, seed=84, relu=True)
+    O.WP_KEY = ("test", lay, M, N, K, prec)
+    outs = []
+    for planes in (False, True):
+        out = torch.empty(M, N, device=dev)
+        O.gemm(A, B, out, M, N, K, resid=R, ldr=N, mask=H, ldmask=N, b_planes=planes, **kw)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    ref = (A.double() @ (B.double().t() if bt else B.double())) * (H > 0).double() + R.double()
+    assert rel(outs[1], ref) < 5e-6
+    idx = torch.randint(0, M, (M // 2,), generator=torch.Generator().manual_seed(85)).to(dev)
+    gathered = []
+    for planes in (False, True):
+        out = torch.empty(M // 2, N, device=dev)
+        O.gemm(A, B, out, M // 2, N, K, a_rows=idx, b_planes=planes, **kw)
+        gathered.append(out)
+    assert torch.equal(gathered[0], gathered[1])
