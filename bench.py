@@ -242,7 +242,7 @@ WORKLOADS = {
 
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 # committed PMC passes of each workload's bench command (tools/profile_round.sh)
-ROOFLINE_JSON = {w: f"r05_{w}_roofline.json" for w in ("cfg2", "cfg3", "cfg4", "cfg5", "rel")}
+ROOFLINE_JSON = {w: f"r06_{w}_roofline.json" for w in ("cfg2", "cfg3", "cfg4", "cfg5", "rel")}
 
 
 def committed_traffic(variant, workload="cfg2"):

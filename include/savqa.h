@@ -33,7 +33,8 @@ extern "C" {
 int savqa_version(void);
 const char* savqa_last_error(void);
 /* sizeof of the descriptor structs, for bindings to check their layouts: out[0] =
- * savqa_gemm_desc, out[1] = savqa_gemm_lp_desc, out[2] = savqa_collate_field; n >= 3 */
+ * savqa_gemm_desc, out[1] = savqa_gemm_lp_desc, out[2] = savqa_collate_field; n >= 3;
+ * with n >= 4 also out[3] = savqa_x6_planes_job */
 int savqa_struct_sizes(int64_t* out, int32_t n);
 
 /* ------------------------------------------------------------------------
@@ -104,6 +105,17 @@ typedef struct savqa_gemm_desc {
 int64_t savqa_x6_weight_planes_bytes(int64_t N, int64_t K);
 int savqa_x6_weight_planes(void* stream, const float* Bp, int64_t ldb, int32_t b_trans, int64_t N,
                            int64_t K, void* out);
+/* Many operands' plane images at once (an optimizer step's weights: a few launches instead of
+ * one per weight). jobs: HOST array of n entries, read before the call returns; each as
+ * savqa_x6_weight_planes' arguments (entries with N or K <= 0 are skipped). */
+typedef struct savqa_x6_planes_job {
+    const float* B;
+    int64_t ldb;
+    int32_t b_trans, reserved;
+    int64_t N, K;
+    void* out;
+} savqa_x6_planes_job;
+int savqa_x6_weight_planes_batch(void* stream, const savqa_x6_planes_job* jobs, int32_t n);
 
 int savqa_gemm(void* stream, const savqa_gemm_desc* d);
 /* fp32 elements of workspace *d's launch would use for split-K / tail-split slabs (0: the plan

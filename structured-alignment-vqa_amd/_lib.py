@@ -77,6 +77,14 @@ class CollateField(C.Structure):
     ]
 
 
+class PlanesJob(C.Structure):
+    """savqa_x6_planes_job (include/savqa.h)."""
+    _fields_ = [
+        ("B", c_p), ("ldb", c_i64), ("b_trans", c_i32), ("reserved", c_i32),
+        ("N", c_i64), ("K", c_i64), ("out", c_p),
+    ]
+
+
 # name -> argtypes (restype is always int except savqa_last_error)
 _SIGS = {
     "savqa_version": [],
@@ -157,6 +165,7 @@ _SIGS = {
     "savqa_segment_add_rows": [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_p, c_i64],
     "savqa_x6_weight_planes": [c_p, c_p, c_i64, c_i32, c_i64, c_i64, c_p],
     "savqa_x6_weight_planes_bytes": [c_i64, c_i64],
+    "savqa_x6_weight_planes_batch": [c_p, c_p, c_i32],
     "savqa_index_get_rows": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "savqa_loss_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f, c_p, c_i32, c_p, c_p, c_p, c_p],
     "savqa_scale_by": [c_p, c_p, c_p, c_i64, c_p],

@@ -33,5 +33,6 @@ extern "C" int savqa_struct_sizes(int64_t* out, int32_t n) {
   out[0] = (int64_t)sizeof(savqa_gemm_desc);
   out[1] = (int64_t)sizeof(savqa_gemm_lp_desc);
   out[2] = (int64_t)sizeof(savqa_collate_field);
+  if (n >= 4) out[3] = (int64_t)sizeof(savqa_x6_planes_job);
   return 0;
 }

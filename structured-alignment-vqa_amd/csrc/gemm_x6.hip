@@ -611,25 +611,78 @@ int savqa_launch_gemm_x6(const savqa_gemm_desc& d, const savqa::GemmGrid& gg, in
 
 // ------------------------------------------------------------------ pre-split B planes
 namespace savqa {
-// one workgroup per (n tile, k tile): the 128 x 32 B tile split like X6Operand<ROW>::store
-// (thread u -> row u / 8, k 4 (u % 8)), zeros past N / K
-__global__ __launch_bounds__(256) void x6_planes_kernel(const float* __restrict__ Bp, int64_t ldb,
-                                                        int b_trans, int64_t N, int64_t K,
-                                                        int64_t KT, char* __restrict__ out) {
-  const int64_t nt = blockIdx.x / KT, kt = blockIdx.x - nt * KT;
-  char* img = out + (int64_t)blockIdx.x * (3 * X6_PLANE);
+// Up to X6_PJOBS operands per launch (an optimizer step's weights in one or a few launches:
+// one launch per weight ran ~6 us each, latency-bound at one workgroup per CU).
+constexpr int X6_PJOBS = 32;
+struct X6PlanesJob {
+  const float* B;
+  int64_t ldb, N, K;
+  char* out;
+  int32_t b_trans, KT;
+};
+struct X6PlanesBatch {
+  X6PlanesJob j[X6_PJOBS];
+  int32_t start[X6_PJOBS + 1];  // first workgroup of each job; start[n] = grid size
+  int32_t n;
+};
+
+// one workgroup per (n tile, k tile) of one job: the 128 x 32 B tile split like the kernel's
+// own staging (X6Operand<ROW / COL>::store), zeros past N / K. k-contiguous B (b_trans):
+// thread u -> row u / 8, k 4 (u % 8), 16-B loads along k; n-contiguous B: thread (g, kg) ->
+// rows 4g .. 4g+3, k 4kg .. 4kg+3, 16-B loads along n, transposed in registers.
+__global__ __launch_bounds__(256) void x6_planes_kernel(const X6PlanesBatch bt) {
+  int j = 0;
+  while (j + 1 < bt.n && (int)blockIdx.x >= bt.start[j + 1]) ++j;  // uniform: scalar loop
+  const X6PlanesJob& J = bt.j[j];
+  const int tile = (int)blockIdx.x - bt.start[j];
+  const int nt = tile / J.KT, kt = tile - nt * J.KT;
+  const float* __restrict__ Bp = J.B;
+  const int64_t n0 = (int64_t)nt * X6_TILE, k0 = (int64_t)kt * X6_BK, ldb = J.ldb;
+  char* img = J.out + (int64_t)tile * (3 * X6_PLANE);
+  const bool full = n0 + X6_TILE <= J.N && k0 + X6_BK <= J.K && (ldb & 3) == 0 &&
+                    ((uintptr_t)Bp & 15) == 0;
+  const int t = threadIdx.x;
+  if (J.b_trans) {
+    f4 v[4];
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int u = threadIdx.x + 256 * it;
-    const int r = u >> 3, k4 = 4 * (u & 7);
-    const int64_t n = nt * X6_TILE + r, k = kt * X6_BK + k4;
-    f4 v = {0.f, 0.f, 0.f, 0.f};
-    if (n < N) {
+    for (int it = 0; it < 4; ++it) {
+      const int u = t + 256 * it, r = u >> 3, k4 = 4 * (u & 7);
+      const float* src = Bp + (n0 + r) * ldb + k0 + k4;
+      if (full) {
+        v[it] = *reinterpret_cast<const f4*>(src);
+      } else {
+        v[it] = f4{0.f, 0.f, 0.f, 0.f};
+        if (n0 + r < J.N)
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (k + e < K) v[e] = b_trans ? Bp[n * ldb + k + e] : Bp[(k + e) * ldb + n];
+          for (int e = 0; e < 4; ++e)
+            if (k0 + k4 + e < J.K) v[it][e] = src[e];
+      }
     }
-    put3(img, x6_off(r, k4), v);
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int u = t + 256 * it;
+      put3(img, x6_off(u >> 3, 4 * (u & 7)), v[it]);
+    }
+  } else {
+    const int g = t >> 3, kg = t & 7;
+    f4 v[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int64_t k = k0 + 4 * kg + it;
+      const float* src = Bp + k * ldb + n0 + 4 * g;
+      if (full) {
+        v[it] = *reinterpret_cast<const f4*>(src);
+      } else {
+        v[it] = f4{0.f, 0.f, 0.f, 0.f};
+        if (k < J.K)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n0 + 4 * g + e < J.N) v[it][e] = src[e];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      put3(img, x6_off(4 * g + s, 4 * kg), f4{v[0][s], v[1][s], v[2][s], v[3][s]});
   }
 }
 }  // namespace savqa
@@ -639,14 +692,53 @@ extern "C" int64_t savqa_x6_weight_planes_bytes(int64_t N, int64_t K) {
   return ((N + 127) / 128) * ((K + 31) / 32) * 3 * (int64_t)savqa::X6_PLANE;
 }
 
+extern "C" int savqa_x6_weight_planes_batch(void* stream, const savqa_x6_planes_job* jobs,
+                                            int32_t n) {
+  using namespace savqa;
+  if (n < 0 || (n > 0 && !jobs))
+    return fail(SAVQA_EINVAL, "savqa_x6_weight_planes_batch: null job list");
+  for (int i = 0; i < n; ++i) {
+    const savqa_x6_planes_job& q = jobs[i];
+    if (q.N <= 0 || q.K <= 0) continue;
+    if (!q.B || !q.out || ((uintptr_t)q.out & 15) || q.ldb < (q.b_trans ? q.K : q.N))
+      return fail(SAVQA_EINVAL, "savqa_x6_weight_planes: null operand, unaligned output or "
+                                "leading dimension below the operand's extent");
+  }
+  X6PlanesBatch bt;
+  int i = 0;
+  while (i < n) {
+    bt.n = 0;
+    int64_t blocks = 0;
+    for (; i < n && bt.n < X6_PJOBS; ++i) {
+      const savqa_x6_planes_job& q = jobs[i];
+      if (q.N <= 0 || q.K <= 0) continue;
+      const int64_t KT = (q.K + X6_BK - 1) / X6_BK, NT = (q.N + X6_TILE - 1) / X6_TILE;
+      if (blocks + NT * KT > (int64_t)INT32_MAX) break;
+      X6PlanesJob& J = bt.j[bt.n];
+      J.B = q.B;
+      J.ldb = q.ldb;
+      J.N = q.N;
+      J.K = q.K;
+      J.out = static_cast<char*>(q.out);
+      J.b_trans = q.b_trans ? 1 : 0;
+      J.KT = (int32_t)KT;
+      bt.start[bt.n++] = (int32_t)blocks;
+      blocks += NT * KT;
+    }
+    if (bt.n == 0) {
+      if (i < n && blocks == 0) return fail(SAVQA_EINVAL, "savqa_x6_weight_planes: operand too large");
+      break;
+    }
+    bt.start[bt.n] = (int32_t)blocks;
+    hipLaunchKernelGGL(x6_planes_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), bt);
+    const int rc = check_launch("savqa_x6_weight_planes");
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 extern "C" int savqa_x6_weight_planes(void* stream, const float* Bp, int64_t ldb, int32_t b_trans,
                                       int64_t N, int64_t K, void* out) {
-  using namespace savqa;
-  if (N <= 0 || K <= 0) return 0;
-  if (!Bp || !out || ((uintptr_t)out & 15))
-    return fail(SAVQA_EINVAL, "savqa_x6_weight_planes: null operand or unaligned output");
-  const int64_t KT = (K + X6_BK - 1) / X6_BK, NT = (N + X6_TILE - 1) / X6_TILE;
-  hipLaunchKernelGGL(x6_planes_kernel, dim3((unsigned)(NT * KT)), dim3(256), 0, as_stream(stream),
-                     Bp, ldb, b_trans, N, K, KT, static_cast<char*>(out));
-  return check_launch("savqa_x6_weight_planes");
+  savqa_x6_planes_job q = {Bp, ldb, b_trans, 0, N, K, out};
+  return savqa_x6_weight_planes_batch(stream, &q, 1);
 }

@@ -708,7 +708,7 @@ def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb
         ops.linear_lp(lp.vis, lp.Wv, W.bv, s.vv, relu=True, x_scale=lp.vis_scale,
                       w_scale=lp.Wv_scale)
     else:
-        ops.linear(s.vis, W.Wv, W.bv, s.vv, relu=True)
+        ops.linear(s.vis, W.Wv, W.bv, s.vv, relu=True, wp=True)
     s.macro = _empty(B * Ns, Hm, dev=dev)
     if lp is not None:  # (forward only: new_macro_ipt is detached, AttModel_x3.py:354)
         ids = macro_ipt.reshape(-1)
@@ -734,7 +734,7 @@ def mil_forward(W: MilWeights, vis_fea, macro_ipt, loc, pos, neg, omask, cat_syb
                       c_group=Ns, c_stride=T_syb, c_offset=0, ldo=cat_syb.shape[1])
     else:
         ops.linear(s.macro, W.Wipt, W.bipt, cat_syb, relu=True, rows=B * Ns, c_group=Ns,
-                   c_stride=T_syb, c_offset=0, ldo=cat_syb.shape[1])
+                   c_stride=T_syb, c_offset=0, ldo=cat_syb.shape[1], wp=True)
     return s
 
 
@@ -781,7 +781,7 @@ def mil_backward(W: MilWeights, G: MilWeights, s: MilSaved, dnode: Optional[torc
             del dnodeb
         else:
             ops.linear_dw(dnode, s.macro, G.Wipt, G.bipt, rows=B * Ns)
-            ops.linear_dx(dnode, W.Wipt, dmacro, rows=B * Ns)
+            ops.linear_dx(dnode, W.Wipt, dmacro, rows=B * Ns, wp=True)
         if rel is not None:  # relation rows: grads to the softmax weights and rel features,
             Lp = rel["Lp"]    # and the overwritten previous contents get none
             rel["dwsm"] = torch.zeros(max(B * Lp, 1), device=dev)
@@ -1038,6 +1038,8 @@ class ModelEngine:
         self.gemm_precision = gemm_precision
         self.nb, self.d, self.H = num_blocks, hidden, heads
         self._shadow = None
+        self._wp_cache = {}   # this model's pre-split x6 weight planes (ops.WP_CACHE)
+        self._wp_key = None
         # AttModel's relation bounds check: a wait that raises for a bad table, called before
         # the first relation kernel is launched (set per forward, consumed by _forward)
         self.pending_rel_check = None
@@ -1182,7 +1184,12 @@ class ModelEngine:
         visual stack and the MIL-NCE + semantic stack run on two HIP streams: one stack's
         latency-bound decoder phase and GEMM tails overlap the other's big GEMMs.
         drop = (seed, p): training-mode dropout (None in eval or at p = 0)."""
-        ops.WP_KEY = self.arena.state_key()  # the weights' pre-split x6 planes follow it
+        # the weights' pre-split x6 planes follow the arena's state: images of the previous
+        # step's weights rebuilt in one batched launch, before the stack streams fork
+        ops.WP_KEY = self._wp_key = self.arena.state_key()
+        ops.WP_CACHE = self._wp_cache
+        if ops.X6_PLANES and ops.WP_BATCH:
+            ops.refresh_weight_planes()
         d, H = self.d, self.H
         vis = inp["vis_fea"]
         dev = vis.device
@@ -1256,6 +1263,9 @@ class ModelEngine:
                 a.offsets["MIL_NCE.ipt_mlp.0.weight"][0])
 
     def backward(self, saved, dlc, dlv, dls, dmil, on_range=None, dmil_rel=None):
+        # this model's weight planes, under the key its forward saw (another model's forward
+        # may have run in between)
+        ops.WP_KEY, ops.WP_CACHE = self._wp_key, self._wp_cache
         with ops.gemm_precision(self._fp32_kernel_precision()):
             return self._backward(saved, dlc, dlv, dls, dmil, on_range, dmil_rel)
 

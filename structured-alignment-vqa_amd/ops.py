@@ -72,8 +72,12 @@ class GemmProbe:
             return f"gemm_skinny16_kernel<{lay}>"
         if d.prec in (1, 5, 6):  # (savqa_gemm's fallback: operands that are not 16-B vectors)
             al = all(p % 16 == 0 and ld % 4 == 0 for p, ld in ((d.A, d.lda), (d.B, d.ldb)))
-            if al:  # third argument: hi / lo accumulators (prec 5: the two-level form)
-                return f"gemm_x6_kernel<{lay},{str(d.prec != 5).lower()}>"
+            if al:  # third argument: hi / lo accumulators (prec 5: the two-level form);
+                # fourth: B from the pre-split weight planes (the conditions savqa_gemm applies)
+                bp = bool(d.b_planes) and plan[0] == 128 and not d.a_trans and \
+                    not d.b_rows and d.b_planes % 16 == 0
+                return (f"gemm_x6_kernel<{lay},{str(d.prec != 5).lower()},"
+                        f"{str(bp).lower()}>")
             return f"gemm_f32_kernel<{plan[0]},{plan[0]},{lay}>"
         if d.prec:
             return f"gemm_bf16_kernel<{lay},{d.prec}>"
@@ -168,16 +172,19 @@ def _attn_bytes(q, B, Tq, Tk, H, dk, n_in, n_out):
 # Pre-split x6 planes of GEMM weights (savqa_x6_weight_planes): a weight's B operand split
 # into the x6 kernel's three bf16 plane images once per optimizer step instead of by every
 # 128x128 tile that reads it (savqa_gemm_desc.b_planes; bit-identical results). The engine
-# sets WP_KEY to the parameter arena's state key at every forward; planes made under another
-# key are rebuilt at their next use, on the stream of that use.
+# points WP_CACHE at its own cache (the images die with the model) and sets WP_KEY to the
+# parameter arena's state key at every forward, then refresh_weight_planes() rebuilds every
+# image made under another key in one batched launch on the current stream; an image seen for
+# the first time is built at its first use, on the stream of that use.
 X6_PLANES = os.environ.get("SAVQA_X6_PLANES", "1") != "0"
+WP_BATCH = os.environ.get("SAVQA_WP_BATCH", "1") != "0"   # 0: rebuild each image at its use
 WP_KEY = None
-_wplanes = {}
+WP_CACHE = {}   # (W ptr, b_trans, N, K, ldb, device) -> [image, key it was built under]
 
 
 def weight_planes(W: Tensor, b_trans: bool, N: int, K: int, ldb: int) -> Tensor:
     key = (W.data_ptr(), bool(b_trans), int(N), int(K), int(ldb), W.device)
-    e = _wplanes.get(key)
+    e = WP_CACHE.get(key)
     if e is not None and e[1] == WP_KEY:
         return e[0]
     buf = e[0] if e is not None else torch.empty(
@@ -185,8 +192,24 @@ def weight_planes(W: Tensor, b_trans: bool, N: int, K: int, ldb: int) -> Tensor:
         device=W.device)
     call("savqa_x6_weight_planes", _stream(), _p(W), int(ldb), int(bool(b_trans)), int(N),
          int(K), _p(buf))
-    _wplanes[key] = (buf, WP_KEY)
+    WP_CACHE[key] = [buf, WP_KEY]
     return buf
+
+
+def refresh_weight_planes() -> int:
+    """Rebuild every WP_CACHE image made under another WP_KEY (one savqa_x6_weight_planes_batch
+    call on the current stream); returns the number rebuilt."""
+    stale = [(k, e) for k, e in WP_CACHE.items() if e[1] != WP_KEY]
+    if not stale:
+        return 0
+    jobs = (_lib.PlanesJob * len(stale))()
+    for i, ((ptr, bt, N, K, ldb, _dev), e) in enumerate(stale):
+        jobs[i].B, jobs[i].ldb, jobs[i].b_trans = ptr, ldb, int(bt)
+        jobs[i].N, jobs[i].K, jobs[i].out = N, K, _p(e[0])
+    call("savqa_x6_weight_planes_batch", _stream(), C.cast(jobs, C.c_void_p), len(stale))
+    for _, e in stale:
+        e[1] = WP_KEY
+    return len(stale)
 
 
 def set_gemm_probe(probe):

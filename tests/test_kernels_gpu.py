@@ -812,3 +812,67 @@ def test_gemm_x6_weight_planes_bit_identical(lay, M, N, K, prec):
         O.gemm(A, B, out, M // 2, N, K, a_rows=idx, b_planes=planes, **kw)
         gathered.append(out)
     assert torch.equal(gathered[0], gathered[1])
+
+
+def _planes_ref(Bv, N, K):
+    """The x6 plane image of an [N][K] fp32 matrix (savqa_x6_weight_planes' layout, restated):
+    per (128-row n tile, 32-k tile) three 128 x 32 bf16 planes, row r at 64 B, 16-B chunk
+    (k / 8) XOR S[(r / 4) % 4] with S = {0, 2, 3, 1}; plane p holds the top 16 bits of the
+    p-th truncation residue (a0 = a with its low 16 bits cleared, a1 of a - a0, ...)."""
+    NT, KT = (N + 127) // 128, (K + 31) // 32
+    P = torch.zeros(NT * 128, KT * 32, dtype=torch.float32, device=Bv.device)
+    P[:N, :K] = Bv
+    x = P.clone()
+    terms = []
+    for _ in range(3):
+        hi = (x.view(torch.int32) & -65536).view(torch.float32)
+        terms.append((hi.view(torch.int32) >> 16).to(torch.int16))
+        x = x - hi
+    img = torch.zeros(NT, KT, 3, 128, 32, dtype=torch.int16, device=Bv.device)
+    r = torch.arange(128, device=Bv.device)
+    swz = (0x1320 >> (4 * ((r >> 2) & 3))) & 3
+    k = torch.arange(32, device=Bv.device)
+    col = (((k[None, :] >> 3) ^ swz[:, None]) << 3) + (k[None, :] & 7)   # [128, 32] -> slot
+    for p in range(3):
+        t = terms[p].view(NT, 128, KT, 32).permute(0, 2, 1, 3)            # [NT, KT, 128, 32]
+        img[:, :, p].scatter_(3, col.expand(NT, KT, 128, 32), t)
+    return img.flatten().view(torch.uint8)
+
+
+def test_x6_weight_planes_batch_matches_reference_layout():
+    """savqa_x6_weight_planes_batch over 40 operands (two launches of <= 32 jobs): k-contiguous
+    and n-contiguous B, ragged N / K, a leading dimension wider than the operand, an operand
+    not 16-B aligned -- every image byte-equal to the layout restated in torch (_planes_ref),
+    and to the one-operand entry point."""
+    import ctypes as C
+    from savqa_amd import _lib
+    O = ops()
+    shapes = [(512, 512), (300, 520), (2048, 512), (129, 33), (1000, 300), (64, 31), (6144, 512)]
+    jobs, refs, keep = [], [], []
+    for i in range(40):
+        N, K = shapes[i % len(shapes)]
+        bt = bool(i % 2)
+        ld = (K if bt else N) + (7 if i % 3 == 0 else 0)
+        off = 1 if i % 5 == 4 else 0
+        rows = N if bt else K
+        store = g(rows * ld + off, 1, seed=200 + i).flatten()
+        W = store[off:]
+        Bv = W[:rows * ld].view(rows, ld)[:, :(K if bt else N)]
+        Bnk = Bv if bt else Bv.t()
+        out = torch.zeros(int(_lib.load().savqa_x6_weight_planes_bytes(N, K)), dtype=torch.uint8,
+                          device=dev)
+        keep += [store, out]
+        jobs.append((W, ld, bt, N, K, out))
+        refs.append(_planes_ref(Bnk, N, K))
+    arr = (_lib.PlanesJob * len(jobs))()
+    for i, (W, ld, bt, N, K, out) in enumerate(jobs):
+        arr[i].B, arr[i].ldb, arr[i].b_trans = W.data_ptr(), ld, int(bt)
+        arr[i].N, arr[i].K, arr[i].out = N, K, out.data_ptr()
+    O.call("savqa_x6_weight_planes_batch", O._stream(), C.cast(arr, C.c_void_p), len(jobs))
+    torch.cuda.synchronize()
+    for i, (W, ld, bt, N, K, out) in enumerate(jobs):
+        assert torch.equal(out, refs[i]), (i, N, K, bt, ld)
+        one = torch.full_like(out, 7)
+        O.call("savqa_x6_weight_planes", O._stream(), W.data_ptr(), ld, int(bt), N, K,
+               one.data_ptr())
+        assert torch.equal(one, out), i

@@ -65,10 +65,10 @@ def test_descriptor_layouts_match_the_library():
     from savqa_amd import _lib
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("libsavqa.so not built")
-    out = (C.c_int64 * 3)()
-    assert _lib.load().savqa_struct_sizes(C.cast(out, C.c_void_p), 3) == 0
+    out = (C.c_int64 * 4)()
+    assert _lib.load().savqa_struct_sizes(C.cast(out, C.c_void_p), 4) == 0
     assert list(out) == [C.sizeof(_lib.GemmDesc), C.sizeof(_lib.GemmLpDesc),
-                         C.sizeof(_lib.CollateField)]
+                         C.sizeof(_lib.CollateField), C.sizeof(_lib.PlanesJob)]
 
 
 def test_library_exports_every_declared_symbol():

@@ -34,7 +34,7 @@ def operand(P, rows, cols, ld, trans, idx):
     return flat[ix].double()
 
 
-def audit(orig, A, B, Cm, M, N, K, kw):
+def audit(orig, A, B, Cm, M, N, K, kw, xprec=6):
     lda, ldb = kw["lda"], kw["ldb"]
     at, bt = bool(kw.get("a_trans")), bool(kw.get("b_trans"))
     ar, br = kw.get("a_rows"), kw.get("b_rows")
@@ -42,18 +42,19 @@ def audit(orig, A, B, Cm, M, N, K, kw):
     Bm = operand(B, N, K, ldb, not bt, br)  # B(k, n) as [n, k]
     ref = Am @ Bm.t()
     errs, stats = {}, {}
-    for prec in (0, 6):
+    for prec in (0, xprec):  # xprec 5: the two-level form (decoder K/V projection)
         out = torch.zeros(M, N, device=A.device)
         orig(A, B, out, M, N, K, lda=lda, ldb=ldb, ldc=N, a_trans=at, b_trans=bt, a_rows=ar,
              b_rows=br, atomic=at, split_k=-1 if at else 1, prec=prec)
         torch.cuda.synchronize()
         e = out.double() - ref
-        errs[prec] = float(e.abs().max() / ref.abs().max().clamp_min(1e-300))
+        errs[6 if prec else 0] = float(e.abs().max() / ref.abs().max().clamp_min(1e-300))
         # bias: error along the sign of the exact value (toward-zero errors give < 0), rms
-        stats[prec] = (float((e * ref.sign()).sum() / e.abs().sum().clamp_min(1e-300)),
+        stats[6 if prec else 0] = (float((e * ref.sign()).sum() / e.abs().sum().clamp_min(1e-300)),
                        float(e.norm() / ref.norm().clamp_min(1e-300)))
     lay = ("T" if at else "N") + ("T" if bt else "N")
-    tag = f"{lay} {M}x{N}x{K}" + (" ar" if ar is not None else "") + (" br" if br is not None else "")
+    tag = f"{lay} {M}x{N}x{K}" + (" ar" if ar is not None else "") + (" br" if br is not None else "") \
+        + (" two-level" if xprec == 5 else "")
     amax = float(Am.abs().max())
     amin = float(Am[Am != 0].abs().min()) if bool((Am != 0).any()) else 0.0
     bmax = float(Bm.abs().max())
@@ -82,9 +83,9 @@ def main():
 
     def hooked(A, B, Cm, M, N, K, **kw):
         prec = ops._prec if kw.get("prec") is None else kw["prec"]
-        if prec == 6 and M * N * K >= 10 ** 8 and min(M, N) >= 128:
+        if prec in (5, 6) and M * N * K >= 10 ** 8 and min(M, N) >= 128:
             torch.cuda.synchronize()
-            audit(orig, A, B, Cm, M, N, K, kw)
+            audit(orig, A, B, Cm, M, N, K, kw, prec)
         return orig(A, B, Cm, M, N, K, **kw)
     ops.gemm = hooked
     model.train()
