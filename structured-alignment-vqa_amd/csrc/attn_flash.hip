@@ -110,6 +110,188 @@ __device__ __forceinline__ void fl_accum(const float* img, const float* Ys, int 
   }
 }
 
+// ------------------------------------------------------------- x6 products (SAVQA_FLASH_X6)
+// The same kernels with every product on v_mfma_f32_16x16x32_bf16 over exact three-term bf16
+// splits (the x6 GEMM's scheme, gemm_x6.hip: a = a0 + a1 + a2 truncated, six of the nine
+// partial products, each exact in the fp32 accumulator): 96 bf16 MFMAs of 16 cycles where the
+// fp32 16x16x4 form takes 128 of 32 per staged tile and wave. Every product is computed
+// "swapped" -- the per-lane strip (the wave's 16 queries, or keys) is the B operand and the
+// staged tile the A operand -- so the score tile comes out with the strip on the lanes and 16
+// tile rows in registers: the online softmax reduces over registers and the 4 lane groups, and
+// the following product (P V, dS K, ...) that sums over those rows takes the registers as its
+// B operand with no LDS round trip. Its A operand (the staged tile, transposed) comes from
+// ds_read_b64_tr_b16 reads of the same row-major bf16 planes the score product reads by rows.
+#ifndef SAVQA_FLASH_X6
+#define SAVQA_FLASH_X6 1
+#endif
+#ifndef SAVQA_FX_WPE_Q
+#define SAVQA_FX_WPE_Q 3   // waves per SIMD the dQ / dK dV kernels are built for
+#endif
+#ifndef SAVQA_FX_WPE_KV
+#define SAVQA_FX_WPE_KV 2
+#endif
+typedef __bf16 fx_bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 fx_bf4 __attribute__((ext_vector_type(4)));
+typedef short fx_s4 __attribute__((ext_vector_type(4)));
+constexpr int FX_ROWB = 128;               // bytes per staged row and plane (64 bf16)
+constexpr int FX_PLANE = FL_KT * FX_ROWB;  // 8 KB
+constexpr int FX_TILE = 3 * FX_PLANE;      // one staged 64 x 64 tile: 24 KB
+
+// Tile rows on the MFMA rows: row m = 4g + r of score block jt is tile row 16g + 4jt + r, so
+// a lane group's registers cover 16 consecutive tile rows (16-B graph / flag loads) and the
+// following product's k step s takes rows 16g + 8s .. +7.
+__device__ __forceinline__ int fx_trow(int jt, int m) { return 16 * (m >> 2) + 4 * jt + (m & 3); }
+// byte offset of (row, d) in a plane: 16-B chunk d / 8 XORed with row bits (5, 1, 4), so the
+// ds_read_b128 row reads (16 lanes: rows fx_trow(jt, 0..15)) and the transposed reads (a
+// 32-lane half: rows 16g + 8s + 4h + 0..3 for two g) hit distinct banks
+__device__ __forceinline__ int fx_off(int row, int d) {
+  const int f = ((row >> 5) & 1) | (((row >> 1) & 1) << 1) | (((row >> 4) & 1) << 2);
+  return row * FX_ROWB + ((((d >> 3) ^ f) & 7) << 4) + ((d & 7) << 1);
+}
+
+// exact truncation split of 4 fp32 values into three bf16 terms (gemm_x6.hip split3)
+__device__ __forceinline__ void fx_split4(f4v v, fx_bf4& p0, fx_bf4& p1, fx_bf4& p2) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  uint32_t t[3][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    f2 x = f2{v[2 * h], v[2 * h + 1]};
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const uint32_t ux = __float_as_uint(x[0]), uy = __float_as_uint(x[1]);
+      t[p][h] = __builtin_amdgcn_perm(uy, ux, 0x07060302u);
+      if (p < 2) x = x - f2{__uint_as_float(ux & 0xffff0000u), __uint_as_float(uy & 0xffff0000u)};
+    }
+  }
+  p0 = __builtin_bit_cast(fx_bf4, u2{t[0][0], t[0][1]});
+  p1 = __builtin_bit_cast(fx_bf4, u2{t[1][0], t[1][1]});
+  p2 = __builtin_bit_cast(fx_bf4, u2{t[2][0], t[2][1]});
+}
+__device__ __forceinline__ fx_bf8 fx_cat(fx_bf4 lo, fx_bf4 hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// 8 fp32 values -> three bf16x8 terms
+__device__ __forceinline__ void fx_split8(f4v lo, f4v hi, fx_bf8 (&p)[3]) {
+  fx_bf4 a[3], b[3];
+  fx_split4(lo, a[0], a[1], a[2]);
+  fx_split4(hi, b[0], b[1], b[2]);
+#pragma unroll
+  for (int t = 0; t < 3; ++t) p[t] = fx_cat(a[t], b[t]);
+}
+__device__ __forceinline__ f4v fx_mfma(fx_bf8 a, fx_bf8 b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// c += A B over one 32-wide k step from split operands, the small products first
+__device__ __forceinline__ f4v fx_mfma6(const fx_bf8 (&a)[3], const fx_bf8 (&b)[3], f4v c) {
+  c = fx_mfma(a[2], b[0], c);
+  c = fx_mfma(a[1], b[1], c);
+  c = fx_mfma(a[0], b[2], c);
+  c = fx_mfma(a[1], b[0], c);
+  c = fx_mfma(a[0], b[1], c);
+  return fx_mfma(a[0], b[0], c);
+}
+
+// Cooperative stage of rows [r0, r0 + 64) of X and Y into LDS as three bf16 planes each
+// (fx_off layout), zero past lim: thread t splits 16-B chunk t % 16 of rows t / 16 + 4 nw p.
+__device__ __forceinline__ void fx_stage2(const BView& X, const BView& Y, int r0, int lim,
+                                          char* Xs, char* Ys) {
+  const int t = threadIdx.x, rstep = blockDim.x >> 4;
+  const uint32_t xvo = (uint32_t)(t >> 4) * X.ld + 16u * (t & 15);
+  const uint32_t yvo = (uint32_t)(t >> 4) * Y.ld + 16u * (t & 15);
+  for (int p0 = 0; p0 < FL_KT; p0 += 4 * rstep) {
+    f4v xv[4], yv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t row = (uint32_t)(r0 + p0 + u * rstep);
+      xv[u] = bld16b<f4v>(X, xvo, row * X.ld);
+      yv[u] = bld16b<f4v>(Y, yvo, row * Y.ld);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = p0 + u * rstep + (t >> 4);
+      if (j < FL_KT) {
+        const bool ok = r0 + j < lim;
+        const f4v z = {0.f, 0.f, 0.f, 0.f};
+        const int off = fx_off(j, 4 * (t & 15));
+        fx_bf4 a0, a1, a2;
+        fx_split4(ok ? xv[u] : z, a0, a1, a2);
+        *reinterpret_cast<fx_bf4*>(Xs + off) = a0;
+        *reinterpret_cast<fx_bf4*>(Xs + FX_PLANE + off) = a1;
+        *reinterpret_cast<fx_bf4*>(Xs + 2 * FX_PLANE + off) = a2;
+        fx_split4(ok ? yv[u] : z, a0, a1, a2);
+        *reinterpret_cast<fx_bf4*>(Ys + off) = a0;
+        *reinterpret_cast<fx_bf4*>(Ys + FX_PLANE + off) = a1;
+        *reinterpret_cast<fx_bf4*>(Ys + 2 * FX_PLANE + off) = a2;
+      }
+    }
+  }
+}
+
+// the lane's strip row as the B operand: X[row][32s + 8g .. +7], split (s = 0, 1)
+__device__ __forceinline__ void fx_load_strip(const BView& X, int row, int g, fx_bf8 (&xp)[2][3]) {
+  const uint32_t vo = (uint32_t)row * X.ld + 32u * g;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    fx_split8(bld16b<f4v>(X, vo, 128u * s), bld16b<f4v>(X, vo, 128u * s + 16u), xp[s]);
+}
+
+// acc[jt][r] = sum_d T[16g + 4jt + r][d] * strip[col][d]: the staged tile's rows
+// against the lane strip (A = tile rows by ds_read_b128, B = the strip's planes)
+template <int NJT>
+__device__ __forceinline__ void fx_dots(const char* Ts, const fx_bf8 (&xp)[2][3], int col, int g,
+                                        f4v (&acc)[NJT]) {
+#pragma unroll
+  for (int jt = 0; jt < NJT; ++jt) {
+    const int row = fx_trow(jt, col);
+    f4v c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int off = fx_off(row, 32 * s + 8 * g);
+      fx_bf8 a[3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) a[t] = *reinterpret_cast<const fx_bf8*>(Ts + t * FX_PLANE + off);
+      c = fx_mfma6(a, xp[s], c);
+    }
+    acc[jt] = c;
+  }
+}
+
+// 4 bf16 of column (lane % 16) of 4 tile rows, by the transposed read (T10): the lane
+// supplies row `row`, columns d .. d + 3
+__device__ __forceinline__ fx_bf4 fx_tr(const char* base, int off) {
+  typedef __attribute__((address_space(3))) fx_s4 lds_s4;
+  const fx_s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(const_cast<char*>(base) + off));
+  return __builtin_bit_cast(fx_bf4, v);
+}
+
+// o[dt][r] += sum over the tile's 64 rows j: T[j][16 dt + 4g + r] * w[j]  -- i.e. the
+// transposed tile (A, by transposed reads) times the lane's per-row weights w (B: element j of
+// k step s = w[2s + j / 4][j % 4], the registers of a preceding fx_dots tile (rows
+// 16g + 8s + j), split here)
+// one k step s of fx_accum: rows 16g + 8s .. +7, weights w0 (rows +0..3), w1 (+4..7)
+__device__ __forceinline__ void fx_accum_s(const char* Ts, f4v w0, f4v w1, int s, int lane,
+                                           f4v (&o)[4]) {
+  const int g = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
+  const int rl = 16 * g + 8 * s + qq;
+  fx_bf8 b[3];
+  fx_split8(w0, w1, b);
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int o0 = fx_off(rl, 16 * dt + 4 * p);
+    const int o1 = fx_off(rl + 4, 16 * dt + 4 * p);
+    fx_bf8 a[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+      a[t] = fx_cat(fx_tr(Ts + t * FX_PLANE, o0), fx_tr(Ts + t * FX_PLANE, o1));
+    o[dt] = fx_mfma6(a, b, o[dt]);
+  }
+}
+__device__ __forceinline__ void fx_accum(const char* Ts, const f4v (&w)[4], int lane, f4v (&o)[4]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) fx_accum_s(Ts, w[2 * s], w[2 * s + 1], s, lane, o);
+}
+
 // ---------------------------------------------------------------------------------- fwd
 // grid = B*H*nqt, block = 64*nw (wave w: query strip qt*16nw + 16w). Scores run in base 2
 // (attn_common.h ATT_SCALE2): m and every exponent below are log2-scaled, in all four kernels.
@@ -206,6 +388,105 @@ __global__ __launch_bounds__(256) void gattn_fwd_flash_kernel(AttnArgs a, float*
         st[1] = Z[r];
         st[2] = W[r];
       }
+    }
+  }
+}
+
+// x6 form of the forward (see "x6 products" above): lane (col, g) of wave w owns query
+// i0 + col; its registers hold the tile's keys 16g + 4jt + r, so the row statistics
+// reduce over 16 registers and the 4 lane groups, and O^T[d][q] accumulates in o[dt][r]
+// (d = 16 dt + 4g + r).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gattn_fwd_flash_x6_kernel(AttnArgs a, float* __restrict__ stats,
+                                                                int nqt) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int nw = blockDim.x >> 6;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = bid % nqt, bh = bid / nqt;
+  const int b = bh / a.H, h = bh % a.H;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = qt * 16 * nw + w * 16;
+  char* Ks = reinterpret_cast<char*>(sm);
+  char* Vs = Ks + FX_TILE;
+  const StripViews<AttnArgs> sv(a, b, h);
+
+  fx_bf8 qp[2][3];
+  fx_load_strip(sv.q, i0 + col, g, qp);
+  float m = -INFINITY, Z = 0.f, W = 0.f;
+  f4v o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f4v{0.f, 0.f, 0.f, 0.f};
+  const uint32_t gvo = (uint32_t)((i0 + col) * a.Tk + 16 * g) * 4u;
+  const int nkt = (a.Tk + FL_KT - 1) / FL_KT;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * FL_KT;
+    __syncthreads();  // every wave is done with the previous tile
+    f4v gv[4];
+    uint32_t kmask = 0;  // bit 4 jt + r: key masked (kflag 0)
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) {
+      const uint32_t so = (uint32_t)(k0 + 4 * jt) * 4u;
+      const f4v kf = bld16b<f4v>(sv.kf, 64u * g, so);
+      gv[jt] = bld16b<f4v>(sv.g, gvo, so);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) kmask |= (kf[r] == 0.f ? 1u : 0u) << (4 * jt + r);
+    }
+    fx_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
+    __syncthreads();
+    f4v s[4];
+    fx_dots<4>(Ks, qp, col, g, s);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = k0 + 16 * g + 4 * jt + r;
+        float v = -INFINITY;
+        if (j < a.Tk) v = (kmask >> (4 * jt + r)) & 1u ? ATT_MASKED : s[jt][r] * ATT_SCALE2;
+        s[jt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mn = fmaxf(m, mx);  // finite: every tile holds a key < Tk
+    const float alpha = att_exp2(m - mn);
+    float zs = 0.f, ws = 0.f;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = k0 + 16 * g + 4 * jt + r;
+        const float e = j < a.Tk ? att_exp2(s[jt][r] - mn) : 0.f;
+        const float gg = j < a.Tk ? gv[jt][r] : 0.f;
+        zs += e;
+        ws += e * fabsf(gg);
+        s[jt][r] = e * gg;
+      }
+    zs += __shfl_xor(zs, 16);
+    zs += __shfl_xor(zs, 32);
+    ws += __shfl_xor(ws, 16);
+    ws += __shfl_xor(ws, 32);
+    Z = Z * alpha + zs;
+    W = W * alpha + ws;
+    m = mn;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+    fx_accum(Vs, s, lane, o);
+  }
+  const int i = i0 + col;
+  if (i < a.Tq) {
+    const int64_t qb = (int64_t)b * a.Tq;
+    const BView O = head_view(a.o, a.ldo, (int64_t)a.B * a.Tq, qb, h * ATT_DK);
+    const float D = fmaxf(W, 1e-12f * Z);
+    const float sc = bld1(sv.qf, 4u * i, 0u) / D;
+    const uint32_t ovo = (uint32_t)i * O.ld + 16u * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) bst16b(O, o[dt] * sc, ovo, 64u * dt);
+    if (g == 0) {
+      float* st = stats + (((int64_t)b * a.H + h) * a.Tq + i) * 4;
+      st[0] = m;
+      st[1] = Z;
+      st[2] = W;
     }
   }
 }
@@ -538,6 +819,273 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   }
 }
 
+// ---------------------------------------------------------------- x6 backward kernels
+// The three backward kernels above with x6 products (see "x6 products"): identical math per
+// (query, key) pair; the strips on the lanes (queries for delta / dQ, keys for dK / dV), the
+// staged tile's rows in registers.
+
+// graph / key-flag values of the lane's query (row q of the sample) for the tile's keys
+// k0 + 16g + 4jt + r (16-B loads; reads past T come back as neighbouring or zero values and are
+// masked by the callers)
+__device__ __forceinline__ void fx_graph_row(const BView& G, const BView& KF, uint32_t gvo,
+                                             int k0, int g, f4v (&gv)[4], uint32_t& kmask) {
+  kmask = 0;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) {
+    const uint32_t so = (uint32_t)(k0 + 4 * jt) * 4u;
+    const f4v kf = bld16b<f4v>(KF, 64u * g, so);
+    gv[jt] = bld16b<f4v>(G, gvo, so);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) kmask |= (kf[r] == 0.f ? 1u : 0u) << (4 * jt + r);
+  }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gattn_bwd_delta_flash_x6_kernel(
+    AttnArgs a, float* __restrict__ stats, int nqt) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int nw = blockDim.x >> 6;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = bid % nqt, bh = bid / nqt;
+  const int b = bh / a.H, h = bh % a.H;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = qt * 16 * nw + w * 16;
+  char* Ks = reinterpret_cast<char*>(sm);
+  char* Vs = Ks + FX_TILE;
+  const int64_t qb = (int64_t)b * a.Tq;
+  const int hd = h * ATT_DK;
+  const float* sth = stats + ((int64_t)b * a.H + h) * a.Tq * 4;
+  const StripViews<AttnArgs> sv(a, b, h);
+  const BView DO = head_view(a.dout, a.lddo, (int64_t)a.B * a.Tq, qb, h * ATT_DK);
+
+  fx_bf8 qp[2][3], op[2][3];
+  fx_load_strip(sv.q, i0 + col, g, qp);
+  fx_load_strip(DO, i0 + col, g, op);
+  const int i = i0 + col;
+  const int ic = min(i, a.Tq - 1);
+  const RowCoef rc = row_coef(sth + (int64_t)ic * 4, a.qflag[qb + ic], i < a.Tq);
+  const uint32_t gvo = (uint32_t)(i * a.Tk + 16 * g) * 4u;
+  double sa = 0., sw = 0., sz = 0.;
+  const int nkt = (a.Tk + FL_KT - 1) / FL_KT;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * FL_KT;
+    __syncthreads();
+    f4v gv[4];
+    uint32_t kmask;
+    fx_graph_row(sv.g, sv.kf, gvo, k0, g, gv, kmask);
+    fx_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
+    __syncthreads();
+    f4v s[4], dp[4];
+    fx_dots<4>(Ks, qp, col, g, s);   // [key 16g + 4jt + r][query col]
+    fx_dots<4>(Vs, op, col, g, dp);
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = k0 + 16 * g + 4 * jt + r;
+        const float x = (kmask >> (4 * jt + r)) & 1u ? ATT_MASKED : s[jt][r] * ATT_SCALE2;
+        const float e = j < a.Tk ? att_exp2(x - rc.m) : 0.f;
+        const float gg = j < a.Tk ? gv[jt][r] : 0.f;
+        sa += (double)(e * gg * rc.qf * dp[jt][r]);
+        sw += (double)(e * fabsf(gg));
+        sz += (double)e;
+      }
+  }
+  double A = sa, Wd = sw, Zd = sz;
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) {
+    A += __shfl_xor(A, o);
+    Wd += __shfl_xor(Wd, o);
+    Zd += __shfl_xor(Zd, o);
+  }
+  if (i < a.Tq && g == 0) {
+    const float wf = (float)Wd, zf = (float)Zd;
+    const bool normal = wf >= 1e-12f * zf;
+    const float rD = 1.f / (normal ? wf : 1e-12f * zf);
+    const double den = normal ? Wd : Zd;
+    const double dx = den > 0. ? A / den : 0.;
+    float* st = stats + (((int64_t)b * a.H + h) * a.Tq + i) * 4;
+    st[1] = zf;
+    st[2] = wf;
+    st[3] = normal ? (float)dx : (float)(dx * (double)rD * Zd);
+    const float hi = (float)dx;
+    float* dxs = a.dq + (qb + i) * a.lddq + hd;
+    dxs[0] = hi;
+    dxs[1] = (float)(dx - (double)hi);
+  }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAVQA_FX_WPE_Q))) void gattn_bwd_q_flash_x6_kernel(
+    AttnArgs a, const float* __restrict__ stats, int nqt) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int nw = blockDim.x >> 6;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = bid % nqt, bh = bid / nqt;
+  const int b = bh / a.H, h = bh % a.H;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = qt * 16 * nw + w * 16;
+  char* Ks = reinterpret_cast<char*>(sm);
+  char* Vs = Ks + FX_TILE;
+  const int64_t qb = (int64_t)b * a.Tq;
+  const int hd = h * ATT_DK;
+  const float* sth = stats + ((int64_t)b * a.H + h) * a.Tq * 4;
+  const StripViews<AttnArgs> sv(a, b, h);
+  const BView DO = head_view(a.dout, a.lddo, (int64_t)a.B * a.Tq, qb, h * ATT_DK);
+
+  fx_bf8 qp[2][3], op[2][3];
+  fx_load_strip(sv.q, i0 + col, g, qp);
+  fx_load_strip(DO, i0 + col, g, op);
+  const int i = i0 + col;
+  const int ic = min(i, a.Tq - 1);
+  const RowCoef c = row_coef(sth + (int64_t)ic * 4, a.qflag[qb + ic], i < a.Tq);
+  const float* dxs = a.dq + (qb + ic) * a.lddq + hd;
+  const double dx = i < a.Tq ? (double)dxs[0] + (double)dxs[1] : 0.;
+  const uint32_t gvo = (uint32_t)(i * a.Tk + 16 * g) * 4u;
+  f4v dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dq[dt] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int nkt = (a.Tk + FL_KT - 1) / FL_KT;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * FL_KT;
+    __syncthreads();
+    f4v gv[4];
+    uint32_t kmask;
+    fx_graph_row(sv.g, sv.kf, gvo, k0, g, gv, kmask);
+    fx_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
+    __syncthreads();
+    f4v s[4], dp[4];
+    fx_dots<4>(Ks, qp, col, g, s);
+    fx_dots<4>(Vs, op, col, g, dp);
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = k0 + 16 * g + 4 * jt + r;
+        const bool masked = (kmask >> (4 * jt + r)) & 1u;
+        const float x = masked ? ATT_MASKED : s[jt][r] * ATT_SCALE2;
+        const float e = j < a.Tk ? att_exp2(x - c.m) : 0.f;
+        const float gg = j < a.Tk ? gv[jt][r] : 0.f;
+        const float av = e * gg * c.qf * dp[jt][r];
+        const float wv = c.normal ? e * fabsf(gg) : e;
+        const float ds = (float)((double)av - dx * (double)wv) * c.rD;
+        s[jt][r] = (masked || j >= a.Tk) ? 0.f : ds;
+      }
+    fx_accum(Ks, s, lane, dq);  // dQ_i += sum_j dS_ij K_j   (x 1/8 at the end)
+  }
+  if (i < a.Tq) {
+    const int64_t row = qb + i;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int cc = hd + dt * 16 + 4 * g + r;
+        a.dq[row * a.lddq + cc] = a.q[row * a.ldq + cc] > 0.f ? dq[dt][r] * 0.125f : 0.f;
+      }
+  }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAVQA_FX_WPE_KV))) void gattn_bwd_kv_flash_x6_kernel(
+    AttnArgs a, const float* __restrict__ stats, int nkt2) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int nw = blockDim.x >> 6;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kt = bid % nkt2, bh = bid / nkt2;
+  const int b = bh / a.H, h = bh % a.H;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int j0 = kt * 16 * nw + w * 16;
+  char* Qs = reinterpret_cast<char*>(sm);
+  char* dOs = Qs + FX_TILE;
+  float* cf = reinterpret_cast<float*>(dOs + FX_TILE);  // [64][8] per-query coefficients
+  const int64_t qb = (int64_t)b * a.Tq, kb = (int64_t)b * a.Tk;
+  const float* sth = stats + ((int64_t)b * a.H + h) * a.Tq * 4;
+  const StripViews<AttnArgs> sv(a, b, h);
+  const BView DO = head_view(a.dout, a.lddo, (int64_t)a.B * a.Tq, qb, h * ATT_DK);
+
+  const int j = j0 + col;  // the lane's key
+  fx_bf8 kp[2][3], vp[2][3];
+  fx_load_strip(sv.k, j, g, kp);
+  fx_load_strip(sv.v, j, g, vp);
+  const bool kval = j < a.Tk;
+  const bool kmasked = bld1(sv.kf, 4u * j, 0u) == 0.f;
+  f4v dk[4], dv[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f4v{0.f, 0.f, 0.f, 0.f};
+  const uint32_t gvo = (uint32_t)(16 * g * a.Tk + j) * 4u;
+  const int nqt = (a.Tq + FL_KT - 1) / FL_KT;
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int iq0 = qt * FL_KT;
+    __syncthreads();
+    float gv[4][4];  // G[query iq0 + 16g + 4jt + r][key j]
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        gv[jt][r] = bld1(sv.g, gvo, (uint32_t)((iq0 + 4 * jt + r) * a.Tk) * 4u);
+    fx_stage2(sv.q, DO, iq0, a.Tq, Qs, dOs);
+    if (threadIdx.x < FL_KT) {
+      const int iq = iq0 + threadIdx.x;
+      const bool valid = iq < a.Tq;
+      const int icl = min(iq, a.Tq - 1);
+      RowCoef c = row_coef(sth + (int64_t)icl * 4, a.qflag[qb + icl], valid);
+      if (valid) coef_delta(c, sth[(int64_t)icl * 4 + 3]);
+      float* cp = cf + threadIdx.x * 8;
+      cp[0] = c.m;
+      cp[1] = c.rD;
+      cp[2] = c.qf;
+      cp[3] = c.cd;
+      cp[4] = c.pd;
+    }
+    __syncthreads();
+    f4v s[4], dp[4];
+    fx_dots<4>(Qs, kp, col, g, s);    // [query 16g + 4jt + r][key col]
+    fx_dots<4>(dOs, vp, col, g, dp);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {  // queries 16g + 8 s2 .. +7: one k step of both products
+      f4v nv[2], dsv[2];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int jt = 2 * s2 + jj;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* cp = cf + (16 * g + 4 * jt + r) * 8;
+          const f4v c0 = ld4(cp);
+          const float pd = cp[4];
+          const float x = kmasked ? ATT_MASKED : s[jt][r] * ATT_SCALE2;
+          const float e = kval ? att_exp2(x - c0.x) : 0.f;
+          const float gg = gv[jt][r];
+          const float n = e * gg * c0.y;
+          nv[jj][r] = n * c0.z;
+          const float ds = n * c0.z * dp[jt][r] - c0.w * e * fabsf(gg) - pd * e;
+          dsv[jj][r] = kmasked ? 0.f : ds;
+        }
+      }
+      fx_accum_s(dOs, nv[0], nv[1], s2, lane, dv);  // dV_j += sum_i nq_ij dO_i
+      fx_accum_s(Qs, dsv[0], dsv[1], s2, lane, dk);  // dK_j += sum_i dS_ij Q_i   (x 1/8 at the end)
+    }
+  }
+  if (kval) {
+    const int64_t nk = (int64_t)a.B * a.Tk;
+    const BView DK = head_view(a.dk, a.lddk, nk, kb, h * ATT_DK);
+    const BView DV = head_view(a.dv, a.lddv, nk, kb, h * ATT_DK);
+    const uint32_t kvo = (uint32_t)j * sv.k.ld + 16u * g;
+    const uint32_t vvo = (uint32_t)j * sv.v.ld + 16u * g;
+    const uint32_t dkvo = (uint32_t)j * DK.ld + 16u * g;
+    const uint32_t dvvo = (uint32_t)j * DV.ld + 16u * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const f4v kx = bld16b<f4v>(sv.k, kvo, 64u * dt);
+      const f4v vx = bld16b<f4v>(sv.v, vvo, 64u * dt);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bst32(DK, kx[r] > 0.f ? dk[dt][r] * 0.125f : 0.f, dkvo, 64u * dt + 4u * r);
+        bst32(DV, vx[r] > 0.f ? dv[dt][r] : 0.f, dvvo, 64u * dt + 4u * r);
+      }
+    }
+  }
+}
+
 static int flash_validate(const AttnArgs& a, int64_t dk, const char* who) {
   if (dk != ATT_DK) return fail(SAVQA_EUNSUP, std::string(who) + ": head dim must be 64");
   if (a.Tk <= 0 || a.Tq <= 0 || a.B <= 0 || a.H <= 0)
@@ -549,6 +1097,14 @@ static int flash_validate(const AttnArgs& a, int64_t dk, const char* who) {
 }
 
 static int waves_for(int rows) { return rows >= 64 ? 4 : (rows + 15) / 16; }
+
+// the x6 kernels (SAVQA_FLASH_X6 at build time; SAVQA_FLASH_X6=0 in the environment selects
+// the fp32-MFMA kernels at run time, for A/B runs)
+static bool flash_x6() {
+  if (!SAVQA_FLASH_X6) return false;
+  const char* e = getenv("SAVQA_FLASH_X6");
+  return !(e && e[0] == '0');
+}
 
 }  // namespace savqa
 
@@ -567,6 +1123,11 @@ extern "C" int savqa_gattn_fwd_flash(void* stream, const float* q, int64_t ldq, 
   if (!stats) return fail(SAVQA_EINVAL, "savqa_gattn_fwd_flash: stats buffer required");
   const int nw = waves_for((int)Tq);
   const int nqt = (int)((Tq + 16 * nw - 1) / (16 * nw));
+  if (flash_x6()) {
+    hipLaunchKernelGGL(gattn_fwd_flash_x6_kernel, dim3((unsigned)(B * H * nqt)), dim3(64 * nw),
+                       (size_t)2 * FX_TILE, as_stream(stream), a, stats, nqt);
+    return check_launch("savqa_gattn_fwd_flash");
+  }
   const size_t lds = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + (size_t)nw * FL_KT * FL_WLD);
   hipLaunchKernelGGL(gattn_fwd_flash_kernel, dim3((unsigned)(B * H * nqt)), dim3(64 * nw), lds,
                      as_stream(stream), a, stats, nqt);
@@ -590,6 +1151,22 @@ extern "C" int savqa_gattn_bwd_flash(void* stream, const float* q, int64_t ldq, 
   if ((((uintptr_t)dout) & 15) || (lddo & 3))
     return fail(SAVQA_EINVAL, "savqa_gattn_bwd_flash: dO must be 16-B aligned, ld % 4 == 0");
   hipStream_t s = as_stream(stream);
+  if (flash_x6()) {
+    const int nw = waves_for((int)Tq);
+    const int nqt = (int)((Tq + 16 * nw - 1) / (16 * nw));
+    hipLaunchKernelGGL(gattn_bwd_delta_flash_x6_kernel, dim3((unsigned)(B * H * nqt)),
+                       dim3(64 * nw), (size_t)2 * FX_TILE, s, a, stats, nqt);
+    if (int rc = check_launch("savqa_gattn_bwd_flash(delta)")) return rc;
+    hipLaunchKernelGGL(gattn_bwd_q_flash_x6_kernel, dim3((unsigned)(B * H * nqt)), dim3(64 * nw),
+                       (size_t)2 * FX_TILE, s, a, stats, nqt);
+    if (int rc = check_launch("savqa_gattn_bwd_flash(dq)")) return rc;
+    const int nwk = waves_for((int)Tk);
+    const int nkt2 = (int)((Tk + 16 * nwk - 1) / (16 * nwk));
+    hipLaunchKernelGGL(gattn_bwd_kv_flash_x6_kernel, dim3((unsigned)(B * H * nkt2)),
+                       dim3(64 * nwk), (size_t)2 * FX_TILE + sizeof(float) * FL_KT * 8, s, a,
+                       stats, nkt2);
+    return check_launch("savqa_gattn_bwd_flash(dkv)");
+  }
   {  // delta (stats[..][3]) for the dK/dV pass and dx for the dQ pass, then dQ
     const int nw = waves_for((int)Tq);
     const int nqt = (int)((Tq + 16 * nw - 1) / (16 * nw));
