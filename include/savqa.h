@@ -327,6 +327,25 @@ int savqa_gattn_bwd_flash(void* stream, const float* q, int64_t ldq, const float
                           int64_t dk, const float* dout, int64_t lddo, float* stats, float* dq, int64_t lddq, float* dk_, int64_t lddk,
                           float* dv, int64_t lddv);
 
+/* The same two entry points with a caller-owned workspace (16-B aligned, at least
+ * savqa_gattn_flash_ws_bytes(B, Tq, Tk, H, backward) bytes; contents not preserved): the
+ * library first splits Q, K, V (and dO) of every (sample, head) into the x6 kernels' bf16 plane
+ * tiles there, so the attention kernels stage tiles by DMA instead of splitting them in every
+ * workgroup. Same results as without (bit-identical: the same splits meet the same MFMAs).
+ * ws = NULL: the kernels split in place, as savqa_gattn_{fwd,bwd}_flash. */
+int64_t savqa_gattn_flash_ws_bytes(int64_t B, int64_t Tq, int64_t Tk, int64_t H, int32_t backward);
+int savqa_gattn_fwd_flash_ws(void* stream, const float* q, int64_t ldq, const float* k,
+                             int64_t ldk, const float* v, int64_t ldv, const float* G,
+                             const float* kflag, const float* qflag, int64_t B, int64_t Tq,
+                             int64_t Tk, int64_t H, int64_t dk, float* o, int64_t ldo,
+                             float* stats, void* ws, int64_t ws_bytes);
+int savqa_gattn_bwd_flash_ws(void* stream, const float* q, int64_t ldq, const float* k,
+                             int64_t ldk, const float* v, int64_t ldv, const float* G,
+                             const float* kflag, const float* qflag, int64_t B, int64_t Tq,
+                             int64_t Tk, int64_t H, int64_t dk, const float* dout, int64_t lddo,
+                             float* stats, float* dq, int64_t lddq, float* dk_, int64_t lddk,
+                             float* dv, int64_t lddv, void* ws, int64_t ws_bytes);
+
 /* Single-query graph attention over long key sequences (T_q = 1: the decoder cross-attention
  * at T_k > 128, AttModel_x3.py:279 -> modules.py:236-311), split over keys so every wave takes
  * 64 keys of one (sample, head): same operator, layouts and ReLU-masked gradients as

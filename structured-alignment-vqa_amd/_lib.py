@@ -130,6 +130,12 @@ _SIGS = {
                               c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p,
                               c_p, c_i64, c_p, c_i64, c_p, c_i64],
     "savqa_gattn_q1s_ws_bytes": [c_i64, c_i64, c_i64],
+    "savqa_gattn_flash_ws_bytes": [c_i64, c_i64, c_i64, c_i64, c_i32],
+    "savqa_gattn_fwd_flash_ws": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
+                                 c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64],
+    "savqa_gattn_bwd_flash_ws": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
+                                 c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p,
+                                 c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64],
     "savqa_gattn_fwd_q1s": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i64,
                             c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64],
     "savqa_gattn_bwd_q1s": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i64,
@@ -178,7 +184,8 @@ _SIGS = {
 }
 
 _I64_RET = {"savqa_ln_bwd_workspace_bytes", "savqa_gemm_ws_elems", "savqa_gattn_q1s_ws_bytes",
-            "savqa_rel_loss_ws_bytes", "savqa_gemm_lp_ws_elems", "savqa_x6_weight_planes_bytes"}
+            "savqa_rel_loss_ws_bytes", "savqa_gemm_lp_ws_elems", "savqa_x6_weight_planes_bytes",
+            "savqa_gattn_flash_ws_bytes"}
 
 _lib = None
 

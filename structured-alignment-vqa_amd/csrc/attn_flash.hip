@@ -130,6 +130,9 @@ __device__ __forceinline__ void fl_accum(const float* img, const float* Ys, int 
 #ifndef SAVQA_FX_WPE_KV
 #define SAVQA_FX_WPE_KV 2
 #endif
+#ifndef SAVQA_FX_WPE_KVP
+#define SAVQA_FX_WPE_KVP 2  // the pre-split (planes) dK / dV kernel (3: 39 VGPRs spilled)
+#endif
 typedef __bf16 fx_bf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 fx_bf4 __attribute__((ext_vector_type(4)));
 typedef short fx_s4 __attribute__((ext_vector_type(4)));
@@ -234,6 +237,51 @@ __device__ __forceinline__ void fx_load_strip(const BView& X, int row, int g, fx
 #pragma unroll
   for (int s = 0; s < 2; ++s)
     fx_split8(bld16b<f4v>(X, vo, 128u * s), bld16b<f4v>(X, vo, 128u * s + 16u), xp[s]);
+}
+
+// Pre-split operands (savqa_gattn_*_flash_ws): Q / K / V / dO of every (sample, head) split
+// ONCE into bf16 plane tiles in global memory, in exactly the LDS image layout above -- tile t
+// of (b, h) at ((b H + h) nt + t) FX_TILE bytes, rows past T zero -- so the kernels stage a tile
+// with 16-B LDS-DMAs (no split VALU, no registers; every query tile's workgroup used to re-split
+// the same K / V tiles) and read their strips' planes directly.
+struct FxPlanes {
+  const char* q;
+  const char* k;
+  const char* v;
+  const char* dout;
+  int ntq, ntk;  // tiles per (sample, head) of the query / key operands
+};
+typedef __attribute__((address_space(3))) void fx_lds_void;
+__device__ __forceinline__ void fx_dma16(const void* src, char* dst) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(fx_lds_void*)dst);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
+}
+// DMA two pre-split tiles into LDS: wave w copies 1-KB chunks w, w + nw, ... of each; the
+// caller's __syncthreads follows
+__device__ __forceinline__ void fx_stage_dma(const char* x, const char* y, char* Xs, char* Ys,
+                                             int w, int nw, int lane) {
+  for (int c = w; c < FX_TILE / 1024; c += nw) {
+    fx_dma16(x + c * 1024 + lane * 16, Xs + c * 1024);
+    fx_dma16(y + c * 1024 + lane * 16, Ys + c * 1024);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// the lane's strip row from pre-split tiles (tiles: the (sample, head)'s first tile)
+__device__ __forceinline__ void fx_strip_planes(const char* tiles, int row, int g,
+                                                fx_bf8 (&xp)[2][3]) {
+  const char* tb = tiles + (int64_t)(row >> 6) * FX_TILE;
+  const int r = row & 63;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+      xp[s][t] = *reinterpret_cast<const fx_bf8*>(tb + t * FX_PLANE + fx_off(r, 32 * s + 8 * g));
+}
+__device__ __forceinline__ const char* fx_tiles(const char* base, int b, int H, int h, int nt) {
+  return base + ((int64_t)b * H + h) * nt * (int64_t)FX_TILE;
 }
 
 // acc[jt][r] = sum_d T[16g + 4jt + r][d] * strip[col][d]: the staged tile's rows
@@ -396,8 +444,9 @@ __global__ __launch_bounds__(256) void gattn_fwd_flash_kernel(AttnArgs a, float*
 // i0 + col; its registers hold the tile's keys 16g + 4jt + r, so the row statistics
 // reduce over 16 registers and the 4 lane groups, and O^T[d][q] accumulates in o[dt][r]
 // (d = 16 dt + 4g + r).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gattn_fwd_flash_x6_kernel(AttnArgs a, float* __restrict__ stats,
-                                                                int nqt) {
+template <bool PL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gattn_fwd_flash_x6_kernel(
+    AttnArgs a, float* __restrict__ stats, int nqt, FxPlanes pl) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int nw = blockDim.x >> 6;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -411,7 +460,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const StripViews<AttnArgs> sv(a, b, h);
 
   fx_bf8 qp[2][3];
-  fx_load_strip(sv.q, i0 + col, g, qp);
+  if constexpr (PL) fx_strip_planes(fx_tiles(pl.q, b, a.H, h, pl.ntq), i0 + col, g, qp);
+  else fx_load_strip(sv.q, i0 + col, g, qp);
   float m = -INFINITY, Z = 0.f, W = 0.f;
   f4v o[4];
 #pragma unroll
@@ -431,7 +481,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
 #pragma unroll
       for (int r = 0; r < 4; ++r) kmask |= (kf[r] == 0.f ? 1u : 0u) << (4 * jt + r);
     }
-    fx_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
+    if constexpr (PL)
+      fx_stage_dma(fx_tiles(pl.k, b, a.H, h, pl.ntk) + (int64_t)kt * FX_TILE,
+                   fx_tiles(pl.v, b, a.H, h, pl.ntk) + (int64_t)kt * FX_TILE, Ks, Vs, w, nw, lane);
+    else
+      fx_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
     __syncthreads();
     f4v s[4];
     fx_dots<4>(Ks, qp, col, g, s);
@@ -840,8 +894,9 @@ __device__ __forceinline__ void fx_graph_row(const BView& G, const BView& KF, ui
   }
 }
 
+template <bool PL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gattn_bwd_delta_flash_x6_kernel(
-    AttnArgs a, float* __restrict__ stats, int nqt) {
+    AttnArgs a, float* __restrict__ stats, int nqt, FxPlanes pl) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int nw = blockDim.x >> 6;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -859,8 +914,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const BView DO = head_view(a.dout, a.lddo, (int64_t)a.B * a.Tq, qb, h * ATT_DK);
 
   fx_bf8 qp[2][3], op[2][3];
-  fx_load_strip(sv.q, i0 + col, g, qp);
-  fx_load_strip(DO, i0 + col, g, op);
+  if constexpr (PL) {
+    fx_strip_planes(fx_tiles(pl.q, b, a.H, h, pl.ntq), i0 + col, g, qp);
+    fx_strip_planes(fx_tiles(pl.dout, b, a.H, h, pl.ntq), i0 + col, g, op);
+  } else {
+    fx_load_strip(sv.q, i0 + col, g, qp);
+    fx_load_strip(DO, i0 + col, g, op);
+  }
   const int i = i0 + col;
   const int ic = min(i, a.Tq - 1);
   const RowCoef rc = row_coef(sth + (int64_t)ic * 4, a.qflag[qb + ic], i < a.Tq);
@@ -873,7 +933,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
     f4v gv[4];
     uint32_t kmask;
     fx_graph_row(sv.g, sv.kf, gvo, k0, g, gv, kmask);
-    fx_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
+    if constexpr (PL)
+      fx_stage_dma(fx_tiles(pl.k, b, a.H, h, pl.ntk) + (int64_t)kt * FX_TILE,
+                   fx_tiles(pl.v, b, a.H, h, pl.ntk) + (int64_t)kt * FX_TILE, Ks, Vs, w, nw, lane);
+    else
+      fx_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
     __syncthreads();
     f4v s[4], dp[4];
     fx_dots<4>(Ks, qp, col, g, s);   // [key 16g + 4jt + r][query col]
@@ -915,8 +979,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   }
 }
 
+template <bool PL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAVQA_FX_WPE_Q))) void gattn_bwd_q_flash_x6_kernel(
-    AttnArgs a, const float* __restrict__ stats, int nqt) {
+    AttnArgs a, const float* __restrict__ stats, int nqt, FxPlanes pl) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int nw = blockDim.x >> 6;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -934,8 +999,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAVQA_FX_WP
   const BView DO = head_view(a.dout, a.lddo, (int64_t)a.B * a.Tq, qb, h * ATT_DK);
 
   fx_bf8 qp[2][3], op[2][3];
-  fx_load_strip(sv.q, i0 + col, g, qp);
-  fx_load_strip(DO, i0 + col, g, op);
+  if constexpr (PL) {
+    fx_strip_planes(fx_tiles(pl.q, b, a.H, h, pl.ntq), i0 + col, g, qp);
+    fx_strip_planes(fx_tiles(pl.dout, b, a.H, h, pl.ntq), i0 + col, g, op);
+  } else {
+    fx_load_strip(sv.q, i0 + col, g, qp);
+    fx_load_strip(DO, i0 + col, g, op);
+  }
   const int i = i0 + col;
   const int ic = min(i, a.Tq - 1);
   const RowCoef c = row_coef(sth + (int64_t)ic * 4, a.qflag[qb + ic], i < a.Tq);
@@ -952,7 +1022,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAVQA_FX_WP
     f4v gv[4];
     uint32_t kmask;
     fx_graph_row(sv.g, sv.kf, gvo, k0, g, gv, kmask);
-    fx_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
+    if constexpr (PL)
+      fx_stage_dma(fx_tiles(pl.k, b, a.H, h, pl.ntk) + (int64_t)kt * FX_TILE,
+                   fx_tiles(pl.v, b, a.H, h, pl.ntk) + (int64_t)kt * FX_TILE, Ks, Vs, w, nw, lane);
+    else
+      fx_stage2(sv.k, sv.v, k0, a.Tk, Ks, Vs);
     __syncthreads();
     f4v s[4], dp[4];
     fx_dots<4>(Ks, qp, col, g, s);
@@ -985,8 +1059,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAVQA_FX_WP
   }
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAVQA_FX_WPE_KV))) void gattn_bwd_kv_flash_x6_kernel(
-    AttnArgs a, const float* __restrict__ stats, int nkt2) {
+template <bool PL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PL ? SAVQA_FX_WPE_KVP : SAVQA_FX_WPE_KV))) void gattn_bwd_kv_flash_x6_kernel(
+    AttnArgs a, const float* __restrict__ stats, int nkt2, FxPlanes pl) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int nw = blockDim.x >> 6;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -1005,8 +1080,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAVQA_FX_WP
 
   const int j = j0 + col;  // the lane's key
   fx_bf8 kp[2][3], vp[2][3];
-  fx_load_strip(sv.k, j, g, kp);
-  fx_load_strip(sv.v, j, g, vp);
+  if constexpr (PL) {
+    fx_strip_planes(fx_tiles(pl.k, b, a.H, h, pl.ntk), j, g, kp);
+    fx_strip_planes(fx_tiles(pl.v, b, a.H, h, pl.ntk), j, g, vp);
+  } else {
+    fx_load_strip(sv.k, j, g, kp);
+    fx_load_strip(sv.v, j, g, vp);
+  }
   const bool kval = j < a.Tk;
   const bool kmasked = bld1(sv.kf, 4u * j, 0u) == 0.f;
   f4v dk[4], dv[4];
@@ -1023,7 +1103,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAVQA_FX_WP
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         gv[jt][r] = bld1(sv.g, gvo, (uint32_t)((iq0 + 4 * jt + r) * a.Tk) * 4u);
-    fx_stage2(sv.q, DO, iq0, a.Tq, Qs, dOs);
+    if constexpr (PL)
+      fx_stage_dma(fx_tiles(pl.q, b, a.H, h, pl.ntq) + (int64_t)qt * FX_TILE,
+                   fx_tiles(pl.dout, b, a.H, h, pl.ntq) + (int64_t)qt * FX_TILE, Qs, dOs, w, nw,
+                   lane);
+    else
+      fx_stage2(sv.q, DO, iq0, a.Tq, Qs, dOs);
     if (threadIdx.x < FL_KT) {
       const int iq = iq0 + threadIdx.x;
       const bool valid = iq < a.Tq;
@@ -1110,28 +1195,184 @@ static bool flash_x6() {
 
 using namespace savqa;
 
+namespace savqa {
+// One (sample, head, 64-row tile) of X per workgroup, split into FX_TILE bytes of bf16 planes
+// (fx_stage2's image, rows past T zero).
+__global__ __launch_bounds__(256) void attn_planes_kernel(const float* __restrict__ X, int64_t ldx,
+                                                          int T, int H, int nt, char* __restrict__ out) {
+  const int blk = blockIdx.x, t = blk % nt, bh = blk / nt;
+  const int b = bh / H, h = bh % H;
+  char* img = out + (int64_t)blk * FX_TILE;
+  const float* base = X + ((int64_t)b * T + (int64_t)t * FL_KT) * ldx + h * ATT_DK;
+  const int d4 = 4 * (threadIdx.x & 15);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int row = (threadIdx.x >> 4) + 16 * u;
+    f4v v = {0.f, 0.f, 0.f, 0.f};
+    if (t * FL_KT + row < T) v = *reinterpret_cast<const f4v*>(base + (int64_t)row * ldx + d4);
+    fx_bf4 a0, a1, a2;
+    fx_split4(v, a0, a1, a2);
+    const int off = fx_off(row, d4);
+    *reinterpret_cast<fx_bf4*>(img + off) = a0;
+    *reinterpret_cast<fx_bf4*>(img + FX_PLANE + off) = a1;
+    *reinterpret_cast<fx_bf4*>(img + 2 * FX_PLANE + off) = a2;
+  }
+}
+
+static int64_t planes_bytes(int64_t B, int64_t T, int64_t H) {
+  return B * H * ((T + FL_KT - 1) / FL_KT) * (int64_t)FX_TILE;
+}
+
+static int make_planes(hipStream_t s, const float* X, int64_t ldx, int64_t B, int64_t T,
+                       int64_t H, char* out) {
+  const int nt = (int)((T + FL_KT - 1) / FL_KT);
+  hipLaunchKernelGGL(attn_planes_kernel, dim3((unsigned)(B * H * nt)), dim3(256), 0, s, X, ldx,
+                     (int)T, (int)H, nt, out);
+  return check_launch("savqa_gattn_flash(planes)");
+}
+
+// Carve the workspace into Q / K / V (/ dO) plane tiles and fill them; false: no workspace
+static int flash_planes(hipStream_t s, const AttnArgs& a, bool bwd, void* ws, int64_t ws_bytes,
+                        FxPlanes& pl, bool& on, const char* who) {
+  on = false;
+  if (!ws) return 0;
+  const int64_t nq = planes_bytes(a.B, a.Tq, a.H), nk = planes_bytes(a.B, a.Tk, a.H);
+  if (((uintptr_t)ws & 15) || ws_bytes < nq + 2 * nk + (bwd ? nq : 0))
+    return fail(SAVQA_EINVAL, std::string(who) + ": workspace smaller than "
+                              "savqa_gattn_flash_ws_bytes or not 16-B aligned");
+  char* w = static_cast<char*>(ws);
+  pl.q = w;
+  pl.k = w + nq;
+  pl.v = w + nq + nk;
+  pl.dout = bwd ? w + nq + 2 * nk : nullptr;
+  pl.ntq = (a.Tq + FL_KT - 1) / FL_KT;
+  pl.ntk = (a.Tk + FL_KT - 1) / FL_KT;
+  if (int rc = make_planes(s, a.q, a.ldq, a.B, a.Tq, a.H, w)) return rc;
+  if (int rc = make_planes(s, a.k, a.ldk, a.B, a.Tk, a.H, w + nq)) return rc;
+  if (int rc = make_planes(s, a.v, a.ldv, a.B, a.Tk, a.H, w + nq + nk)) return rc;
+  if (bwd)
+    if (int rc = make_planes(s, a.dout, a.lddo, a.B, a.Tq, a.H, w + nq + 2 * nk)) return rc;
+  on = true;
+  return 0;
+}
+
+static int flash_fwd(hipStream_t s, AttnArgs& a, int64_t dk, float* stats, void* ws,
+                     int64_t ws_bytes) {
+  if (int rc = flash_validate(a, dk, "savqa_gattn_fwd_flash")) return rc;
+  if (!stats) return fail(SAVQA_EINVAL, "savqa_gattn_fwd_flash: stats buffer required");
+  const int nw = waves_for(a.Tq);
+  const int nqt = (a.Tq + 16 * nw - 1) / (16 * nw);
+  const dim3 grid((unsigned)((int64_t)a.B * a.H * nqt)), block(64 * nw);
+  if (flash_x6()) {
+    FxPlanes pl{};
+    bool on;
+    if (int rc = flash_planes(s, a, false, ws, ws_bytes, pl, on, "savqa_gattn_fwd_flash"))
+      return rc;
+    if (on)
+      hipLaunchKernelGGL(gattn_fwd_flash_x6_kernel<true>, grid, block, (size_t)2 * FX_TILE, s, a,
+                         stats, nqt, pl);
+    else
+      hipLaunchKernelGGL(gattn_fwd_flash_x6_kernel<false>, grid, block, (size_t)2 * FX_TILE, s, a,
+                         stats, nqt, pl);
+    return check_launch("savqa_gattn_fwd_flash");
+  }
+  const size_t lds = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + (size_t)nw * FL_KT * FL_WLD);
+  hipLaunchKernelGGL(gattn_fwd_flash_kernel, grid, block, lds, s, a, stats, nqt);
+  return check_launch("savqa_gattn_fwd_flash");
+}
+
+static int flash_bwd(hipStream_t s, AttnArgs& a, int64_t dk, float* stats, void* ws,
+                     int64_t ws_bytes) {
+  if (int rc = flash_validate(a, dk, "savqa_gattn_bwd_flash")) return rc;
+  if (!stats) return fail(SAVQA_EINVAL, "savqa_gattn_bwd_flash: stats required");
+  if ((((uintptr_t)a.dout) & 15) || (a.lddo & 3))
+    return fail(SAVQA_EINVAL, "savqa_gattn_bwd_flash: dO must be 16-B aligned, ld % 4 == 0");
+  const int nw = waves_for(a.Tq);
+  const int nqt = (a.Tq + 16 * nw - 1) / (16 * nw);
+  const int nwk = waves_for(a.Tk);
+  const int nkt2 = (a.Tk + 16 * nwk - 1) / (16 * nwk);
+  const dim3 gq((unsigned)((int64_t)a.B * a.H * nqt)), bq(64 * nw);
+  const dim3 gk((unsigned)((int64_t)a.B * a.H * nkt2)), bk(64 * nwk);
+  if (flash_x6()) {
+    FxPlanes pl{};
+    bool on;
+    if (int rc = flash_planes(s, a, true, ws, ws_bytes, pl, on, "savqa_gattn_bwd_flash"))
+      return rc;
+    const size_t lq = (size_t)2 * FX_TILE, lk = lq + sizeof(float) * FL_KT * 8;
+    // delta (stats[..][3]) for the dK/dV pass and dx for the dQ pass, then dQ, then dK / dV
+    if (on) {
+      hipLaunchKernelGGL(gattn_bwd_delta_flash_x6_kernel<true>, gq, bq, lq, s, a, stats, nqt, pl);
+      if (int rc = check_launch("savqa_gattn_bwd_flash(delta)")) return rc;
+      hipLaunchKernelGGL(gattn_bwd_q_flash_x6_kernel<true>, gq, bq, lq, s, a, stats, nqt, pl);
+      if (int rc = check_launch("savqa_gattn_bwd_flash(dq)")) return rc;
+      hipLaunchKernelGGL(gattn_bwd_kv_flash_x6_kernel<true>, gk, bk, lk, s, a, stats, nkt2, pl);
+    } else {
+      hipLaunchKernelGGL(gattn_bwd_delta_flash_x6_kernel<false>, gq, bq, lq, s, a, stats, nqt, pl);
+      if (int rc = check_launch("savqa_gattn_bwd_flash(delta)")) return rc;
+      hipLaunchKernelGGL(gattn_bwd_q_flash_x6_kernel<false>, gq, bq, lq, s, a, stats, nqt, pl);
+      if (int rc = check_launch("savqa_gattn_bwd_flash(dq)")) return rc;
+      hipLaunchKernelGGL(gattn_bwd_kv_flash_x6_kernel<false>, gk, bk, lk, s, a, stats, nkt2, pl);
+    }
+    return check_launch("savqa_gattn_bwd_flash(dkv)");
+  }
+  hipLaunchKernelGGL(gattn_bwd_delta_flash_kernel, gq, bq,
+                     sizeof(float) * (size_t)2 * FL_KT * ATT_KLD, s, a, stats, nqt);
+  if (int rc = check_launch("savqa_gattn_bwd_flash(delta)")) return rc;
+  const size_t lds = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + (size_t)nw * FL_KT * FL_WLD);
+  hipLaunchKernelGGL(gattn_bwd_q_flash_kernel, gq, bq, lds, s, a, stats, nqt);
+  if (int rc = check_launch("savqa_gattn_bwd_flash(dq)")) return rc;
+  const size_t ldk = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + FL_KT * 8 +
+                                      (size_t)nwk * FL_KT * FL_WLD);
+  hipLaunchKernelGGL(gattn_bwd_kv_flash_kernel, gk, bk, ldk, s, a, stats, nkt2);
+  return check_launch("savqa_gattn_bwd_flash(dkv)");
+}
+}  // namespace savqa
+
+static AttnArgs flash_args(const float* q, int64_t ldq, const float* k, int64_t ldk,
+                           const float* v, int64_t ldv, const float* G, const float* kflag,
+                           const float* qflag, int64_t B, int64_t Tq, int64_t Tk, int64_t H) {
+  AttnArgs a{};
+  a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv; a.G = G;
+  a.kflag = kflag; a.qflag = qflag; a.B = (int)B; a.Tq = (int)Tq; a.Tk = (int)Tk; a.H = (int)H;
+  return a;
+}
+
+extern "C" int64_t savqa_gattn_flash_ws_bytes(int64_t B, int64_t Tq, int64_t Tk, int64_t H,
+                                              int32_t backward) {
+  if (B <= 0 || Tq <= 0 || Tk <= 0 || H <= 0) return 0;
+  return (backward ? 2 : 1) * planes_bytes(B, Tq, H) + 2 * planes_bytes(B, Tk, H);
+}
+
+extern "C" int savqa_gattn_fwd_flash_ws(void* stream, const float* q, int64_t ldq, const float* k,
+                                        int64_t ldk, const float* v, int64_t ldv, const float* G,
+                                        const float* kflag, const float* qflag, int64_t B,
+                                        int64_t Tq, int64_t Tk, int64_t H, int64_t dk, float* o,
+                                        int64_t ldo, float* stats, void* ws, int64_t ws_bytes) {
+  AttnArgs a = flash_args(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H);
+  a.o = o; a.ldo = ldo;
+  return flash_fwd(as_stream(stream), a, dk, stats, ws, ws_bytes);
+}
+
 extern "C" int savqa_gattn_fwd_flash(void* stream, const float* q, int64_t ldq, const float* k,
                                      int64_t ldk, const float* v, int64_t ldv, const float* G,
                                      const float* kflag, const float* qflag, int64_t B,
                                      int64_t Tq, int64_t Tk, int64_t H, int64_t dk, float* o,
                                      int64_t ldo, float* stats) {
-  AttnArgs a{};
-  a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv; a.G = G;
-  a.kflag = kflag; a.qflag = qflag; a.B = (int)B; a.Tq = (int)Tq; a.Tk = (int)Tk; a.H = (int)H;
-  a.o = o; a.ldo = ldo;
-  if (int rc = flash_validate(a, dk, "savqa_gattn_fwd_flash")) return rc;
-  if (!stats) return fail(SAVQA_EINVAL, "savqa_gattn_fwd_flash: stats buffer required");
-  const int nw = waves_for((int)Tq);
-  const int nqt = (int)((Tq + 16 * nw - 1) / (16 * nw));
-  if (flash_x6()) {
-    hipLaunchKernelGGL(gattn_fwd_flash_x6_kernel, dim3((unsigned)(B * H * nqt)), dim3(64 * nw),
-                       (size_t)2 * FX_TILE, as_stream(stream), a, stats, nqt);
-    return check_launch("savqa_gattn_fwd_flash");
-  }
-  const size_t lds = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + (size_t)nw * FL_KT * FL_WLD);
-  hipLaunchKernelGGL(gattn_fwd_flash_kernel, dim3((unsigned)(B * H * nqt)), dim3(64 * nw), lds,
-                     as_stream(stream), a, stats, nqt);
-  return check_launch("savqa_gattn_fwd_flash");
+  return savqa_gattn_fwd_flash_ws(stream, q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H,
+                                  dk, o, ldo, stats, nullptr, 0);
+}
+
+extern "C" int savqa_gattn_bwd_flash_ws(void* stream, const float* q, int64_t ldq, const float* k,
+                                        int64_t ldk, const float* v, int64_t ldv, const float* G,
+                                        const float* kflag, const float* qflag, int64_t B,
+                                        int64_t Tq, int64_t Tk, int64_t H, int64_t dk,
+                                        const float* dout, int64_t lddo, float* stats, float* dq,
+                                        int64_t lddq, float* dk_, int64_t lddk, float* dv,
+                                        int64_t lddv, void* ws, int64_t ws_bytes) {
+  AttnArgs a = flash_args(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H);
+  a.dout = dout; a.lddo = lddo; a.dq = dq; a.lddq = lddq; a.dk = dk_; a.lddk = lddk;
+  a.dv = dv; a.lddv = lddv;
+  return flash_bwd(as_stream(stream), a, dk, stats, ws, ws_bytes);
 }
 
 extern "C" int savqa_gattn_bwd_flash(void* stream, const float* q, int64_t ldq, const float* k,
@@ -1141,50 +1382,6 @@ extern "C" int savqa_gattn_bwd_flash(void* stream, const float* q, int64_t ldq, 
                                      const float* dout, int64_t lddo, float* stats,
                                      float* dq, int64_t lddq, float* dk_, int64_t lddk, float* dv,
                                      int64_t lddv) {
-  AttnArgs a{};
-  a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv; a.G = G;
-  a.kflag = kflag; a.qflag = qflag; a.B = (int)B; a.Tq = (int)Tq; a.Tk = (int)Tk; a.H = (int)H;
-  a.dout = dout; a.lddo = lddo; a.dq = dq; a.lddq = lddq; a.dk = dk_; a.lddk = lddk;
-  a.dv = dv; a.lddv = lddv;
-  if (int rc = flash_validate(a, dk, "savqa_gattn_bwd_flash")) return rc;
-  if (!stats) return fail(SAVQA_EINVAL, "savqa_gattn_bwd_flash: stats required");
-  if ((((uintptr_t)dout) & 15) || (lddo & 3))
-    return fail(SAVQA_EINVAL, "savqa_gattn_bwd_flash: dO must be 16-B aligned, ld % 4 == 0");
-  hipStream_t s = as_stream(stream);
-  if (flash_x6()) {
-    const int nw = waves_for((int)Tq);
-    const int nqt = (int)((Tq + 16 * nw - 1) / (16 * nw));
-    hipLaunchKernelGGL(gattn_bwd_delta_flash_x6_kernel, dim3((unsigned)(B * H * nqt)),
-                       dim3(64 * nw), (size_t)2 * FX_TILE, s, a, stats, nqt);
-    if (int rc = check_launch("savqa_gattn_bwd_flash(delta)")) return rc;
-    hipLaunchKernelGGL(gattn_bwd_q_flash_x6_kernel, dim3((unsigned)(B * H * nqt)), dim3(64 * nw),
-                       (size_t)2 * FX_TILE, s, a, stats, nqt);
-    if (int rc = check_launch("savqa_gattn_bwd_flash(dq)")) return rc;
-    const int nwk = waves_for((int)Tk);
-    const int nkt2 = (int)((Tk + 16 * nwk - 1) / (16 * nwk));
-    hipLaunchKernelGGL(gattn_bwd_kv_flash_x6_kernel, dim3((unsigned)(B * H * nkt2)),
-                       dim3(64 * nwk), (size_t)2 * FX_TILE + sizeof(float) * FL_KT * 8, s, a,
-                       stats, nkt2);
-    return check_launch("savqa_gattn_bwd_flash(dkv)");
-  }
-  {  // delta (stats[..][3]) for the dK/dV pass and dx for the dQ pass, then dQ
-    const int nw = waves_for((int)Tq);
-    const int nqt = (int)((Tq + 16 * nw - 1) / (16 * nw));
-    hipLaunchKernelGGL(gattn_bwd_delta_flash_kernel, dim3((unsigned)(B * H * nqt)), dim3(64 * nw),
-                       sizeof(float) * (size_t)2 * FL_KT * ATT_KLD, s, a, stats, nqt);
-    if (int rc = check_launch("savqa_gattn_bwd_flash(delta)")) return rc;
-    const size_t lds = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + (size_t)nw * FL_KT * FL_WLD);
-    hipLaunchKernelGGL(gattn_bwd_q_flash_kernel, dim3((unsigned)(B * H * nqt)), dim3(64 * nw), lds,
-                       s, a, stats, nqt);
-    if (int rc = check_launch("savqa_gattn_bwd_flash(dq)")) return rc;
-  }
-  {
-    const int nw = waves_for((int)Tk);
-    const int nkt2 = (int)((Tk + 16 * nw - 1) / (16 * nw));
-    const size_t lds = sizeof(float) * ((size_t)2 * FL_KT * ATT_KLD + FL_KT * 8 +
-                                        (size_t)nw * FL_KT * FL_WLD);
-    hipLaunchKernelGGL(gattn_bwd_kv_flash_kernel, dim3((unsigned)(B * H * nkt2)), dim3(64 * nw),
-                       lds, s, a, stats, nkt2);
-  }
-  return check_launch("savqa_gattn_bwd_flash(dkv)");
+  return savqa_gattn_bwd_flash_ws(stream, q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H,
+                                  dk, dout, lddo, stats, dq, lddq, dk_, lddk, dv, lddv, nullptr, 0);
 }

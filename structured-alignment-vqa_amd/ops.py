@@ -566,19 +566,38 @@ def gattn_bwd(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout, lddo,
            _p(dk_), lddk, _p(dv), lddv)
 
 
+# The key-tiled kernels' operands pre-split into bf16 plane tiles in a workspace
+# (savqa_gattn_*_flash_ws) instead of by every workgroup. The split pass costs what the kernels
+# save except where many query tiles re-split each key tile: "auto" (default) pre-splits for
+# the backward at T_q >= 1024 only (tools/attn_bench.py --flash, profiles/r06_ab_flash_x6.txt);
+# SAVQA_FLASH_PLANES=1 always, 0 never.
+FLASH_PLANES = os.environ.get("SAVQA_FLASH_PLANES", "auto")
+
+
+def _flash_ws(B, Tq, Tk, H, bwd, dev):
+    if FLASH_PLANES == "0" or (FLASH_PLANES != "1" and not (bwd and Tq >= 1024)):
+        return None, 0
+    nb = int(_lib.load().savqa_gattn_flash_ws_bytes(B, Tq, Tk, H, int(bwd)))
+    ws = _workspace((nb + 3) // 4, dev)   # the stream's slab workspace: launches are ordered
+    return ws, nb
+
+
 def gattn_fwd_flash(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, o, ldo, stats, dk=64):
+    ws, nb = _flash_ws(B, Tq, Tk, H, False, q.device)
     _kcall(f"gattn_fwd_flash T{Tq}x{Tk}", _attn_bytes(q, B, Tq, Tk, H, dk, Tq + 2 * Tk, Tq),
-           4.0 * B * H * Tq * Tk * dk, "savqa_gattn_fwd_flash", _stream(), _p(q), ldq, _p(k), ldk,
-           _p(v), ldv, _p(G), _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(stats))
+           4.0 * B * H * Tq * Tk * dk, "savqa_gattn_fwd_flash_ws", _stream(), _p(q), ldq, _p(k),
+           ldk, _p(v), ldv, _p(G), _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(o), ldo, _p(stats),
+           _p(ws), nb)
 
 
 def gattn_bwd_flash(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout, lddo,
                     stats, dq, lddq, dk_, lddk, dv, lddv, dk=64):
+    ws, nb = _flash_ws(B, Tq, Tk, H, True, q.device)
     _kcall(f"gattn_bwd_flash T{Tq}x{Tk}",
            _attn_bytes(q, B, Tq, Tk, H, dk, 2 * Tq + 2 * Tk, Tq + 2 * Tk),
-           10.0 * B * H * Tq * Tk * dk, "savqa_gattn_bwd_flash", _stream(), _p(q), ldq, _p(k), ldk,
-           _p(v), ldv, _p(G), _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo, _p(stats),
-           _p(dq), lddq, _p(dk_), lddk, _p(dv), lddv)
+           10.0 * B * H * Tq * Tk * dk, "savqa_gattn_bwd_flash_ws", _stream(), _p(q), ldq, _p(k),
+           ldk, _p(v), ldv, _p(G), _p(kflag), _p(qflag), B, Tq, Tk, H, dk, _p(dout), lddo,
+           _p(stats), _p(dq), lddq, _p(dk_), lddk, _p(dv), lddv, _p(ws), nb)
 
 
 def gattn_fwd_q1s(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tk, H, o, ldo, stats, dk=64):

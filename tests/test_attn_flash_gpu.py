@@ -104,3 +104,34 @@ def test_flash_matches_full_row_kernels():
     O.gattn_bwd_flash(Q, 3 * D, K, 3 * D, V, 3 * D, G, kf, qf, B, T, T, H, dO, D, stats,
                       d2, 3 * D, d2[:, D:], 3 * D, d2[:, 2 * D:], 3 * D)
     assert rel(d2, d1) < 1e-4
+
+
+@pytest.mark.parametrize("B,Tq,Tk,H,D", [(2, 449, 449, 8, 512), (2, 17, 129, 4, 256),
+                                         (1, 1314, 1314, 8, 512), (3, 200, 7, 8, 512)])
+def test_flash_presplit_planes_bit_identical(B, Tq, Tk, H, D, monkeypatch):
+    """savqa_gattn_{fwd,bwd}_flash_ws (Q / K / V / dO split once into bf16 plane tiles, DMA'd
+    by the kernels) against the kernels splitting their own tiles (ws = NULL): the same splits
+    meet the same MFMAs in the same order, so outputs, dQ / dK / dV and the stats are
+    bit-identical -- ragged T (rows past T zero in the last tile), T_q != T_k, one tile."""
+    O = ops()
+    Q = g(B * Tq, D, seed=71, relu=True)
+    kv = g(B * Tk, 2 * D, seed=72, relu=True)
+    K, V = kv[:, :D], kv[:, D:]
+    G = (torch.rand(B, Tq, Tk, generator=torch.Generator().manual_seed(73)) < 0.3).float().to(dev)
+    kf = torch.ones(B, Tk, device=dev)
+    kf[0, -1] = 0.0
+    qf = torch.ones(B, Tq, device=dev)
+    dO = g(B * Tq, D, seed=74)
+    res = []
+    for mode in ("0", "1"):
+        monkeypatch.setattr(O, "FLASH_PLANES", mode)
+        out = torch.empty(B * Tq, D, device=dev)
+        st = torch.empty(B * H * Tq * 4, device=dev)
+        O.gattn_fwd_flash(Q, D, K, 2 * D, V, 2 * D, G, kf, qf, B, Tq, Tk, H, out, D, st)
+        dq = torch.empty(B * Tq, D, device=dev)
+        dkv = torch.empty(B * Tk, 2 * D, device=dev)
+        O.gattn_bwd_flash(Q, D, K, 2 * D, V, 2 * D, G, kf, qf, B, Tq, Tk, H, dO, D, st,
+                          dq, D, dkv, 2 * D, dkv[:, D:], 2 * D)
+        res.append((out, st, dq, dkv))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
