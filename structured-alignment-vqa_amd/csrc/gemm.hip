@@ -972,6 +972,18 @@ static int64_t sk_min_tiles() {
   }();
   return v;
 }
+// ... except tall launches (M >= SK_TALL_M, not the M = B decoder / head rows the skinny
+// kernels are tuned for) with at least SK_TALL_TILES workgroups: the cfg-2 M = 3584 launches of
+// 84 / 112 tiles (the question tokens' dX and GloVe-row gradients) run faster on 128 x 128
+// tiles. Round 6, interleaved (profiles/r06_ab_sk_tiles.txt): a plain threshold of 80 gave
+// cfg 2 7689 / 7682 -> 7749 / 7689 but cfg 5 24725 / 24674 -> 24590 / 24489 (its M = 1024
+// decoder launches of 128 tiles moved too); the tall rule: cfg 2 7558 / 7646 -> 7688 / 7730,
+// cfg 5 24652 / 24714 -> 24664 / 24753.
+constexpr int64_t SK_TALL_M = 2048, SK_TALL_TILES = 80;
+static bool sk_tiles_overridden() {
+  static const bool v = getenv("SAVQA_SK_TILES") != nullptr;
+  return v;
+}
 
 static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   if (d.M < 0 || d.N < 0 || d.K < 0) return fail(SAVQA_EINVAL, "savqa_gemm: negative dims");
@@ -997,7 +1009,8 @@ static int plan_gemm(savqa_gemm_desc& d, GemmPlan& p) {
   // 128x128 tiles once there is enough parallelism (split-K counts), else the skinny
   // kernel (32x32 tiles, K split over the 8 waves of a workgroup; no split-K launch),
   // 16x16 tiles while 32x32 ones would leave CUs idle (< SK16_MAX_TILES tiles)
-  if (tiles128 * split < sk_min_tiles()) {
+  if (tiles128 * split < sk_min_tiles() &&
+      !(d.M >= SK_TALL_M && tiles128 * split >= SK_TALL_TILES && !sk_tiles_overridden())) {
     const int64_t tiles32 = ((d.M + 31) / 32) * ((d.N + 31) / 32);
     p.tile = tiles32 < SK16_MAX_TILES ? 16 : 32;
     p.split = 1;
