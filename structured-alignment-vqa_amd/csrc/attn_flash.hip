@@ -269,6 +269,16 @@ __device__ __forceinline__ void fx_stage_dma(const char* x, const char* y, char*
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
+// DMA one pre-split tile (no wait): wave w copies 1-KB chunks w, w + nw, ...
+__device__ __forceinline__ void fx_dma_tile(const char* x, char* Xs, int w, int nw, int lane) {
+  for (int c = w; c < FX_TILE / 1024; c += nw) fx_dma16(x + c * 1024 + lane * 16, Xs + c * 1024);
+}
+// vmcnt(0) through the builtin (expcnt / lgkmcnt left at their maxima), so that the
+// compiler's waitcnt pass sees it too and drops its own later waits for loads it covers (an
+// asm wait is invisible to it: it then waits again, and that wait also drains the DMAs issued
+// after those loads)
+__device__ __forceinline__ void fx_wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // the lane's strip row from pre-split tiles (tiles: the (sample, head)'s first tile)
 __device__ __forceinline__ void fx_strip_planes(const char* tiles, int row, int g,
                                                 fx_bf8 (&xp)[2][3]) {
@@ -282,6 +292,22 @@ __device__ __forceinline__ void fx_strip_planes(const char* tiles, int row, int 
 }
 __device__ __forceinline__ const char* fx_tiles(const char* base, int b, int H, int h, int nt) {
   return base + ((int64_t)b * H + h) * nt * (int64_t)FX_TILE;
+}
+
+// graph / key-flag values of the lane's query (row q of the sample) for the tile's keys
+// k0 + 16g + 4jt + r (16-B loads; reads past T come back as neighbouring or zero values and are
+// masked by the callers)
+__device__ __forceinline__ void fx_graph_row(const BView& G, const BView& KF, uint32_t gvo,
+                                             int k0, int g, f4v (&gv)[4], uint32_t& kmask) {
+  kmask = 0;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) {
+    const uint32_t so = (uint32_t)(k0 + 4 * jt) * 4u;
+    const f4v kf = bld16b<f4v>(KF, 64u * g, so);
+    gv[jt] = bld16b<f4v>(G, gvo, so);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) kmask |= (kf[r] == 0.f ? 1u : 0u) << (4 * jt + r);
+  }
 }
 
 // acc[jt][r] = sum_d T[16g + 4jt + r][d] * strip[col][d]: the staged tile's rows
@@ -526,6 +552,118 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
     fx_accum(Vs, s, lane, o);
+  }
+  const int i = i0 + col;
+  if (i < a.Tq) {
+    const int64_t qb = (int64_t)b * a.Tq;
+    const BView O = head_view(a.o, a.ldo, (int64_t)a.B * a.Tq, qb, h * ATT_DK);
+    const float D = fmaxf(W, 1e-12f * Z);
+    const float sc = bld1(sv.qf, 4u * i, 0u) / D;
+    const uint32_t ovo = (uint32_t)i * O.ld + 16u * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) bst16b(O, o[dt] * sc, ovo, 64u * dt);
+    if (g == 0) {
+      float* st = stats + (((int64_t)b * a.H + h) * a.Tq + i) * 4;
+      st[0] = m;
+      st[1] = Z;
+      st[2] = W;
+    }
+  }
+}
+
+// The forward over pre-split tiles with the K / V DMAs pipelined behind compute: K(t+1) is
+// fetched while P V reads V(t), V(t+1) while the next tile's scores read K(t+1) and its
+// softmax runs (two barriers per tile, as the unpipelined form, and the same 48 KB of LDS).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gattn_fwd_flash_x6pp_kernel(
+    AttnArgs a, float* __restrict__ stats, int nqt, FxPlanes pl) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int nw = blockDim.x >> 6;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = bid % nqt, bh = bid / nqt;
+  const int b = bh / a.H, h = bh % a.H;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = qt * 16 * nw + w * 16;
+  char* Ks = reinterpret_cast<char*>(sm);
+  char* Vs = Ks + FX_TILE;
+  const StripViews<AttnArgs> sv(a, b, h);
+  const char* ktl = fx_tiles(pl.k, b, a.H, h, pl.ntk);
+  const char* vtl = fx_tiles(pl.v, b, a.H, h, pl.ntk);
+
+  fx_dma_tile(ktl, Ks, w, nw, lane);
+  fx_dma_tile(vtl, Vs, w, nw, lane);
+  fx_bf8 qp[2][3];
+  fx_strip_planes(fx_tiles(pl.q, b, a.H, h, pl.ntq), i0 + col, g, qp);
+  float m = -INFINITY, Z = 0.f, W = 0.f;
+  f4v o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f4v{0.f, 0.f, 0.f, 0.f};
+  const uint32_t gvo = (uint32_t)((i0 + col) * a.Tk + 16 * g) * 4u;
+  const int nkt = (a.Tk + FL_KT - 1) / FL_KT;
+  fx_wait_vm0();
+  __syncthreads();  // K(0), V(0) staged
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * FL_KT;
+    f4v gv[4], kf[4];  // consumed only after the scores: their wait (which also covers
+                       // the V DMAs issued before them) sits behind the score MFMAs
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) {
+      const uint32_t so = (uint32_t)(k0 + 4 * jt) * 4u;
+      kf[jt] = bld16b<f4v>(sv.kf, 64u * g, so);
+      gv[jt] = bld16b<f4v>(sv.g, gvo, so);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // ... issued ahead of the score MFMAs
+    f4v s[4];
+    fx_dots<4>(Ks, qp, col, g, s);
+    __builtin_amdgcn_sched_barrier(0);  // the flags' first use (and its wait) stays behind
+    uint32_t kmask = 0;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) kmask |= (kf[jt][r] == 0.f ? 1u : 0u) << (4 * jt + r);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = k0 + 16 * g + 4 * jt + r;
+        float v = -INFINITY;
+        if (j < a.Tk) v = (kmask >> (4 * jt + r)) & 1u ? ATT_MASKED : s[jt][r] * ATT_SCALE2;
+        s[jt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mn = fmaxf(m, mx);
+    const float alpha = att_exp2(m - mn);
+    float zs = 0.f, ws = 0.f;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = k0 + 16 * g + 4 * jt + r;
+        const float e = j < a.Tk ? att_exp2(s[jt][r] - mn) : 0.f;
+        const float gg = j < a.Tk ? gv[jt][r] : 0.f;
+        zs += e;
+        ws += e * fabsf(gg);
+        s[jt][r] = e * gg;
+      }
+    zs += __shfl_xor(zs, 16);
+    zs += __shfl_xor(zs, 32);
+    ws += __shfl_xor(ws, 16);
+    ws += __shfl_xor(ws, 32);
+    Z = Z * alpha + zs;
+    W = W * alpha + ws;
+    m = mn;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+    fx_wait_vm0();    // this wave's V(kt) DMAs (issued last tile) have landed
+    __syncthreads();  // every wave: done with K(kt), V(kt) staged
+    if (kt + 1 < nkt) fx_dma_tile(ktl + (int64_t)(kt + 1) * FX_TILE, Ks, w, nw, lane);
+    fx_accum(Vs, s, lane, o);
+    fx_wait_vm0();    // this wave's K(kt + 1) DMAs have landed
+    __syncthreads();  // every wave: done with V(kt), K(kt + 1) staged
+    if (kt + 1 < nkt) fx_dma_tile(vtl + (int64_t)(kt + 1) * FX_TILE, Vs, w, nw, lane);
   }
   const int i = i0 + col;
   if (i < a.Tq) {
@@ -877,22 +1015,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
 // The three backward kernels above with x6 products (see "x6 products"): identical math per
 // (query, key) pair; the strips on the lanes (queries for delta / dQ, keys for dK / dV), the
 // staged tile's rows in registers.
-
-// graph / key-flag values of the lane's query (row q of the sample) for the tile's keys
-// k0 + 16g + 4jt + r (16-B loads; reads past T come back as neighbouring or zero values and are
-// masked by the callers)
-__device__ __forceinline__ void fx_graph_row(const BView& G, const BView& KF, uint32_t gvo,
-                                             int k0, int g, f4v (&gv)[4], uint32_t& kmask) {
-  kmask = 0;
-#pragma unroll
-  for (int jt = 0; jt < 4; ++jt) {
-    const uint32_t so = (uint32_t)(k0 + 4 * jt) * 4u;
-    const f4v kf = bld16b<f4v>(KF, 64u * g, so);
-    gv[jt] = bld16b<f4v>(G, gvo, so);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) kmask |= (kf[r] == 0.f ? 1u : 0u) << (4 * jt + r);
-  }
-}
 
 template <bool PL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gattn_bwd_delta_flash_x6_kernel(
@@ -1268,7 +1390,11 @@ static int flash_fwd(hipStream_t s, AttnArgs& a, int64_t dk, float* stats, void*
     bool on;
     if (int rc = flash_planes(s, a, false, ws, ws_bytes, pl, on, "savqa_gattn_fwd_flash"))
       return rc;
-    if (on)
+    const char* pe = getenv("SAVQA_FX_PIPE");
+    if (on && !(pe && pe[0] == '0'))
+      hipLaunchKernelGGL(gattn_fwd_flash_x6pp_kernel, grid, block, (size_t)2 * FX_TILE, s, a,
+                         stats, nqt, pl);
+    else if (on)
       hipLaunchKernelGGL(gattn_fwd_flash_x6_kernel<true>, grid, block, (size_t)2 * FX_TILE, s, a,
                          stats, nqt, pl);
     else

@@ -568,14 +568,16 @@ def gattn_bwd(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout, lddo,
 
 # The key-tiled kernels' operands pre-split into bf16 plane tiles in a workspace
 # (savqa_gattn_*_flash_ws) instead of by every workgroup. The split pass costs what the kernels
-# save except where many query tiles re-split each key tile: "auto" (default) pre-splits for
-# the backward at T_q >= 1024 only (tools/attn_bench.py --flash, profiles/r06_ab_flash_x6.txt);
-# SAVQA_FLASH_PLANES=1 always, 0 never.
+# save except where many query tiles re-split each key tile: "auto" (default) pre-splits at
+# T_q >= 1024 only (tools/attn_bench.py --flash, profiles/r06_ab_flash_x6.txt: at T = 1314
+# forward 149 -> 142 us with the DMA-pipelined kernel, backward 571 -> 521 us; at T = 449 both
+# slower); SAVQA_FLASH_PLANES=1 always, 0 never, "bwd" the backward at T_q >= 1024 only.
 FLASH_PLANES = os.environ.get("SAVQA_FLASH_PLANES", "auto")
 
 
 def _flash_ws(B, Tq, Tk, H, bwd, dev):
-    if FLASH_PLANES == "0" or (FLASH_PLANES != "1" and not (bwd and Tq >= 1024)):
+    if FLASH_PLANES == "0" or (FLASH_PLANES != "1" and Tq < 1024) or \
+            (FLASH_PLANES == "bwd" and not bwd):
         return None, 0
     nb = int(_lib.load().savqa_gattn_flash_ws_bytes(B, Tq, Tk, H, int(bwd)))
     ws = _workspace((nb + 3) // 4, dev)   # the stream's slab workspace: launches are ordered
