@@ -568,11 +568,12 @@ def gattn_bwd(q, ldq, k, ldk, v, ldv, G, kflag, qflag, B, Tq, Tk, H, dout, lddo,
 
 # The key-tiled kernels' operands pre-split into bf16 plane tiles in a workspace
 # (savqa_gattn_*_flash_ws) instead of by every workgroup. The split pass costs what the kernels
-# save except where many query tiles re-split each key tile: "auto" (default) pre-splits at
-# T_q >= 1024 only (tools/attn_bench.py --flash, profiles/r06_ab_flash_x6.txt: at T = 1314
-# forward 149 -> 142 us with the DMA-pipelined kernel, backward 571 -> 521 us; at T = 449 both
-# slower); SAVQA_FLASH_PLANES=1 always, 0 never, "bwd" the backward at T_q >= 1024 only.
-FLASH_PLANES = os.environ.get("SAVQA_FLASH_PLANES", "auto")
+# save except where many query tiles re-split each key tile (profiles/r06_ab_flash_x6.txt): "bwd"
+# (default) pre-splits the backward at T_q >= 1024 (571 -> 521 us at T = 1314); "auto" the
+# forward there too (the DMA-pipelined kernel: 149 -> 142 us alone, but the relation workload's
+# step measured 258.8 vs 249.3 QA-samples/s mean in favour of "bwd", 4 interleaved runs each);
+# SAVQA_FLASH_PLANES=1 always, 0 never.
+FLASH_PLANES = os.environ.get("SAVQA_FLASH_PLANES", "bwd")
 
 
 def _flash_ws(B, Tq, Tk, H, bwd, dev):
