@@ -876,3 +876,22 @@ def test_x6_weight_planes_batch_matches_reference_layout():
         O.call("savqa_x6_weight_planes", O._stream(), W.data_ptr(), ld, int(bt), N, K,
                one.data_ptr())
         assert torch.equal(one, out), i
+
+
+@pytest.mark.parametrize("M,N,K,tile", [(3584, 512, 1024, 128), (3584, 300, 2048, 128),
+                                        (1024, 2048, 512, 32), (256, 2048, 512, 32)])
+def test_gemm_planner_tall_launches(M, N, K, tile):
+    """plan_gemm: 128x128-tile launches with < 160 tiles go to the skinny kernels (tuned on the
+    M = B decoder rows) except tall ones (M >= 2048) with >= 80 tiles, which take the x6 kernel
+    (the cfg-2 question-token dX / GloVe-row gradient shapes); results to fp32 accuracy either
+    way, with an A row gather as the engine's dX launch has."""
+    if "SAVQA_SK_TILES" in __import__("os").environ:
+        pytest.skip("SAVQA_SK_TILES overrides the planner")
+    O = ops()
+    A, B = g(M + 17, K, seed=91), g(K, N, seed=92)
+    idx = torch.randint(0, M + 17, (M,), generator=torch.Generator().manual_seed(93)).to(dev)
+    kw = dict(lda=K, ldb=N, ldc=N, a_rows=idx, prec=6)
+    assert O.gemm(A, B, None, M, N, K, plan_only=True, **kw)[0] == tile
+    out = torch.empty(M, N, device=dev)
+    O.gemm(A, B, out, M, N, K, **kw)
+    assert rel(out, A[idx].double() @ B.double()) < 1e-5
